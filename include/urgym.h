@@ -1,0 +1,107 @@
+/* urgym.h -- C-ABI of the MI355X-native URGym hot path (liburgym.so).
+ *
+ * The reference reaches its physics through the `pybullet` module's free
+ * functions, one env per process.  This boundary replaces
+ * that per-substep Python<->C traffic with one batched call per env-step:
+ * the whole move_ee -> wait_until_stable -> reward pipeline runs on the GPU.
+ * Each entry point names the reference interface it replaces.
+ *
+ * Conventions: plain pointers and sizes, no torch types.  Host-pointer entry
+ * points are synchronous; *_device variants take device pointers, enqueue on
+ * the handle's HIP stream and return immediately (urgym_sync waits).
+ * Return 0 on success, <0 on error (message via urgym_last_error).  A handle
+ * owns its device memory and stream; it is not thread-safe, distinct handles
+ * are.  One handle per GPU (device_ordinal); env batches shard across GPUs
+ * by creating one handle per rank.
+ */
+#ifndef URGYM_H
+#define URGYM_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct urgym_handle urgym_handle;
+
+#define URGYM_TASK_BALLBALANCE 0 /* urgym/envs/__init__.py:28-32  URGym/BallBalance-v0 */
+#define URGYM_TASK_CUBESPUSH 1   /* urgym/envs/__init__.py:10-14  URGym/CubesPush-v0   */
+#define URGYM_TASK_CUBESGRASP 2  /* urgym/envs/__init__.py:22-26  URGym/CubesGrasp-v0  */
+#define URGYM_TASK_GOLF 3        /* urgym/envs/__init__.py:40-44  URGym/Golf-v0        */
+
+/* Replaces: gym.make(id) -> Env.__init__ (p.connect(DIRECT), loadURDF plane/table/robot,
+ *   UR5Robotiq85.load(), env_ball_balance_v0.py:34-80; robot.py:178-211).
+ * n_envs independent environments on GPU `device_ordinal`; precision must be 64
+ * (FP64, PyBullet's double build [ext]); env i seeds its Python-`random`-compatible
+ * MT19937 stream with seed + env_offset + i (env_*: random.uniform draws).
+ * Returns NULL on error (urgym_last_error(NULL) explains). */
+urgym_handle* urgym_create(int task_id, int n_envs, int device_ordinal, int precision, uint32_t seed,
+                           int env_offset);
+
+/* Replaces: Env.close() -> p.disconnect (env_ball_balance_v0.py:172-173). */
+void urgym_destroy(urgym_handle* h);
+
+/* Last error message for h (or the last creation error when h == NULL). */
+const char* urgym_last_error(const urgym_handle* h);
+
+/* Static shapes: observation_space / action_space (env_ball_balance_v0.py:52-54 etc.). */
+int urgym_obs_dim(int task_id);
+int urgym_act_dim(int task_id);
+int urgym_state_dim(void);
+int urgym_num_envs(const urgym_handle* h);
+
+/* gymnasium TimeLimit (envs/__init__.py max_episode_steps) and VectorEnv same-step autoreset:
+ * when enabled, an env that terminates or truncates inside urgym_step is reset in the same call
+ * (obs then holds the reset observation, final_obs the terminal one). max_episode_steps <= 0
+ * disables truncation. */
+int urgym_set_autoreset(urgym_handle* h, int enable, int max_episode_steps);
+
+/* Replaces: Env.reset() (env_ball_balance_v0.py:145-170 and per-env reset()).
+ * mask: n_envs bytes (nonzero = reset that env) or NULL for all.
+ * reset_draws: n_envs x urgym_num_draws(task) uniforms in [0,1) replacing random.random()
+ * for each env's reset, or NULL to use the per-env device MT19937 streams.
+ * obs: n_envs x obs_dim (FP64), rows of unmasked envs untouched. */
+int urgym_reset(urgym_handle* h, const uint8_t* mask, const double* reset_draws, double* obs);
+int urgym_num_draws(int task_id);
+
+/* Replaces: Env.step(action) (env_ball_balance_v0.py:105-134; robot.py:113-128 move_ee ->
+ * p.calculateInverseKinematics + p.setJointMotorControl2; wait_until_stable :94-103 ->
+ * <=480 x p.stepSimulation + getJointState/getLinkState; reward/termination).
+ * actions: n_envs x act_dim float32.  Outputs (any may be NULL except obs):
+ * obs n x obs_dim, final_obs n x obs_dim (only rows of reset envs written), reward n,
+ * terminated n, truncated n, success n (info['is_success']), substeps n (int32: physics
+ * substeps spent in this call, reset included). */
+int urgym_step(urgym_handle* h, const float* actions, double* obs, double* final_obs, double* reward,
+               uint8_t* terminated, uint8_t* truncated, uint8_t* success, int32_t* substeps);
+
+/* Same as urgym_step with device pointers; asynchronous on the handle's stream. */
+int urgym_step_device(urgym_handle* h, const float* d_actions, double* d_obs, double* d_final_obs,
+                      double* d_reward, uint8_t* d_terminated, uint8_t* d_truncated, uint8_t* d_success,
+                      int32_t* d_substeps);
+int urgym_reset_device(urgym_handle* h, const uint8_t* d_mask, const double* d_reset_draws, double* d_obs);
+int urgym_sync(urgym_handle* h);
+/* hipStream_t of the handle (as void*), for callers that order their own work after ours. */
+void* urgym_stream(urgym_handle* h);
+
+/* Checkpoint / parity: full per-env simulator state, n_envs x urgym_state_dim() doubles
+ * (layout: urgym_amd/csrc/ug_layout.h).  No reference counterpart (the reference never
+ * saves env state). */
+int urgym_get_state(urgym_handle* h, double* state);
+int urgym_set_state(urgym_handle* h, const double* state);
+
+/* Replaces: one p.stepSimulation() for every env (fine-grained parity tests). */
+int urgym_substep(urgym_handle* h);
+/* Replaces: p.getLinkState(robot, link)[0:2] -> n_envs x 7 (pos, quat xyzw). */
+int urgym_link_state(urgym_handle* h, int link, double* out);
+/* Replaces: p.calculateInverseKinematics(robot, 7, pos, orn, ...) (robot.py:119-121):
+ * target n_envs x 7 (pos, quat) -> q_out n_envs x 12, from each env's current joints. */
+int urgym_ik(urgym_handle* h, const double* target, double* q_out);
+
+/* Device time (ms) of the most recent step/reset kernel, measured with HIP events on the
+ * handle's stream (bench.py roofline). */
+double urgym_last_kernel_ms(const urgym_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,128 @@
+"""ctypes binding of the CPU restatement (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module.  It builds nothing at import time; run `make -C oracle` (done by
+__graft_entry__.build()).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libugoracle.so")
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("oracle not built: run `make -C oracle`")
+        L = ctypes.CDLL(LIB_PATH)
+        P, D, I, U32 = ctypes.c_void_p, ctypes.c_double, ctypes.c_int, ctypes.c_uint32
+        L.ugo_create.restype = P
+        L.ugo_create.argtypes = [I, U32]
+        L.ugo_destroy.argtypes = [P]
+        L.ugo_obs_dim.argtypes = [I]
+        L.ugo_act_dim.argtypes = [I]
+        L.ugo_state_dim.argtypes = []
+        L.ugo_reset.argtypes = [P, P]
+        L.ugo_step.argtypes = [P, P, P, P, P, P]
+        L.ugo_get_state.argtypes = [P, P]
+        L.ugo_set_state.argtypes = [P, P]
+        L.ugo_substep.argtypes = [P]
+        L.ugo_rng_seed.argtypes = [P, U32]
+        L.ugo_rng_random.argtypes = [P]
+        L.ugo_rng_random.restype = D
+        L.ugo_gdr.argtypes = [D, D, D]
+        L.ugo_gdr.restype = D
+        L.ugo_euler_from_quat.argtypes = [P, P]
+        L.ugo_quat_from_euler.argtypes = [P, P]
+        L.ugo_gripper_angle.argtypes = [D]
+        L.ugo_gripper_angle.restype = D
+        L.ugo_link_state.argtypes = [P, I, P]
+        L.ugo_ik.argtypes = [P, P, P, P]
+        L.ugo_batch_step.restype = ctypes.c_long
+        L.ugo_batch_step.argtypes = [P, I, P, P, P, P, P, P, I, I, P]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class OracleEnv:
+    """One environment of the CPU restatement."""
+
+    def __init__(self, task, seed):
+        self.L = lib()
+        self.task = task
+        self.h = self.L.ugo_create(task, seed)
+        self.obs_dim = self.L.ugo_obs_dim(task)
+        self.act_dim = self.L.ugo_act_dim(task)
+        self.state_dim = self.L.ugo_state_dim()
+
+    def __del__(self):
+        try:
+            self.L.ugo_destroy(self.h)
+        except Exception:
+            pass
+
+    def reset(self):
+        obs = np.zeros(self.obs_dim)
+        n = self.L.ugo_reset(self.h, _p(obs))
+        return obs, n
+
+    def step(self, action):
+        a = np.ascontiguousarray(action, dtype=np.float32)
+        obs = np.zeros(self.obs_dim)
+        rew = np.zeros(1)
+        term = np.zeros(1, np.uint8)
+        succ = np.zeros(1, np.uint8)
+        n = self.L.ugo_step(self.h, _p(a), _p(obs), _p(rew), _p(term), _p(succ))
+        return obs, float(rew[0]), bool(term[0]), bool(succ[0]), n
+
+    def substep(self):
+        self.L.ugo_substep(self.h)
+
+    def get_state(self):
+        s = np.zeros(self.state_dim)
+        self.L.ugo_get_state(self.h, _p(s))
+        return s
+
+    def set_state(self, s):
+        s = np.ascontiguousarray(s, dtype=np.float64)
+        self.L.ugo_set_state(self.h, _p(s))
+
+    def link_state(self, link):
+        out = np.zeros(7)
+        self.L.ugo_link_state(self.h, link, _p(out))
+        return out
+
+    def ik(self, pos, orn):
+        q = np.zeros(12)
+        self.L.ugo_ik(self.h, _p(np.asarray(pos, np.float64)), _p(np.asarray(orn, np.float64)), _p(q))
+        return q
+
+
+def gdr(v, s, m):
+    return lib().ugo_gdr(v, s, m)
+
+
+def euler_from_quat(q):
+    out = np.zeros(3)
+    lib().ugo_euler_from_quat(_p(np.asarray(q, np.float64)), _p(out))
+    return out
+
+
+def quat_from_euler(e):
+    out = np.zeros(4)
+    lib().ugo_quat_from_euler(_p(np.asarray(e, np.float64)), _p(out))
+    return out
+
+
+def gripper_angle(L):
+    return lib().ugo_gripper_angle(L)

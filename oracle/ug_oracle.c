@@ -1,0 +1,1872 @@
+/* ug_oracle.c -- CPU restatement of URGym's hot path (TEST INFRASTRUCTURE ONLY).
+ *
+ * Plain C99, one environment at a time, array-of-structs, no vectorisation:
+ * the readable statement of the algorithm that the HIP kernels in
+ * urgym_amd/csrc must reproduce bit-for-bit (same operation order, no FMA
+ * contraction: build with -ffp-contract=off; transcendentals from
+ * urgym_amd/csrc/ug_detmath.h).  See ug_oracle.h for scope and DESIGN.md for
+ * the Bullet behaviours restated here ([ext] = from Bullet/PyBullet, not
+ * checkable in this build).
+ */
+#include "ug_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#include "../urgym_amd/csrc/model_data.h"
+#include "../urgym_amd/csrc/scene_data.h"
+#include "../urgym_amd/csrc/ug_detmath.h"
+
+#define NB UG_NB
+#define MAXOBJ 2
+#define NV (NB + 6 * MAXOBJ)
+#define MAXMAN 16
+#define MAXROWS 128
+#define MAXCOL 24
+#define MAXPAIR 96
+#define MAXCAND 64
+#define PT_DOUBLES 13
+#define MAN_DOUBLES (2 + 4 * PT_DOUBLES)
+#define STATE_DIM (66 + 1 + MAXMAN * MAN_DOUBLES + 4)
+
+/* ======================================================================== */
+/* small linear algebra (fixed evaluation order, mirrored by the HIP side)   */
+/* ======================================================================== */
+typedef struct { double x, y, z; } v3;
+typedef struct { double m[9]; } m3; /* row-major */
+typedef struct { double x, y, z, w; } q4;
+
+static v3 V(double x, double y, double z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
+static v3 vadd(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+static v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+static v3 vscale(v3 a, double s) { return V(a.x * s, a.y * s, a.z * s); }
+static v3 vneg(v3 a) { return V(-a.x, -a.y, -a.z); }
+static double vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static v3 vcross(v3 a, v3 b) { return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+static double vlen(v3 a) { return ug_sqrt(vdot(a, a)); }
+static v3 mv(const m3* M, v3 v) {
+    const double* m = M->m;
+    return V(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[3] * v.x + m[4] * v.y + m[5] * v.z,
+             m[6] * v.x + m[7] * v.y + m[8] * v.z);
+}
+static v3 mtv(const m3* M, v3 v) { /* M^T v */
+    const double* m = M->m;
+    return V(m[0] * v.x + m[3] * v.y + m[6] * v.z, m[1] * v.x + m[4] * v.y + m[7] * v.z,
+             m[2] * v.x + m[5] * v.y + m[8] * v.z);
+}
+static m3 mm(const m3* A, const m3* B) {
+    m3 C;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            C.m[3 * i + j] = A->m[3 * i] * B->m[j] + A->m[3 * i + 1] * B->m[3 + j] + A->m[3 * i + 2] * B->m[6 + j];
+    return C;
+}
+static m3 mtm(const m3* A, const m3* B) { /* A^T B */
+    m3 C;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            C.m[3 * i + j] = A->m[i] * B->m[j] + A->m[3 + i] * B->m[3 + j] + A->m[6 + i] * B->m[6 + j];
+    return C;
+}
+static m3 mload(const double* p) { m3 r; memcpy(r.m, p, sizeof(r.m)); return r; }
+static m3 mident(void) { m3 r; memset(r.m, 0, sizeof(r.m)); r.m[0] = r.m[4] = r.m[8] = 1.0; return r; }
+/* symmetric inertia (xx,yy,zz,xy,xz,yz) in frame R -> world: R I R^T */
+static m3 inertia_world(const m3* R, const double* I6) {
+    m3 I;
+    I.m[0] = I6[0]; I.m[4] = I6[1]; I.m[8] = I6[2];
+    I.m[1] = I.m[3] = I6[3]; I.m[2] = I.m[6] = I6[4]; I.m[5] = I.m[7] = I6[5];
+    m3 T = mm(R, &I);
+    m3 C;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            C.m[3 * i + j] = T.m[3 * i] * R->m[3 * j] + T.m[3 * i + 1] * R->m[3 * j + 1] + T.m[3 * i + 2] * R->m[3 * j + 2];
+    return C;
+}
+/* Rodrigues rotation about unit axis a by angle q */
+static m3 axis_angle(v3 a, double q) {
+    double c = ug_cos(q), s = ug_sin(q), t = 1.0 - c;
+    m3 R;
+    R.m[0] = t * a.x * a.x + c;       R.m[1] = t * a.x * a.y - s * a.z; R.m[2] = t * a.x * a.z + s * a.y;
+    R.m[3] = t * a.x * a.y + s * a.z; R.m[4] = t * a.y * a.y + c;       R.m[5] = t * a.y * a.z - s * a.x;
+    R.m[6] = t * a.x * a.z - s * a.y; R.m[7] = t * a.y * a.z + s * a.x; R.m[8] = t * a.z * a.z + c;
+    return R;
+}
+static q4 Q(double x, double y, double z, double w) { q4 r; r.x = x; r.y = y; r.z = z; r.w = w; return r; }
+/* btQuaternion operator* (Hamilton product, (x,y,z,w)) */
+static q4 qmul(q4 a, q4 b) {
+    return Q(a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y, a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z,
+             a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x, a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z);
+}
+static q4 qnormalize(q4 a) {
+    double l = ug_sqrt(a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w);
+    return Q(a.x / l, a.y / l, a.z / l, a.w / l);
+}
+/* btMatrix3x3::setRotation */
+static m3 qmat(q4 q) {
+    double d = q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w;
+    double s = 2.0 / d;
+    double xs = q.x * s, ys = q.y * s, zs = q.z * s;
+    double wx = q.w * xs, wy = q.w * ys, wz = q.w * zs;
+    double xx = q.x * xs, xy = q.x * ys, xz = q.x * zs;
+    double yy = q.y * ys, yz = q.y * zs, zz = q.z * zs;
+    m3 R;
+    R.m[0] = 1.0 - (yy + zz); R.m[1] = xy - wz; R.m[2] = xz + wy;
+    R.m[3] = xy + wz; R.m[4] = 1.0 - (xx + zz); R.m[5] = yz - wx;
+    R.m[6] = xz - wy; R.m[7] = yz + wx; R.m[8] = 1.0 - (xx + yy);
+    return R;
+}
+/* btMatrix3x3::getRotation */
+static q4 mquat(const m3* M) {
+    const double* m = M->m;
+    double trace = m[0] + m[4] + m[8];
+    double t[4];
+    if (trace > 0.0) {
+        double s = ug_sqrt(trace + 1.0);
+        t[3] = s * 0.5;
+        s = 0.5 / s;
+        t[0] = (m[7] - m[5]) * s;
+        t[1] = (m[2] - m[6]) * s;
+        t[2] = (m[3] - m[1]) * s;
+    } else {
+        int i = m[0] < m[4] ? (m[4] < m[8] ? 2 : 1) : (m[0] < m[8] ? 2 : 0);
+        int j = (i + 1) % 3, k = (i + 2) % 3;
+        double s = ug_sqrt(m[4 * i] - m[4 * j] - m[4 * k] + 1.0);
+        t[i] = s * 0.5;
+        s = 0.5 / s;
+        t[3] = (m[3 * k + j] - m[3 * j + k]) * s;
+        t[j] = (m[3 * j + i] + m[3 * i + j]) * s;
+        t[k] = (m[3 * k + i] + m[3 * i + k]) * s;
+    }
+    return Q(t[0], t[1], t[2], t[3]);
+}
+
+/* pybullet.c getEulerFromQuaternion / getQuaternionFromEuler [ext] (used by env_ball_balance_v0.py:114-116,139) */
+static v3 euler_from_quat(q4 q) {
+    double sqx = q.x * q.x, sqy = q.y * q.y, sqz = q.z * q.z, squ = q.w * q.w;
+    double sarg = -2.0 * (q.x * q.z - q.w * q.y);
+    v3 r;
+    if (sarg <= -0.99999) {
+        r.x = 0.0; r.y = -0.5 * UG_PI; r.z = 2.0 * ug_atan2(q.x, -q.y);
+    } else if (sarg >= 0.99999) {
+        r.x = 0.0; r.y = 0.5 * UG_PI; r.z = 2.0 * ug_atan2(-q.x, q.y);
+    } else {
+        r.x = ug_atan2(2.0 * (q.y * q.z + q.w * q.x), squ - sqx - sqy + sqz);
+        r.y = ug_asin(sarg);
+        r.z = ug_atan2(2.0 * (q.x * q.y + q.w * q.z), squ + sqx - sqy - sqz);
+    }
+    return r;
+}
+static q4 quat_from_euler(v3 rpy) {
+    double phi = rpy.x / 2.0, the = rpy.y / 2.0, psi = rpy.z / 2.0;
+    double sp = ug_sin(phi), cp = ug_cos(phi), st = ug_sin(the), ct = ug_cos(the), ss = ug_sin(psi), cs = ug_cos(psi);
+    q4 q = Q(sp * ct * cs - cp * st * ss, cp * st * cs + sp * ct * ss, cp * ct * ss - sp * st * cs,
+             cp * ct * cs + sp * st * ss);
+    double len = ug_sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    return Q(q.x / len, q.y / len, q.z / len, q.w / len);
+}
+
+/* ======================================================================== */
+/* Python `random` (MT19937) -- reset draws, env_*:create_ball/create_cube   */
+/* ======================================================================== */
+typedef struct { uint32_t mt[624]; int idx; } mt19937;
+static void mt_init_genrand(mt19937* r, uint32_t s) {
+    r->mt[0] = s;
+    for (int i = 1; i < 624; i++) r->mt[i] = 1812433253u * (r->mt[i - 1] ^ (r->mt[i - 1] >> 30)) + (uint32_t)i;
+    r->idx = 624;
+}
+/* CPython random.seed(int) -> init_by_array([seed]) for 0 <= seed < 2^32 */
+static void mt_seed(mt19937* r, uint32_t seed) {
+    uint32_t key[1] = {seed};
+    int klen = 1;
+    mt_init_genrand(r, 19650218u);
+    int i = 1, j = 0;
+    for (int k = 624 > klen ? 624 : klen; k; k--) {
+        r->mt[i] = (r->mt[i] ^ ((r->mt[i - 1] ^ (r->mt[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+        i++; j++;
+        if (i >= 624) { r->mt[0] = r->mt[623]; i = 1; }
+        if (j >= klen) j = 0;
+    }
+    for (int k = 623; k; k--) {
+        r->mt[i] = (r->mt[i] ^ ((r->mt[i - 1] ^ (r->mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+        i++;
+        if (i >= 624) { r->mt[0] = r->mt[623]; i = 1; }
+    }
+    r->mt[0] = 0x80000000u;
+    r->idx = 624;
+}
+static uint32_t mt_next(mt19937* r) {
+    if (r->idx >= 624) {
+        for (int k = 0; k < 624; k++) {
+            uint32_t y = (r->mt[k] & 0x80000000u) | (r->mt[(k + 1) % 624] & 0x7fffffffu);
+            r->mt[k] = r->mt[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        r->idx = 0;
+    }
+    uint32_t y = r->mt[r->idx++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+static double mt_random(mt19937* r) {
+    uint32_t a = mt_next(r) >> 5, b = mt_next(r) >> 6;
+    return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+}
+static double mt_uniform(mt19937* r, double a, double b) { return a + (b - a) * mt_random(r); }
+
+/* ======================================================================== */
+/* scene description                                                         */
+/* ======================================================================== */
+typedef struct {
+    int kind;
+    double half[3];   /* box half extents (margin inside) / sphere radius in half[0] */
+    double margin;    /* box: inner margin; hull: outer margin; sphere: radius */
+    int v0, nv, f0, nf;
+    m3 R; v3 P;       /* shape frame in owner frame */
+    m3 aR; v3 aP;     /* AABB frame in owner frame */
+    v3 ac, ah;        /* AABB centre / half extents in the AABB frame */
+    double disc;      /* angular motion disc */
+    double friction, restitution;
+    int owner;        /* >=0 robot body, -1 fixed robot base, -2-i object i, -100 static */
+    int ent;          /* 0 robot, 1+i object i, 10+s static s */
+    int link;         /* pybullet link index for robot colliders, -1 otherwise */
+} collider;
+
+typedef struct { int a, b; double thr, friction, restitution; } pairdef;
+
+typedef struct {
+    int task;
+    double gravity;
+    int nobj;
+    double omass[MAXOBJ];
+    v3 oinertia[MAXOBJ];
+    int ncol;
+    collider col[MAXCOL];
+    int ocol[MAXOBJ]; /* collider index of each object */
+    int npair;
+    pairdef pair[MAXPAIR];
+} scene;
+
+typedef struct { v3 lpA, lpB, n; double dist, imp, imp1, imp2; } cpoint;
+typedef struct { int pair, npts; cpoint pt[4]; } manifold;
+
+struct ugo_env {
+    scene sc;
+    double q[NB], qd[NB];
+    double mtarget[7];
+    int mon[7];
+    int oactive[MAXOBJ];
+    v3 opos[MAXOBJ];
+    q4 oquat[MAXOBJ];
+    v3 ov[MAXOBJ], ow[MAXOBJ];
+    int nman;
+    manifold man[MAXMAN];
+    int goal_approached, goal_grasped;
+    int overflow;
+    mt19937 rng;
+};
+
+static void box_collider(collider* c, double hx, double hy, double hz, double margin, double friction) {
+    memset(c, 0, sizeof(*c));
+    c->kind = UG_SHAPE_BOX;
+    c->half[0] = hx; c->half[1] = hy; c->half[2] = hz;
+    c->margin = margin;
+    c->R = mident(); c->P = V(0, 0, 0);
+    c->aR = mident(); c->aP = V(0, 0, 0);
+    c->ac = V(0, 0, 0); c->ah = V(hx, hy, hz);
+    c->disc = ug_sqrt(hx * hx + hy * hy + hz * hz);
+    c->friction = friction;
+    c->link = -1;
+}
+/* btBoxShape::setSafeMargin for createCollisionShape(GEOM_BOX) [ext] */
+static double safe_margin(double hx, double hy, double hz) {
+    double m = hx < hy ? hx : hy;
+    m = m < hz ? m : hz;
+    m = 0.1 * m;
+    return m < 0.04 ? m : 0.04;
+}
+
+static void add_pair(scene* s, int a, int b) {
+    pairdef* p = &s->pair[s->npair++];
+    p->a = a; p->b = b;
+    double d = s->col[a].disc < s->col[b].disc ? s->col[a].disc : s->col[b].disc;
+    p->thr = d * UG_CONTACT_BREAK;
+    double f = s->col[a].friction * s->col[b].friction;
+    if (f < -UG_MAX_FRICTION) f = -UG_MAX_FRICTION;
+    if (f > UG_MAX_FRICTION) f = UG_MAX_FRICTION;
+    p->friction = f;
+    p->restitution = s->col[a].restitution * s->col[b].restitution;
+}
+
+static void build_scene(scene* s, int task) {
+    memset(s, 0, sizeof(*s));
+    s->task = task;
+    s->gravity = task == UG_TASK_CUBESGRASP ? -10.0 : -9.8; /* env_cubes_grasp_v0.py:43 vs :59 */
+    /* robot links 1..18 (link 0 is welded to the fixed base: its contacts carry no dynamics and no
+     * reward predicate reads them -- env_cubes_push_v0.py:180 excludes it) */
+    for (int l = 1; l < UG_NL; l++) {
+        collider* c = &s->col[s->ncol++];
+        memset(c, 0, sizeof(*c));
+        int si = -1;
+        for (int k = 0; k < UG_NSHAPE; k++)
+            if (UG_SHAPE_LINK[k] == l) si = k;
+        c->kind = UG_SHAPE_KIND[si] == 0 ? UG_SHAPE_BOX : UG_SHAPE_HULL;
+        c->half[0] = UG_SHAPE_HALF[3 * si]; c->half[1] = UG_SHAPE_HALF[3 * si + 1]; c->half[2] = UG_SHAPE_HALF[3 * si + 2];
+        c->margin = UG_URDF_MARGIN;
+        c->v0 = UG_SHAPE_V0[si]; c->nv = UG_SHAPE_NV[si]; c->f0 = UG_SHAPE_F0[si]; c->nf = UG_SHAPE_NF[si];
+        c->R = mload(&UG_SHAPE_R[9 * si]);
+        c->P = V(UG_SHAPE_P[3 * si], UG_SHAPE_P[3 * si + 1], UG_SHAPE_P[3 * si + 2]);
+        c->aR = mload(&UG_LINK_COMR[9 * l]);
+        c->aP = V(UG_LINK_COMP[3 * l], UG_LINK_COMP[3 * l + 1], UG_LINK_COMP[3 * l + 2]);
+        c->ac = V(UG_LINK_AABB_C[3 * l], UG_LINK_AABB_C[3 * l + 1], UG_LINK_AABB_C[3 * l + 2]);
+        c->ah = V(UG_LINK_AABB_H[3 * l], UG_LINK_AABB_H[3 * l + 1], UG_LINK_AABB_H[3 * l + 2]);
+        c->disc = UG_LINK_DISC[l];
+        c->friction = UG_DEFAULT_FRICTION;
+        c->owner = UG_LINK_BODY[l];
+        c->ent = 0;
+        c->link = l;
+    }
+    int nrobot = s->ncol;
+    int statics[4], nstat = 0;
+    if (task == UG_TASK_BALLBALANCE) {
+        /* paddle (env_ball_balance_v0.py:175-184), ball (:186-205) */
+        s->nobj = 2;
+        double hx = UG_BB_PADDLE_HX, hy = UG_BB_PADDLE_HY, hz = UG_BB_PADDLE_HZ, m = UG_BB_PADDLE_MASS;
+        s->omass[0] = m;
+        s->oinertia[0] = V(m / 12.0 * (4.0 * hy * hy + 4.0 * hz * hz), m / 12.0 * (4.0 * hx * hx + 4.0 * hz * hz),
+                           m / 12.0 * (4.0 * hx * hx + 4.0 * hy * hy));
+        collider* c = &s->col[s->ncol];
+        box_collider(c, hx, hy, hz, safe_margin(hx, hy, hz), UG_DEFAULT_FRICTION);
+        c->owner = -2; c->ent = 1;
+        s->ocol[0] = s->ncol++;
+        double r = UG_BB_BALL_R, mb = UG_BB_BALL_MASS;
+        s->omass[1] = mb;
+        double ib = 0.4 * mb * r * r; /* btSphereShape::calculateLocalInertia [ext] */
+        s->oinertia[1] = V(ib, ib, ib);
+        c = &s->col[s->ncol];
+        box_collider(c, r, r, r, r, UG_DEFAULT_FRICTION);
+        c->kind = UG_SHAPE_SPHERE;
+        c->half[1] = c->half[2] = 0.0;
+        c->disc = ug_sqrt(3.0) * r;
+        c->owner = -3; c->ent = 2;
+        s->ocol[1] = s->ncol++;
+    }
+    if (task == UG_TASK_BALLBALANCE || task == UG_TASK_CUBESPUSH || task == UG_TASK_GOLF) {
+        /* table (env_ball_balance_v0.py:71,216-247) and plane at z=-0.5 (:70) */
+        collider* c = &s->col[s->ncol];
+        box_collider(c, 0.5, 1.0, 0.25, safe_margin(0.5, 1.0, 0.25), UG_DEFAULT_FRICTION);
+        c->P = V(0.0, 0.0, -0.25); c->aP = c->P;
+        c->owner = -100; c->ent = 10;
+        statics[nstat++] = s->ncol++;
+        c = &s->col[s->ncol];
+        box_collider(c, UG_PLANE_HALF_XY, UG_PLANE_HALF_XY, UG_PLANE_HALF_Z, UG_URDF_MARGIN, UG_PLANE_FRICTION);
+        c->P = V(0.0, 0.0, -0.5 - UG_PLANE_HALF_Z); c->aP = c->P;
+        c->disc = ug_sqrt(15.0 * 15.0 * 2.0 + 25.0) + 5.0;
+        c->owner = -100; c->ent = 11;
+        statics[nstat++] = s->ncol++;
+    }
+    /* pairs: robot x objects, robot x statics, object x object, object x static */
+    for (int o = 0; o < s->nobj; o++)
+        for (int l = 0; l < nrobot; l++) add_pair(s, l, s->ocol[o]);
+    for (int t = 0; t < nstat; t++)
+        for (int l = 0; l < nrobot; l++) add_pair(s, l, statics[t]);
+    for (int o = 0; o < s->nobj; o++)
+        for (int p = o + 1; p < s->nobj; p++) {
+            int a = s->ocol[o], b = s->ocol[p];
+            /* canonical order for the narrowphase: sphere first, then box */
+            if (s->col[b].kind == UG_SHAPE_SPHERE && s->col[a].kind != UG_SHAPE_SPHERE) { int t = a; a = b; b = t; }
+            add_pair(s, a, b);
+        }
+    for (int o = 0; o < s->nobj; o++)
+        for (int t = 0; t < nstat; t++) add_pair(s, s->ocol[o], statics[t]);
+}
+
+/* ======================================================================== */
+/* kinematics                                                                */
+/* ======================================================================== */
+typedef struct {
+    m3 R[NB];
+    v3 p[NB];
+    v3 a[NB];  /* joint axis, world */
+    v3 c[NB];  /* body COM, world */
+} kin;
+
+static void fk(const double* q, kin* k) {
+    for (int b = 0; b < NB; b++) {
+        int pb = UG_BODY_PARENT[b];
+        m3 Rpb = mload(&UG_BODY_R[9 * b]);
+        v3 Ppb = V(UG_BODY_P[3 * b], UG_BODY_P[3 * b + 1], UG_BODY_P[3 * b + 2]);
+        v3 ax = V(UG_BODY_AXIS[3 * b], UG_BODY_AXIS[3 * b + 1], UG_BODY_AXIS[3 * b + 2]);
+        m3 Rj = axis_angle(ax, q[b]);
+        m3 Rp, Rtmp;
+        v3 pp;
+        if (pb < 0) { Rp = mident(); pp = V(0, 0, 0); }
+        else { Rp = k->R[pb]; pp = k->p[pb]; }
+        Rtmp = mm(&Rp, &Rpb);
+        k->R[b] = mm(&Rtmp, &Rj);
+        k->p[b] = vadd(pp, mv(&Rp, Ppb));
+        k->a[b] = mv(&Rtmp, ax);
+        v3 com = V(UG_BODY_COM[3 * b], UG_BODY_COM[3 * b + 1], UG_BODY_COM[3 * b + 2]);
+        k->c[b] = vadd(k->p[b], mv(&k->R[b], com));
+    }
+}
+/* link frame (URDF link frame) or link COM frame (getLinkState[0:2], collision object frame) */
+static void link_frame(const kin* k, int l, int com, m3* R, v3* p) {
+    int b = UG_LINK_BODY[l];
+    m3 Rl = mload(com ? &UG_LINK_COMR[9 * l] : &UG_LINK_R[9 * l]);
+    const double* P = com ? &UG_LINK_COMP[3 * l] : &UG_LINK_P[3 * l];
+    v3 Pl = V(P[0], P[1], P[2]);
+    if (b < 0) { *R = Rl; *p = Pl; return; }
+    *R = mm(&k->R[b], &Rl);
+    *p = vadd(k->p[b], mv(&k->R[b], Pl));
+}
+/* does dof d move body b? */
+static int moves(int d, int b) {
+    while (b >= 0) {
+        if (b == d) return 1;
+        b = UG_BODY_PARENT[b];
+    }
+    return 0;
+}
+
+/* ======================================================================== */
+/* robot dynamics: CRBA mass matrix + RNEA bias forces in world-frame        */
+/* spatial coordinates (Featherstone).  Equivalent to btMultiBody's ABA      */
+/* (computeAccelerationsArticulatedBodyAlgorithmMultiDof [ext]) with gravity, */
+/* gyroscopic terms and the default quadratic link damping.                  */
+/* ======================================================================== */
+typedef struct { v3 w, v; } sv; /* spatial vector (angular, linear at world origin) */
+
+static sv spatial_inertia_mul(double m, v3 h, const m3* J, sv x) {
+    sv r;
+    r.w = vadd(mv(J, x.w), vcross(h, x.v));
+    r.v = vsub(vscale(x.v, m), vcross(h, x.w));
+    return r;
+}
+
+/* returns M (row-major NBxNB) and bias C (generalised force with qdd = 0) */
+static void robot_dynamics(const double* qd, const kin* k, double g, double* M, double* C) {
+    double m[NB];
+    v3 h[NB];
+    m3 J[NB];
+    double cm[NB];
+    v3 ch[NB];
+    m3 cJ[NB];
+    for (int b = 0; b < NB; b++) {
+        m[b] = UG_BODY_MASS[b];
+        v3 c = k->c[b];
+        h[b] = vscale(c, m[b]);
+        m3 Iw = inertia_world(&k->R[b], &UG_BODY_I[6 * b]);
+        double cc = vdot(c, c);
+        m3 Jb;
+        Jb.m[0] = Iw.m[0] + m[b] * (cc - c.x * c.x); Jb.m[1] = Iw.m[1] - m[b] * (c.x * c.y); Jb.m[2] = Iw.m[2] - m[b] * (c.x * c.z);
+        Jb.m[3] = Iw.m[3] - m[b] * (c.y * c.x); Jb.m[4] = Iw.m[4] + m[b] * (cc - c.y * c.y); Jb.m[5] = Iw.m[5] - m[b] * (c.y * c.z);
+        Jb.m[6] = Iw.m[6] - m[b] * (c.z * c.x); Jb.m[7] = Iw.m[7] - m[b] * (c.z * c.y); Jb.m[8] = Iw.m[8] + m[b] * (cc - c.z * c.z);
+        J[b] = Jb;
+        cm[b] = m[b]; ch[b] = h[b]; cJ[b] = Jb;
+    }
+    /* composite inertias, leaves to root (parents have lower index) */
+    for (int b = NB - 1; b >= 0; b--) {
+        int p = UG_BODY_PARENT[b];
+        if (p < 0) continue;
+        cm[p] += cm[b];
+        ch[p] = vadd(ch[p], ch[b]);
+        for (int i = 0; i < 9; i++) cJ[p].m[i] += cJ[b].m[i];
+    }
+    sv S[NB];
+    for (int b = 0; b < NB; b++) { S[b].w = k->a[b]; S[b].v = vcross(k->p[b], k->a[b]); }
+    memset(M, 0, sizeof(double) * NB * NB);
+    for (int b = 0; b < NB; b++) {
+        sv F = spatial_inertia_mul(cm[b], ch[b], &cJ[b], S[b]);
+        M[b * NB + b] = vdot(S[b].w, F.w) + vdot(S[b].v, F.v);
+        int j = UG_BODY_PARENT[b];
+        while (j >= 0) {
+            double x = vdot(S[j].w, F.w) + vdot(S[j].v, F.v);
+            M[j * NB + b] = x;
+            M[b * NB + j] = x;
+            j = UG_BODY_PARENT[j];
+        }
+    }
+    /* RNEA with qdd = 0: velocities, bias accelerations, forces */
+    sv Vb[NB], Ab[NB], f[NB];
+    for (int b = 0; b < NB; b++) {
+        int p = UG_BODY_PARENT[b];
+        sv Vp, Ap;
+        if (p < 0) { Vp.w = V(0, 0, 0); Vp.v = V(0, 0, 0); Ap.w = V(0, 0, 0); Ap.v = V(0, 0, -g); }
+        else { Vp = Vb[p]; Ap = Ab[p]; }
+        sv vj; vj.w = vscale(S[b].w, qd[b]); vj.v = vscale(S[b].v, qd[b]);
+        Vb[b].w = vadd(Vp.w, vj.w); Vb[b].v = vadd(Vp.v, vj.v);
+        /* A = Ap + V x vj (motion cross product) */
+        Ab[b].w = vadd(Ap.w, vcross(Vb[b].w, vj.w));
+        Ab[b].v = vadd(Ap.v, vadd(vcross(Vb[b].w, vj.v), vcross(Vb[b].v, vj.w)));
+        sv IA = spatial_inertia_mul(m[b], h[b], &J[b], Ab[b]);
+        sv IV = spatial_inertia_mul(m[b], h[b], &J[b], Vb[b]);
+        /* V x* IV  = (w x n + v x f, w x f) */
+        f[b].w = vadd(IA.w, vadd(vcross(Vb[b].w, IV.w), vcross(Vb[b].v, IV.v)));
+        f[b].v = vadd(IA.v, vcross(Vb[b].w, IV.v));
+        /* damping (btMultiBody DAMPING_K1/K2 = 0.04), bias includes +damping */
+        double wn = vlen(Vb[b].w);
+        m3 D = inertia_world(&k->R[b], &UG_BODY_DAMPI[6 * b]);
+        v3 tau = vscale(mv(&D, Vb[b].w), UG_ANG_DAMP + UG_ANG_DAMP * wn);
+        f[b].w = vadd(f[b].w, tau);
+    }
+    for (int l = 1; l < UG_NL; l++) {
+        int b = UG_LINK_BODY[l];
+        if (b < 0) continue;
+        v3 cl = vadd(k->p[b], mv(&k->R[b], V(UG_LINK_COMP[3 * l], UG_LINK_COMP[3 * l + 1], UG_LINK_COMP[3 * l + 2])));
+        v3 vl = vadd(Vb[b].v, vcross(Vb[b].w, cl));
+        double vn = vlen(vl);
+        v3 fd = vscale(vl, UG_LINK_MASS[l] * (UG_LIN_DAMP + UG_LIN_DAMP * vn));
+        f[b].v = vadd(f[b].v, fd);
+        f[b].w = vadd(f[b].w, vcross(cl, fd));
+    }
+    for (int b = NB - 1; b >= 0; b--) {
+        C[b] = vdot(S[b].w, f[b].w) + vdot(S[b].v, f[b].v);
+        int p = UG_BODY_PARENT[b];
+        if (p >= 0) { f[p].w = vadd(f[p].w, f[b].w); f[p].v = vadd(f[p].v, f[b].v); }
+    }
+}
+
+/* dense LDL^T of the SPD mass matrix (in place: strict lower = L, diag = D) */
+static void ldlt(double* A, int n) {
+    for (int j = 0; j < n; j++) {
+        double d = A[j * n + j];
+        for (int k2 = 0; k2 < j; k2++) d -= A[j * n + k2] * A[j * n + k2] * A[k2 * n + k2];
+        A[j * n + j] = d;
+        for (int i = j + 1; i < n; i++) {
+            double s = A[i * n + j];
+            for (int k2 = 0; k2 < j; k2++) s -= A[i * n + k2] * A[j * n + k2] * A[k2 * n + k2];
+            A[i * n + j] = s / d;
+        }
+    }
+}
+static void ldlt_solve(const double* A, int n, double* x) {
+    for (int i = 0; i < n; i++)
+        for (int k2 = 0; k2 < i; k2++) x[i] -= A[i * n + k2] * x[k2];
+    for (int i = 0; i < n; i++) x[i] = x[i] / A[i * n + i];
+    for (int i = n - 1; i >= 0; i--)
+        for (int k2 = i + 1; k2 < n; k2++) x[i] -= A[k2 * n + i] * x[k2];
+}
+
+/* ======================================================================== */
+/* collision: world transforms, broadphase, narrowphase, persistent manifolds */
+/* ======================================================================== */
+typedef struct { m3 R; v3 p; } xf;
+static v3 xf_apply(const xf* T, v3 x) { return vadd(mv(&T->R, x), T->p); }
+static v3 xf_inv_apply(const xf* T, v3 x) { return mtv(&T->R, vsub(x, T->p)); }
+
+/* owner frame (robot body / object COM / world) */
+static xf owner_xf(const ugo_env* e, const kin* k, int owner) {
+    xf T;
+    if (owner >= 0) { T.R = k->R[owner]; T.p = k->p[owner]; }
+    else if (owner <= -2 && owner > -100) { int o = -2 - owner; T.R = qmat(e->oquat[o]); T.p = e->opos[o]; }
+    else { T.R = mident(); T.p = V(0, 0, 0); }
+    return T;
+}
+static xf shape_xf(const xf* O, const collider* c) {
+    xf T;
+    T.R = mm(&O->R, &c->R);
+    T.p = vadd(O->p, mv(&O->R, c->P));
+    return T;
+}
+static void world_aabb(const xf* O, const collider* c, v3* lo, v3* hi) {
+    m3 Rw = mm(&O->R, &c->aR);
+    v3 pw = vadd(O->p, mv(&O->R, c->aP));
+    v3 ctr = vadd(mv(&Rw, c->ac), pw);
+    const double* r = Rw.m;
+    v3 ext = V(ug_fabs(r[0]) * c->ah.x + ug_fabs(r[1]) * c->ah.y + ug_fabs(r[2]) * c->ah.z,
+               ug_fabs(r[3]) * c->ah.x + ug_fabs(r[4]) * c->ah.y + ug_fabs(r[5]) * c->ah.z,
+               ug_fabs(r[6]) * c->ah.x + ug_fabs(r[7]) * c->ah.y + ug_fabs(r[8]) * c->ah.z);
+    *lo = vsub(ctr, ext);
+    *hi = vadd(ctr, ext);
+}
+
+/* contact candidate: normal on B (world, B->A), point on B (world), signed distance */
+typedef struct { v3 n, pB; double d; } cand;
+typedef struct { int n; cand c[MAXCAND]; } candlist;
+static void cand_add(candlist* L, v3 n, v3 pB, double d) {
+    if (L->n < MAXCAND) { L->c[L->n].n = n; L->c[L->n].pB = pB; L->c[L->n].d = d; L->n++; }
+}
+
+/* btSphereBoxCollisionAlgorithm::getSphereDistance [ext]: sphere A, box B */
+static void nc_sphere_box(const xf* TA, const collider* A, const xf* TB, const collider* B, double thr, candlist* out) {
+    double r = A->half[0];
+    double bm = B->margin;
+    v3 he = V(B->half[0] - bm, B->half[1] - bm, B->half[2] - bm);
+    v3 rel = xf_inv_apply(TB, TA->p);
+    v3 cp = rel;
+    cp.x = ug_min(he.x, cp.x); cp.x = ug_max(-he.x, cp.x);
+    cp.y = ug_min(he.y, cp.y); cp.y = ug_max(-he.y, cp.y);
+    cp.z = ug_min(he.z, cp.z); cp.z = ug_max(-he.z, cp.z);
+    double idist = r + bm;
+    double cdist = idist + thr;
+    v3 n = vsub(rel, cp);
+    double d2 = vdot(n, n);
+    if (d2 > cdist * cdist) return;
+    double dist;
+    if (d2 <= 2.220446049250313e-16) {
+        /* getSpherePenetration: project onto the closest face */
+        double fd = he.x - rel.x, mind = fd;
+        cp.x = he.x; n = V(1, 0, 0);
+        fd = he.x + rel.x; if (fd < mind) { mind = fd; cp = rel; cp.x = -he.x; n = V(-1, 0, 0); }
+        fd = he.y - rel.y; if (fd < mind) { mind = fd; cp = rel; cp.y = he.y; n = V(0, 1, 0); }
+        fd = he.y + rel.y; if (fd < mind) { mind = fd; cp = rel; cp.y = -he.y; n = V(0, -1, 0); }
+        fd = he.z - rel.z; if (fd < mind) { mind = fd; cp = rel; cp.z = he.z; n = V(0, 0, 1); }
+        fd = he.z + rel.z; if (fd < mind) { mind = fd; cp = rel; cp.z = -he.z; n = V(0, 0, -1); }
+        dist = -mind;
+    } else {
+        dist = ug_sqrt(d2);
+        n = vscale(n, 1.0 / dist);
+    }
+    v3 pb = vadd(cp, vscale(n, bm));
+    double depth = dist - idist;
+    cand_add(out, mv(&TB->R, n), xf_apply(TB, pb), depth);
+}
+
+static void nc_sphere_sphere(const xf* TA, const collider* A, const xf* TB, const collider* B, double thr, candlist* out) {
+    v3 d = vsub(TA->p, TB->p);
+    double len = vlen(d);
+    double dist = len - (A->half[0] + B->half[0]);
+    if (dist > thr) return;
+    v3 n = len > 2.220446049250313e-16 ? vscale(d, 1.0 / len) : V(1, 0, 0);
+    cand_add(out, n, vadd(TB->p, vscale(n, B->half[0])), dist);
+}
+
+/* --- box-box: ODE dBoxBox2 as used by btBoxBoxDetector [ext] --- */
+static int intersect_rect_quad(const double h[2], double p[8], double ret[16]) {
+    int nq = 4, nr = 0;
+    double buffer[16];
+    double* q = p;
+    double* r = ret;
+    for (int dir = 0; dir <= 1; dir++) {
+        for (int sign = -1; sign <= 1; sign += 2) {
+            double* pq = q;
+            double* pr = r;
+            nr = 0;
+            for (int i = nq; i > 0; i--) {
+                if (sign * pq[dir] < h[dir]) {
+                    pr[0] = pq[0]; pr[1] = pq[1];
+                    pr += 2; nr++;
+                    if (nr & 8) { q = r; goto done; }
+                }
+                double* nextq = (i > 1) ? pq + 2 : q;
+                if ((sign * pq[dir] < h[dir]) ^ (sign * nextq[dir] < h[dir])) {
+                    pr[1 - dir] = pq[1 - dir] + (nextq[1 - dir] - pq[1 - dir]) / (nextq[dir] - pq[dir]) * (sign * h[dir] - pq[dir]);
+                    pr[dir] = sign * h[dir];
+                    pr += 2; nr++;
+                    if (nr & 8) { q = r; goto done; }
+                }
+                pq += 2;
+            }
+            q = r;
+            r = (q == ret) ? buffer : ret;
+            nq = nr;
+        }
+    }
+done:
+    if (q != ret) memcpy(ret, q, (size_t)nr * 2 * sizeof(double));
+    return nr;
+}
+static void cull_points(int n, const double p[], int m, int i0, int iret[]) {
+    double a, cx, cy, qq;
+    if (n == 1) { cx = p[0]; cy = p[1]; }
+    else if (n == 2) { cx = 0.5 * (p[0] + p[2]); cy = 0.5 * (p[1] + p[3]); }
+    else {
+        a = 0; cx = 0; cy = 0;
+        for (int i = 0; i < n - 1; i++) {
+            qq = p[i * 2] * p[i * 2 + 3] - p[i * 2 + 2] * p[i * 2 + 1];
+            a += qq;
+            cx += qq * (p[i * 2] + p[i * 2 + 2]);
+            cy += qq * (p[i * 2 + 1] + p[i * 2 + 3]);
+        }
+        qq = p[n * 2 - 2] * p[1] - p[0] * p[n * 2 - 1];
+        if (ug_fabs(a + qq) > 2.220446049250313e-16) a = 1.0 / (3.0 * (a + qq));
+        else a = 1e30;
+        cx = a * (cx + qq * (p[n * 2 - 2] + p[0]));
+        cy = a * (cy + qq * (p[n * 2 - 1] + p[1]));
+    }
+    double A[8];
+    for (int i = 0; i < n; i++) A[i] = ug_atan2(p[i * 2 + 1] - cy, p[i * 2] - cx);
+    int avail[8];
+    for (int i = 0; i < n; i++) avail[i] = 1;
+    avail[i0] = 0;
+    iret[0] = i0;
+    for (int j = 1; j < m; j++) {
+        a = (double)j * (2.0 * UG_PI / m) + A[i0];
+        if (a > UG_PI) a -= 2.0 * UG_PI;
+        double maxdiff = 1e9, diff;
+        iret[j] = i0;
+        for (int i = 0; i < n; i++) {
+            if (avail[i]) {
+                diff = ug_fabs(A[i] - a);
+                if (diff > UG_PI) diff = 2.0 * UG_PI - diff;
+                if (diff < maxdiff) { maxdiff = diff; iret[j] = i; }
+            }
+        }
+        avail[iret[j]] = 0;
+    }
+}
+/* R[i*4+j] addressing of dMatrix3 replaced by m3 row-major: element (i,j) = m[3i+j]; column j = axis j */
+static double col_dot(const m3* A, int i, const m3* B, int j) { /* column i of A . column j of B */
+    return A->m[i] * B->m[j] + A->m[3 + i] * B->m[3 + j] + A->m[6 + i] * B->m[6 + j];
+}
+static double col_dotv(const m3* A, int i, v3 v) { return A->m[i] * v.x + A->m[3 + i] * v.y + A->m[6 + i] * v.z; }
+static double vget(v3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+static void vsetc(v3* v, int i, double x) { if (i == 0) v->x = x; else if (i == 1) v->y = x; else v->z = x; }
+
+static void nc_box_box(const xf* TA, const collider* A, const xf* TB, const collider* B, double thr, candlist* out) {
+    (void)thr;
+    const double fudge = 1.05;
+    const m3* R1 = &TA->R;
+    const m3* R2 = &TB->R;
+    v3 p1 = TA->p, p2 = TB->p;
+    v3 p = vsub(p2, p1);
+    v3 pp = mtv(R1, p);
+    double Ah[3] = {A->half[0], A->half[1], A->half[2]};
+    double Bh[3] = {B->half[0], B->half[1], B->half[2]};
+    double R11 = col_dot(R1, 0, R2, 0), R12 = col_dot(R1, 0, R2, 1), R13 = col_dot(R1, 0, R2, 2);
+    double R21 = col_dot(R1, 1, R2, 0), R22 = col_dot(R1, 1, R2, 1), R23 = col_dot(R1, 1, R2, 2);
+    double R31 = col_dot(R1, 2, R2, 0), R32 = col_dot(R1, 2, R2, 1), R33 = col_dot(R1, 2, R2, 2);
+    double Q11 = ug_fabs(R11), Q12 = ug_fabs(R12), Q13 = ug_fabs(R13);
+    double Q21 = ug_fabs(R21), Q22 = ug_fabs(R22), Q23 = ug_fabs(R23);
+    double Q31 = ug_fabs(R31), Q32 = ug_fabs(R32), Q33 = ug_fabs(R33);
+    double s = -1e300, s2, l, e1;
+    int invert_normal = 0, code = 0;
+    int nR = -1; /* 0..2 column of R1, 3..5 column of R2, -1 use normalC */
+    v3 normalC = V(0, 0, 0);
+#define TST(expr1, expr2, norm, cc)             \
+    e1 = (expr1);                               \
+    s2 = ug_fabs(e1) - (expr2);                 \
+    if (s2 > 0) return;                         \
+    if (s2 > s) { s = s2; nR = norm; invert_normal = (e1 < 0); code = (cc); }
+    TST(pp.x, (Ah[0] + Bh[0] * Q11 + Bh[1] * Q12 + Bh[2] * Q13), 0, 1);
+    TST(pp.y, (Ah[1] + Bh[0] * Q21 + Bh[1] * Q22 + Bh[2] * Q23), 1, 2);
+    TST(pp.z, (Ah[2] + Bh[0] * Q31 + Bh[1] * Q32 + Bh[2] * Q33), 2, 3);
+    TST(col_dotv(R2, 0, p), (Ah[0] * Q11 + Ah[1] * Q21 + Ah[2] * Q31 + Bh[0]), 3, 4);
+    TST(col_dotv(R2, 1, p), (Ah[0] * Q12 + Ah[1] * Q22 + Ah[2] * Q32 + Bh[1]), 4, 5);
+    TST(col_dotv(R2, 2, p), (Ah[0] * Q13 + Ah[1] * Q23 + Ah[2] * Q33 + Bh[2]), 5, 6);
+#undef TST
+#define TST(expr1, expr2, n1, n2, n3, cc)                                      \
+    e1 = (expr1);                                                              \
+    s2 = ug_fabs(e1) - (expr2);                                                \
+    if (s2 > 0) return;                                                        \
+    l = ug_sqrt((n1) * (n1) + (n2) * (n2) + (n3) * (n3));                      \
+    if (l > 0) {                                                               \
+        s2 /= l;                                                               \
+        if (s2 * fudge > s) {                                                  \
+            s = s2; nR = -1;                                                   \
+            normalC = V((n1) / l, (n2) / l, (n3) / l);                         \
+            invert_normal = (e1 < 0); code = (cc);                             \
+        }                                                                      \
+    }
+    TST(pp.z * R21 - pp.y * R31, (Ah[1] * Q31 + Ah[2] * Q21 + Bh[1] * Q13 + Bh[2] * Q12), 0, -R31, R21, 7);
+    TST(pp.z * R22 - pp.y * R32, (Ah[1] * Q32 + Ah[2] * Q22 + Bh[0] * Q13 + Bh[2] * Q11), 0, -R32, R22, 8);
+    TST(pp.z * R23 - pp.y * R33, (Ah[1] * Q33 + Ah[2] * Q23 + Bh[0] * Q12 + Bh[1] * Q11), 0, -R33, R23, 9);
+    TST(pp.x * R31 - pp.z * R11, (Ah[0] * Q31 + Ah[2] * Q11 + Bh[1] * Q23 + Bh[2] * Q22), R31, 0, -R11, 10);
+    TST(pp.x * R32 - pp.z * R12, (Ah[0] * Q32 + Ah[2] * Q12 + Bh[0] * Q23 + Bh[2] * Q21), R32, 0, -R12, 11);
+    TST(pp.x * R33 - pp.z * R13, (Ah[0] * Q33 + Ah[2] * Q13 + Bh[0] * Q22 + Bh[1] * Q21), R33, 0, -R13, 12);
+    TST(pp.y * R11 - pp.x * R21, (Ah[0] * Q21 + Ah[1] * Q11 + Bh[1] * Q33 + Bh[2] * Q32), -R21, R11, 0, 13);
+    TST(pp.y * R12 - pp.x * R22, (Ah[0] * Q22 + Ah[1] * Q12 + Bh[0] * Q33 + Bh[2] * Q31), -R22, R12, 0, 14);
+    TST(pp.y * R13 - pp.x * R23, (Ah[0] * Q23 + Ah[1] * Q13 + Bh[0] * Q32 + Bh[1] * Q31), -R23, R13, 0, 15);
+#undef TST
+    if (!code) return;
+    v3 normal;
+    if (nR >= 0) {
+        const m3* Rn = nR < 3 ? R1 : R2;
+        int c = nR % 3;
+        normal = V(Rn->m[c], Rn->m[3 + c], Rn->m[6 + c]);
+    } else {
+        normal = mv(R1, normalC);
+    }
+    if (invert_normal) normal = vneg(normal);
+    double depth = -s;
+    if (code > 6) {
+        v3 pa = p1;
+        for (int j = 0; j < 3; j++) {
+            double sign = (col_dotv(R1, j, normal) > 0) ? 1.0 : -1.0;
+            pa = vadd(pa, V(sign * Ah[j] * R1->m[j], sign * Ah[j] * R1->m[3 + j], sign * Ah[j] * R1->m[6 + j]));
+        }
+        v3 pb = p2;
+        for (int j = 0; j < 3; j++) {
+            double sign = (col_dotv(R2, j, normal) > 0) ? -1.0 : 1.0;
+            pb = vadd(pb, V(sign * Bh[j] * R2->m[j], sign * Bh[j] * R2->m[3 + j], sign * Bh[j] * R2->m[6 + j]));
+        }
+        int ia = (code - 7) / 3, ib = (code - 7) % 3;
+        v3 ua = V(R1->m[ia], R1->m[3 + ia], R1->m[6 + ia]);
+        v3 ub = V(R2->m[ib], R2->m[3 + ib], R2->m[6 + ib]);
+        /* dLineClosestApproach */
+        v3 pd = vsub(pb, pa);
+        double uaub = vdot(ua, ub), q1 = vdot(ua, pd), q2 = -vdot(ub, pd);
+        double d = 1.0 - uaub * uaub, alpha, beta;
+        if (d <= 0.0001) { alpha = 0; beta = 0; }
+        else { d = 1.0 / d; alpha = (q1 + uaub * q2) * d; beta = (uaub * q1 + q2) * d; }
+        (void)alpha;
+        pb = vadd(pb, vscale(ub, beta));
+        cand_add(out, vneg(normal), pb, -depth);
+        return;
+    }
+    const m3 *Ra, *Rb;
+    v3 pa, pb;
+    const double *Sa, *Sb;
+    if (code <= 3) { Ra = R1; Rb = R2; pa = p1; pb = p2; Sa = Ah; Sb = Bh; }
+    else { Ra = R2; Rb = R1; pa = p2; pb = p1; Sa = Bh; Sb = Ah; }
+    v3 normal2 = code <= 3 ? normal : vneg(normal);
+    v3 nr = mtv(Rb, normal2);
+    v3 anr = V(ug_fabs(nr.x), ug_fabs(nr.y), ug_fabs(nr.z));
+    int lanr, a1, a2;
+    if (anr.y > anr.x) {
+        if (anr.y > anr.z) { a1 = 0; lanr = 1; a2 = 2; }
+        else { a1 = 0; a2 = 1; lanr = 2; }
+    } else {
+        if (anr.x > anr.z) { lanr = 0; a1 = 1; a2 = 2; }
+        else { a1 = 0; a2 = 1; lanr = 2; }
+    }
+    v3 center;
+    v3 rbl = V(Rb->m[lanr], Rb->m[3 + lanr], Rb->m[6 + lanr]);
+    if (vget(nr, lanr) < 0) center = vadd(vsub(pb, pa), vscale(rbl, Sb[lanr]));
+    else center = vsub(vsub(pb, pa), vscale(rbl, Sb[lanr]));
+    int codeN, code1, code2;
+    codeN = code <= 3 ? code - 1 : code - 4;
+    if (codeN == 0) { code1 = 1; code2 = 2; }
+    else if (codeN == 1) { code1 = 0; code2 = 2; }
+    else { code1 = 0; code2 = 1; }
+    double quad[8];
+    double c1 = col_dotv(Ra, code1, center), c2 = col_dotv(Ra, code2, center);
+    double m11 = col_dot(Ra, code1, Rb, a1), m12 = col_dot(Ra, code1, Rb, a2);
+    double m21 = col_dot(Ra, code2, Rb, a1), m22 = col_dot(Ra, code2, Rb, a2);
+    {
+        double k1 = m11 * Sb[a1], k2 = m21 * Sb[a1], k3 = m12 * Sb[a2], k4 = m22 * Sb[a2];
+        quad[0] = c1 - k1 - k3; quad[1] = c2 - k2 - k4;
+        quad[2] = c1 - k1 + k3; quad[3] = c2 - k2 + k4;
+        quad[4] = c1 + k1 + k3; quad[5] = c2 + k2 + k4;
+        quad[6] = c1 + k1 - k3; quad[7] = c2 + k2 - k4;
+    }
+    double rect[2] = {Sa[code1], Sa[code2]};
+    double ret[16];
+    int n = intersect_rect_quad(rect, quad, ret);
+    if (n < 1) return;
+    v3 point[8];
+    double dep[8];
+    double det1 = 1.0 / (m11 * m22 - m12 * m21);
+    m11 *= det1; m12 *= det1; m21 *= det1; m22 *= det1;
+    int cnum = 0;
+    v3 rba1 = V(Rb->m[a1], Rb->m[3 + a1], Rb->m[6 + a1]);
+    v3 rba2 = V(Rb->m[a2], Rb->m[3 + a2], Rb->m[6 + a2]);
+    for (int j = 0; j < n; j++) {
+        double k1 = m22 * (ret[j * 2] - c1) - m12 * (ret[j * 2 + 1] - c2);
+        double k2 = -m21 * (ret[j * 2] - c1) + m11 * (ret[j * 2 + 1] - c2);
+        point[cnum] = vadd(vadd(center, vscale(rba1, k1)), vscale(rba2, k2));
+        dep[cnum] = Sa[codeN] - vdot(normal2, point[cnum]);
+        if (dep[cnum] >= 0) {
+            ret[cnum * 2] = ret[j * 2];
+            ret[cnum * 2 + 1] = ret[j * 2 + 1];
+            cnum++;
+        }
+    }
+    if (cnum < 1) return;
+    int maxc = 4;
+    if (maxc > cnum) maxc = cnum;
+    if (cnum <= maxc) {
+        for (int j = 0; j < cnum; j++) {
+            v3 pw = vadd(point[j], pa);
+            if (code >= 4) pw = vsub(pw, vscale(normal, dep[j]));
+            cand_add(out, vneg(normal), pw, -dep[j]);
+        }
+    } else {
+        int i1 = 0;
+        double maxdepth = dep[0];
+        for (int i = 1; i < cnum; i++)
+            if (dep[i] > maxdepth) { maxdepth = dep[i]; i1 = i; }
+        int iret[8];
+        cull_points(cnum, ret, maxc, i1, iret);
+        for (int j = 0; j < maxc; j++) {
+            v3 pw = vadd(point[iret[j]], pa);
+            if (code >= 4) pw = vsub(pw, vscale(normal, dep[iret[j]]));
+            cand_add(out, vneg(normal), pw, -dep[iret[j]]);
+        }
+    }
+}
+
+/* convex hull (robot link, A) vs box (B): vertex-in-box + corner-in-hull
+ * (restated substitute for btConvexConvexAlgorithm GJK/EPA + polyhedral
+ * clipping [ext]; see DESIGN.md "contact generation") */
+static void reduce4(candlist* L) {
+    if (L->n <= 4) return;
+    cand sel[4];
+    int used[MAXCAND];
+    memset(used, 0, sizeof(used));
+    int best = 0;
+    for (int i = 1; i < L->n; i++)
+        if (L->c[i].d < L->c[best].d) best = i;
+    sel[0] = L->c[best];
+    used[best] = 1;
+    for (int s = 1; s < 4; s++) {
+        int bi = -1;
+        double bd = -1.0;
+        for (int i = 0; i < L->n; i++) {
+            if (used[i]) continue;
+            double md = 1e300;
+            for (int t = 0; t < s; t++) {
+                v3 dd = vsub(L->c[i].pB, sel[t].pB);
+                double x = vdot(dd, dd);
+                if (x < md) md = x;
+            }
+            if (md > bd) { bd = md; bi = i; }
+        }
+        sel[s] = L->c[bi];
+        used[bi] = 1;
+    }
+    for (int s = 0; s < 4; s++) L->c[s] = sel[s];
+    L->n = 4;
+}
+static void nc_hull_box(const xf* TA, const collider* A, const xf* TB, const collider* B, double thr, candlist* out) {
+    m3 RAB = mtm(&TB->R, &TA->R);
+    v3 pAB = mtv(&TB->R, vsub(TA->p, TB->p));
+    v3 h = V(B->half[0], B->half[1], B->half[2]);
+    double mA = A->margin;
+    candlist L;
+    L.n = 0;
+    for (int i = 0; i < A->nv; i++) {
+        const double* vv = &UG_HULL_V[3 * (A->v0 + i)];
+        v3 x = vadd(mv(&RAB, V(vv[0], vv[1], vv[2])), pAB);
+        v3 d = V(ug_fabs(x.x) - h.x, ug_fabs(x.y) - h.y, ug_fabs(x.z) - h.z);
+        double dist;
+        v3 nl, pl;
+        if (d.x < 0 && d.y < 0 && d.z < 0) {
+            int k = 0;
+            double dm = d.x;
+            if (d.y > dm) { dm = d.y; k = 1; }
+            if (d.z > dm) { dm = d.z; k = 2; }
+            dist = dm;
+            double sg = vget(x, k) < 0 ? -1.0 : 1.0;
+            nl = V(0, 0, 0); vsetc(&nl, k, sg);
+            pl = x; vsetc(&pl, k, sg * vget(h, k));
+        } else {
+            v3 q = V(ug_max(-h.x, ug_min(h.x, x.x)), ug_max(-h.y, ug_min(h.y, x.y)), ug_max(-h.z, ug_min(h.z, x.z)));
+            v3 df = vsub(x, q);
+            double dl = vlen(df);
+            if (dl - mA >= thr) continue;
+            dist = dl;
+            nl = vscale(df, 1.0 / dl);
+            pl = q;
+        }
+        double depth = dist - mA;
+        if (depth < thr) cand_add(&L, mv(&TB->R, nl), xf_apply(TB, pl), depth);
+    }
+    m3 RBA = mtm(&TA->R, &TB->R);
+    v3 pBA = mtv(&TA->R, vsub(TB->p, TA->p));
+    for (int c = 0; c < 8; c++) {
+        v3 cl = V((c & 1) ? h.x : -h.x, (c & 2) ? h.y : -h.y, (c & 4) ? h.z : -h.z);
+        v3 y = vadd(mv(&RBA, cl), pBA);
+        double smax = -1e300;
+        int fm = -1;
+        for (int f = 0; f < A->nf; f++) {
+            const double* F = &UG_HULL_F[4 * (A->f0 + f)];
+            double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
+            if (sd > smax) { smax = sd; fm = f; }
+            if (sd - mA >= thr) break; /* outside this face: cannot be a contact */
+        }
+        double depth = smax - mA;
+        if (depth < thr) {
+            const double* F = &UG_HULL_F[4 * (A->f0 + fm)];
+            v3 nw = mv(&TA->R, V(F[0], F[1], F[2]));
+            cand_add(&L, vneg(nw), xf_apply(TB, cl), depth);
+        }
+    }
+    reduce4(&L);
+    for (int i = 0; i < L.n; i++) cand_add(out, L.c[i].n, L.c[i].pB, L.c[i].d);
+}
+/* hull (robot link, A) vs sphere (B): deepest face plane */
+static void nc_hull_sphere(const xf* TA, const collider* A, const xf* TB, const collider* B, double thr, candlist* out) {
+    v3 y = mtv(&TA->R, vsub(TB->p, TA->p));
+    double r = B->half[0];
+    double smax = -1e300;
+    int fm = -1;
+    for (int f = 0; f < A->nf; f++) {
+        const double* F = &UG_HULL_F[4 * (A->f0 + f)];
+        double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
+        if (sd > smax) { smax = sd; fm = f; }
+    }
+    double depth = smax - r - A->margin;
+    if (depth >= thr) return;
+    const double* F = &UG_HULL_F[4 * (A->f0 + fm)];
+    v3 nw = vneg(mv(&TA->R, V(F[0], F[1], F[2])));
+    cand_add(out, nw, vadd(TB->p, vscale(nw, r)), depth);
+}
+
+/* btPersistentManifold [ext]: getCacheEntry / replaceContactPoint / addManifoldPoint / sortCachedPoints */
+static int sort_cached(const manifold* M, const cpoint* pt) {
+    int maxi = -1;
+    double maxpen = pt->dist;
+    for (int i = 0; i < 4; i++)
+        if (M->pt[i].dist < maxpen) { maxi = i; maxpen = M->pt[i].dist; }
+    double res[4] = {0, 0, 0, 0};
+    if (maxi != 0) { v3 a = vsub(pt->lpA, M->pt[1].lpA), b = vsub(M->pt[3].lpA, M->pt[2].lpA); v3 c = vcross(a, b); res[0] = vdot(c, c); }
+    if (maxi != 1) { v3 a = vsub(pt->lpA, M->pt[0].lpA), b = vsub(M->pt[3].lpA, M->pt[2].lpA); v3 c = vcross(a, b); res[1] = vdot(c, c); }
+    if (maxi != 2) { v3 a = vsub(pt->lpA, M->pt[0].lpA), b = vsub(M->pt[3].lpA, M->pt[1].lpA); v3 c = vcross(a, b); res[2] = vdot(c, c); }
+    if (maxi != 3) { v3 a = vsub(pt->lpA, M->pt[0].lpA), b = vsub(M->pt[2].lpA, M->pt[1].lpA); v3 c = vcross(a, b); res[3] = vdot(c, c); }
+    int bi = -1;
+    double bv = -1e300;
+    for (int i = 0; i < 4; i++)
+        if (ug_fabs(res[i]) > bv) { bv = ug_fabs(res[i]); bi = i; }
+    return bi;
+}
+static void manifold_add(manifold* M, const xf* TA, const xf* TB, const cand* c, double thr) {
+    if (c->d > thr) return;
+    v3 pA = vadd(c->pB, vscale(c->n, c->d));
+    cpoint np;
+    np.lpA = xf_inv_apply(TA, pA);
+    np.lpB = xf_inv_apply(TB, c->pB);
+    np.n = c->n;
+    np.dist = c->d;
+    np.imp = np.imp1 = np.imp2 = 0.0;
+    double shortest = thr * thr;
+    int near = -1;
+    for (int i = 0; i < M->npts; i++) {
+        v3 d = vsub(M->pt[i].lpA, np.lpA);
+        double x = vdot(d, d);
+        if (x < shortest) { shortest = x; near = i; }
+    }
+    if (near >= 0) {
+        np.imp = M->pt[near].imp; np.imp1 = M->pt[near].imp1; np.imp2 = M->pt[near].imp2;
+        M->pt[near] = np;
+        return;
+    }
+    int ins = M->npts;
+    if (ins == 4) ins = sort_cached(M, &np);
+    else M->npts++;
+    if (ins < 0) ins = 0;
+    M->pt[ins] = np;
+}
+static void manifold_refresh(manifold* M, const xf* TA, const xf* TB, double thr) {
+    for (int i = M->npts - 1; i >= 0; i--) {
+        cpoint* p = &M->pt[i];
+        v3 pA = xf_apply(TA, p->lpA), pB = xf_apply(TB, p->lpB);
+        p->dist = vdot(vsub(pA, pB), p->n);
+    }
+    for (int i = M->npts - 1; i >= 0; i--) {
+        cpoint* p = &M->pt[i];
+        int rm = 0;
+        if (p->dist > thr) rm = 1;
+        else {
+            v3 pA = xf_apply(TA, p->lpA), pB = xf_apply(TB, p->lpB);
+            v3 proj = vsub(pA, vscale(p->n, p->dist));
+            v3 d = vsub(pB, proj);
+            if (vdot(d, d) > thr * thr) rm = 1;
+        }
+        if (rm) {
+            int last = M->npts - 1;
+            if (i != last) M->pt[i] = M->pt[last];
+            M->npts--;
+        }
+    }
+}
+
+static int collider_active(const ugo_env* e, const collider* c) {
+    if (c->owner <= -2 && c->owner > -100) return e->oactive[-2 - c->owner];
+    return 1;
+}
+
+/* performDiscreteCollisionDetection: broadphase + narrowphase + manifold update */
+static void collide(ugo_env* e, const kin* k) {
+    const scene* s = &e->sc;
+    xf O[MAXCOL];
+    v3 lo[MAXCOL], hi[MAXCOL];
+    for (int i = 0; i < s->ncol; i++) {
+        const collider* c = &s->col[i];
+        O[i] = owner_xf(e, k, c->owner);
+        world_aabb(&O[i], c, &lo[i], &hi[i]);
+        lo[i] = vsub(lo[i], V(UG_AABB_PAD, UG_AABB_PAD, UG_AABB_PAD));
+        hi[i] = vadd(hi[i], V(UG_AABB_PAD, UG_AABB_PAD, UG_AABB_PAD));
+    }
+    /* Narrowphase for every overlapping pair, in pair-table order.  A manifold slot is held only
+     * while the pair has contact points (empty manifolds carry neither rows nor predicates);
+     * releasing a slot swaps the last one in (btCollisionDispatcher::releaseManifold). */
+    for (int p = 0; p < s->npair; p++) {
+        const pairdef* P = &s->pair[p];
+        int a = P->a, b = P->b;
+        int slot = -1;
+        for (int m = 0; m < e->nman; m++)
+            if (e->man[m].pair == p) { slot = m; break; }
+        int ov = collider_active(e, &s->col[a]) && collider_active(e, &s->col[b]) &&
+                 !(lo[a].x > hi[b].x || hi[a].x < lo[b].x || lo[a].y > hi[b].y || hi[a].y < lo[b].y ||
+                   lo[a].z > hi[b].z || hi[a].z < lo[b].z);
+        if (!ov) {
+            if (slot >= 0) {
+                int last = e->nman - 1;
+                if (slot != last) e->man[slot] = e->man[last];
+                e->nman--;
+            }
+            continue;
+        }
+        const collider* A = &s->col[a];
+        const collider* B = &s->col[b];
+        xf TA = shape_xf(&O[a], A), TB = shape_xf(&O[b], B);
+        candlist L;
+        L.n = 0;
+        if (A->kind == UG_SHAPE_SPHERE && B->kind == UG_SHAPE_BOX) nc_sphere_box(&TA, A, &TB, B, P->thr, &L);
+        else if (A->kind == UG_SHAPE_SPHERE && B->kind == UG_SHAPE_SPHERE) nc_sphere_sphere(&TA, A, &TB, B, P->thr, &L);
+        else if (A->kind == UG_SHAPE_BOX && B->kind == UG_SHAPE_BOX) nc_box_box(&TA, A, &TB, B, P->thr, &L);
+        else if (A->kind == UG_SHAPE_HULL && B->kind == UG_SHAPE_BOX) nc_hull_box(&TA, A, &TB, B, P->thr, &L);
+        else if (A->kind == UG_SHAPE_HULL && B->kind == UG_SHAPE_SPHERE) nc_hull_sphere(&TA, A, &TB, B, P->thr, &L);
+        else if (A->kind == UG_SHAPE_BOX && B->kind == UG_SHAPE_SPHERE) {
+            /* sphere-box with swapped roles: flip normal, move the point onto the sphere */
+            candlist L2;
+            L2.n = 0;
+            nc_sphere_box(&TB, B, &TA, A, P->thr, &L2);
+            for (int i = 0; i < L2.n; i++)
+                cand_add(&L, vneg(L2.c[i].n), vadd(L2.c[i].pB, vscale(L2.c[i].n, L2.c[i].d)), L2.c[i].d);
+        }
+        if (slot < 0) {
+            if (L.n == 0) continue;
+            if (e->nman >= MAXMAN) { e->overflow++; continue; }
+            slot = e->nman++;
+            e->man[slot].pair = p;
+            e->man[slot].npts = 0;
+        }
+        manifold* M = &e->man[slot];
+        /* manifold frames = owner frames */
+        for (int i = 0; i < L.n; i++) manifold_add(M, &O[a], &O[b], &L.c[i], P->thr);
+        if (M->npts) manifold_refresh(M, &O[a], &O[b], P->thr);
+        if (M->npts == 0) {
+            int last = e->nman - 1;
+            if (slot != last) e->man[slot] = e->man[last];
+            e->nman--;
+        }
+    }
+}
+
+/* ======================================================================== */
+/* constraint rows + projected Gauss-Seidel (btMultiBodyConstraintSolver)    */
+/* ======================================================================== */
+typedef struct {
+    int entA, entB;            /* -1 none, 0 robot, 1+i object i */
+    double JA[NB], MiJA[NB];   /* robot: NB entries; object: 6 (lin, ang) */
+    double JB[NB], MiJB[NB];
+    double invD, rhs, rhsPen, lo, hi, imp, impPen, fric;
+    int man, pt, kind;         /* kind 0 non-contact, 1 normal, 2 friction dir1, 3 friction dir2 */
+    int nrow;                  /* friction rows: index of their normal row */
+} row;
+
+typedef struct {
+    int n, nnc, nn, nf;
+    row r[MAXROWS];
+    int idx_nc[MAXROWS], idx_n[MAXROWS], idx_f[MAXROWS];
+} rowset;
+
+static int ent_dofs(int ent) { return ent == 0 ? NB : 6; }
+static int ent_off(int ent) { return ent == 0 ? 0 : NB + 6 * (ent - 1); }
+static double ent_dot(int ent, const double* J, const double* v) {
+    int n = ent_dofs(ent), o = ent_off(ent);
+    double s = 0.0;
+    for (int i = 0; i < n; i++) s += J[i] * v[o + i];
+    return s;
+}
+static double ent_dot_local(int ent, const double* a, const double* b) {
+    int n = ent_dofs(ent);
+    double s = 0.0;
+    for (int i = 0; i < n; i++) s += a[i] * b[i];
+    return s;
+}
+static void ent_axpy(int ent, const double* MiJ, double a, double* v) {
+    int n = ent_dofs(ent), o = ent_off(ent);
+    for (int i = 0; i < n; i++) v[o + i] += MiJ[i] * a;
+}
+
+/* Jacobian of a point p on entity ent along direction d (linear) */
+static void point_jac(const ugo_env* e, const kin* k, int ent, int body, v3 p, v3 d, double* J, double* MiJ,
+                      const double* LDL) {
+    if (ent == 0) {
+        for (int i = 0; i < NB; i++) {
+            J[i] = moves(i, body) ? vdot(d, vcross(k->a[i], vsub(p, k->p[i]))) : 0.0;
+            MiJ[i] = J[i];
+        }
+        ldlt_solve(LDL, NB, MiJ);
+    } else {
+        int o = ent - 1;
+        v3 r = vsub(p, e->opos[o]);
+        v3 rn = vcross(r, d);
+        J[0] = d.x; J[1] = d.y; J[2] = d.z; J[3] = rn.x; J[4] = rn.y; J[5] = rn.z;
+        double im = 1.0 / e->sc.omass[o];
+        m3 R = qmat(e->oquat[o]);
+        v3 ir = mtv(&R, rn);
+        ir = V(ir.x / e->sc.oinertia[o].x, ir.y / e->sc.oinertia[o].y, ir.z / e->sc.oinertia[o].z);
+        ir = mv(&R, ir);
+        MiJ[0] = d.x * im; MiJ[1] = d.y * im; MiJ[2] = d.z * im; MiJ[3] = ir.x; MiJ[4] = ir.y; MiJ[5] = ir.z;
+    }
+}
+
+static int ent_of_collider(const collider* c, int* body) {
+    *body = -1;
+    if (c->owner >= 0) { *body = c->owner; return 0; }
+    if (c->owner == -1) return -1; /* fixed robot base */
+    if (c->owner > -100) return -1 - c->owner; /* object i -> 1+i */
+    return -1;
+}
+
+static void contact_row(const ugo_env* e, const kin* k, const double* LDL, const double* v0, row* r, int entA, int bodyA,
+                        int entB, int bodyB, v3 pA, v3 pB, v3 d) {
+    r->entA = entA; r->entB = entB;
+    double dA = 0.0, dB = 0.0;
+    double relv = 0.0;
+    if (entA >= 0) {
+        point_jac(e, k, entA, bodyA, pA, d, r->JA, r->MiJA, LDL);
+        dA = ent_dot_local(entA, r->JA, r->MiJA);
+        relv += ent_dot(entA, r->JA, v0);
+    }
+    if (entB >= 0) {
+        point_jac(e, k, entB, bodyB, pB, vneg(d), r->JB, r->MiJB, LDL);
+        dB = ent_dot_local(entB, r->JB, r->MiJB);
+        relv += ent_dot(entB, r->JB, v0);
+    }
+    double den = dA + dB;
+    r->invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
+    r->rhs = relv; /* caller turns rel_vel into rhs */
+}
+
+static void build_rows(ugo_env* e, const kin* k, const double* LDL, const double* v0, rowset* rs) {
+    rs->n = rs->nnc = rs->nn = rs->nf = 0;
+    const double dt = UG_DT;
+    /* joint limits (btMultiBodyJointLimitConstraint, created at URDF load in link order) */
+    for (int d = 0; d < NB; d++) {
+        for (int side = 0; side < 2; side++) {
+            double pen = side == 0 ? e->q[d] - UG_DOF_LOWER[d] : UG_DOF_UPPER[d] - e->q[d];
+            if (pen > 0) continue;
+            if (rs->n >= MAXROWS) { e->overflow++; continue; }
+            row* r = &rs->r[rs->n];
+            memset(r, 0, sizeof(*r));
+            r->entA = 0; r->entB = -1;
+            r->JA[d] = side == 0 ? 1.0 : -1.0;
+            memcpy(r->MiJA, r->JA, sizeof(r->JA));
+            ldlt_solve(LDL, NB, r->MiJA);
+            double den = ent_dot_local(0, r->JA, r->MiJA);
+            r->invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
+            double relv = ent_dot(0, r->JA, v0);
+            double erp = (pen > UG_SPLIT_PEN_THR) ? UG_ERP : UG_ERP2;
+            double perr = -pen * erp / dt, verr = -relv;
+            double pimp = perr * r->invD, vimp = verr * r->invD;
+            r->rhs = (pen > UG_SPLIT_PEN_THR) ? pimp + vimp : vimp;
+            r->lo = 0.0; r->hi = UG_LIMIT_MAXIMP;
+            r->kind = 0;
+            rs->idx_nc[rs->nnc++] = rs->n++;
+        }
+    }
+    /* position motors (btMultiBodyJointMotor, created per joint at load; zero-force ones carry no impulse) */
+    for (int m = 0; m < 7; m++) {
+        if (!e->mon[m]) continue;
+        int d = m < 6 ? m : UG_FINGER_DOF;
+        double maxImp = UG_DOF_MAXFORCE[d] * dt;
+        if (rs->n >= MAXROWS) { e->overflow++; continue; }
+        row* r = &rs->r[rs->n];
+        memset(r, 0, sizeof(*r));
+        r->entA = 0; r->entB = -1;
+        r->JA[d] = 1.0;
+        memcpy(r->MiJA, r->JA, sizeof(r->JA));
+        ldlt_solve(LDL, NB, r->MiJA);
+        double den = ent_dot_local(0, r->JA, r->MiJA);
+        r->invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
+        double qd = v0[d];
+        double pst = 1.0 * (e->mtarget[m] - e->q[d]) / dt;
+        double verr = 0.0 - qd;
+        double des = UG_MOTOR_KP * pst + qd + UG_MOTOR_KD * verr;
+        double clamp = UG_DOF_MAXVEL[d];
+        if (des > clamp) des = clamp;
+        if (des < -clamp) des = -clamp;
+        double relv = ent_dot(0, r->JA, v0);
+        r->rhs = 0.0 * r->invD + (des - relv) * r->invD;
+        r->lo = -maxImp; r->hi = maxImp;
+        r->kind = 0;
+        rs->idx_nc[rs->nnc++] = rs->n++;
+    }
+    /* mimic gears (robot.py:202-211): J_A = e_finger, J_B = ratio e_child */
+    for (int g = 0; g < 5; g++) {
+        if (rs->n >= MAXROWS) { e->overflow++; continue; }
+        int pa = UG_FINGER_DOF, cb = UG_GEAR_CHILD[g];
+        double ratio = UG_GEAR_RATIO[g];
+        row* r = &rs->r[rs->n];
+        memset(r, 0, sizeof(*r));
+        r->entA = 0; r->entB = 0;
+        r->JA[pa] = 1.0;
+        r->JB[cb] = ratio;
+        memcpy(r->MiJA, r->JA, sizeof(r->JA));
+        memcpy(r->MiJB, r->JB, sizeof(r->JB));
+        ldlt_solve(LDL, NB, r->MiJA);
+        ldlt_solve(LDL, NB, r->MiJB);
+        double den = ent_dot_local(0, r->JA, r->MiJA) + ent_dot_local(0, r->JB, r->MiJB);
+        r->invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
+        double relv = ent_dot(0, r->JA, v0) + ent_dot(0, r->JB, v0);
+        double diff = e->q[cb] * ratio + e->q[pa];
+        double pen = -UG_GEAR_ERP * (0.0 - diff);
+        /* fillMultiBodyConstraint: split impulse not implemented for multibody rows -> always m_erp, combined */
+        double perr = -pen * UG_ERP / dt, verr = 0.0 - relv;
+        r->rhs = perr * r->invD + verr * r->invD;
+        double maxImp = UG_GEAR_MAXF * dt;
+        r->lo = -maxImp; r->hi = maxImp;
+        r->kind = 0;
+        rs->idx_nc[rs->nnc++] = rs->n++;
+    }
+    /* contacts, manifold order: normal row + two friction rows per point */
+    const scene* s = &e->sc;
+    for (int m = 0; m < e->nman; m++) {
+        const manifold* M = &e->man[m];
+        const pairdef* P = &s->pair[M->pair];
+        int bodyA, bodyB;
+        int entA = ent_of_collider(&s->col[P->a], &bodyA);
+        int entB = ent_of_collider(&s->col[P->b], &bodyB);
+        if (entA < 0 && entB < 0) continue;
+        xf OA = owner_xf(e, k, s->col[P->a].owner), OB = owner_xf(e, k, s->col[P->b].owner);
+        for (int j = 0; j < M->npts; j++) {
+            if (rs->n + 3 > MAXROWS) { e->overflow++; continue; }
+            const cpoint* cp = &M->pt[j];
+            v3 pA = xf_apply(&OA, cp->lpA), pB = xf_apply(&OB, cp->lpB);
+            v3 n = cp->n;
+            int ni = rs->n;
+            row* r = &rs->r[ni];
+            memset(r, 0, sizeof(*r));
+            contact_row(e, k, LDL, v0, r, entA, bodyA, entB, bodyB, pA, pB, n);
+            if (r->invD == 0.0) continue; /* no dynamic effect (e.g. fixed link) */
+            double relv = r->rhs;
+            double pen = cp->dist + UG_LINEAR_SLOP;
+            double rest = 0.0;
+            if (!(ug_fabs(relv) < UG_REST_VEL_THR)) rest = P->restitution * -relv;
+            if (rest <= 0.0) rest = 0.0;
+            double verr = rest - relv, perr;
+            double erp = (pen > UG_SPLIT_PEN_THR) ? UG_ERP : UG_ERP2;
+            if (pen > 0) { perr = 0.0; verr -= pen / UG_DT; }
+            else perr = -pen * erp / UG_DT;
+            double pimp = perr * r->invD, vimp = verr * r->invD;
+            if (pen > UG_SPLIT_PEN_THR) { r->rhs = pimp + vimp; r->rhsPen = 0.0; }
+            else { r->rhs = vimp; r->rhsPen = pimp; }
+            r->lo = 0.0; r->hi = 1e10;
+            r->imp = cp->imp * UG_WARMSTART;
+            r->kind = 1; r->man = m; r->pt = j;
+            rs->idx_n[rs->nn++] = rs->n++;
+            /* btPlaneSpace1 friction directions */
+            v3 t1, t2;
+            if (ug_fabs(n.z) > 0.7071067811865475244) {
+                double a = n.y * n.y + n.z * n.z, kk = 1.0 / ug_sqrt(a);
+                t1 = V(0, -n.z * kk, n.y * kk);
+                t2 = V(a * kk, -n.x * t1.z, n.x * t1.y);
+            } else {
+                double a = n.x * n.x + n.y * n.y, kk = 1.0 / ug_sqrt(a);
+                t1 = V(-n.y * kk, n.x * kk, 0);
+                t2 = V(-n.z * t1.y, n.z * t1.x, a * kk);
+            }
+            for (int fdir = 0; fdir < 2; fdir++) {
+                row* f = &rs->r[rs->n];
+                memset(f, 0, sizeof(*f));
+                contact_row(e, k, LDL, v0, f, entA, bodyA, entB, bodyB, pA, pB, fdir == 0 ? t1 : t2);
+                double frel = f->rhs;
+                f->rhs = 0.0 * f->invD + (0.0 - frel) * f->invD;
+                f->fric = P->friction;
+                f->lo = 0.0; f->hi = 0.0;
+                f->imp = 0.0;
+                f->kind = 2 + fdir; f->man = m; f->pt = j; f->nrow = ni;
+                rs->idx_f[rs->nf++] = rs->n++;
+            }
+        }
+    }
+}
+
+/* resolveSingleConstraintRowGeneric [ext] */
+static double solve_row(row* r, double* dv, int pen) {
+    double imp = pen ? r->impPen : r->imp;
+    double di = (pen ? r->rhsPen : r->rhs) - imp * 0.0;
+    if (r->entA >= 0) di -= ent_dot(r->entA, r->JA, dv) * r->invD;
+    if (r->entB >= 0) di -= ent_dot(r->entB, r->JB, dv) * r->invD;
+    double sum = imp + di;
+    if (sum < r->lo) { di = r->lo - imp; imp = r->lo; }
+    else if (sum > r->hi) { di = r->hi - imp; imp = r->hi; }
+    else imp = sum;
+    if (pen) r->impPen = imp; else r->imp = imp;
+    if (r->entA >= 0) ent_axpy(r->entA, r->MiJA, di, dv);
+    if (r->entB >= 0) ent_axpy(r->entB, r->MiJB, di, dv);
+    return di * (1.0 / r->invD);
+}
+
+static void pgs(rowset* rs, double* dv) {
+    for (int i = 0; i < rs->nn; i++) {
+        row* r = &rs->r[rs->idx_n[i]];
+        if (r->imp != 0.0) {
+            if (r->entA >= 0) ent_axpy(r->entA, r->MiJA, r->imp, dv);
+            if (r->entB >= 0) ent_axpy(r->entB, r->MiJB, r->imp, dv);
+        }
+    }
+    for (int it = 0; it < UG_PGS_ITERS; it++) {
+        double res = 0.0;
+        for (int j = 0; j < rs->nnc; j++) {
+            int idx = (it & 1) ? j : rs->nnc - 1 - j;
+            double x = solve_row(&rs->r[rs->idx_nc[idx]], dv, 0);
+            x = x * x;
+            res = res > x ? res : x;
+        }
+        for (int j = 0; j < rs->nn; j++) {
+            double x = solve_row(&rs->r[rs->idx_n[j]], dv, 0);
+            x = x * x;
+            res = res > x ? res : x;
+        }
+        for (int j = 0; j < rs->nf; j++) {
+            row* f = &rs->r[rs->idx_f[j]];
+            double tot = rs->r[f->nrow].imp;
+            if (tot > 0.0) {
+                f->lo = -(f->fric * tot);
+                f->hi = f->fric * tot;
+                double x = solve_row(f, dv, 0);
+                x = x * x;
+                res = res > x ? res : x;
+            }
+        }
+        if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
+    }
+}
+/* split-impulse pass for deep penetrations (rhsPenetration rows) */
+static int pgs_split(rowset* rs, double* dvs) {
+    int any = 0;
+    for (int j = 0; j < rs->nn; j++)
+        if (rs->r[rs->idx_n[j]].rhsPen != 0.0) any = 1;
+    if (!any) return 0;
+    for (int it = 0; it < UG_PGS_ITERS; it++) {
+        double res = 0.0;
+        for (int j = 0; j < rs->nn; j++) {
+            double x = solve_row(&rs->r[rs->idx_n[j]], dvs, 1);
+            x = x * x;
+            res = res > x ? res : x;
+        }
+        if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
+    }
+    return 1;
+}
+
+/* ======================================================================== */
+/* one p.stepSimulation()                                                    */
+/* ======================================================================== */
+static void substep(ugo_env* e) {
+    const double dt = UG_DT;
+    const scene* s = &e->sc;
+    kin k;
+    fk(e->q, &k);
+    /* collision detection on current positions */
+    collide(e, &k);
+    /* external forces: robot (gravity, gyroscopic, damping) */
+    double M[NB * NB], C[NB];
+    robot_dynamics(e->qd, &k, s->gravity, M, C);
+    ldlt(M, NB);
+    double qdd[NB];
+    for (int i = 0; i < NB; i++) qdd[i] = -C[i];
+    ldlt_solve(M, NB, qdd);
+    double v0[NV];
+    memset(v0, 0, sizeof(v0));
+    for (int i = 0; i < NB; i++) { e->qd[i] = e->qd[i] + qdd[i] * dt; v0[i] = e->qd[i]; }
+    /* free objects: gravity + default damping + gyroscopic (btMultiBody floating base, 0 links) */
+    for (int o = 0; o < s->nobj; o++) {
+        if (!e->oactive[o]) continue;
+        v3 v = e->ov[o];
+        double vn = vlen(v);
+        v3 a = vsub(V(0, 0, s->gravity), vscale(v, UG_LIN_DAMP + UG_LIN_DAMP * vn));
+        e->ov[o] = vadd(v, vscale(a, dt));
+        m3 R = qmat(e->oquat[o]);
+        v3 wl = mtv(&R, e->ow[o]);
+        v3 I = s->oinertia[o];
+        v3 Iw = V(I.x * wl.x, I.y * wl.y, I.z * wl.z);
+        double wn = vlen(wl);
+        v3 z = vadd(vscale(Iw, UG_ANG_DAMP + UG_ANG_DAMP * wn), vcross(wl, Iw));
+        v3 al = V(-z.x / I.x, -z.y / I.y, -z.z / I.z);
+        e->ow[o] = vadd(e->ow[o], vscale(mv(&R, al), dt));
+        int off = NB + 6 * o;
+        v0[off] = e->ov[o].x; v0[off + 1] = e->ov[o].y; v0[off + 2] = e->ov[o].z;
+        v0[off + 3] = e->ow[o].x; v0[off + 4] = e->ow[o].y; v0[off + 5] = e->ow[o].z;
+    }
+    /* constraint solve */
+    static __thread rowset rs;
+    build_rows(e, &k, M, v0, &rs);
+    double dv[NV], dvs[NV];
+    memset(dv, 0, sizeof(dv));
+    memset(dvs, 0, sizeof(dvs));
+    pgs(&rs, dv);
+    int split = pgs_split(&rs, dvs);
+    for (int i = 0; i < rs.nn; i++) {
+        const row* r = &rs.r[rs.idx_n[i]];
+        e->man[r->man].pt[r->pt].imp = r->imp;
+    }
+    for (int i = 0; i < rs.nf; i++) {
+        const row* r = &rs.r[rs.idx_f[i]];
+        if (r->kind == 2) e->man[r->man].pt[r->pt].imp1 = r->imp;
+        else e->man[r->man].pt[r->pt].imp2 = r->imp;
+    }
+    /* velocities += solver delta; positions integrate (v + split velocity) */
+    for (int i = 0; i < NB; i++) {
+        e->qd[i] = e->qd[i] + dv[i];
+        double vi = split ? e->qd[i] + dvs[i] : e->qd[i];
+        e->q[i] = e->q[i] + vi * dt;
+    }
+    for (int o = 0; o < s->nobj; o++) {
+        if (!e->oactive[o]) continue;
+        int off = NB + 6 * o;
+        e->ov[o] = vadd(e->ov[o], V(dv[off], dv[off + 1], dv[off + 2]));
+        e->ow[o] = vadd(e->ow[o], V(dv[off + 3], dv[off + 4], dv[off + 5]));
+        v3 vl = e->ov[o], wa = e->ow[o];
+        if (split) {
+            vl = vadd(vl, V(dvs[off], dvs[off + 1], dvs[off + 2]));
+            wa = vadd(wa, V(dvs[off + 3], dvs[off + 4], dvs[off + 5]));
+        }
+        e->opos[o] = vadd(e->opos[o], vscale(vl, dt));
+        /* btMultiBody::stepPositionsMultiDof base quaternion update [ext] */
+        double ang = vlen(wa);
+        if (ang * dt > UG_ANGULAR_MOTION_THR) ang = UG_ANGULAR_MOTION_THR / dt;
+        v3 ax;
+        if (ang < 0.001) ax = vscale(wa, 0.5 * dt - (dt * dt * dt) * 0.020833333333 * ang * ang);
+        else ax = vscale(wa, ug_sin(0.5 * ang * dt) / ang);
+        q4 dq = Q(ax.x, ax.y, ax.z, ug_cos(0.5 * ang * dt));
+        e->oquat[o] = qnormalize(qmul(dq, e->oquat[o]));
+    }
+}
+
+/* ======================================================================== */
+/* robot control layer (urgym/base/robot.py)                                 */
+/* ======================================================================== */
+/* numpy pairwise sum of 12 |dq| (np.sum, env_ball_balance_v0.py:100) */
+static double np_sum12(const double* a) {
+    double r = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    for (int i = 8; i < 12; i++) r += a[i];
+    return r;
+}
+/* wait_until_stable (env_ball_balance_v0.py:94-103): returns substeps taken */
+static int wait_until_stable(ugo_env* e) {
+    double pos[NB];
+    memcpy(pos, e->q, sizeof(pos));
+    for (int i = 0; i < UG_STABLE_STEPS; i++) {
+        substep(e);
+        double a[NB];
+        for (int j = 0; j < NB; j++) a[j] = ug_fabs(pos[j] - e->q[j]);
+        if (np_sum12(a) < UG_STABLE_EPS) return i + 1;
+        memcpy(pos, e->q, sizeof(pos));
+    }
+    return UG_STABLE_STEPS;
+}
+/* UR5Robotiq85.move_gripper (robot.py:213-218) */
+double ugo_gripper_angle(double L) { return 0.715 - ug_asin((L - 0.010) / 0.1143); }
+static void open_gripper(ugo_env* e, double pct) {
+    double L = UG_GRIP_MIN + (UG_GRIP_MAX - UG_GRIP_MIN) * (pct / 100.0);
+    e->mtarget[6] = ugo_gripper_angle(L);
+    e->mon[6] = 1;
+}
+static void close_gripper(ugo_env* e, double pct) {
+    double L = UG_GRIP_MAX - (UG_GRIP_MAX - UG_GRIP_MIN) * (pct / 100.0);
+    e->mtarget[6] = ugo_gripper_angle(L);
+    e->mon[6] = 1;
+}
+
+/* p.calculateInverseKinematics(robot, 7, pos, orn, ..6-long arrays.., maxNumIterations=20)
+ * [ext]: PhysicsServerCommandProcessor IK loop + IKTrajectoryHelper::computeIK with
+ * IK2_VEL_DLS_WITH_ORIENTATION (null space skipped: arrays shorter than the dof count) */
+static void ik_solve(const double* q0, v3 tp, q4 to, double* qout) {
+    double q[NB];
+    memcpy(q, q0, sizeof(q));
+    double diff = 1e30;
+    for (int it = 0; it < UG_IK_ITERS && diff > UG_IK_RESIDUAL; it++) {
+        kin k;
+        fk(q, &k);
+        m3 Re;
+        v3 pe;
+        link_frame(&k, UG_EE_LINK, 1, &Re, &pe);
+        q4 oe = mquat(&Re);
+        diff = vlen(vsub(pe, tp));
+        double ds[6];
+        ds[0] = 1.0 * (tp.x - pe.x); ds[1] = 1.0 * (tp.y - pe.y); ds[2] = 1.0 * (tp.z - pe.z);
+        q4 inv = Q(-oe.x, -oe.y, -oe.z, oe.w);
+        q4 dq = qmul(to, inv);
+        double w = dq.w;
+        if (w < -1.0) w = -1.0;
+        if (w > 1.0) w = 1.0;
+        float angle = (float)(2.0 * ug_acos(w));
+        if (angle > UG_PI) angle = (float)(angle - 2.0 * UG_PI);
+        else if (angle < -UG_PI) angle = (float)(angle + 2.0 * UG_PI);
+        v3 axis;
+        double s2 = 1.0 - dq.w * dq.w;
+        if (s2 < 10.0 * 2.220446049250313e-16) axis = V(1.0, 0.0, 0.0);
+        else { double sq = 1.0 / ug_sqrt(s2); axis = V(dq.x * sq, dq.y * sq, dq.z * sq); }
+        axis = vscale(axis, 1.0 / vlen(axis));
+        ds[3] = 1.0 * ((double)angle * axis.x);
+        ds[4] = 1.0 * ((double)angle * axis.y);
+        ds[5] = 1.0 * ((double)angle * axis.z);
+        /* Jacobian of the EE link origin wrt the 6 arm dofs (gripper columns are zero) */
+        double J[6][6];
+        for (int d = 0; d < 6; d++) {
+            v3 jl = vcross(k.a[d], vsub(pe, k.p[d]));
+            J[0][d] = jl.x; J[1][d] = jl.y; J[2][d] = jl.z;
+            J[3][d] = k.a[d].x; J[4][d] = k.a[d].y; J[5][d] = k.a[d].z;
+        }
+        /* (J^T J + diag(0.5)) dtheta = J^T ds  (BussIK CalcDeltaThetasDLS2) */
+        double U[36], rhs[6];
+        for (int i = 0; i < 6; i++) {
+            for (int j = 0; j < 6; j++) {
+                double sum = 0.0;
+                for (int r = 0; r < 6; r++) sum += J[r][i] * J[r][j];
+                U[i * 6 + j] = sum;
+            }
+            U[i * 6 + i] += UG_IK_DAMPING;
+            double sr = 0.0;
+            for (int r = 0; r < 6; r++) sr += J[r][i] * ds[r];
+            rhs[i] = sr;
+        }
+        ldlt(U, 6);
+        ldlt_solve(U, 6, rhs);
+        double mx = 0.0;
+        for (int i = 0; i < 6; i++) mx = ug_fabs(rhs[i]) > mx ? ug_fabs(rhs[i]) : mx;
+        if (mx > UG_IK_MAXANGLE)
+            for (int i = 0; i < 6; i++) rhs[i] *= UG_IK_MAXANGLE / mx;
+        for (int i = 0; i < 6; i++) q[i] = rhs[i] + q[i];
+    }
+    memcpy(qout, q, sizeof(q));
+}
+static void move_ee_end(ugo_env* e, v3 pos, q4 orn) {
+    double qt[NB];
+    ik_solve(e->q, pos, orn, qt);
+    for (int i = 0; i < 6; i++) { e->mtarget[i] = qt[i]; e->mon[i] = 1; }
+}
+static void move_ee_joint(ugo_env* e, const double* q6) {
+    for (int i = 0; i < 6; i++) { e->mtarget[i] = q6[i]; e->mon[i] = 1; }
+}
+/* getLinkState(robot, l)[0:2]: link COM world pose */
+static void link_state(const ugo_env* e, int l, v3* p, q4* o) {
+    kin k;
+    fk(e->q, &k);
+    m3 R;
+    link_frame(&k, l, 1, &R, p);
+    *o = mquat(&R);
+}
+/* get_gripper_geometrical_center (env_ball_balance_v0.py:249-275): union of getAABB(11), getAABB(16) */
+static v3 gripper_center(const ugo_env* e) {
+    kin k;
+    fk(e->q, &k);
+    v3 lo = V(1e300, 1e300, 1e300), hi = V(-1e300, -1e300, -1e300);
+    const int links[2] = {11, 16};
+    for (int i = 0; i < 2; i++) {
+        int l = links[i];
+        m3 R;
+        v3 p;
+        link_frame(&k, l, 1, &R, &p);
+        v3 c = vadd(mv(&R, V(UG_LINK_AABB_C[3 * l], UG_LINK_AABB_C[3 * l + 1], UG_LINK_AABB_C[3 * l + 2])), p);
+        v3 h = V(UG_LINK_AABB_H[3 * l], UG_LINK_AABB_H[3 * l + 1], UG_LINK_AABB_H[3 * l + 2]);
+        const double* r = R.m;
+        v3 ext = V(ug_fabs(r[0]) * h.x + ug_fabs(r[1]) * h.y + ug_fabs(r[2]) * h.z,
+                   ug_fabs(r[3]) * h.x + ug_fabs(r[4]) * h.y + ug_fabs(r[5]) * h.z,
+                   ug_fabs(r[6]) * h.x + ug_fabs(r[7]) * h.y + ug_fabs(r[8]) * h.z);
+        v3 mn = vsub(c, ext), mx = vadd(c, ext);
+        lo = V(ug_min(lo.x, mn.x), ug_min(lo.y, mn.y), ug_min(lo.z, mn.z));
+        hi = V(ug_max(hi.x, mx.x), ug_max(hi.y, mx.y), ug_max(hi.z, mx.z));
+    }
+    return V((hi.x + lo.x) / 2.0, (hi.y + lo.y) / 2.0, (hi.z + lo.z) / 2.0);
+}
+static void remove_object(ugo_env* e, int o) {
+    e->oactive[o] = 0;
+    int ci = e->sc.ocol[o];
+    for (int m = e->nman - 1; m >= 0; m--) {
+        const pairdef* P = &e->sc.pair[e->man[m].pair];
+        if (P->a == ci || P->b == ci) {
+            int last = e->nman - 1;
+            if (m != last) e->man[m] = e->man[last];
+            e->nman--;
+        }
+    }
+}
+static void place_object(ugo_env* e, int o, v3 pos, q4 orn) {
+    e->oactive[o] = 1;
+    e->opos[o] = pos;
+    e->oquat[o] = orn;
+    e->ov[o] = V(0, 0, 0);
+    e->ow[o] = V(0, 0, 0);
+}
+/* RobotBase.reset -> reset_arm (robot.py:89-98) + reset_gripper/open_gripper (robot.py:100-106) */
+static int robot_reset(ugo_env* e) {
+    for (int i = 0; i < 6; i++) { e->q[i] = UG_ARM_REST[i]; e->qd[i] = 0.0; }
+    for (int i = 0; i < 10; i++) substep(e);
+    open_gripper(e, 100.0);
+    return 10;
+}
+
+/* ======================================================================== */
+/* tasks                                                                     */
+/* ======================================================================== */
+int ugo_obs_dim(int task) { return task == UG_TASK_BALLBALANCE ? 6 : (task == UG_TASK_CUBESGRASP ? 17 : 9); }
+int ugo_act_dim(int task) { return task == UG_TASK_CUBESGRASP ? 9 : 3; }
+int ugo_state_dim(void) { return STATE_DIM; }
+
+static void bb_obs(const ugo_env* e, double* obs) {
+    /* env_ball_balance_v0.py:137-143 */
+    v3 eu = euler_from_quat(e->oquat[0]);
+    obs[0] = eu.x; obs[1] = eu.y; obs[2] = eu.z;
+    obs[3] = e->opos[0].x - e->opos[1].x;
+    obs[4] = e->opos[0].y - e->opos[1].y;
+    obs[5] = e->opos[0].z - e->opos[1].z;
+}
+static int bb_reset(ugo_env* e, double* obs) {
+    /* env_ball_balance_v0.py:145-170 */
+    int n = robot_reset(e);
+    remove_object(e, 0);
+    remove_object(e, 1);
+    move_ee_end(e, V(0.0, -0.60, 0.60), Q(0.50, -0.50, -0.50, 0.50));
+    open_gripper(e, 20.0);
+    n += wait_until_stable(e);
+    v3 pe;
+    q4 oe;
+    link_state(e, UG_EE_LINK, &pe, &oe);
+    v3 gc = gripper_center(e);
+    v3 pose = V(pe.x, pe.y - 0.2, gc.z);
+    place_object(e, 0, pose, Q(0, 0, 0, 1));
+    /* create_ball (:186-205) */
+    v3 bp = V(pose.x, pose.y, pose.z + 0.2 + UG_BB_BALL_R);
+    bp.x += mt_uniform(&e->rng, -0.03, 0.03);
+    bp.y += mt_uniform(&e->rng, -0.08, 0.02);
+    place_object(e, 1, bp, e->oquat[0]);
+    close_gripper(e, 100.0);
+    n += wait_until_stable(e);
+    bb_obs(e, obs);
+    return n;
+}
+static int bb_step(ugo_env* e, const float* a, double* obs, double* rew, uint8_t* term, uint8_t* succ) {
+    /* env_ball_balance_v0.py:105-134 */
+    v3 pe;
+    q4 oe;
+    link_state(e, UG_EE_LINK, &pe, &oe);
+    v3 eu = euler_from_quat(oe);
+    eu.x += (double)a[0]; eu.y += (double)a[1]; eu.z += (double)a[2];
+    q4 qn = quat_from_euler(eu);
+    move_ee_end(e, pe, qn);
+    int n = wait_until_stable(e);
+    *rew = 1.0;
+    *term = e->opos[1].z < e->opos[0].z;
+    *succ = 0;
+    bb_obs(e, obs);
+    return n;
+}
+
+/* ======================================================================== */
+/* public API                                                                */
+/* ======================================================================== */
+ugo_env* ugo_create(int task, uint32_t seed) {
+    ugo_env* e = (ugo_env*)calloc(1, sizeof(ugo_env));
+    build_scene(&e->sc, task);
+    mt_seed(&e->rng, seed);
+    return e;
+}
+void ugo_destroy(ugo_env* e) { free(e); }
+void ugo_substep(ugo_env* e) { substep(e); }
+int ugo_reset(ugo_env* e, double* obs) {
+    e->goal_approached = e->goal_grasped = 0;
+    if (e->sc.task == UG_TASK_BALLBALANCE) return bb_reset(e, obs);
+    return -1;
+}
+int ugo_step(ugo_env* e, const float* action, double* obs, double* reward, uint8_t* terminated, uint8_t* success) {
+    if (e->sc.task == UG_TASK_BALLBALANCE) return bb_step(e, action, obs, reward, terminated, success);
+    return -1;
+}
+void ugo_get_state(const ugo_env* e, double* s) {
+    memset(s, 0, sizeof(double) * STATE_DIM);
+    int i = 0;
+    for (int j = 0; j < NB; j++) s[i++] = e->q[j];
+    for (int j = 0; j < NB; j++) s[i++] = e->qd[j];
+    for (int j = 0; j < 7; j++) s[i++] = e->mtarget[j];
+    for (int j = 0; j < 7; j++) s[i++] = e->mon[j];
+    for (int o = 0; o < MAXOBJ; o++) s[i++] = e->oactive[o];
+    for (int o = 0; o < MAXOBJ; o++) {
+        s[i++] = e->opos[o].x; s[i++] = e->opos[o].y; s[i++] = e->opos[o].z;
+        s[i++] = e->oquat[o].x; s[i++] = e->oquat[o].y; s[i++] = e->oquat[o].z; s[i++] = e->oquat[o].w;
+        s[i++] = e->ov[o].x; s[i++] = e->ov[o].y; s[i++] = e->ov[o].z;
+        s[i++] = e->ow[o].x; s[i++] = e->ow[o].y; s[i++] = e->ow[o].z;
+    }
+    s[i++] = e->nman;
+    for (int m = 0; m < MAXMAN; m++) {
+        const manifold* M = &e->man[m];
+        s[i++] = m < e->nman ? M->pair : -1;
+        s[i++] = m < e->nman ? M->npts : 0;
+        for (int p = 0; p < 4; p++) {
+            const cpoint* c = &M->pt[p];
+            int live = m < e->nman && p < M->npts;
+            double v[PT_DOUBLES] = {c->lpA.x, c->lpA.y, c->lpA.z, c->lpB.x, c->lpB.y, c->lpB.z,
+                                    c->n.x, c->n.y, c->n.z, c->dist, c->imp, c->imp1, c->imp2};
+            for (int t = 0; t < PT_DOUBLES; t++) s[i++] = live ? v[t] : 0.0;
+        }
+    }
+    s[i++] = e->goal_approached;
+    s[i++] = e->goal_grasped;
+    s[i++] = e->overflow;
+    s[i++] = 0.0;
+}
+void ugo_set_state(ugo_env* e, const double* s) {
+    int i = 0;
+    for (int j = 0; j < NB; j++) e->q[j] = s[i++];
+    for (int j = 0; j < NB; j++) e->qd[j] = s[i++];
+    for (int j = 0; j < 7; j++) e->mtarget[j] = s[i++];
+    for (int j = 0; j < 7; j++) e->mon[j] = (int)s[i++];
+    for (int o = 0; o < MAXOBJ; o++) e->oactive[o] = (int)s[i++];
+    for (int o = 0; o < MAXOBJ; o++) {
+        e->opos[o].x = s[i++]; e->opos[o].y = s[i++]; e->opos[o].z = s[i++];
+        e->oquat[o].x = s[i++]; e->oquat[o].y = s[i++]; e->oquat[o].z = s[i++]; e->oquat[o].w = s[i++];
+        e->ov[o].x = s[i++]; e->ov[o].y = s[i++]; e->ov[o].z = s[i++];
+        e->ow[o].x = s[i++]; e->ow[o].y = s[i++]; e->ow[o].z = s[i++];
+    }
+    e->nman = (int)s[i++];
+    for (int m = 0; m < MAXMAN; m++) {
+        manifold* M = &e->man[m];
+        M->pair = (int)s[i++];
+        M->npts = (int)s[i++];
+        for (int p = 0; p < 4; p++) {
+            cpoint* c = &M->pt[p];
+            c->lpA = V(s[i], s[i + 1], s[i + 2]); c->lpB = V(s[i + 3], s[i + 4], s[i + 5]);
+            c->n = V(s[i + 6], s[i + 7], s[i + 8]);
+            c->dist = s[i + 9]; c->imp = s[i + 10]; c->imp1 = s[i + 11]; c->imp2 = s[i + 12];
+            i += PT_DOUBLES;
+        }
+    }
+    e->goal_approached = (int)s[i++];
+    e->goal_grasped = (int)s[i++];
+    e->overflow = (int)s[i++];
+}
+void ugo_rng_seed(ugo_env* e, uint32_t seed) { mt_seed(&e->rng, seed); }
+double ugo_rng_random(ugo_env* e) { return mt_random(&e->rng); }
+double ugo_gdr(double value, double ts, double tm) {
+    /* geometric_distance_reward (utilities.py:192-207) */
+    value = value > 1e-10 ? value : 1e-10;
+    double f1 = (value - ts) / value;
+    double f2 = (tm - value) > 1e-10 ? (tm - value) : 1e-10;
+    return -ug_tanh(f1 / f2);
+}
+void ugo_euler_from_quat(const double* q, double* rpy) {
+    v3 r = euler_from_quat(Q(q[0], q[1], q[2], q[3]));
+    rpy[0] = r.x; rpy[1] = r.y; rpy[2] = r.z;
+}
+void ugo_quat_from_euler(const double* rpy, double* q) {
+    q4 r = quat_from_euler(V(rpy[0], rpy[1], rpy[2]));
+    q[0] = r.x; q[1] = r.y; q[2] = r.z; q[3] = r.w;
+}
+void ugo_link_state(const ugo_env* e, int link, double* pos7) {
+    v3 p;
+    q4 o;
+    link_state(e, link, &p, &o);
+    pos7[0] = p.x; pos7[1] = p.y; pos7[2] = p.z; pos7[3] = o.x; pos7[4] = o.y; pos7[5] = o.z; pos7[6] = o.w;
+}
+void ugo_ik(const ugo_env* e, const double* tp, const double* to, double* q_out) {
+    ik_solve(e->q, V(tp[0], tp[1], tp[2]), Q(to[0], to[1], to[2], to[3]), q_out);
+}
+long ugo_batch_step(ugo_env** envs, int n, const float* actions, double* obs, double* reward, uint8_t* terminated,
+                    uint8_t* success, int32_t* substeps, int autoreset, int max_episode_steps, int32_t* elapsed) {
+    long total = 0;
+    if (n <= 0) return 0;
+    int task = envs[0]->sc.task;
+    int A = ugo_act_dim(task), O = ugo_obs_dim(task);
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total)
+    for (int i = 0; i < n; i++) {
+        int ns = ugo_step(envs[i], actions + (size_t)i * A, obs + (size_t)i * O, reward + i, terminated + i, success + i);
+        if (elapsed) elapsed[i] += 1;
+        int trunc = elapsed && max_episode_steps > 0 && elapsed[i] >= max_episode_steps;
+        if (autoreset && (terminated[i] || trunc)) {
+            ns += ugo_reset(envs[i], obs + (size_t)i * O);
+            if (elapsed) elapsed[i] = 0;
+        }
+        substeps[i] = ns;
+        total += ns;
+    }
+    return total;
+}

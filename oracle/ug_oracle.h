@@ -1,0 +1,60 @@
+/* ug_oracle.h -- CPU restatement of URGym's per-step hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity oracle for the HIP product
+ * path (urgym_amd/csrc).  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it (oracle/_build/libugoracle.so).  The product
+ * never links or calls it.
+ *
+ * What it restates (file:line in /root/reference):
+ *   env.step()              urgym/envs/env_ball_balance_v0.py:105-134 (and the other envs)
+ *   robot.move_ee / IK      urgym/base/robot.py:113-128  -> p.calculateInverseKinematics [ext]
+ *   wait_until_stable       urgym/envs/env_ball_balance_v0.py:94-103
+ *   p.stepSimulation        PyBullet/Bullet3 btMultiBodyDynamicsWorld [ext, parity unpinned]
+ *   obs/reward/termination  per env file (see oracle/ug_oracle.c)
+ * Parity vs PyBullet itself is UNPINNED (pybullet absent);
+ * the glue (rewards, euler/quaternion conventions, gripper map, RNG) is
+ * pinned by tests/golden fixtures generated from the reference's own code.
+ */
+#ifndef UG_ORACLE_H
+#define UG_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ugo_env ugo_env;
+
+/* task: 0 BallBalance, 1 CubesPush, 2 CubesGrasp, 3 Golf */
+ugo_env* ugo_create(int task, uint32_t seed);
+void ugo_destroy(ugo_env* e);
+int ugo_obs_dim(int task);
+int ugo_act_dim(int task);
+int ugo_state_dim(void);
+/* reset(): fills obs; returns substeps spent */
+int ugo_reset(ugo_env* e, double* obs);
+/* step(): action float32[act_dim]; returns substeps spent in wait_until_stable */
+int ugo_step(ugo_env* e, const float* action, double* obs, double* reward, uint8_t* terminated,
+             uint8_t* success);
+void ugo_get_state(const ugo_env* e, double* s);
+void ugo_set_state(ugo_env* e, const double* s);
+/* one physics substep (p.stepSimulation) -- for fine-grained parity tests */
+void ugo_substep(ugo_env* e);
+/* helpers exposed for known-answer tests */
+void ugo_rng_seed(ugo_env* e, uint32_t seed);
+double ugo_rng_random(ugo_env* e);
+double ugo_gdr(double value, double thr_sign, double thr_max);
+void ugo_euler_from_quat(const double* q, double* rpy);
+void ugo_quat_from_euler(const double* rpy, double* q);
+double ugo_gripper_angle(double open_length);
+void ugo_link_state(const ugo_env* e, int link, double* pos7);
+void ugo_ik(const ugo_env* e, const double* target_pos, const double* target_orn, double* q_out);
+/* batched CPU baseline: n envs, OpenMP over envs; returns total substeps */
+long ugo_batch_step(ugo_env** envs, int n, const float* actions, double* obs, double* reward,
+                    uint8_t* terminated, uint8_t* success, int32_t* substeps, int autoreset,
+                    int max_episode_steps, int32_t* elapsed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,151 @@
+"""ctypes binding of liburgym.so (the HIP product path, include/urgym.h).
+
+There is deliberately no CPU fallback: if the in-tree library is missing, or
+no GPU is visible, constructing an environment raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "liburgym.so")
+
+# C-ABI symbols declared in include/urgym.h (checked by tests/test_capi_symbols.py)
+SYMBOLS = [
+    "urgym_create", "urgym_destroy", "urgym_last_error", "urgym_obs_dim", "urgym_act_dim", "urgym_state_dim",
+    "urgym_num_envs", "urgym_set_autoreset", "urgym_reset", "urgym_num_draws", "urgym_step", "urgym_step_device",
+    "urgym_reset_device", "urgym_sync", "urgym_stream", "urgym_get_state", "urgym_set_state", "urgym_substep",
+    "urgym_link_state", "urgym_ik", "urgym_last_kernel_ms",
+]
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"liburgym.so not built ({LIB_PATH}); run __graft_entry__.build() -- no CPU fallback exists")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, D, U32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_uint32
+    L.urgym_create.restype = P
+    L.urgym_create.argtypes = [I, I, I, I, U32, I]
+    L.urgym_destroy.argtypes = [P]
+    L.urgym_last_error.restype = ctypes.c_char_p
+    L.urgym_last_error.argtypes = [P]
+    for name in ("urgym_obs_dim", "urgym_act_dim", "urgym_num_draws"):
+        getattr(L, name).argtypes = [I]
+    L.urgym_state_dim.argtypes = []
+    L.urgym_num_envs.argtypes = [P]
+    L.urgym_set_autoreset.argtypes = [P, I, I]
+    L.urgym_reset.argtypes = [P, P, P, P]
+    L.urgym_reset_device.argtypes = [P, P, P, P]
+    L.urgym_step.argtypes = [P, P, P, P, P, P, P, P, P]
+    L.urgym_step_device.argtypes = [P, P, P, P, P, P, P, P, P]
+    L.urgym_sync.argtypes = [P]
+    L.urgym_stream.restype = P
+    L.urgym_stream.argtypes = [P]
+    L.urgym_get_state.argtypes = [P, P]
+    L.urgym_set_state.argtypes = [P, P]
+    L.urgym_substep.argtypes = [P]
+    L.urgym_link_state.argtypes = [P, I, P]
+    L.urgym_ik.argtypes = [P, P, P]
+    L.urgym_last_kernel_ms.restype = D
+    L.urgym_last_kernel_ms.argtypes = [P]
+    _lib = L
+    return L
+
+
+def ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Sim:
+    """One handle = n_envs environments of one task on one GPU."""
+
+    def __init__(self, task, n_envs, device=0, seed=0, env_offset=0):
+        self.L = lib()
+        self.task = task
+        self.n = n_envs
+        self.h = self.L.urgym_create(task, n_envs, device, 64, seed & 0xFFFFFFFF, env_offset)
+        if not self.h:
+            raise RuntimeError("urgym_create failed: " + self.L.urgym_last_error(None).decode())
+        self.obs_dim = self.L.urgym_obs_dim(task)
+        self.act_dim = self.L.urgym_act_dim(task)
+        self.state_dim = self.L.urgym_state_dim()
+        self.ndraw = self.L.urgym_num_draws(task)
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed: " + self.L.urgym_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.urgym_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_autoreset(self, enable, max_episode_steps):
+        self._chk(self.L.urgym_set_autoreset(self.h, int(enable), int(max_episode_steps)), "urgym_set_autoreset")
+
+    def reset(self, mask=None, draws=None, obs=None):
+        if obs is None:
+            obs = np.zeros((self.n, self.obs_dim))
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        d = None if draws is None else np.ascontiguousarray(draws, dtype=np.float64)
+        self._chk(self.L.urgym_reset(self.h, ptr(m), ptr(d), ptr(obs)), "urgym_reset")
+        return obs
+
+    def step(self, actions):
+        a = np.ascontiguousarray(actions, dtype=np.float32).reshape(self.n, self.act_dim)
+        n = self.n
+        out = dict(obs=np.zeros((n, self.obs_dim)), final_obs=np.zeros((n, self.obs_dim)), reward=np.zeros(n),
+                   terminated=np.zeros(n, np.uint8), truncated=np.zeros(n, np.uint8), success=np.zeros(n, np.uint8),
+                   substeps=np.zeros(n, np.int32))
+        self._chk(self.L.urgym_step(self.h, ptr(a), ptr(out["obs"]), ptr(out["final_obs"]), ptr(out["reward"]),
+                                    ptr(out["terminated"]), ptr(out["truncated"]), ptr(out["success"]),
+                                    ptr(out["substeps"])), "urgym_step")
+        return out
+
+    def step_device(self, d_act, d_obs, d_final=0, d_rew=0, d_term=0, d_trunc=0, d_succ=0, d_sub=0):
+        """Device-pointer variant (ints = device addresses, e.g. torch.Tensor.data_ptr())."""
+        v = ctypes.c_void_p
+        self._chk(self.L.urgym_step_device(self.h, v(d_act), v(d_obs), v(d_final or None), v(d_rew or None),
+                                           v(d_term or None), v(d_trunc or None), v(d_succ or None),
+                                           v(d_sub or None)), "urgym_step_device")
+
+    def sync(self):
+        self._chk(self.L.urgym_sync(self.h), "urgym_sync")
+
+    def last_kernel_ms(self):
+        return self.L.urgym_last_kernel_ms(self.h)
+
+    def get_state(self):
+        s = np.zeros((self.n, self.state_dim))
+        self._chk(self.L.urgym_get_state(self.h, ptr(s)), "urgym_get_state")
+        return s
+
+    def set_state(self, s):
+        s = np.ascontiguousarray(s, dtype=np.float64).reshape(self.n, self.state_dim)
+        self._chk(self.L.urgym_set_state(self.h, ptr(s)), "urgym_set_state")
+
+    def substep(self):
+        self._chk(self.L.urgym_substep(self.h), "urgym_substep")
+
+    def link_state(self, link):
+        out = np.zeros((self.n, 7))
+        self._chk(self.L.urgym_link_state(self.h, int(link), ptr(out)), "urgym_link_state")
+        return out
+
+    def ik(self, target):
+        t = np.ascontiguousarray(target, dtype=np.float64).reshape(self.n, 7)
+        q = np.zeros((self.n, 12))
+        self._chk(self.L.urgym_ik(self.h, ptr(t), ptr(q)), "urgym_ik")
+        return q

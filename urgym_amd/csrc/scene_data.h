@@ -1,0 +1,83 @@
+/* scene_data.h -- per-task scene constants (data, not code), restated from the
+ * reference env files and PyBullet defaults.  Shared as *input data* by the CPU
+ * restatement (oracle/) and the HIP kernels.  Every number cites its source;
+ * [ext] marks a PyBullet/Bullet default that cannot be checked in this build
+ * (SURVEY.md Appendix A).
+ */
+#ifndef URGYM_SCENE_DATA_H
+#define URGYM_SCENE_DATA_H
+#ifndef UG_CONST
+#define UG_CONST static const
+#endif
+
+/* ---- world / solver (PyBullet defaults, none overridden by the reference) ---- */
+#define UG_DT (1.0 / 240.0)            /* fixed 240 Hz step [ext], env_*:SIMULATION_STEP_DELAY */
+#define UG_PGS_ITERS 50                /* m_numIterations [ext] */
+#define UG_RESIDUAL_THR 1e-7           /* m_leastSquaresResidualThreshold [ext] */
+#define UG_ERP 0.2                     /* m_erp (joints, shallow contacts) [ext] */
+#define UG_ERP2 0.08                   /* m_erp2 (deep-penetration split impulse) [ext] */
+#define UG_SPLIT_PEN_THR (-0.04)       /* m_splitImpulsePenetrationThreshold [ext] */
+#define UG_WARMSTART 0.1               /* m_warmstartingFactor [ext] */
+#define UG_LINEAR_SLOP 0.00001         /* m_linearSlop [ext] */
+#define UG_REST_VEL_THR 0.2            /* m_restitutionVelocityThreshold [ext] */
+#define UG_CONTACT_BREAK 0.02          /* gContactBreakingThreshold (relative to shape size) [ext] */
+#define UG_AABB_PAD 0.02               /* broadphase AABB padding [ext] */
+#define UG_LIN_DAMP 0.04               /* btMultiBody default linear damping [ext] */
+#define UG_ANG_DAMP 0.04               /* btMultiBody default angular damping [ext] */
+#define UG_MAX_FRICTION 10.0           /* MAX_FRICTION clamp of the combined friction [ext] */
+#define UG_ANGULAR_MOTION_THR (0.5 * 1.5707963267948966)   /* ANGULAR_MOTION_THRESHOLD [ext] */
+#define UG_MOTOR_KP 0.1                /* pybullet positionGain default [ext] */
+#define UG_MOTOR_KD 1.0                /* pybullet velocityGain default [ext] */
+#define UG_GEAR_MAXF 100.0             /* robot.py:211 maxForce=100 */
+#define UG_GEAR_ERP 1.0                /* robot.py:211 erp=1 */
+#define UG_LIMIT_MAXIMP 100.0          /* btMultiBodyJointLimitConstraint default max impulse [ext] */
+#define UG_STABLE_STEPS 480            /* env_ball_balance_v0.py:94 sim_steps=480 */
+#define UG_STABLE_EPS 5e-3             /* env_ball_balance_v0.py:100 */
+#define UG_IK_ITERS 20                 /* robot.py:121 maxNumIterations=20 */
+#define UG_IK_RESIDUAL 1e-4            /* pybullet IK residualThreshold default [ext] */
+#define UG_IK_DAMPING 0.5              /* PhysicsServer IK joint damping default [ext] */
+#define UG_IK_MAXANGLE (45.0 * 3.14159265358979311600e+00 / 180.0)  /* BussIK MaxAngleDLS [ext] */
+
+/* ---- gripper (robot.py:188, 213-218; gear table robot.py:194-211) ---- */
+#define UG_GRIP_MIN 0.0
+#define UG_GRIP_MAX 0.085
+#define UG_FINGER_DOF 6                /* finger_joint = link 9 = dof 6 */
+/* constraints are created in joint-id order (robot.py:202 iterates self.joints): links 11,13,14,16,18
+ * = dofs 7,8,9,10,11; gearRatio = -multiplier (robot.py:196-200, 211) */
+UG_CONST int UG_GEAR_CHILD[5] = {7, 8, 9, 10, 11};
+UG_CONST double UG_GEAR_RATIO[5] = {1.0, -1.0, -1.0, 1.0, -1.0};
+
+/* ---- task ids (urgym/envs/__init__.py) ---- */
+#define UG_TASK_BALLBALANCE 0
+#define UG_TASK_CUBESPUSH 1
+#define UG_TASK_CUBESGRASP 2
+#define UG_TASK_GOLF 3
+
+/* ---- shapes ---- */
+#define UG_SHAPE_BOX 0
+#define UG_SHAPE_HULL 1
+#define UG_SHAPE_SPHERE 2
+
+/* statics: plane.urdf = 30x30x10 box, top at the load height, lateral friction 1 [ext];
+ * table = box 1 x 2 x 0.5 centred at (0,0,-0.25) (env_ball_balance_v0.py:69-71, 216-247);
+ * golf pitch = convex hull of golf_pitch.obj = 0.8 x 0.8 x 0.05 box at (0,-0.6,0.02) (env_golf_v0.py:87, 428-446) */
+#define UG_PLANE_HALF_XY 15.0
+#define UG_PLANE_HALF_Z 5.0
+#define UG_PLANE_FRICTION 1.0
+#define UG_DEFAULT_FRICTION 0.5        /* btCollisionObject / URDF default lateral friction [ext] */
+#define UG_URDF_MARGIN 0.001           /* gUrdfDefaultCollisionMargin [ext] */
+
+/* BallBalance (env_ball_balance_v0.py) */
+#define UG_BB_PADDLE_HX 0.05           /* :177 halfExtents */
+#define UG_BB_PADDLE_HY 0.1
+#define UG_BB_PADDLE_HZ 0.005
+#define UG_BB_PADDLE_MASS 0.1          /* :183 */
+#define UG_BB_BALL_R 0.02              /* :186 */
+#define UG_BB_BALL_MASS 0.01           /* :202 */
+
+/* CubesPush / CubesGrasp: cube.urdf x 0.04 (mass 1, lateral friction 1) [ext] */
+#define UG_CUBE_HALF 0.02
+#define UG_CUBE_MASS 1.0
+#define UG_CUBE_FRICTION 1.0
+
+#endif

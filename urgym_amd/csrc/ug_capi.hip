@@ -1,0 +1,532 @@
+// ug_capi.hip -- kernels + C-ABI (include/urgym.h) of the MI355X URGym hot path.
+//
+// One launch per batched env-step: k_step gives every lane one environment and
+// runs the reference's whole step() -- IK, joint motors, wait_until_stable's
+// <=480 physics substeps, reward/termination, and (gymnasium same-step
+// autoreset) the reset of an env whose episode just ended -- without leaving
+// the kernel.  State is SoA in HBM (ug_layout.h), read once and written once
+// per launch.  Block = one wavefront (64 lanes = 64 envs); the grid covers
+// n_envs.  There is no CPU fallback: if this library is missing, nothing runs.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/urgym.h"
+#include "ug_device.h"
+
+using namespace ugd;
+
+#define WAVE 64
+
+// ---------------------------------------------------------------------------
+// scene construction (device, one thread): statics, objects, collision pairs
+// ---------------------------------------------------------------------------
+__device__ static void box_collider(Collider* c, double hx, double hy, double hz, double margin, double friction) {
+    c->kind = UG_SHAPE_BOX;
+    c->half[0] = hx; c->half[1] = hy; c->half[2] = hz;
+    c->margin = margin;
+    c->v0 = c->nv = c->f0 = c->nf = 0;
+    c->R = mident(); c->P = V(0, 0, 0);
+    c->aR = mident(); c->aP = V(0, 0, 0);
+    c->ac = V(0, 0, 0); c->ah = V(hx, hy, hz);
+    c->disc = ug_sqrt(hx * hx + hy * hy + hz * hz);
+    c->friction = friction;
+    c->restitution = 0.0;
+    c->owner = -100; c->ent = 0;
+    c->link = -1;
+}
+__device__ static double safe_margin(double hx, double hy, double hz) {
+    double m = hx < hy ? hx : hy;
+    m = m < hz ? m : hz;
+    m = 0.1 * m;
+    return m < 0.04 ? m : 0.04;
+}
+__device__ static void add_pair(Scene* s, int a, int b) {
+    PairDef* p = &s->pair[s->npair++];
+    p->a = a; p->b = b;
+    double d = s->col[a].disc < s->col[b].disc ? s->col[a].disc : s->col[b].disc;
+    p->thr = d * UG_CONTACT_BREAK;
+    double f = s->col[a].friction * s->col[b].friction;
+    if (f < -UG_MAX_FRICTION) f = -UG_MAX_FRICTION;
+    if (f > UG_MAX_FRICTION) f = UG_MAX_FRICTION;
+    p->friction = f;
+    p->restitution = s->col[a].restitution * s->col[b].restitution;
+}
+__global__ void k_build_scene(Scene* s, int task) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    s->task = task;
+    s->gravity = task == UG_TASK_CUBESGRASP ? -10.0 : -9.8;
+    s->nobj = 0;
+    s->ncol = 0;
+    s->npair = 0;
+    for (int l = 1; l < UG_NL; l++) {
+        Collider* c = &s->col[s->ncol++];
+        int si = -1;
+        for (int k = 0; k < UG_NSHAPE; k++)
+            if (UG_SHAPE_LINK[k] == l) si = k;
+        c->kind = UG_SHAPE_KIND[si] == 0 ? UG_SHAPE_BOX : UG_SHAPE_HULL;
+        c->half[0] = UG_SHAPE_HALF[3 * si]; c->half[1] = UG_SHAPE_HALF[3 * si + 1]; c->half[2] = UG_SHAPE_HALF[3 * si + 2];
+        c->margin = UG_URDF_MARGIN;
+        c->v0 = UG_SHAPE_V0[si]; c->nv = UG_SHAPE_NV[si]; c->f0 = UG_SHAPE_F0[si]; c->nf = UG_SHAPE_NF[si];
+        c->R = mload(&UG_SHAPE_R[9 * si]);
+        c->P = V(UG_SHAPE_P[3 * si], UG_SHAPE_P[3 * si + 1], UG_SHAPE_P[3 * si + 2]);
+        c->aR = mload(&UG_LINK_COMR[9 * l]);
+        c->aP = V(UG_LINK_COMP[3 * l], UG_LINK_COMP[3 * l + 1], UG_LINK_COMP[3 * l + 2]);
+        c->ac = V(UG_LINK_AABB_C[3 * l], UG_LINK_AABB_C[3 * l + 1], UG_LINK_AABB_C[3 * l + 2]);
+        c->ah = V(UG_LINK_AABB_H[3 * l], UG_LINK_AABB_H[3 * l + 1], UG_LINK_AABB_H[3 * l + 2]);
+        c->disc = UG_LINK_DISC[l];
+        c->friction = UG_DEFAULT_FRICTION;
+        c->restitution = 0.0;
+        c->owner = UG_LINK_BODY[l];
+        c->ent = 0;
+        c->link = l;
+    }
+    int nrobot = s->ncol;
+    int statics[4], nstat = 0;
+    if (task == UG_TASK_BALLBALANCE) {
+        s->nobj = 2;
+        double hx = UG_BB_PADDLE_HX, hy = UG_BB_PADDLE_HY, hz = UG_BB_PADDLE_HZ, m = UG_BB_PADDLE_MASS;
+        s->omass[0] = m;
+        s->oinertia[0] = V(m / 12.0 * (4.0 * hy * hy + 4.0 * hz * hz), m / 12.0 * (4.0 * hx * hx + 4.0 * hz * hz),
+                           m / 12.0 * (4.0 * hx * hx + 4.0 * hy * hy));
+        Collider* c = &s->col[s->ncol];
+        box_collider(c, hx, hy, hz, safe_margin(hx, hy, hz), UG_DEFAULT_FRICTION);
+        c->owner = -2; c->ent = 1;
+        s->ocol[0] = s->ncol++;
+        double r = UG_BB_BALL_R, mb = UG_BB_BALL_MASS;
+        s->omass[1] = mb;
+        double ib = 0.4 * mb * r * r;
+        s->oinertia[1] = V(ib, ib, ib);
+        c = &s->col[s->ncol];
+        box_collider(c, r, r, r, r, UG_DEFAULT_FRICTION);
+        c->kind = UG_SHAPE_SPHERE;
+        c->half[1] = c->half[2] = 0.0;
+        c->disc = ug_sqrt(3.0) * r;
+        c->owner = -3; c->ent = 2;
+        s->ocol[1] = s->ncol++;
+    }
+    if (task == UG_TASK_BALLBALANCE || task == UG_TASK_CUBESPUSH || task == UG_TASK_GOLF) {
+        Collider* c = &s->col[s->ncol];
+        box_collider(c, 0.5, 1.0, 0.25, safe_margin(0.5, 1.0, 0.25), UG_DEFAULT_FRICTION);
+        c->P = V(0.0, 0.0, -0.25); c->aP = c->P;
+        c->owner = -100; c->ent = 10;
+        statics[nstat++] = s->ncol++;
+        c = &s->col[s->ncol];
+        box_collider(c, UG_PLANE_HALF_XY, UG_PLANE_HALF_XY, UG_PLANE_HALF_Z, UG_URDF_MARGIN, UG_PLANE_FRICTION);
+        c->P = V(0.0, 0.0, -0.5 - UG_PLANE_HALF_Z); c->aP = c->P;
+        c->disc = ug_sqrt(15.0 * 15.0 * 2.0 + 25.0) + 5.0;
+        c->owner = -100; c->ent = 11;
+        statics[nstat++] = s->ncol++;
+    }
+    for (int o = 0; o < s->nobj; o++)
+        for (int l = 0; l < nrobot; l++) add_pair(s, l, s->ocol[o]);
+    for (int t = 0; t < nstat; t++)
+        for (int l = 0; l < nrobot; l++) add_pair(s, l, statics[t]);
+    for (int o = 0; o < s->nobj; o++)
+        for (int p = o + 1; p < s->nobj; p++) {
+            int a = s->ocol[o], b = s->ocol[p];
+            if (s->col[b].kind == UG_SHAPE_SPHERE && s->col[a].kind != UG_SHAPE_SPHERE) { int t = a; a = b; b = t; }
+            add_pair(s, a, b);
+        }
+    for (int o = 0; o < s->nobj; o++)
+        for (int t = 0; t < nstat; t++) add_pair(s, s->ocol[o], statics[t]);
+}
+
+// ---------------------------------------------------------------------------
+// kernels: one env per lane
+// ---------------------------------------------------------------------------
+static __device__ int task_obs_dim(int task) { return task == UG_TASK_BALLBALANCE ? 6 : (task == UG_TASK_CUBESGRASP ? 17 : 9); }
+static __device__ int task_act_dim(int task) { return task == UG_TASK_CUBESGRASP ? 9 : 3; }
+static __device__ int task_ndraw(int task) { return task == UG_TASK_CUBESPUSH ? 1 : 2; }
+
+__global__ void __launch_bounds__(WAVE) k_reset(const Scene* sc, double* S, uint32_t* mt, int* elapsed, int n,
+                                                const uint8_t* mask, const double* draws, double* obs,
+                                                int32_t* substeps) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (mask && !mask[i]) return;
+    Env e;
+    e.sc = sc;
+    env_load(e, S, n, i);
+    RowSet rs;
+    Rng rng{mt, n, i};
+    Draws dr{&rng, draws ? draws + (size_t)i * task_ndraw(sc->task) : nullptr, 0};
+    int O = task_obs_dim(sc->task);
+    int ns = task_reset(e, rs, dr, obs + (size_t)i * O);
+    env_store(e, S, n, i);
+    elapsed[i] = 0;
+    if (substeps) substeps[i] = ns;
+}
+
+__global__ void __launch_bounds__(WAVE) k_step(const Scene* sc, double* S, uint32_t* mt, int* elapsed, int n,
+                                               const float* act, double* obs, double* final_obs, double* rew,
+                                               uint8_t* term, uint8_t* trunc, uint8_t* succ, int32_t* substeps,
+                                               int autoreset, int max_steps) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Env e;
+    e.sc = sc;
+    env_load(e, S, n, i);
+    RowSet rs;
+    int O = task_obs_dim(sc->task), A = task_act_dim(sc->task);
+    double* ob = obs + (size_t)i * O;
+    double r = 0.0;
+    int t = 0, su = 0;
+    int ns = task_step(e, rs, act + (size_t)i * A, ob, &r, &t, &su);
+    int el = elapsed[i] + 1;
+    int tr = (max_steps > 0 && el >= max_steps) ? 1 : 0;
+    if (autoreset && (t || tr)) {
+        if (final_obs)
+            for (int j = 0; j < O; j++) final_obs[(size_t)i * O + j] = ob[j];
+        Rng rng{mt, n, i};
+        Draws dr{&rng, nullptr, 0};
+        ns += task_reset(e, rs, dr, ob);
+        el = 0;
+    }
+    env_store(e, S, n, i);
+    elapsed[i] = el;
+    if (rew) rew[i] = r;
+    if (term) term[i] = (uint8_t)t;
+    if (trunc) trunc[i] = (uint8_t)tr;
+    if (succ) succ[i] = (uint8_t)su;
+    if (substeps) substeps[i] = ns;
+}
+
+__global__ void __launch_bounds__(WAVE) k_substep(const Scene* sc, double* S, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Env e;
+    e.sc = sc;
+    env_load(e, S, n, i);
+    RowSet rs;
+    substep(e, rs);
+    env_store(e, S, n, i);
+}
+
+__global__ void __launch_bounds__(WAVE) k_link_state(const Scene* sc, const double* S, int n, int link, double* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double q[NB];
+    for (int j = 0; j < NB; j++) q[j] = S[(size_t)(UG_F_Q + j) * n + i];
+    Kin k;
+    fk(q, k);
+    m3 R;
+    v3 p;
+    link_frame(k, link, 1, R, p);
+    q4 o = mquat(R);
+    double* r = out + (size_t)i * 7;
+    r[0] = p.x; r[1] = p.y; r[2] = p.z; r[3] = o.x; r[4] = o.y; r[5] = o.z; r[6] = o.w;
+}
+
+__global__ void __launch_bounds__(WAVE) k_ik(const Scene* sc, const double* S, int n, const double* target, double* qout) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double q[NB], qo[NB];
+    for (int j = 0; j < NB; j++) q[j] = S[(size_t)(UG_F_Q + j) * n + i];
+    const double* t = target + (size_t)i * 7;
+    ik_solve(q, V(t[0], t[1], t[2]), Q(t[3], t[4], t[5], t[6]), qo);
+    for (int j = 0; j < NB; j++) qout[(size_t)i * NB + j] = qo[j];
+}
+
+// AoS <-> SoA transposes for get/set_state
+__global__ void k_soa_to_aos(const double* S, double* out, int n) {
+    size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t tot = (size_t)n * UG_STATE_DIM;
+    if (idx >= tot) return;
+    int i = (int)(idx / UG_STATE_DIM), f = (int)(idx % UG_STATE_DIM);
+    out[idx] = S[(size_t)f * n + i];
+}
+__global__ void k_aos_to_soa(const double* in, double* S, int n) {
+    size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t tot = (size_t)n * UG_STATE_DIM;
+    if (idx >= tot) return;
+    int i = (int)(idx / UG_STATE_DIM), f = (int)(idx % UG_STATE_DIM);
+    S[(size_t)f * n + i] = in[idx];
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static std::string g_create_error;
+
+struct urgym_handle {
+    int task = 0, n = 0, dev = 0;
+    hipStream_t stream = nullptr;
+    Scene* d_scene = nullptr;
+    double* d_state = nullptr;
+    uint32_t* d_mt = nullptr;
+    int* d_elapsed = nullptr;
+    // staging for the host-pointer API
+    float* d_act = nullptr;
+    double *d_obs = nullptr, *d_final = nullptr, *d_rew = nullptr, *d_draws = nullptr, *d_aux = nullptr;
+    uint8_t *d_term = nullptr, *d_trunc = nullptr, *d_succ = nullptr, *d_mask = nullptr;
+    int32_t* d_sub = nullptr;
+    int autoreset = 0, max_steps = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    std::string err;
+};
+
+static int fail(urgym_handle* h, const std::string& msg) {
+    if (h) h->err = msg;
+    else g_create_error = msg;
+    return -1;
+}
+#define HIPCHK(h, call)                                                                       \
+    do {                                                                                      \
+        hipError_t _e = (call);                                                               \
+        if (_e != hipSuccess) return fail((h), std::string(#call) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+static int grid_of(int n) { return (n + WAVE - 1) / WAVE; }
+
+// CPython random.seed(int) (init_by_array) -- host copy for per-env stream seeding
+static void mt_seed_host(uint32_t* mt, uint32_t seed) {
+    mt[0] = 19650218u;
+    for (int i = 1; i < 624; i++) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+    uint32_t key = seed;
+    int i = 1, j = 0;
+    for (int k = 624; k; k--) {
+        mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + key + (uint32_t)j;
+        i++; j++;
+        if (i >= 624) { mt[0] = mt[623]; i = 1; }
+        if (j >= 1) j = 0;
+    }
+    for (int k = 623; k; k--) {
+        mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+        i++;
+        if (i >= 624) { mt[0] = mt[623]; i = 1; }
+    }
+    mt[0] = 0x80000000u;
+    mt[624] = 624;
+}
+
+extern "C" {
+
+int urgym_obs_dim(int task) { return task == 0 ? 6 : (task == 2 ? 17 : 9); }
+int urgym_act_dim(int task) { return task == 2 ? 9 : 3; }
+int urgym_state_dim(void) { return UG_STATE_DIM; }
+int urgym_num_draws(int task) { return task == 1 ? 1 : 2; }
+int urgym_num_envs(const urgym_handle* h) { return h ? h->n : 0; }
+const char* urgym_last_error(const urgym_handle* h) { return h ? h->err.c_str() : g_create_error.c_str(); }
+
+static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed, int env_offset) {
+    HIPCHK(h, hipSetDevice(dev));
+    HIPCHK(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    HIPCHK(h, hipEventCreate(&h->ev0));
+    HIPCHK(h, hipEventCreate(&h->ev1));
+    // deep per-lane call chains keep their arrays in scratch: raise the stack limit
+    HIPCHK(h, hipDeviceSetLimit(hipLimitStackSize, 64 * 1024));
+    HIPCHK(h, hipMalloc(&h->d_scene, sizeof(Scene)));
+    size_t N = (size_t)n;
+    HIPCHK(h, hipMalloc(&h->d_state, sizeof(double) * UG_STATE_DIM * N));
+    HIPCHK(h, hipMalloc(&h->d_mt, sizeof(uint32_t) * UG_MT_WORDS * N));
+    HIPCHK(h, hipMalloc(&h->d_elapsed, sizeof(int) * N));
+    HIPCHK(h, hipMalloc(&h->d_act, sizeof(float) * 9 * N));
+    HIPCHK(h, hipMalloc(&h->d_obs, sizeof(double) * 17 * N));
+    HIPCHK(h, hipMalloc(&h->d_final, sizeof(double) * 17 * N));
+    HIPCHK(h, hipMalloc(&h->d_rew, sizeof(double) * N));
+    HIPCHK(h, hipMalloc(&h->d_draws, sizeof(double) * 4 * N));
+    HIPCHK(h, hipMalloc(&h->d_aux, sizeof(double) * UG_STATE_DIM * N));
+    HIPCHK(h, hipMalloc(&h->d_term, N));
+    HIPCHK(h, hipMalloc(&h->d_trunc, N));
+    HIPCHK(h, hipMalloc(&h->d_succ, N));
+    HIPCHK(h, hipMalloc(&h->d_mask, N));
+    HIPCHK(h, hipMalloc(&h->d_sub, sizeof(int32_t) * N));
+    HIPCHK(h, hipMemsetAsync(h->d_state, 0, sizeof(double) * UG_STATE_DIM * N, h->stream));
+    HIPCHK(h, hipMemsetAsync(h->d_elapsed, 0, sizeof(int) * N, h->stream));
+    // per-env MT19937 streams seeded with seed + env_offset + i, stored SoA
+    std::vector<uint32_t> host(UG_MT_WORDS * N);
+    std::vector<uint32_t> one(UG_MT_WORDS);
+    for (int i = 0; i < n; i++) {
+        mt_seed_host(one.data(), seed + (uint32_t)env_offset + (uint32_t)i);
+        for (int w = 0; w < UG_MT_WORDS; w++) host[(size_t)w * N + i] = one[w];
+    }
+    HIPCHK(h, hipMemcpyAsync(h->d_mt, host.data(), sizeof(uint32_t) * host.size(), hipMemcpyHostToDevice, h->stream));
+    k_build_scene<<<1, 1, 0, h->stream>>>(h->d_scene, task);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+urgym_handle* urgym_create(int task, int n, int dev, int precision, uint32_t seed, int env_offset) {
+    if (task != URGYM_TASK_BALLBALANCE) {
+        fail(nullptr, "urgym_create: task " + std::to_string(task) + " not implemented in this build (BallBalance only)");
+        return nullptr;
+    }
+    if (n <= 0) { fail(nullptr, "urgym_create: n_envs must be > 0"); return nullptr; }
+    if (precision != 64) { fail(nullptr, "urgym_create: only precision=64 (FP64) is supported"); return nullptr; }
+    urgym_handle* h = new urgym_handle();
+    h->task = task; h->n = n; h->dev = dev;
+    if (create_impl(h, task, n, dev, seed, env_offset) != 0) {
+        g_create_error = h->err;
+        urgym_destroy(h);
+        return nullptr;
+    }
+    return h;
+}
+
+void urgym_destroy(urgym_handle* h) {
+    if (!h) return;
+    hipSetDevice(h->dev);
+    if (h->stream) hipStreamSynchronize(h->stream);
+    void* ptrs[] = {h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->d_act, h->d_obs, h->d_final, h->d_rew,
+                    h->d_draws, h->d_aux, h->d_term, h->d_trunc, h->d_succ, h->d_mask, h->d_sub};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    if (h->ev0) hipEventDestroy(h->ev0);
+    if (h->ev1) hipEventDestroy(h->ev1);
+    if (h->stream) hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int urgym_set_autoreset(urgym_handle* h, int enable, int max_episode_steps) {
+    if (!h) return -1;
+    h->autoreset = enable;
+    h->max_steps = max_episode_steps;
+    return 0;
+}
+
+void* urgym_stream(urgym_handle* h) { return h ? (void*)h->stream : nullptr; }
+int urgym_sync(urgym_handle* h) {
+    if (!h) return -1;
+    HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+double urgym_last_kernel_ms(const urgym_handle* h) {
+    if (!h || !h->timed) return -1.0;
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, h->ev0, h->ev1) != hipSuccess) return -1.0;
+    return (double)ms;
+}
+
+int urgym_reset_device(urgym_handle* h, const uint8_t* d_mask, const double* d_draws, double* d_obs) {
+    if (!h) return -1;
+    HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+    k_reset<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->n, d_mask,
+                                                    d_draws, d_obs, nullptr);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+    h->timed = true;
+    return 0;
+}
+
+int urgym_reset(urgym_handle* h, const uint8_t* mask, const double* draws, double* obs) {
+    if (!h) return -1;
+    if (!obs) return fail(h, "urgym_reset: obs must not be NULL");
+    size_t N = (size_t)h->n;
+    int O = urgym_obs_dim(h->task);
+    HIPCHK(h, hipSetDevice(h->dev));
+    if (mask) HIPCHK(h, hipMemcpyAsync(h->d_mask, mask, N, hipMemcpyHostToDevice, h->stream));
+    if (draws)
+        HIPCHK(h, hipMemcpyAsync(h->d_draws, draws, sizeof(double) * urgym_num_draws(h->task) * N, hipMemcpyHostToDevice,
+                                 h->stream));
+    // unmasked rows must come back untouched
+    HIPCHK(h, hipMemcpyAsync(h->d_obs, obs, sizeof(double) * O * N, hipMemcpyHostToDevice, h->stream));
+    if (urgym_reset_device(h, mask ? h->d_mask : nullptr, draws ? h->d_draws : nullptr, h->d_obs) != 0) return -1;
+    HIPCHK(h, hipMemcpyAsync(obs, h->d_obs, sizeof(double) * O * N, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int urgym_step_device(urgym_handle* h, const float* d_act, double* d_obs, double* d_final, double* d_rew,
+                      uint8_t* d_term, uint8_t* d_trunc, uint8_t* d_succ, int32_t* d_sub) {
+    if (!h) return -1;
+    if (!d_act || !d_obs) return fail(h, "urgym_step_device: actions and obs must not be NULL");
+    HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+    k_step<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->n, d_act, d_obs,
+                                                   d_final, d_rew, d_term, d_trunc, d_succ, d_sub, h->autoreset,
+                                                   h->max_steps);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+    h->timed = true;
+    return 0;
+}
+
+int urgym_step(urgym_handle* h, const float* act, double* obs, double* final_obs, double* rew, uint8_t* term,
+               uint8_t* trunc, uint8_t* succ, int32_t* sub) {
+    if (!h) return -1;
+    if (!act || !obs) return fail(h, "urgym_step: actions and obs must not be NULL");
+    size_t N = (size_t)h->n;
+    int O = urgym_obs_dim(h->task), A = urgym_act_dim(h->task);
+    HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipMemcpyAsync(h->d_act, act, sizeof(float) * A * N, hipMemcpyHostToDevice, h->stream));
+    if (final_obs)
+        HIPCHK(h, hipMemcpyAsync(h->d_final, final_obs, sizeof(double) * O * N, hipMemcpyHostToDevice, h->stream));
+    if (urgym_step_device(h, h->d_act, h->d_obs, final_obs ? h->d_final : nullptr, h->d_rew, h->d_term, h->d_trunc,
+                          h->d_succ, h->d_sub) != 0)
+        return -1;
+    HIPCHK(h, hipMemcpyAsync(obs, h->d_obs, sizeof(double) * O * N, hipMemcpyDeviceToHost, h->stream));
+    if (final_obs) HIPCHK(h, hipMemcpyAsync(final_obs, h->d_final, sizeof(double) * O * N, hipMemcpyDeviceToHost, h->stream));
+    if (rew) HIPCHK(h, hipMemcpyAsync(rew, h->d_rew, sizeof(double) * N, hipMemcpyDeviceToHost, h->stream));
+    if (term) HIPCHK(h, hipMemcpyAsync(term, h->d_term, N, hipMemcpyDeviceToHost, h->stream));
+    if (trunc) HIPCHK(h, hipMemcpyAsync(trunc, h->d_trunc, N, hipMemcpyDeviceToHost, h->stream));
+    if (succ) HIPCHK(h, hipMemcpyAsync(succ, h->d_succ, N, hipMemcpyDeviceToHost, h->stream));
+    if (sub) HIPCHK(h, hipMemcpyAsync(sub, h->d_sub, sizeof(int32_t) * N, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int urgym_get_state(urgym_handle* h, double* state) {
+    if (!h || !state) return -1;
+    size_t tot = (size_t)h->n * UG_STATE_DIM;
+    HIPCHK(h, hipSetDevice(h->dev));
+    k_soa_to_aos<<<(unsigned)((tot + 255) / 256), 256, 0, h->stream>>>(h->d_state, h->d_aux, h->n);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipMemcpyAsync(state, h->d_aux, sizeof(double) * tot, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int urgym_set_state(urgym_handle* h, const double* state) {
+    if (!h || !state) return -1;
+    size_t tot = (size_t)h->n * UG_STATE_DIM;
+    HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipMemcpyAsync(h->d_aux, state, sizeof(double) * tot, hipMemcpyHostToDevice, h->stream));
+    k_aos_to_soa<<<(unsigned)((tot + 255) / 256), 256, 0, h->stream>>>(h->d_aux, h->d_state, h->n);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int urgym_substep(urgym_handle* h) {
+    if (!h) return -1;
+    HIPCHK(h, hipSetDevice(h->dev));
+    k_substep<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_scene, h->d_state, h->n);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int urgym_link_state(urgym_handle* h, int link, double* out) {
+    if (!h || !out) return -1;
+    if (link < 0 || link >= UG_NL) return fail(h, "urgym_link_state: link out of range");
+    HIPCHK(h, hipSetDevice(h->dev));
+    k_link_state<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_scene, h->d_state, h->n, link, h->d_aux);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipMemcpyAsync(out, h->d_aux, sizeof(double) * 7 * h->n, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int urgym_ik(urgym_handle* h, const double* target, double* q_out) {
+    if (!h || !target || !q_out) return -1;
+    size_t N = (size_t)h->n;
+    HIPCHK(h, hipSetDevice(h->dev));
+    double* d_t = h->d_aux;
+    double* d_q = h->d_aux + 7 * N;
+    HIPCHK(h, hipMemcpyAsync(d_t, target, sizeof(double) * 7 * N, hipMemcpyHostToDevice, h->stream));
+    k_ik<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_scene, h->d_state, h->n, d_t, d_q);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipMemcpyAsync(q_out, d_q, sizeof(double) * NB * N, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+}  // extern "C"
