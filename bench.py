@@ -104,10 +104,6 @@ def main():
     trunc = torch.zeros_like(term)
     succ = torch.zeros_like(term)
     sub = torch.zeros(n, dtype=torch.int32, device=dev)
-    gathered = None
-    if world > 1:
-        packed = torch.zeros(n, O + 3, dtype=torch.float64, device=dev)
-        gathered = [torch.zeros_like(packed) for _ in range(world)]
     stream = torch.cuda.ExternalStream(sim.L.urgym_stream(sim.h), device=dev)
 
     def one_step(t):
@@ -115,12 +111,9 @@ def main():
                         trunc.data_ptr(), succ.data_ptr(), sub.data_ptr())
         if world > 1:
             # returns gathered over RCCL (xGMI): obs | reward | terminated | truncated
+            from urgym_amd.parallel import gather_returns
             with torch.cuda.stream(stream):
-                packed[:, :O] = obs
-                packed[:, O] = rew
-                packed[:, O + 1] = term.double()
-                packed[:, O + 2] = trunc.double()
-                dist.all_gather(gathered, packed)
+                gather_returns(obs, rew, term, trunc)
 
     for t in range(W):
         one_step(t)

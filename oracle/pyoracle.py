@@ -44,6 +44,11 @@ def lib():
         L.ugo_gripper_angle.restype = D
         L.ugo_link_state.argtypes = [P, I, P]
         L.ugo_ik.argtypes = [P, P, P, P]
+        L.ugo_bb_ball_position.argtypes = [P, P, P]
+        L.ugo_stable_sum.argtypes = [P]
+        L.ugo_stable_sum.restype = D
+        L.ugo_observe.argtypes = [P, P]
+        L.ugo_terminated.argtypes = [P]
         L.ugo_batch_step.restype = ctypes.c_long
         L.ugo_batch_step.argtypes = [P, I, P, P, P, P, P, P, I, I, P]
         _lib = L
@@ -97,6 +102,25 @@ class OracleEnv:
         s = np.ascontiguousarray(s, dtype=np.float64)
         self.L.ugo_set_state(self.h, _p(s))
 
+    def observe(self):
+        obs = np.zeros(self.obs_dim)
+        self.L.ugo_observe(self.h, _p(obs))
+        return obs
+
+    def terminated(self):
+        return bool(self.L.ugo_terminated(self.h))
+
+    def rng_seed(self, seed):
+        self.L.ugo_rng_seed(self.h, seed)
+
+    def rng_random(self):
+        return self.L.ugo_rng_random(self.h)
+
+    def bb_ball_position(self, paddle):
+        out = np.zeros(3)
+        self.L.ugo_bb_ball_position(self.h, _p(np.asarray(paddle, np.float64)), _p(out))
+        return out
+
     def link_state(self, link):
         out = np.zeros(7)
         self.L.ugo_link_state(self.h, link, _p(out))
@@ -126,3 +150,7 @@ def quat_from_euler(e):
 
 def gripper_angle(L):
     return lib().ugo_gripper_angle(L)
+
+
+def stable_sum(a12):
+    return lib().ugo_stable_sum(_p(np.ascontiguousarray(a12, np.float64)))

@@ -1701,6 +1701,13 @@ static void bb_obs(const ugo_env* e, double* obs) {
     obs[4] = e->opos[0].y - e->opos[1].y;
     obs[5] = e->opos[0].z - e->opos[1].z;
 }
+/* create_ball (env_ball_balance_v0.py:186-205): 0.2 m + r above the paddle, x += U(-0.03,0.03), y += U(-0.08,0.02) */
+static v3 bb_ball_position(ugo_env* e, v3 paddle) {
+    v3 bp = V(paddle.x, paddle.y, paddle.z + 0.2 + UG_BB_BALL_R);
+    bp.x += mt_uniform(&e->rng, -0.03, 0.03);
+    bp.y += mt_uniform(&e->rng, -0.08, 0.02);
+    return bp;
+}
 static int bb_reset(ugo_env* e, double* obs) {
     /* env_ball_balance_v0.py:145-170 */
     int n = robot_reset(e);
@@ -1715,11 +1722,7 @@ static int bb_reset(ugo_env* e, double* obs) {
     v3 gc = gripper_center(e);
     v3 pose = V(pe.x, pe.y - 0.2, gc.z);
     place_object(e, 0, pose, Q(0, 0, 0, 1));
-    /* create_ball (:186-205) */
-    v3 bp = V(pose.x, pose.y, pose.z + 0.2 + UG_BB_BALL_R);
-    bp.x += mt_uniform(&e->rng, -0.03, 0.03);
-    bp.y += mt_uniform(&e->rng, -0.08, 0.02);
-    place_object(e, 1, bp, e->oquat[0]);
+    place_object(e, 1, bb_ball_position(e, pose), e->oquat[0]);
     close_gripper(e, 100.0);
     n += wait_until_stable(e);
     bb_obs(e, obs);
@@ -1869,4 +1872,18 @@ long ugo_batch_step(ugo_env** envs, int n, const float* actions, double* obs, do
         total += ns;
     }
     return total;
+}
+
+/* ---- hooks for known-answer / golden tests ---- */
+void ugo_bb_ball_position(ugo_env* e, const double* paddle, double* out) {
+    v3 b = bb_ball_position(e, V(paddle[0], paddle[1], paddle[2]));
+    out[0] = b.x; out[1] = b.y; out[2] = b.z;
+}
+double ugo_stable_sum(const double* a12) { return np_sum12(a12); }
+void ugo_observe(const ugo_env* e, double* obs) {
+    if (e->sc.task == UG_TASK_BALLBALANCE) bb_obs(e, obs);
+}
+int ugo_terminated(const ugo_env* e) {
+    if (e->sc.task == UG_TASK_BALLBALANCE) return e->opos[1].z < e->opos[0].z;
+    return 0;
 }

@@ -49,6 +49,10 @@ void ugo_quat_from_euler(const double* rpy, double* q);
 double ugo_gripper_angle(double open_length);
 void ugo_link_state(const ugo_env* e, int link, double* pos7);
 void ugo_ik(const ugo_env* e, const double* target_pos, const double* target_orn, double* q_out);
+void ugo_bb_ball_position(ugo_env* e, const double* paddle, double* out);
+double ugo_stable_sum(const double* a12);
+void ugo_observe(const ugo_env* e, double* obs);
+int ugo_terminated(const ugo_env* e);
 /* batched CPU baseline: n envs, OpenMP over envs; returns total substeps */
 long ugo_batch_step(ugo_env** envs, int n, const float* actions, double* obs, double* reward,
                     uint8_t* terminated, uint8_t* success, int32_t* substeps, int autoreset,

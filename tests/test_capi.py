@@ -1,0 +1,50 @@
+"""The C-ABI library: builds, loads, exports every symbol include/urgym.h declares, and refuses to
+run without a GPU (no CPU fallback)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "urgym.h")).read()
+    return sorted(set(re.findall(r"\b(urgym_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_and_binding_agree(built):
+    from urgym_amd._native import SYMBOLS
+    assert sorted(SYMBOLS) == header_symbols()
+
+
+def test_library_exports_every_declared_symbol(built):
+    from urgym_amd._native import LIB_PATH
+    L = ctypes.CDLL(LIB_PATH)
+    for s in header_symbols():
+        assert hasattr(L, s), s
+
+
+def test_static_shapes(built):
+    from urgym_amd._native import lib
+    L = lib()
+    assert [L.urgym_obs_dim(t) for t in range(4)] == [6, 9, 17, 9]
+    assert [L.urgym_act_dim(t) for t in range(4)] == [3, 3, 9, 3]
+    from oracle.pyoracle import lib as olib
+    assert L.urgym_state_dim() == olib().ugo_state_dim()
+
+
+def test_spaces_match_reference(built):
+    import numpy as np
+    from urgym_amd.envs import spaces_for
+    obs, act = spaces_for(0)
+    assert obs.shape == (6,) and act.shape == (3,) and act.dtype == np.float32 and obs.dtype == np.float64
+    assert np.allclose(act.low, -0.1) and np.allclose(obs.high[:3], np.pi)
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="GPU present")
+def test_no_cpu_fallback_without_gpu(built):
+    from urgym_amd._native import Sim
+    with pytest.raises(RuntimeError):
+        Sim(0, 4)

@@ -1,0 +1,163 @@
+#!/usr/bin/env python3
+"""Generate golden fixtures from the reference's own Python glue (run in the build container only).
+
+The reference (/root/reference/urgym) imports pybullet, pybullet_data, gymnasium
+and cv2, none of which exist here.  We import it with *stub* modules: a
+recording fake `pybullet` (unittest.mock) that returns scripted physics
+queries and records every call the glue makes.  This pins the pure-Python
+parts of the hot path -- reward helpers, gripper angle map, Python-`random`
+draw order, euler+action arithmetic, obs assembly, termination -- without
+PyBullet.  The physics itself stays unpinned.
+
+Writes tests/golden/*.json (data only: inputs and expected outputs).
+"""
+import json
+import math
+import os
+import random
+import sys
+import types
+from unittest import mock
+
+import numpy as np
+
+REF = os.environ.get("URGYM_REFERENCE", "/root/reference")
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden")
+
+
+def install_stubs():
+    gym = types.ModuleType("gymnasium")
+
+    class Env:
+        def reset(self, *, seed=None, options=None):
+            return None
+
+    gym.Env = Env
+    spaces = types.ModuleType("gymnasium.spaces")
+
+    class Box:
+        def __init__(self, low=None, high=None, dtype=None, shape=None):
+            self.low, self.high, self.dtype = low, high, dtype
+
+    spaces.Box = Box
+    gym.spaces = spaces
+    reg = types.ModuleType("gymnasium.envs.registration")
+    reg.register = lambda **kw: None
+    envs = types.ModuleType("gymnasium.envs")
+    envs.registration = reg
+    sys.modules.update({"gymnasium": gym, "gymnasium.spaces": spaces, "gymnasium.envs": envs,
+                        "gymnasium.envs.registration": reg})
+    sys.modules["cv2"] = types.ModuleType("cv2")
+    pd = types.ModuleType("pybullet_data")
+    pd.getDataPath = lambda: "/nonexistent"
+    sys.modules["pybullet_data"] = pd
+    p = mock.MagicMock(name="pybullet")
+    sys.modules["pybullet"] = p
+    sys.path.insert(0, REF)
+    return p
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    p = install_stubs()
+    from urgym.base import utilities as U  # noqa: E402
+
+    # 1. geometric_distance_reward (utilities.py:192-207) on a grid of (value, sign, max)
+    gdr = []
+    for v in [0.0, 1e-12, 0.01, 0.05, 0.0999, 0.1, 0.2, 0.3, 0.45, 0.4999, 0.5, 0.7, 1.0, 2.5]:
+        for s, m in [(0.1, 0.5), (0.5, 2.0), (0.05, 0.2)]:
+            gdr.append([v, s, m, float(U.geometric_distance_reward(v, s, m))])
+    # 2. quaternion_multiply (utilities.py:155-174)
+    rng = np.random.default_rng(0)
+    qm = []
+    for _ in range(16):
+        a, b = rng.normal(size=4), rng.normal(size=4)
+        qm.append([a.tolist(), b.tolist(), list(U.quaternion_multiply(a.tolist(), b.tolist()))])
+    json.dump({"geometric_distance_reward": gdr, "quaternion_multiply": qm},
+              open(os.path.join(OUT, "utilities.json"), "w"), indent=1)
+
+    # 3. gripper angle map: UR5Robotiq85.move_gripper via open/close_gripper (robot.py:100-111, 213-218)
+    from urgym.base.robot import UR5Robotiq85  # noqa: E402
+    r = UR5Robotiq85.__new__(UR5Robotiq85)
+    r.gripper_range = [0, 0.085]
+    r.id = 1
+    r.mimic_parent_id = 9
+    r.joints = {9: types.SimpleNamespace(maxForce=1000.0, maxVelocity=2.0)}
+    grip = []
+    for kind, pct in [("open", 100), ("open", 20), ("close", 100), ("open", 0), ("close", 50), ("open", 73)]:
+        p.reset_mock()
+        (r.open_gripper if kind == "open" else r.close_gripper)(pct)
+        kw = p.setJointMotorControl2.call_args.kwargs
+        grip.append([kind, pct, kw["targetPosition"], kw["force"], kw["maxVelocity"]])
+    json.dump({"gripper": grip}, open(os.path.join(OUT, "gripper.json"), "w"), indent=1)
+
+    # 4. Python `random` streams (per-env seeding = random.seed(seed + env_id)) and the
+    #    BallBalance create_ball draw order (env_ball_balance_v0.py:186-205)
+    from urgym.envs.env_ball_balance_v0 import BallBalance  # noqa: E402
+    draws = []
+    for seed in [0, 1, 7, 12345, 20241220, 4294967295]:
+        random.seed(seed)
+        draws.append([seed, [random.random() for _ in range(8)]])
+    balls = []
+    for seed, paddle in [(0, (0.01, -0.8, 0.61)), (20241220, (-0.02, -0.79, 0.612)), (99, (0.0, -0.8, 0.6))]:
+        env = BallBalance.__new__(BallBalance)
+        env.paddle_id = 5
+        p.reset_mock()
+        p.getBasePositionAndOrientation.return_value = (paddle, (0.0, 0.0, 0.0, 1.0))
+        random.seed(seed)
+        env.create_ball()
+        kw = p.createMultiBody.call_args
+        pos = kw.args[3] if len(kw.args) > 3 else kw.kwargs["basePosition"]
+        balls.append([seed, list(paddle), list(pos)])
+    json.dump({"random": draws, "ballbalance_create_ball": balls},
+              open(os.path.join(OUT, "random.json"), "w"), indent=1)
+
+    # 5. BallBalance.step glue (env_ball_balance_v0.py:105-143) with scripted physics:
+    #    records the euler+action sent to getQuaternionFromEuler, the IK target, the obs and termination.
+    steps = []
+    env = BallBalance.__new__(BallBalance)
+    env.visualize = False
+    env.control_method = "end"
+    env.paddle_id, env.ball_id = 5, 6
+    env.robot = types.SimpleNamespace()
+    ee_pose = (0.1, -0.6, 0.6, 0.5, -0.5, -0.5, 0.5)
+    env.robot.get_ee_pose = lambda: ee_pose
+    moves = []
+    env.robot.move_ee = lambda pose, method: moves.append((list(pose), method))
+    env.wait_until_stable = lambda: True
+    cases = [((0.05, -0.02, 0.03), (0.01, -0.8, 0.61, 0.0, 0.0, 0.0, 1.0), (0.02, -0.85, 0.64)),
+             ((-0.1, 0.1, 0.0), (0.0, -0.8, 0.6, 0.01, -0.02, 0.003, 0.9997), (0.0, -0.8, 0.59)),
+             ((0.0, 0.0, -0.07), (0.03, -0.81, 0.605, 0.05, 0.0, 0.0, 0.99875), (0.05, -0.76, 0.63))]
+    for act, paddle7, ball3 in cases:
+        a = np.array(act, dtype=np.float32)
+        moves.clear()
+        p.reset_mock()
+        p.getEulerFromQuaternion.side_effect = lambda q: (0.25, -0.125, 0.5) if tuple(q) == ee_pose[3:] else (0.01, 0.02, 0.03)
+        p.getQuaternionFromEuler.side_effect = lambda e: (0.1, 0.2, 0.3, 0.9)
+        p.getBasePositionAndOrientation.side_effect = lambda bid: ((paddle7[:3], paddle7[3:]) if bid == 5 else (ball3, (0, 0, 0, 1)))
+        obs, rew, term, trunc, info = env.step(a)
+        euler_in = [float(x) for x in p.getQuaternionFromEuler.call_args.args[0]]
+        steps.append({"action": a.tolist(), "ee_pose": list(ee_pose), "ee_euler": [0.25, -0.125, 0.5],
+                      "euler_plus_action": euler_in, "ik_target": moves[0][0], "ik_method": moves[0][1],
+                      "paddle": list(paddle7), "ball": list(ball3), "paddle_euler": [0.01, 0.02, 0.03],
+                      "obs": [float(x) for x in obs], "reward": rew, "terminated": bool(term), "truncated": trunc,
+                      "info": info})
+    json.dump({"ballbalance_step": steps}, open(os.path.join(OUT, "ballbalance_glue.json"), "w"), indent=1)
+
+    # 6. wait_until_stable decision (env_ball_balance_v0.py:94-103): np.sum of |dq| over 12 joints
+    env2 = BallBalance.__new__(BallBalance)
+    env2.visualize = False
+    seq = [rng.normal(size=12) * 1e-3 for _ in range(6)]
+    qs = [np.cumsum(seq[:k + 1], axis=0)[-1].tolist() for k in range(6)]
+    it = iter(qs)
+    env2.robot = types.SimpleNamespace(get_joint_obs=lambda: {"positions": next(it)})
+    env2.step_simulation = lambda: None
+    stable = env2.wait_until_stable(sim_steps=5)
+    sums = [float(np.sum(np.abs(np.array(qs[k]) - np.array(qs[k + 1])))) for k in range(5)]
+    json.dump({"positions": qs, "abs_sums": sums, "stable": bool(stable)},
+              open(os.path.join(OUT, "wait_until_stable.json"), "w"), indent=1)
+    print("wrote", sorted(os.listdir(OUT)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1559,6 +1559,13 @@ DF void bb_obs(const Env& e, double* obs) {
     obs[4] = e.opos[0].y - e.opos[1].y;
     obs[5] = e.opos[0].z - e.opos[1].z;
 }
+/* create_ball (env_ball_balance_v0.py:186-205) */
+DF v3 bb_ball_position(Draws& dr, v3 paddle) {
+    v3 bp = V(paddle.x, paddle.y, paddle.z + 0.2 + UG_BB_BALL_R);
+    bp.x += uniform(dr, -0.03, 0.03);
+    bp.y += uniform(dr, -0.08, 0.02);
+    return bp;
+}
 DF int bb_reset(Env& e, RowSet& rs, Draws& dr, double* obs) {
     int n = robot_reset(e, rs);
     remove_object(e, 0);
@@ -1572,10 +1579,7 @@ DF int bb_reset(Env& e, RowSet& rs, Draws& dr, double* obs) {
     v3 gc = gripper_center(e);
     v3 pose = V(pe.x, pe.y - 0.2, gc.z);
     place_object(e, 0, pose, Q(0, 0, 0, 1));
-    v3 bp = V(pose.x, pose.y, pose.z + 0.2 + UG_BB_BALL_R);
-    bp.x += uniform(dr, -0.03, 0.03);
-    bp.y += uniform(dr, -0.08, 0.02);
-    place_object(e, 1, bp, e.oquat[0]);
+    place_object(e, 1, bb_ball_position(dr, pose), e.oquat[0]);
     close_gripper(e, 100.0);
     n += wait_until_stable(e, rs);
     bb_obs(e, obs);
