@@ -1080,26 +1080,25 @@ static void collide(ugo_env* e, const kin* k) {
         lo[i] = vsub(lo[i], V(UG_AABB_PAD, UG_AABB_PAD, UG_AABB_PAD));
         hi[i] = vadd(hi[i], V(UG_AABB_PAD, UG_AABB_PAD, UG_AABB_PAD));
     }
-    /* Narrowphase for every overlapping pair, in pair-table order.  A manifold slot is held only
-     * while the pair has contact points (empty manifolds carry neither rows nor predicates);
-     * releasing a slot swaps the last one in (btCollisionDispatcher::releaseManifold). */
+    /* Narrowphase for every overlapping pair, in pair-table order.  The manifold list is kept
+     * sorted by pair id and holds only pairs with contact points (an empty manifold carries neither
+     * rows nor predicates); a pair whose AABBs stop overlapping loses its manifold (Bullet destroys
+     * the algorithm with the broadphase pair).  Bullet's own manifold order (dispatcher array, then
+     * island sort) is not reproducible, so the row order here is: by pair id, then point. */
+    manifold nm[MAXMAN];
+    int nn = 0, cursor = 0;
     for (int p = 0; p < s->npair; p++) {
         const pairdef* P = &s->pair[p];
         int a = P->a, b = P->b;
-        int slot = -1;
-        for (int m = 0; m < e->nman; m++)
-            if (e->man[m].pair == p) { slot = m; break; }
+        manifold M;
+        M.pair = p;
+        M.npts = 0;
+        while (cursor < e->nman && e->man[cursor].pair < p) cursor++;
+        if (cursor < e->nman && e->man[cursor].pair == p) M = e->man[cursor];
         int ov = collider_active(e, &s->col[a]) && collider_active(e, &s->col[b]) &&
                  !(lo[a].x > hi[b].x || hi[a].x < lo[b].x || lo[a].y > hi[b].y || hi[a].y < lo[b].y ||
                    lo[a].z > hi[b].z || hi[a].z < lo[b].z);
-        if (!ov) {
-            if (slot >= 0) {
-                int last = e->nman - 1;
-                if (slot != last) e->man[slot] = e->man[last];
-                e->nman--;
-            }
-            continue;
-        }
+        if (!ov) continue;
         const collider* A = &s->col[a];
         const collider* B = &s->col[b];
         xf TA = shape_xf(&O[a], A), TB = shape_xf(&O[b], B);
@@ -1118,32 +1117,26 @@ static void collide(ugo_env* e, const kin* k) {
             for (int i = 0; i < L2.n; i++)
                 cand_add(&L, vneg(L2.c[i].n), vadd(L2.c[i].pB, vscale(L2.c[i].n, L2.c[i].d)), L2.c[i].d);
         }
-        if (slot < 0) {
-            if (L.n == 0) continue;
-            if (e->nman >= MAXMAN) { e->overflow++; continue; }
-            slot = e->nman++;
-            e->man[slot].pair = p;
-            e->man[slot].npts = 0;
-        }
-        manifold* M = &e->man[slot];
         /* manifold frames = owner frames */
-        for (int i = 0; i < L.n; i++) manifold_add(M, &O[a], &O[b], &L.c[i], P->thr);
-        if (M->npts) manifold_refresh(M, &O[a], &O[b], P->thr);
-        if (M->npts == 0) {
-            int last = e->nman - 1;
-            if (slot != last) e->man[slot] = e->man[last];
-            e->nman--;
-        }
+        for (int i = 0; i < L.n; i++) manifold_add(&M, &O[a], &O[b], &L.c[i], P->thr);
+        if (M.npts) manifold_refresh(&M, &O[a], &O[b], P->thr);
+        if (M.npts == 0) continue;
+        if (nn < MAXMAN) nm[nn++] = M;
+        else e->overflow++;
     }
+    for (int m = 0; m < nn; m++) e->man[m] = nm[m];
+    e->nman = nn;
 }
 
 /* ======================================================================== */
 /* constraint rows + projected Gauss-Seidel (btMultiBodyConstraintSolver)    */
 /* ======================================================================== */
+/* A row holds its Jacobian J and M^-1 J^T over the full generalized-velocity vector
+ * (robot dofs 0..11, object 0 at 12..17, object 1 at 18..23, zero-padded to UG_NVP = 32 slots), so the
+ * PGS dot product is one fixed pairwise tree -- the order the HIP kernel's DPP reduction realises. */
+#define UG_NVP 32
 typedef struct {
-    int entA, entB;            /* -1 none, 0 robot, 1+i object i */
-    double JA[NB], MiJA[NB];   /* robot: NB entries; object: 6 (lin, ang) */
-    double JB[NB], MiJB[NB];
+    double J[UG_NVP], MiJ[UG_NVP];
     double invD, rhs, rhsPen, lo, hi, imp, impPen, fric;
     int man, pt, kind;         /* kind 0 non-contact, 1 normal, 2 friction dir1, 3 friction dir2 */
     int nrow;                  /* friction rows: index of their normal row */
@@ -1169,9 +1162,23 @@ static double ent_dot_local(int ent, const double* a, const double* b) {
     for (int i = 0; i < n; i++) s += a[i] * b[i];
     return s;
 }
-static void ent_axpy(int ent, const double* MiJ, double a, double* v) {
+/* pairwise tree over 16 products: ((x0+x1)+(x2+x3)) + ((x4+x5)+(x6+x7)) ... */
+static double tree16(const double* x) {
+    double a[16];
+    for (int i = 0; i < 16; i++) a[i] = x[i];
+    for (int w = 1; w < 16; w <<= 1)
+        for (int i = 0; i < 16; i += 2 * w) a[i] = a[i] + a[i + w];
+    return a[0];
+}
+/* J . v over the 32-slot layout: two 16-lane rows, each reduced as a tree, then added */
+static double pdot(const double* J, const double* v) {
+    double p[UG_NVP];
+    for (int d = 0; d < UG_NVP; d++) p[d] = J[d] * v[d];
+    return tree16(p) + tree16(p + 16);
+}
+static void scatter(int ent, const double* src, double* dst) {
     int n = ent_dofs(ent), o = ent_off(ent);
-    for (int i = 0; i < n; i++) v[o + i] += MiJ[i] * a;
+    for (int i = 0; i < n; i++) dst[o + i] = src[i];
 }
 
 /* Jacobian of a point p on entity ent along direction d (linear) */
@@ -1205,24 +1212,43 @@ static int ent_of_collider(const collider* c, int* body) {
     return -1;
 }
 
-static void contact_row(const ugo_env* e, const kin* k, const double* LDL, const double* v0, row* r, int entA, int bodyA,
-                        int entB, int bodyB, v3 pA, v3 pB, v3 d) {
-    r->entA = entA; r->entB = entB;
-    double dA = 0.0, dB = 0.0;
-    double relv = 0.0;
+static void row_clear(row* r) { memset(r, 0, sizeof(*r)); }
+
+/* contact-type row: J_A at pA along +d, J_B at pB along -d; returns relative velocity J.v0 */
+static double contact_row(const ugo_env* e, const kin* k, const double* LDL, const double* v0, row* r, int entA,
+                          int bodyA, int entB, int bodyB, v3 pA, v3 pB, v3 d) {
+    double JA[NB], MiJA[NB], JB[NB], MiJB[NB];
+    double dA = 0.0, dB = 0.0, relv = 0.0;
     if (entA >= 0) {
-        point_jac(e, k, entA, bodyA, pA, d, r->JA, r->MiJA, LDL);
-        dA = ent_dot_local(entA, r->JA, r->MiJA);
-        relv += ent_dot(entA, r->JA, v0);
+        point_jac(e, k, entA, bodyA, pA, d, JA, MiJA, LDL);
+        dA = ent_dot_local(entA, JA, MiJA);
+        relv += ent_dot(entA, JA, v0);
+        scatter(entA, JA, r->J);
+        scatter(entA, MiJA, r->MiJ);
     }
     if (entB >= 0) {
-        point_jac(e, k, entB, bodyB, pB, vneg(d), r->JB, r->MiJB, LDL);
-        dB = ent_dot_local(entB, r->JB, r->MiJB);
-        relv += ent_dot(entB, r->JB, v0);
+        point_jac(e, k, entB, bodyB, pB, vneg(d), JB, MiJB, LDL);
+        dB = ent_dot_local(entB, JB, MiJB);
+        relv += ent_dot(entB, JB, v0);
+        scatter(entB, JB, r->J);
+        scatter(entB, MiJB, r->MiJ);
     }
     double den = dA + dB;
     r->invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
-    r->rhs = relv; /* caller turns rel_vel into rhs */
+    return relv;
+}
+/* single-dof row (limit / motor): J = sgn * e_d */
+static double dof_row(const double* LDL, const double* v0, row* r, int d, double sgn) {
+    double J[NB], MiJ[NB];
+    memset(J, 0, sizeof(J));
+    J[d] = sgn;
+    memcpy(MiJ, J, sizeof(J));
+    ldlt_solve(LDL, NB, MiJ);
+    double den = ent_dot_local(0, J, MiJ);
+    r->invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
+    scatter(0, J, r->J);
+    scatter(0, MiJ, r->MiJ);
+    return ent_dot(0, J, v0);
 }
 
 static void build_rows(ugo_env* e, const kin* k, const double* LDL, const double* v0, rowset* rs) {
@@ -1235,14 +1261,8 @@ static void build_rows(ugo_env* e, const kin* k, const double* LDL, const double
             if (pen > 0) continue;
             if (rs->n >= MAXROWS) { e->overflow++; continue; }
             row* r = &rs->r[rs->n];
-            memset(r, 0, sizeof(*r));
-            r->entA = 0; r->entB = -1;
-            r->JA[d] = side == 0 ? 1.0 : -1.0;
-            memcpy(r->MiJA, r->JA, sizeof(r->JA));
-            ldlt_solve(LDL, NB, r->MiJA);
-            double den = ent_dot_local(0, r->JA, r->MiJA);
-            r->invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
-            double relv = ent_dot(0, r->JA, v0);
+            row_clear(r);
+            double relv = dof_row(LDL, v0, r, d, side == 0 ? 1.0 : -1.0);
             double erp = (pen > UG_SPLIT_PEN_THR) ? UG_ERP : UG_ERP2;
             double perr = -pen * erp / dt, verr = -relv;
             double pimp = perr * r->invD, vimp = verr * r->invD;
@@ -1259,13 +1279,8 @@ static void build_rows(ugo_env* e, const kin* k, const double* LDL, const double
         double maxImp = UG_DOF_MAXFORCE[d] * dt;
         if (rs->n >= MAXROWS) { e->overflow++; continue; }
         row* r = &rs->r[rs->n];
-        memset(r, 0, sizeof(*r));
-        r->entA = 0; r->entB = -1;
-        r->JA[d] = 1.0;
-        memcpy(r->MiJA, r->JA, sizeof(r->JA));
-        ldlt_solve(LDL, NB, r->MiJA);
-        double den = ent_dot_local(0, r->JA, r->MiJA);
-        r->invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
+        row_clear(r);
+        double relv = dof_row(LDL, v0, r, d, 1.0);
         double qd = v0[d];
         double pst = 1.0 * (e->mtarget[m] - e->q[d]) / dt;
         double verr = 0.0 - qd;
@@ -1273,29 +1288,32 @@ static void build_rows(ugo_env* e, const kin* k, const double* LDL, const double
         double clamp = UG_DOF_MAXVEL[d];
         if (des > clamp) des = clamp;
         if (des < -clamp) des = -clamp;
-        double relv = ent_dot(0, r->JA, v0);
         r->rhs = 0.0 * r->invD + (des - relv) * r->invD;
         r->lo = -maxImp; r->hi = maxImp;
         r->kind = 0;
         rs->idx_nc[rs->nnc++] = rs->n++;
     }
-    /* mimic gears (robot.py:202-211): J_A = e_finger, J_B = ratio e_child */
+    /* mimic gears (robot.py:202-211): J_A = e_finger, J_B = ratio e_child (same multibody: Bullet's
+     * diagonal omits the A/B cross term; J and M^-1 J^T of the two parts are summed) */
     for (int g = 0; g < 5; g++) {
         if (rs->n >= MAXROWS) { e->overflow++; continue; }
         int pa = UG_FINGER_DOF, cb = UG_GEAR_CHILD[g];
         double ratio = UG_GEAR_RATIO[g];
         row* r = &rs->r[rs->n];
-        memset(r, 0, sizeof(*r));
-        r->entA = 0; r->entB = 0;
-        r->JA[pa] = 1.0;
-        r->JB[cb] = ratio;
-        memcpy(r->MiJA, r->JA, sizeof(r->JA));
-        memcpy(r->MiJB, r->JB, sizeof(r->JB));
-        ldlt_solve(LDL, NB, r->MiJA);
-        ldlt_solve(LDL, NB, r->MiJB);
-        double den = ent_dot_local(0, r->JA, r->MiJA) + ent_dot_local(0, r->JB, r->MiJB);
+        row_clear(r);
+        double JA[NB], JB[NB], MiJA[NB], MiJB[NB];
+        memset(JA, 0, sizeof(JA));
+        memset(JB, 0, sizeof(JB));
+        JA[pa] = 1.0;
+        JB[cb] = ratio;
+        memcpy(MiJA, JA, sizeof(JA));
+        memcpy(MiJB, JB, sizeof(JB));
+        ldlt_solve(LDL, NB, MiJA);
+        ldlt_solve(LDL, NB, MiJB);
+        double den = ent_dot_local(0, JA, MiJA) + ent_dot_local(0, JB, MiJB);
         r->invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
-        double relv = ent_dot(0, r->JA, v0) + ent_dot(0, r->JB, v0);
+        for (int i = 0; i < NB; i++) { r->J[i] = JA[i] + JB[i]; r->MiJ[i] = MiJA[i] + MiJB[i]; }
+        double relv = ent_dot(0, JA, v0) + ent_dot(0, JB, v0);
         double diff = e->q[cb] * ratio + e->q[pa];
         double pen = -UG_GEAR_ERP * (0.0 - diff);
         /* fillMultiBodyConstraint: split impulse not implemented for multibody rows -> always m_erp, combined */
@@ -1323,10 +1341,10 @@ static void build_rows(ugo_env* e, const kin* k, const double* LDL, const double
             v3 n = cp->n;
             int ni = rs->n;
             row* r = &rs->r[ni];
-            memset(r, 0, sizeof(*r));
-            contact_row(e, k, LDL, v0, r, entA, bodyA, entB, bodyB, pA, pB, n);
-            if (r->invD == 0.0) continue; /* no dynamic effect (e.g. fixed link) */
-            double relv = r->rhs;
+            row_clear(r);
+            double relv = contact_row(e, k, LDL, v0, r, entA, bodyA, entB, bodyB, pA, pB, n);
+            /* a row with zero effective mass (e.g. a contact normal parallel to the only joint axis)
+             * is kept as a no-op: rhs = 0, impulse stays 0, residual 0 (Bullet drops it) */
             double pen = cp->dist + UG_LINEAR_SLOP;
             double rest = 0.0;
             if (!(ug_fabs(relv) < UG_REST_VEL_THR)) rest = P->restitution * -relv;
@@ -1355,9 +1373,8 @@ static void build_rows(ugo_env* e, const kin* k, const double* LDL, const double
             }
             for (int fdir = 0; fdir < 2; fdir++) {
                 row* f = &rs->r[rs->n];
-                memset(f, 0, sizeof(*f));
-                contact_row(e, k, LDL, v0, f, entA, bodyA, entB, bodyB, pA, pB, fdir == 0 ? t1 : t2);
-                double frel = f->rhs;
+                row_clear(f);
+                double frel = contact_row(e, k, LDL, v0, f, entA, bodyA, entB, bodyB, pA, pB, fdir == 0 ? t1 : t2);
                 f->rhs = 0.0 * f->invD + (0.0 - frel) * f->invD;
                 f->fric = P->friction;
                 f->lo = 0.0; f->hi = 0.0;
@@ -1369,29 +1386,26 @@ static void build_rows(ugo_env* e, const kin* k, const double* LDL, const double
     }
 }
 
-/* resolveSingleConstraintRowGeneric [ext] */
+/* resolveSingleConstraintRowGeneric [ext] over the full generalized vector */
 static double solve_row(row* r, double* dv, int pen) {
     double imp = pen ? r->impPen : r->imp;
     double di = (pen ? r->rhsPen : r->rhs) - imp * 0.0;
-    if (r->entA >= 0) di -= ent_dot(r->entA, r->JA, dv) * r->invD;
-    if (r->entB >= 0) di -= ent_dot(r->entB, r->JB, dv) * r->invD;
+    di -= pdot(r->J, dv) * r->invD;
     double sum = imp + di;
     if (sum < r->lo) { di = r->lo - imp; imp = r->lo; }
     else if (sum > r->hi) { di = r->hi - imp; imp = r->hi; }
     else imp = sum;
     if (pen) r->impPen = imp; else r->imp = imp;
-    if (r->entA >= 0) ent_axpy(r->entA, r->MiJA, di, dv);
-    if (r->entB >= 0) ent_axpy(r->entB, r->MiJB, di, dv);
-    return di * (1.0 / r->invD);
+    for (int d = 0; d < NV; d++) dv[d] = dv[d] + r->MiJ[d] * di;
+    return r->invD == 0.0 ? 0.0 : di * (1.0 / r->invD);
 }
 
 static void pgs(rowset* rs, double* dv) {
+    /* warm start (normal rows only; Bullet warm-starts friction with 0) */
     for (int i = 0; i < rs->nn; i++) {
         row* r = &rs->r[rs->idx_n[i]];
-        if (r->imp != 0.0) {
-            if (r->entA >= 0) ent_axpy(r->entA, r->MiJA, r->imp, dv);
-            if (r->entB >= 0) ent_axpy(r->entB, r->MiJB, r->imp, dv);
-        }
+        if (r->imp != 0.0)
+            for (int d = 0; d < NV; d++) dv[d] = dv[d] + r->MiJ[d] * r->imp;
     }
     for (int it = 0; it < UG_PGS_ITERS; it++) {
         double res = 0.0;
@@ -1480,7 +1494,7 @@ static void substep(ugo_env* e) {
     /* constraint solve */
     static __thread rowset rs;
     build_rows(e, &k, M, v0, &rs);
-    double dv[NV], dvs[NV];
+    double dv[UG_NVP], dvs[UG_NVP];
     memset(dv, 0, sizeof(dv));
     memset(dvs, 0, sizeof(dvs));
     pgs(&rs, dv);
@@ -1662,14 +1676,14 @@ static v3 gripper_center(const ugo_env* e) {
 static void remove_object(ugo_env* e, int o) {
     e->oactive[o] = 0;
     int ci = e->sc.ocol[o];
-    for (int m = e->nman - 1; m >= 0; m--) {
+    int k = 0;
+    for (int m = 0; m < e->nman; m++) {
         const pairdef* P = &e->sc.pair[e->man[m].pair];
-        if (P->a == ci || P->b == ci) {
-            int last = e->nman - 1;
-            if (m != last) e->man[m] = e->man[last];
-            e->nman--;
-        }
+        if (P->a == ci || P->b == ci) continue;
+        if (k != m) e->man[k] = e->man[m];
+        k++;
     }
+    e->nman = k;
 }
 static void place_object(ugo_env* e, int o, v3 pos, q4 orn) {
     e->oactive[o] = 1;

@@ -1,12 +1,12 @@
 // ug_capi.hip -- kernels + C-ABI (include/urgym.h) of the MI355X URGym hot path.
 //
-// One launch per batched env-step: k_step gives every lane one environment and
-// runs the reference's whole step() -- IK, joint motors, wait_until_stable's
-// <=480 physics substeps, reward/termination, and (gymnasium same-step
-// autoreset) the reset of an env whose episode just ended -- without leaving
-// the kernel.  State is SoA in HBM (ug_layout.h), read once and written once
-// per launch.  Block = one wavefront (64 lanes = 64 envs); the grid covers
-// n_envs.  There is no CPU fallback: if this library is missing, nothing runs.
+// One launch per batched env-step: k_step gives every environment one
+// wavefront (block of 64 lanes) and runs the reference's whole step() -- IK,
+// joint motors, wait_until_stable's <=480 physics substeps, reward /
+// termination, and (gymnasium same-step autoreset) the reset of an env whose
+// episode just ended -- without leaving the kernel (ug_team.h).  State is
+// array-of-structs in HBM (ug_layout.h), loaded into LDS once and stored once
+// per launch.  There is no CPU fallback: if this library is missing, nothing runs.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -15,7 +15,7 @@
 #include <vector>
 
 #include "../../include/urgym.h"
-#include "ug_device.h"
+#include "ug_team.h"
 
 using namespace ugd;
 
@@ -136,115 +136,100 @@ __global__ void k_build_scene(Scene* s, int task) {
 }
 
 // ---------------------------------------------------------------------------
-// kernels: one env per lane
+// kernels: one wavefront (block of 64) per environment, state resident in LDS
 // ---------------------------------------------------------------------------
+#define WS_DOUBLES (UG_MAXMAN * UG_MAN_DOUBLES)   // per-env global workspace (old manifolds)
+
 static __device__ int task_obs_dim(int task) { return task == UG_TASK_BALLBALANCE ? 6 : (task == UG_TASK_CUBESGRASP ? 17 : 9); }
 static __device__ int task_act_dim(int task) { return task == UG_TASK_CUBESGRASP ? 9 : 3; }
 static __device__ int task_ndraw(int task) { return task == UG_TASK_CUBESPUSH ? 1 : 2; }
 
-__global__ void __launch_bounds__(WAVE) k_reset(const Scene* sc, double* S, uint32_t* mt, int* elapsed, int n,
-                                                const uint8_t* mask, const double* draws, double* obs,
-                                                int32_t* substeps) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(TEAM, 1) k_reset(const Scene* sc, double* S, uint32_t* mt, int* elapsed, double* ws,
+                                                   int n, const uint8_t* mask, const double* draws, double* obs,
+                                                   int32_t* substeps) {
+    __shared__ Shared sh;
+    const int i = blockIdx.x;
     if (i >= n) return;
     if (mask && !mask[i]) return;
-    Env e;
-    e.sc = sc;
-    env_load(e, S, n, i);
-    RowSet rs;
-    Rng rng{mt, n, i};
-    Draws dr{&rng, draws ? draws + (size_t)i * task_ndraw(sc->task) : nullptr, 0};
+    double* Si = S + (size_t)i * UG_STATE_DIM;
+    double* wsi = ws + (size_t)i * WS_DOUBLES;
+    team_load(sh, Si);
+    Draws dr{Rng{mt + (size_t)i * UG_MT_WORDS, 1, 0}, draws ? draws + (size_t)i * task_ndraw(sc->task) : nullptr, 0};
     int O = task_obs_dim(sc->task);
-    int ns = task_reset(e, rs, dr, obs + (size_t)i * O);
-    env_store(e, S, n, i);
-    elapsed[i] = 0;
-    if (substeps) substeps[i] = ns;
+    int ns = team_bb_reset(sh, sc, wsi, dr, obs + (size_t)i * O);
+    team_store(sh, Si);
+    if (threadIdx.x == 0) {
+        elapsed[i] = 0;
+        if (substeps) substeps[i] = ns;
+    }
 }
 
-__global__ void __launch_bounds__(WAVE) k_step(const Scene* sc, double* S, uint32_t* mt, int* elapsed, int n,
-                                               const float* act, double* obs, double* final_obs, double* rew,
-                                               uint8_t* term, uint8_t* trunc, uint8_t* succ, int32_t* substeps,
-                                               int autoreset, int max_steps) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, uint32_t* mt, int* elapsed, double* ws,
+                                                  int n, const float* act, double* obs, double* final_obs, double* rew,
+                                                  uint8_t* term, uint8_t* trunc, uint8_t* succ, int32_t* substeps,
+                                                  int autoreset, int max_steps) {
+    __shared__ Shared sh;
+    const int i = blockIdx.x;
     if (i >= n) return;
-    Env e;
-    e.sc = sc;
-    env_load(e, S, n, i);
-    RowSet rs;
+    double* Si = S + (size_t)i * UG_STATE_DIM;
+    double* wsi = ws + (size_t)i * WS_DOUBLES;
+    team_load(sh, Si);
     int O = task_obs_dim(sc->task), A = task_act_dim(sc->task);
     double* ob = obs + (size_t)i * O;
     double r = 0.0;
     int t = 0, su = 0;
-    int ns = task_step(e, rs, act + (size_t)i * A, ob, &r, &t, &su);
+    int ns = team_bb_step(sh, sc, wsi, act + (size_t)i * A, ob, &r, &t, &su);
     int el = elapsed[i] + 1;
     int tr = (max_steps > 0 && el >= max_steps) ? 1 : 0;
     if (autoreset && (t || tr)) {
-        if (final_obs)
+        if (final_obs && threadIdx.x == 0)
             for (int j = 0; j < O; j++) final_obs[(size_t)i * O + j] = ob[j];
-        Rng rng{mt, n, i};
-        Draws dr{&rng, nullptr, 0};
-        ns += task_reset(e, rs, dr, ob);
+        Draws dr{Rng{mt + (size_t)i * UG_MT_WORDS, 1, 0}, nullptr, 0};
+        ns += team_bb_reset(sh, sc, wsi, dr, ob);
         el = 0;
     }
-    env_store(e, S, n, i);
-    elapsed[i] = el;
-    if (rew) rew[i] = r;
-    if (term) term[i] = (uint8_t)t;
-    if (trunc) trunc[i] = (uint8_t)tr;
-    if (succ) succ[i] = (uint8_t)su;
-    if (substeps) substeps[i] = ns;
+    team_store(sh, Si);
+    if (threadIdx.x == 0) {
+        elapsed[i] = el;
+        if (rew) rew[i] = r;
+        if (term) term[i] = (uint8_t)t;
+        if (trunc) trunc[i] = (uint8_t)tr;
+        if (succ) succ[i] = (uint8_t)su;
+        if (substeps) substeps[i] = ns;
+    }
 }
 
-__global__ void __launch_bounds__(WAVE) k_substep(const Scene* sc, double* S, int n) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(TEAM, 1) k_substep(const Scene* sc, double* S, double* ws, int n) {
+    __shared__ Shared sh;
+    const int i = blockIdx.x;
     if (i >= n) return;
-    Env e;
-    e.sc = sc;
-    env_load(e, S, n, i);
-    RowSet rs;
-    substep(e, rs);
-    env_store(e, S, n, i);
+    double* Si = S + (size_t)i * UG_STATE_DIM;
+    team_load(sh, Si);
+    team_substep(sh, sc, ws + (size_t)i * WS_DOUBLES);
+    team_store(sh, Si);
 }
 
-__global__ void __launch_bounds__(WAVE) k_link_state(const Scene* sc, const double* S, int n, int link, double* out) {
+// getLinkState / calculateInverseKinematics queries: one env per lane (not on the step path)
+__global__ void __launch_bounds__(WAVE) k_link_state(const double* S, int n, int link, double* out) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     double q[NB];
-    for (int j = 0; j < NB; j++) q[j] = S[(size_t)(UG_F_Q + j) * n + i];
-    Kin k;
-    fk(q, k);
-    m3 R;
+    for (int j = 0; j < NB; j++) q[j] = S[(size_t)i * UG_STATE_DIM + UG_F_Q + j];
     v3 p;
-    link_frame(k, link, 1, R, p);
-    q4 o = mquat(R);
+    q4 o;
+    link_state_of(q, link, p, o);
     double* r = out + (size_t)i * 7;
     r[0] = p.x; r[1] = p.y; r[2] = p.z; r[3] = o.x; r[4] = o.y; r[5] = o.z; r[6] = o.w;
 }
 
-__global__ void __launch_bounds__(WAVE) k_ik(const Scene* sc, const double* S, int n, const double* target, double* qout) {
+__global__ void __launch_bounds__(WAVE) k_ik(const double* S, int n, const double* target, double* qout) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     double q[NB], qo[NB];
-    for (int j = 0; j < NB; j++) q[j] = S[(size_t)(UG_F_Q + j) * n + i];
+    for (int j = 0; j < NB; j++) q[j] = S[(size_t)i * UG_STATE_DIM + UG_F_Q + j];
     const double* t = target + (size_t)i * 7;
     ik_solve(q, V(t[0], t[1], t[2]), Q(t[3], t[4], t[5], t[6]), qo);
     for (int j = 0; j < NB; j++) qout[(size_t)i * NB + j] = qo[j];
-}
-
-// AoS <-> SoA transposes for get/set_state
-__global__ void k_soa_to_aos(const double* S, double* out, int n) {
-    size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    size_t tot = (size_t)n * UG_STATE_DIM;
-    if (idx >= tot) return;
-    int i = (int)(idx / UG_STATE_DIM), f = (int)(idx % UG_STATE_DIM);
-    out[idx] = S[(size_t)f * n + i];
-}
-__global__ void k_aos_to_soa(const double* in, double* S, int n) {
-    size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    size_t tot = (size_t)n * UG_STATE_DIM;
-    if (idx >= tot) return;
-    int i = (int)(idx / UG_STATE_DIM), f = (int)(idx % UG_STATE_DIM);
-    S[(size_t)f * n + i] = in[idx];
 }
 
 // ---------------------------------------------------------------------------
@@ -257,6 +242,7 @@ struct urgym_handle {
     hipStream_t stream = nullptr;
     Scene* d_scene = nullptr;
     double* d_state = nullptr;
+    double* d_ws = nullptr;
     uint32_t* d_mt = nullptr;
     int* d_elapsed = nullptr;
     // staging for the host-pointer API
@@ -318,12 +304,13 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     HIPCHK(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     HIPCHK(h, hipEventCreate(&h->ev0));
     HIPCHK(h, hipEventCreate(&h->ev1));
-    // deep per-lane call chains keep their arrays in scratch: raise the stack limit
-    HIPCHK(h, hipDeviceSetLimit(hipLimitStackSize, 64 * 1024));
+    // lane-serial helpers (dynamics, IK) keep their arrays in scratch
+    HIPCHK(h, hipDeviceSetLimit(hipLimitStackSize, 16 * 1024));
     HIPCHK(h, hipMalloc(&h->d_scene, sizeof(Scene)));
     size_t N = (size_t)n;
     HIPCHK(h, hipMalloc(&h->d_state, sizeof(double) * UG_STATE_DIM * N));
     HIPCHK(h, hipMalloc(&h->d_mt, sizeof(uint32_t) * UG_MT_WORDS * N));
+    HIPCHK(h, hipMalloc(&h->d_ws, sizeof(double) * WS_DOUBLES * N));
     HIPCHK(h, hipMalloc(&h->d_elapsed, sizeof(int) * N));
     HIPCHK(h, hipMalloc(&h->d_act, sizeof(float) * 9 * N));
     HIPCHK(h, hipMalloc(&h->d_obs, sizeof(double) * 17 * N));
@@ -338,13 +325,9 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     HIPCHK(h, hipMalloc(&h->d_sub, sizeof(int32_t) * N));
     HIPCHK(h, hipMemsetAsync(h->d_state, 0, sizeof(double) * UG_STATE_DIM * N, h->stream));
     HIPCHK(h, hipMemsetAsync(h->d_elapsed, 0, sizeof(int) * N, h->stream));
-    // per-env MT19937 streams seeded with seed + env_offset + i, stored SoA
+    // per-env MT19937 streams seeded with seed + env_offset + i, UG_MT_WORDS words per env
     std::vector<uint32_t> host(UG_MT_WORDS * N);
-    std::vector<uint32_t> one(UG_MT_WORDS);
-    for (int i = 0; i < n; i++) {
-        mt_seed_host(one.data(), seed + (uint32_t)env_offset + (uint32_t)i);
-        for (int w = 0; w < UG_MT_WORDS; w++) host[(size_t)w * N + i] = one[w];
-    }
+    for (int i = 0; i < n; i++) mt_seed_host(host.data() + (size_t)i * UG_MT_WORDS, seed + (uint32_t)env_offset + (uint32_t)i);
     HIPCHK(h, hipMemcpyAsync(h->d_mt, host.data(), sizeof(uint32_t) * host.size(), hipMemcpyHostToDevice, h->stream));
     k_build_scene<<<1, 1, 0, h->stream>>>(h->d_scene, task);
     HIPCHK(h, hipGetLastError());
@@ -373,7 +356,7 @@ void urgym_destroy(urgym_handle* h) {
     if (!h) return;
     hipSetDevice(h->dev);
     if (h->stream) hipStreamSynchronize(h->stream);
-    void* ptrs[] = {h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->d_act, h->d_obs, h->d_final, h->d_rew,
+    void* ptrs[] = {h->d_scene, h->d_state, h->d_ws, h->d_mt, h->d_elapsed, h->d_act, h->d_obs, h->d_final, h->d_rew,
                     h->d_draws, h->d_aux, h->d_term, h->d_trunc, h->d_succ, h->d_mask, h->d_sub};
     for (void* p : ptrs)
         if (p) hipFree(p);
@@ -408,8 +391,8 @@ int urgym_reset_device(urgym_handle* h, const uint8_t* d_mask, const double* d_d
     if (!h) return -1;
     HIPCHK(h, hipSetDevice(h->dev));
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-    k_reset<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->n, d_mask,
-                                                    d_draws, d_obs, nullptr);
+    k_reset<<<h->n, TEAM, 0, h->stream>>>(h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->d_ws, h->n, d_mask,
+                                           d_draws, d_obs, nullptr);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     h->timed = true;
@@ -440,9 +423,8 @@ int urgym_step_device(urgym_handle* h, const float* d_act, double* d_obs, double
     if (!d_act || !d_obs) return fail(h, "urgym_step_device: actions and obs must not be NULL");
     HIPCHK(h, hipSetDevice(h->dev));
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-    k_step<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->n, d_act, d_obs,
-                                                   d_final, d_rew, d_term, d_trunc, d_succ, d_sub, h->autoreset,
-                                                   h->max_steps);
+    k_step<<<h->n, TEAM, 0, h->stream>>>(h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->d_ws, h->n, d_act, d_obs,
+                                          d_final, d_rew, d_term, d_trunc, d_succ, d_sub, h->autoreset, h->max_steps);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     h->timed = true;
@@ -477,9 +459,7 @@ int urgym_get_state(urgym_handle* h, double* state) {
     if (!h || !state) return -1;
     size_t tot = (size_t)h->n * UG_STATE_DIM;
     HIPCHK(h, hipSetDevice(h->dev));
-    k_soa_to_aos<<<(unsigned)((tot + 255) / 256), 256, 0, h->stream>>>(h->d_state, h->d_aux, h->n);
-    HIPCHK(h, hipGetLastError());
-    HIPCHK(h, hipMemcpyAsync(state, h->d_aux, sizeof(double) * tot, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipMemcpyAsync(state, h->d_state, sizeof(double) * tot, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
 }
@@ -488,9 +468,7 @@ int urgym_set_state(urgym_handle* h, const double* state) {
     if (!h || !state) return -1;
     size_t tot = (size_t)h->n * UG_STATE_DIM;
     HIPCHK(h, hipSetDevice(h->dev));
-    HIPCHK(h, hipMemcpyAsync(h->d_aux, state, sizeof(double) * tot, hipMemcpyHostToDevice, h->stream));
-    k_aos_to_soa<<<(unsigned)((tot + 255) / 256), 256, 0, h->stream>>>(h->d_aux, h->d_state, h->n);
-    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipMemcpyAsync(h->d_state, state, sizeof(double) * tot, hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
 }
@@ -498,7 +476,7 @@ int urgym_set_state(urgym_handle* h, const double* state) {
 int urgym_substep(urgym_handle* h) {
     if (!h) return -1;
     HIPCHK(h, hipSetDevice(h->dev));
-    k_substep<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_scene, h->d_state, h->n);
+    k_substep<<<h->n, TEAM, 0, h->stream>>>(h->d_scene, h->d_state, h->d_ws, h->n);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
@@ -508,7 +486,7 @@ int urgym_link_state(urgym_handle* h, int link, double* out) {
     if (!h || !out) return -1;
     if (link < 0 || link >= UG_NL) return fail(h, "urgym_link_state: link out of range");
     HIPCHK(h, hipSetDevice(h->dev));
-    k_link_state<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_scene, h->d_state, h->n, link, h->d_aux);
+    k_link_state<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_state, h->n, link, h->d_aux);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipMemcpyAsync(out, h->d_aux, sizeof(double) * 7 * h->n, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -522,7 +500,7 @@ int urgym_ik(urgym_handle* h, const double* target, double* q_out) {
     double* d_t = h->d_aux;
     double* d_q = h->d_aux + 7 * N;
     HIPCHK(h, hipMemcpyAsync(d_t, target, sizeof(double) * 7 * N, hipMemcpyHostToDevice, h->stream));
-    k_ik<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_scene, h->d_state, h->n, d_t, d_q);
+    k_ik<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_state, h->n, d_t, d_q);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipMemcpyAsync(q_out, d_q, sizeof(double) * NB * N, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));

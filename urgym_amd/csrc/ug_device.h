@@ -1,9 +1,8 @@
-/* ug_device.h -- gfx950 device code of the URGym hot path (one env per lane).
- *
- * Each lane owns one environment for a whole env-step: it loads the env's
- * state from the structure-of-arrays buffer (UG layout, coalesced across the
- * wavefront), runs move_ee -> wait_until_stable -> reward (and an autoreset
- * when the episode ends) entirely on-chip, and stores the state once.
+/* ug_device.h -- gfx950 device building blocks of the URGym hot path: vector /
+ * quaternion algebra, MT19937, scene tables, forward kinematics, CRBA/RNEA
+ * robot dynamics, LDL^T, per-pair narrowphases, persistent-manifold update,
+ * damped-least-squares IK.  They are lane-serial functions; ug_team.h
+ * composes them into the one-wavefront-per-env kernel.
  * Model constants (UR5/Robotiq tree, hulls) sit in __constant__ memory and
  * are wave-uniform (scalar loads).  Arithmetic follows the CPU restatement
  * (oracle/ug_oracle.c) operation for operation, compiled with
@@ -28,7 +27,7 @@
 #define MAXROWS 128
 #define MAXCOL 24
 #define MAXPAIR 96
-#define MAXCAND 64
+#define MAXCAND 8   /* per-lane narrowphases emit <= 4 points */
 
 #define DF __device__ static
 #define DFI __device__ static inline
@@ -237,94 +236,6 @@ struct Scene {
 struct CPoint { v3 lpA, lpB, n; double dist, imp, imp1, imp2; };
 struct Manifold { int pair, npts; CPoint pt[4]; };
 
-struct Env {
-    const Scene* sc;
-    double q[NB], qd[NB];
-    double mtarget[7];
-    int mon[7];
-    int oactive[MAXOBJ];
-    v3 opos[MAXOBJ];
-    q4 oquat[MAXOBJ];
-    v3 ov[MAXOBJ], ow[MAXOBJ];
-    int nman;
-    Manifold man[MAXMAN];
-    int goal_approached, goal_grasped, overflow;
-};
-
-/* SoA <-> lane-private state */
-DF void env_load(Env& e, const double* S, int n, int i) {
-#define LD(f) S[(size_t)(f) * n + i]
-    for (int j = 0; j < NB; j++) e.q[j] = LD(UG_F_Q + j);
-    for (int j = 0; j < NB; j++) e.qd[j] = LD(UG_F_QD + j);
-    for (int j = 0; j < 7; j++) e.mtarget[j] = LD(UG_F_MTARGET + j);
-    for (int j = 0; j < 7; j++) e.mon[j] = (int)LD(UG_F_MON + j);
-    for (int o = 0; o < MAXOBJ; o++) e.oactive[o] = (int)LD(UG_F_OACTIVE + o);
-    for (int o = 0; o < MAXOBJ; o++) {
-        int b = UG_F_OBJ + UG_OBJ_DOUBLES * o;
-        e.opos[o] = V(LD(b), LD(b + 1), LD(b + 2));
-        e.oquat[o] = Q(LD(b + 3), LD(b + 4), LD(b + 5), LD(b + 6));
-        e.ov[o] = V(LD(b + 7), LD(b + 8), LD(b + 9));
-        e.ow[o] = V(LD(b + 10), LD(b + 11), LD(b + 12));
-    }
-    e.nman = (int)LD(UG_F_NMAN);
-    for (int m = 0; m < e.nman; m++) {
-        int b = UG_F_MAN + m * UG_MAN_DOUBLES;
-        Manifold& M = e.man[m];
-        M.pair = (int)LD(b);
-        M.npts = (int)LD(b + 1);
-        for (int p = 0; p < M.npts; p++) {
-            int c = b + 2 + p * UG_PT_DOUBLES;
-            CPoint& P = M.pt[p];
-            P.lpA = V(LD(c), LD(c + 1), LD(c + 2));
-            P.lpB = V(LD(c + 3), LD(c + 4), LD(c + 5));
-            P.n = V(LD(c + 6), LD(c + 7), LD(c + 8));
-            P.dist = LD(c + 9); P.imp = LD(c + 10); P.imp1 = LD(c + 11); P.imp2 = LD(c + 12);
-        }
-    }
-    e.goal_approached = (int)LD(UG_F_TASK);
-    e.goal_grasped = (int)LD(UG_F_TASK + 1);
-    e.overflow = (int)LD(UG_F_TASK + 2);
-#undef LD
-}
-DF void env_store(const Env& e, double* S, int n, int i) {
-#define ST(f, x) S[(size_t)(f) * n + i] = (x)
-    for (int j = 0; j < NB; j++) ST(UG_F_Q + j, e.q[j]);
-    for (int j = 0; j < NB; j++) ST(UG_F_QD + j, e.qd[j]);
-    for (int j = 0; j < 7; j++) ST(UG_F_MTARGET + j, e.mtarget[j]);
-    for (int j = 0; j < 7; j++) ST(UG_F_MON + j, (double)e.mon[j]);
-    for (int o = 0; o < MAXOBJ; o++) ST(UG_F_OACTIVE + o, (double)e.oactive[o]);
-    for (int o = 0; o < MAXOBJ; o++) {
-        int b = UG_F_OBJ + UG_OBJ_DOUBLES * o;
-        ST(b, e.opos[o].x); ST(b + 1, e.opos[o].y); ST(b + 2, e.opos[o].z);
-        ST(b + 3, e.oquat[o].x); ST(b + 4, e.oquat[o].y); ST(b + 5, e.oquat[o].z); ST(b + 6, e.oquat[o].w);
-        ST(b + 7, e.ov[o].x); ST(b + 8, e.ov[o].y); ST(b + 9, e.ov[o].z);
-        ST(b + 10, e.ow[o].x); ST(b + 11, e.ow[o].y); ST(b + 12, e.ow[o].z);
-    }
-    ST(UG_F_NMAN, (double)e.nman);
-    for (int m = 0; m < MAXMAN; m++) {
-        int b = UG_F_MAN + m * UG_MAN_DOUBLES;
-        const Manifold& M = e.man[m];
-        int live = m < e.nman;
-        ST(b, live ? (double)M.pair : -1.0);
-        ST(b + 1, live ? (double)M.npts : 0.0);
-        for (int p = 0; p < 4; p++) {
-            int c = b + 2 + p * UG_PT_DOUBLES;
-            int lp = live && p < M.npts;
-            const CPoint& P = M.pt[p];
-            ST(c, lp ? P.lpA.x : 0.0); ST(c + 1, lp ? P.lpA.y : 0.0); ST(c + 2, lp ? P.lpA.z : 0.0);
-            ST(c + 3, lp ? P.lpB.x : 0.0); ST(c + 4, lp ? P.lpB.y : 0.0); ST(c + 5, lp ? P.lpB.z : 0.0);
-            ST(c + 6, lp ? P.n.x : 0.0); ST(c + 7, lp ? P.n.y : 0.0); ST(c + 8, lp ? P.n.z : 0.0);
-            ST(c + 9, lp ? P.dist : 0.0); ST(c + 10, lp ? P.imp : 0.0);
-            ST(c + 11, lp ? P.imp1 : 0.0); ST(c + 12, lp ? P.imp2 : 0.0);
-        }
-    }
-    ST(UG_F_TASK, (double)e.goal_approached);
-    ST(UG_F_TASK + 1, (double)e.goal_grasped);
-    ST(UG_F_TASK + 2, (double)e.overflow);
-    ST(UG_F_TASK + 3, 0.0);
-#undef ST
-}
-
 /* ---------------- kinematics ---------------- */
 struct Kin {
     m3 R[NB];
@@ -476,13 +387,6 @@ DF void ldlt_solve(const double* A, int n, double* x) {
 struct XF { m3 R; v3 p; };
 DFI v3 xf_apply(const XF& T, v3 x) { return vadd(mv(T.R, x), T.p); }
 DFI v3 xf_inv_apply(const XF& T, v3 x) { return mtv(T.R, vsub(x, T.p)); }
-DF XF owner_xf(const Env& e, const Kin& k, int owner) {
-    XF T;
-    if (owner >= 0) { T.R = k.R[owner]; T.p = k.p[owner]; }
-    else if (owner <= -2 && owner > -100) { int o = -2 - owner; T.R = qmat(e.oquat[o]); T.p = e.opos[o]; }
-    else { T.R = mident(); T.p = V(0, 0, 0); }
-    return T;
-}
 DFI XF shape_xf(const XF& O, const Collider& c) {
     XF T;
     T.R = mm(O.R, c.R);
@@ -802,91 +706,7 @@ DF void nc_box_box(const XF& TA, const Collider& A, const XF& TB, const Collider
     }
 }
 
-DF void reduce4(CandList& L) {
-    if (L.n <= 4) return;
-    Cand sel[4];
-    uint64_t used = 0;
-    int best = 0;
-    for (int i = 1; i < L.n; i++)
-        if (L.c[i].d < L.c[best].d) best = i;
-    sel[0] = L.c[best];
-    used |= 1ull << best;
-    for (int s = 1; s < 4; s++) {
-        int bi = -1;
-        double bd = -1.0;
-        for (int i = 0; i < L.n; i++) {
-            if (used & (1ull << i)) continue;
-            double md = 1e300;
-            for (int t = 0; t < s; t++) {
-                v3 dd = vsub(L.c[i].pB, sel[t].pB);
-                double x = vdot(dd, dd);
-                if (x < md) md = x;
-            }
-            if (md > bd) { bd = md; bi = i; }
-        }
-        sel[s] = L.c[bi];
-        used |= 1ull << bi;
-    }
-    for (int s = 0; s < 4; s++) L.c[s] = sel[s];
-    L.n = 4;
-}
-DF void nc_hull_box(const XF& TA, const Collider& A, const XF& TB, const Collider& B, double thr, CandList& out) {
-    m3 RAB = mtm(TB.R, TA.R);
-    v3 pAB = mtv(TB.R, vsub(TA.p, TB.p));
-    v3 h = V(B.half[0], B.half[1], B.half[2]);
-    double mA = A.margin;
-    CandList L;
-    L.n = 0;
-    for (int i = 0; i < A.nv; i++) {
-        const double* vv = &UG_HULL_V[3 * (A.v0 + i)];
-        v3 x = vadd(mv(RAB, V(vv[0], vv[1], vv[2])), pAB);
-        v3 d = V(ug_fabs(x.x) - h.x, ug_fabs(x.y) - h.y, ug_fabs(x.z) - h.z);
-        double dist;
-        v3 nl, pl;
-        if (d.x < 0 && d.y < 0 && d.z < 0) {
-            int kk = 0;
-            double dm = d.x;
-            if (d.y > dm) { dm = d.y; kk = 1; }
-            if (d.z > dm) { dm = d.z; kk = 2; }
-            dist = dm;
-            double sg = vget(x, kk) < 0 ? -1.0 : 1.0;
-            nl = V(0, 0, 0); vsetc(nl, kk, sg);
-            pl = x; vsetc(pl, kk, sg * vget(h, kk));
-        } else {
-            v3 q = V(ug_max(-h.x, ug_min(h.x, x.x)), ug_max(-h.y, ug_min(h.y, x.y)), ug_max(-h.z, ug_min(h.z, x.z)));
-            v3 df = vsub(x, q);
-            double dl = vlen(df);
-            if (dl - mA >= thr) continue;
-            dist = dl;
-            nl = vscale(df, 1.0 / dl);
-            pl = q;
-        }
-        double depth = dist - mA;
-        if (depth < thr) cand_add(L, mv(TB.R, nl), xf_apply(TB, pl), depth);
-    }
-    m3 RBA = mtm(TA.R, TB.R);
-    v3 pBA = mtv(TA.R, vsub(TB.p, TA.p));
-    for (int c = 0; c < 8; c++) {
-        v3 cl = V((c & 1) ? h.x : -h.x, (c & 2) ? h.y : -h.y, (c & 4) ? h.z : -h.z);
-        v3 y = vadd(mv(RBA, cl), pBA);
-        double smax = -1e300;
-        int fm = -1;
-        for (int f = 0; f < A.nf; f++) {
-            const double* F = &UG_HULL_F[4 * (A.f0 + f)];
-            double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
-            if (sd > smax) { smax = sd; fm = f; }
-            if (sd - mA >= thr) break;
-        }
-        double depth = smax - mA;
-        if (depth < thr) {
-            const double* F = &UG_HULL_F[4 * (A.f0 + fm)];
-            v3 nw = mv(TA.R, V(F[0], F[1], F[2]));
-            cand_add(L, vneg(nw), xf_apply(TB, cl), depth);
-        }
-    }
-    reduce4(L);
-    for (int i = 0; i < L.n; i++) cand_add(out, L.c[i].n, L.c[i].pB, L.c[i].d);
-}
+/* hull (robot link) vs box: cooperative, one wavefront per pair -- ug_team.h team_hull_box */
 DF void nc_hull_sphere(const XF& TA, const Collider& A, const XF& TB, const Collider& B, double thr, CandList& out) {
     v3 y = mtv(TA.R, vsub(TB.p, TA.p));
     double r = B.half[0];
@@ -970,461 +790,13 @@ DF void manifold_refresh(Manifold& M, const XF& TA, const XF& TB, double thr) {
         }
     }
 }
-DFI int collider_active(const Env& e, const Collider& c) {
-    if (c.owner <= -2 && c.owner > -100) return e.oactive[-2 - c.owner];
-    return 1;
-}
-DF void collide(Env& e, const Kin& k) {
-    const Scene* s = e.sc;
-    XF O[MAXCOL];
-    v3 lo[MAXCOL], hi[MAXCOL];
-    for (int i = 0; i < s->ncol; i++) {
-        const Collider& c = s->col[i];
-        O[i] = owner_xf(e, k, c.owner);
-        world_aabb(O[i], c, lo[i], hi[i]);
-        lo[i] = vsub(lo[i], V(UG_AABB_PAD, UG_AABB_PAD, UG_AABB_PAD));
-        hi[i] = vadd(hi[i], V(UG_AABB_PAD, UG_AABB_PAD, UG_AABB_PAD));
-    }
-    for (int p = 0; p < s->npair; p++) {
-        const PairDef& P = s->pair[p];
-        int a = P.a, b = P.b;
-        int slot = -1;
-        for (int m = 0; m < e.nman; m++)
-            if (e.man[m].pair == p) { slot = m; break; }
-        int ov = collider_active(e, s->col[a]) && collider_active(e, s->col[b]) &&
-                 !(lo[a].x > hi[b].x || hi[a].x < lo[b].x || lo[a].y > hi[b].y || hi[a].y < lo[b].y ||
-                   lo[a].z > hi[b].z || hi[a].z < lo[b].z);
-        if (!ov) {
-            if (slot >= 0) {
-                int last = e.nman - 1;
-                if (slot != last) e.man[slot] = e.man[last];
-                e.nman--;
-            }
-            continue;
-        }
-        const Collider& A = s->col[a];
-        const Collider& B = s->col[b];
-        XF TA = shape_xf(O[a], A), TB = shape_xf(O[b], B);
-        CandList L;
-        L.n = 0;
-        if (A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_BOX) nc_sphere_box(TA, A, TB, B, P.thr, L);
-        else if (A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_SPHERE) nc_sphere_sphere(TA, A, TB, B, P.thr, L);
-        else if (A.kind == UG_SHAPE_BOX && B.kind == UG_SHAPE_BOX) nc_box_box(TA, A, TB, B, P.thr, L);
-        else if (A.kind == UG_SHAPE_HULL && B.kind == UG_SHAPE_BOX) nc_hull_box(TA, A, TB, B, P.thr, L);
-        else if (A.kind == UG_SHAPE_HULL && B.kind == UG_SHAPE_SPHERE) nc_hull_sphere(TA, A, TB, B, P.thr, L);
-        else if (A.kind == UG_SHAPE_BOX && B.kind == UG_SHAPE_SPHERE) {
-            CandList L2;
-            L2.n = 0;
-            nc_sphere_box(TB, B, TA, A, P.thr, L2);
-            for (int i = 0; i < L2.n; i++)
-                cand_add(L, vneg(L2.c[i].n), vadd(L2.c[i].pB, vscale(L2.c[i].n, L2.c[i].d)), L2.c[i].d);
-        }
-        if (slot < 0) {
-            if (L.n == 0) continue;
-            if (e.nman >= MAXMAN) { e.overflow++; continue; }
-            slot = e.nman++;
-            e.man[slot].pair = p;
-            e.man[slot].npts = 0;
-        }
-        Manifold& M = e.man[slot];
-        for (int i = 0; i < L.n; i++) manifold_add(M, O[a], O[b], L.c[i], P.thr);
-        if (M.npts) manifold_refresh(M, O[a], O[b], P.thr);
-        if (M.npts == 0) {
-            int last = e.nman - 1;
-            if (slot != last) e.man[slot] = e.man[last];
-            e.nman--;
-        }
-    }
-}
-
-/* ---------------- constraint rows + PGS ---------------- */
-struct Row {
-    int entA, entB;
-    double JA[NB], MiJA[NB];
-    double JB[NB], MiJB[NB];
-    double invD, rhs, rhsPen, lo, hi, imp, impPen, fric;
-    int man, pt, kind, nrow;
-};
-struct RowSet {
-    int n, nnc, nn, nf;
-    Row r[MAXROWS];
-    int idx_nc[MAXROWS], idx_n[MAXROWS], idx_f[MAXROWS];
-};
-DFI int ent_dofs(int ent) { return ent == 0 ? NB : 6; }
-DFI int ent_off(int ent) { return ent == 0 ? 0 : NB + 6 * (ent - 1); }
-DFI double ent_dot(int ent, const double* J, const double* v) {
-    int n = ent_dofs(ent), o = ent_off(ent);
-    double s = 0.0;
-    for (int i = 0; i < n; i++) s += J[i] * v[o + i];
-    return s;
-}
-DFI double ent_dot_local(int ent, const double* a, const double* b) {
-    int n = ent_dofs(ent);
-    double s = 0.0;
-    for (int i = 0; i < n; i++) s += a[i] * b[i];
-    return s;
-}
-DFI void ent_axpy(int ent, const double* MiJ, double a, double* v) {
-    int n = ent_dofs(ent), o = ent_off(ent);
-    for (int i = 0; i < n; i++) v[o + i] += MiJ[i] * a;
-}
-DFI void row_clear(Row& r) {
-    for (int i = 0; i < NB; i++) { r.JA[i] = 0.0; r.MiJA[i] = 0.0; r.JB[i] = 0.0; r.MiJB[i] = 0.0; }
-    r.entA = r.entB = -1;
-    r.invD = r.rhs = r.rhsPen = r.lo = r.hi = r.imp = r.impPen = r.fric = 0.0;
-    r.man = r.pt = r.kind = r.nrow = 0;
-}
-DF void point_jac(const Env& e, const Kin& k, int ent, int body, v3 p, v3 d, double* J, double* MiJ, const double* LDL) {
-    if (ent == 0) {
-        for (int i = 0; i < NB; i++) {
-            J[i] = moves(i, body) ? vdot(d, vcross(k.a[i], vsub(p, k.p[i]))) : 0.0;
-            MiJ[i] = J[i];
-        }
-        ldlt_solve(LDL, NB, MiJ);
-    } else {
-        int o = ent - 1;
-        v3 r = vsub(p, e.opos[o]);
-        v3 rn = vcross(r, d);
-        J[0] = d.x; J[1] = d.y; J[2] = d.z; J[3] = rn.x; J[4] = rn.y; J[5] = rn.z;
-        double im = 1.0 / e.sc->omass[o];
-        m3 R = qmat(e.oquat[o]);
-        v3 ir = mtv(R, rn);
-        ir = V(ir.x / e.sc->oinertia[o].x, ir.y / e.sc->oinertia[o].y, ir.z / e.sc->oinertia[o].z);
-        ir = mv(R, ir);
-        MiJ[0] = d.x * im; MiJ[1] = d.y * im; MiJ[2] = d.z * im; MiJ[3] = ir.x; MiJ[4] = ir.y; MiJ[5] = ir.z;
-    }
-}
-DFI int ent_of_collider(const Collider& c, int& body) {
-    body = -1;
-    if (c.owner >= 0) { body = c.owner; return 0; }
-    if (c.owner == -1) return -1;
-    if (c.owner > -100) return -1 - c.owner;
-    return -1;
-}
-DF void contact_row(const Env& e, const Kin& k, const double* LDL, const double* v0, Row& r, int entA, int bodyA,
-                    int entB, int bodyB, v3 pA, v3 pB, v3 d) {
-    r.entA = entA; r.entB = entB;
-    double dA = 0.0, dB = 0.0;
-    double relv = 0.0;
-    if (entA >= 0) {
-        point_jac(e, k, entA, bodyA, pA, d, r.JA, r.MiJA, LDL);
-        dA = ent_dot_local(entA, r.JA, r.MiJA);
-        relv += ent_dot(entA, r.JA, v0);
-    }
-    if (entB >= 0) {
-        point_jac(e, k, entB, bodyB, pB, vneg(d), r.JB, r.MiJB, LDL);
-        dB = ent_dot_local(entB, r.JB, r.MiJB);
-        relv += ent_dot(entB, r.JB, v0);
-    }
-    double den = dA + dB;
-    r.invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
-    r.rhs = relv;
-}
-DF void build_rows(Env& e, const Kin& k, const double* LDL, const double* v0, RowSet& rs) {
-    rs.n = rs.nnc = rs.nn = rs.nf = 0;
-    const double dt = UG_DT;
-    for (int d = 0; d < NB; d++) {
-        for (int side = 0; side < 2; side++) {
-            double pen = side == 0 ? e.q[d] - UG_DOF_LOWER[d] : UG_DOF_UPPER[d] - e.q[d];
-            if (pen > 0) continue;
-            if (rs.n >= MAXROWS) { e.overflow++; continue; }
-            Row& r = rs.r[rs.n];
-            row_clear(r);
-            r.entA = 0; r.entB = -1;
-            r.JA[d] = side == 0 ? 1.0 : -1.0;
-            for (int i = 0; i < NB; i++) r.MiJA[i] = r.JA[i];
-            ldlt_solve(LDL, NB, r.MiJA);
-            double den = ent_dot_local(0, r.JA, r.MiJA);
-            r.invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
-            double relv = ent_dot(0, r.JA, v0);
-            double erp = (pen > UG_SPLIT_PEN_THR) ? UG_ERP : UG_ERP2;
-            double perr = -pen * erp / dt, verr = -relv;
-            double pimp = perr * r.invD, vimp = verr * r.invD;
-            r.rhs = (pen > UG_SPLIT_PEN_THR) ? pimp + vimp : vimp;
-            r.lo = 0.0; r.hi = UG_LIMIT_MAXIMP;
-            r.kind = 0;
-            rs.idx_nc[rs.nnc++] = rs.n++;
-        }
-    }
-    for (int m = 0; m < 7; m++) {
-        if (!e.mon[m]) continue;
-        int d = m < 6 ? m : UG_FINGER_DOF;
-        double maxImp = UG_DOF_MAXFORCE[d] * dt;
-        if (rs.n >= MAXROWS) { e.overflow++; continue; }
-        Row& r = rs.r[rs.n];
-        row_clear(r);
-        r.entA = 0; r.entB = -1;
-        r.JA[d] = 1.0;
-        for (int i = 0; i < NB; i++) r.MiJA[i] = r.JA[i];
-        ldlt_solve(LDL, NB, r.MiJA);
-        double den = ent_dot_local(0, r.JA, r.MiJA);
-        r.invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
-        double qd = v0[d];
-        double pst = 1.0 * (e.mtarget[m] - e.q[d]) / dt;
-        double verr = 0.0 - qd;
-        double des = UG_MOTOR_KP * pst + qd + UG_MOTOR_KD * verr;
-        double clamp = UG_DOF_MAXVEL[d];
-        if (des > clamp) des = clamp;
-        if (des < -clamp) des = -clamp;
-        double relv = ent_dot(0, r.JA, v0);
-        r.rhs = 0.0 * r.invD + (des - relv) * r.invD;
-        r.lo = -maxImp; r.hi = maxImp;
-        r.kind = 0;
-        rs.idx_nc[rs.nnc++] = rs.n++;
-    }
-    for (int g = 0; g < 5; g++) {
-        if (rs.n >= MAXROWS) { e.overflow++; continue; }
-        int pa = UG_FINGER_DOF, cb = UG_GEAR_CHILD[g];
-        double ratio = UG_GEAR_RATIO[g];
-        Row& r = rs.r[rs.n];
-        row_clear(r);
-        r.entA = 0; r.entB = 0;
-        r.JA[pa] = 1.0;
-        r.JB[cb] = ratio;
-        for (int i = 0; i < NB; i++) { r.MiJA[i] = r.JA[i]; r.MiJB[i] = r.JB[i]; }
-        ldlt_solve(LDL, NB, r.MiJA);
-        ldlt_solve(LDL, NB, r.MiJB);
-        double den = ent_dot_local(0, r.JA, r.MiJA) + ent_dot_local(0, r.JB, r.MiJB);
-        r.invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
-        double relv = ent_dot(0, r.JA, v0) + ent_dot(0, r.JB, v0);
-        double diff = e.q[cb] * ratio + e.q[pa];
-        double pen = -UG_GEAR_ERP * (0.0 - diff);
-        double perr = -pen * UG_ERP / dt, verr = 0.0 - relv;
-        r.rhs = perr * r.invD + verr * r.invD;
-        double maxImp = UG_GEAR_MAXF * dt;
-        r.lo = -maxImp; r.hi = maxImp;
-        r.kind = 0;
-        rs.idx_nc[rs.nnc++] = rs.n++;
-    }
-    const Scene* s = e.sc;
-    for (int m = 0; m < e.nman; m++) {
-        const Manifold& M = e.man[m];
-        const PairDef& P = s->pair[M.pair];
-        int bodyA, bodyB;
-        int entA = ent_of_collider(s->col[P.a], bodyA);
-        int entB = ent_of_collider(s->col[P.b], bodyB);
-        if (entA < 0 && entB < 0) continue;
-        XF OA = owner_xf(e, k, s->col[P.a].owner), OB = owner_xf(e, k, s->col[P.b].owner);
-        for (int j = 0; j < M.npts; j++) {
-            if (rs.n + 3 > MAXROWS) { e.overflow++; continue; }
-            const CPoint& cp = M.pt[j];
-            v3 pA = xf_apply(OA, cp.lpA), pB = xf_apply(OB, cp.lpB);
-            v3 n = cp.n;
-            int ni = rs.n;
-            Row& r = rs.r[ni];
-            row_clear(r);
-            contact_row(e, k, LDL, v0, r, entA, bodyA, entB, bodyB, pA, pB, n);
-            if (r.invD == 0.0) continue;
-            double relv = r.rhs;
-            double pen = cp.dist + UG_LINEAR_SLOP;
-            double rest = 0.0;
-            if (!(ug_fabs(relv) < UG_REST_VEL_THR)) rest = P.restitution * -relv;
-            if (rest <= 0.0) rest = 0.0;
-            double verr = rest - relv, perr;
-            double erp = (pen > UG_SPLIT_PEN_THR) ? UG_ERP : UG_ERP2;
-            if (pen > 0) { perr = 0.0; verr -= pen / UG_DT; }
-            else perr = -pen * erp / UG_DT;
-            double pimp = perr * r.invD, vimp = verr * r.invD;
-            if (pen > UG_SPLIT_PEN_THR) { r.rhs = pimp + vimp; r.rhsPen = 0.0; }
-            else { r.rhs = vimp; r.rhsPen = pimp; }
-            r.lo = 0.0; r.hi = 1e10;
-            r.imp = cp.imp * UG_WARMSTART;
-            r.kind = 1; r.man = m; r.pt = j;
-            rs.idx_n[rs.nn++] = rs.n++;
-            v3 t1, t2;
-            if (ug_fabs(n.z) > 0.7071067811865475244) {
-                double a = n.y * n.y + n.z * n.z, kk = 1.0 / ug_sqrt(a);
-                t1 = V(0, -n.z * kk, n.y * kk);
-                t2 = V(a * kk, -n.x * t1.z, n.x * t1.y);
-            } else {
-                double a = n.x * n.x + n.y * n.y, kk = 1.0 / ug_sqrt(a);
-                t1 = V(-n.y * kk, n.x * kk, 0);
-                t2 = V(-n.z * t1.y, n.z * t1.x, a * kk);
-            }
-            for (int fdir = 0; fdir < 2; fdir++) {
-                Row& f = rs.r[rs.n];
-                row_clear(f);
-                contact_row(e, k, LDL, v0, f, entA, bodyA, entB, bodyB, pA, pB, fdir == 0 ? t1 : t2);
-                double frel = f.rhs;
-                f.rhs = 0.0 * f.invD + (0.0 - frel) * f.invD;
-                f.fric = P.friction;
-                f.lo = 0.0; f.hi = 0.0;
-                f.imp = 0.0;
-                f.kind = 2 + fdir; f.man = m; f.pt = j; f.nrow = ni;
-                rs.idx_f[rs.nf++] = rs.n++;
-            }
-        }
-    }
-}
-DF double solve_row(Row& r, double* dv, int pen) {
-    double imp = pen ? r.impPen : r.imp;
-    double di = (pen ? r.rhsPen : r.rhs) - imp * 0.0;
-    if (r.entA >= 0) di -= ent_dot(r.entA, r.JA, dv) * r.invD;
-    if (r.entB >= 0) di -= ent_dot(r.entB, r.JB, dv) * r.invD;
-    double sum = imp + di;
-    if (sum < r.lo) { di = r.lo - imp; imp = r.lo; }
-    else if (sum > r.hi) { di = r.hi - imp; imp = r.hi; }
-    else imp = sum;
-    if (pen) r.impPen = imp; else r.imp = imp;
-    if (r.entA >= 0) ent_axpy(r.entA, r.MiJA, di, dv);
-    if (r.entB >= 0) ent_axpy(r.entB, r.MiJB, di, dv);
-    return di * (1.0 / r.invD);
-}
-DF void pgs(RowSet& rs, double* dv) {
-    for (int i = 0; i < rs.nn; i++) {
-        Row& r = rs.r[rs.idx_n[i]];
-        if (r.imp != 0.0) {
-            if (r.entA >= 0) ent_axpy(r.entA, r.MiJA, r.imp, dv);
-            if (r.entB >= 0) ent_axpy(r.entB, r.MiJB, r.imp, dv);
-        }
-    }
-    for (int it = 0; it < UG_PGS_ITERS; it++) {
-        double res = 0.0;
-        for (int j = 0; j < rs.nnc; j++) {
-            int idx = (it & 1) ? j : rs.nnc - 1 - j;
-            double x = solve_row(rs.r[rs.idx_nc[idx]], dv, 0);
-            x = x * x;
-            res = res > x ? res : x;
-        }
-        for (int j = 0; j < rs.nn; j++) {
-            double x = solve_row(rs.r[rs.idx_n[j]], dv, 0);
-            x = x * x;
-            res = res > x ? res : x;
-        }
-        for (int j = 0; j < rs.nf; j++) {
-            Row& f = rs.r[rs.idx_f[j]];
-            double tot = rs.r[f.nrow].imp;
-            if (tot > 0.0) {
-                f.lo = -(f.fric * tot);
-                f.hi = f.fric * tot;
-                double x = solve_row(f, dv, 0);
-                x = x * x;
-                res = res > x ? res : x;
-            }
-        }
-        if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
-    }
-}
-DF int pgs_split(RowSet& rs, double* dvs) {
-    int any = 0;
-    for (int j = 0; j < rs.nn; j++)
-        if (rs.r[rs.idx_n[j]].rhsPen != 0.0) any = 1;
-    if (!any) return 0;
-    for (int it = 0; it < UG_PGS_ITERS; it++) {
-        double res = 0.0;
-        for (int j = 0; j < rs.nn; j++) {
-            double x = solve_row(rs.r[rs.idx_n[j]], dvs, 1);
-            x = x * x;
-            res = res > x ? res : x;
-        }
-        if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
-    }
-    return 1;
-}
-
-/* ---------------- one p.stepSimulation() ---------------- */
-DF void substep(Env& e, RowSet& rs) {
-    const double dt = UG_DT;
-    const Scene* s = e.sc;
-    Kin k;
-    fk(e.q, k);
-    collide(e, k);
-    double M[NB * NB], C[NB];
-    robot_dynamics(e.qd, k, s->gravity, M, C);
-    ldlt(M, NB);
-    double qdd[NB];
-    for (int i = 0; i < NB; i++) qdd[i] = -C[i];
-    ldlt_solve(M, NB, qdd);
-    double v0[NV];
-    for (int i = 0; i < NV; i++) v0[i] = 0.0;
-    for (int i = 0; i < NB; i++) { e.qd[i] = e.qd[i] + qdd[i] * dt; v0[i] = e.qd[i]; }
-    for (int o = 0; o < s->nobj; o++) {
-        if (!e.oactive[o]) continue;
-        v3 v = e.ov[o];
-        double vn = vlen(v);
-        v3 a = vsub(V(0, 0, s->gravity), vscale(v, UG_LIN_DAMP + UG_LIN_DAMP * vn));
-        e.ov[o] = vadd(v, vscale(a, dt));
-        m3 R = qmat(e.oquat[o]);
-        v3 wl = mtv(R, e.ow[o]);
-        v3 I = s->oinertia[o];
-        v3 Iw = V(I.x * wl.x, I.y * wl.y, I.z * wl.z);
-        double wn = vlen(wl);
-        v3 z = vadd(vscale(Iw, UG_ANG_DAMP + UG_ANG_DAMP * wn), vcross(wl, Iw));
-        v3 al = V(-z.x / I.x, -z.y / I.y, -z.z / I.z);
-        e.ow[o] = vadd(e.ow[o], vscale(mv(R, al), dt));
-        int off = NB + 6 * o;
-        v0[off] = e.ov[o].x; v0[off + 1] = e.ov[o].y; v0[off + 2] = e.ov[o].z;
-        v0[off + 3] = e.ow[o].x; v0[off + 4] = e.ow[o].y; v0[off + 5] = e.ow[o].z;
-    }
-    build_rows(e, k, M, v0, rs);
-    double dv[NV], dvs[NV];
-    for (int i = 0; i < NV; i++) { dv[i] = 0.0; dvs[i] = 0.0; }
-    pgs(rs, dv);
-    int split = pgs_split(rs, dvs);
-    for (int i = 0; i < rs.nn; i++) {
-        const Row& r = rs.r[rs.idx_n[i]];
-        e.man[r.man].pt[r.pt].imp = r.imp;
-    }
-    for (int i = 0; i < rs.nf; i++) {
-        const Row& r = rs.r[rs.idx_f[i]];
-        if (r.kind == 2) e.man[r.man].pt[r.pt].imp1 = r.imp;
-        else e.man[r.man].pt[r.pt].imp2 = r.imp;
-    }
-    for (int i = 0; i < NB; i++) {
-        e.qd[i] = e.qd[i] + dv[i];
-        double vi = split ? e.qd[i] + dvs[i] : e.qd[i];
-        e.q[i] = e.q[i] + vi * dt;
-    }
-    for (int o = 0; o < s->nobj; o++) {
-        if (!e.oactive[o]) continue;
-        int off = NB + 6 * o;
-        e.ov[o] = vadd(e.ov[o], V(dv[off], dv[off + 1], dv[off + 2]));
-        e.ow[o] = vadd(e.ow[o], V(dv[off + 3], dv[off + 4], dv[off + 5]));
-        v3 vl = e.ov[o], wa = e.ow[o];
-        if (split) {
-            vl = vadd(vl, V(dvs[off], dvs[off + 1], dvs[off + 2]));
-            wa = vadd(wa, V(dvs[off + 3], dvs[off + 4], dvs[off + 5]));
-        }
-        e.opos[o] = vadd(e.opos[o], vscale(vl, dt));
-        double ang = vlen(wa);
-        if (ang * dt > UG_ANGULAR_MOTION_THR) ang = UG_ANGULAR_MOTION_THR / dt;
-        v3 ax;
-        if (ang < 0.001) ax = vscale(wa, 0.5 * dt - (dt * dt * dt) * 0.020833333333 * ang * ang);
-        else ax = vscale(wa, ug_sin(0.5 * ang * dt) / ang);
-        q4 dq = Q(ax.x, ax.y, ax.z, ug_cos(0.5 * ang * dt));
-        e.oquat[o] = qnormalize(qmul(dq, e.oquat[o]));
-    }
-}
-
-/* ---------------- robot control layer (robot.py) ---------------- */
+/* ---------------- robot control helpers (robot.py) ---------------- */
 DFI double np_sum12(const double* a) {
     double r = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     for (int i = 8; i < 12; i++) r += a[i];
     return r;
 }
-DF int wait_until_stable(Env& e, RowSet& rs) {
-    double pos[NB];
-    for (int j = 0; j < NB; j++) pos[j] = e.q[j];
-    for (int i = 0; i < UG_STABLE_STEPS; i++) {
-        substep(e, rs);
-        double a[NB];
-        for (int j = 0; j < NB; j++) a[j] = ug_fabs(pos[j] - e.q[j]);
-        if (np_sum12(a) < UG_STABLE_EPS) return i + 1;
-        for (int j = 0; j < NB; j++) pos[j] = e.q[j];
-    }
-    return UG_STABLE_STEPS;
-}
 DFI double gripper_angle(double L) { return 0.715 - ug_asin((L - 0.010) / 0.1143); }
-DFI void open_gripper(Env& e, double pct) {
-    double L = UG_GRIP_MIN + (UG_GRIP_MAX - UG_GRIP_MIN) * (pct / 100.0);
-    e.mtarget[6] = gripper_angle(L);
-    e.mon[6] = 1;
-}
-DFI void close_gripper(Env& e, double pct) {
-    double L = UG_GRIP_MAX - (UG_GRIP_MAX - UG_GRIP_MIN) * (pct / 100.0);
-    e.mtarget[6] = gripper_angle(L);
-    e.mon[6] = 1;
-}
 DF void ik_solve(const double* q0, v3 tp, q4 to, double* qout) {
     double q[NB];
     for (int i = 0; i < NB; i++) q[i] = q0[i];
@@ -1482,132 +854,6 @@ DF void ik_solve(const double* q0, v3 tp, q4 to, double* qout) {
         for (int i = 0; i < 6; i++) q[i] = rhs[i] + q[i];
     }
     for (int i = 0; i < NB; i++) qout[i] = q[i];
-}
-DF void move_ee_end(Env& e, v3 pos, q4 orn) {
-    double qt[NB];
-    ik_solve(e.q, pos, orn, qt);
-    for (int i = 0; i < 6; i++) { e.mtarget[i] = qt[i]; e.mon[i] = 1; }
-}
-DF void link_state(const Env& e, int l, v3& p, q4& o) {
-    Kin k;
-    fk(e.q, k);
-    m3 R;
-    link_frame(k, l, 1, R, p);
-    o = mquat(R);
-}
-DF v3 gripper_center(const Env& e) {
-    Kin k;
-    fk(e.q, k);
-    v3 lo = V(1e300, 1e300, 1e300), hi = V(-1e300, -1e300, -1e300);
-    for (int i = 0; i < 2; i++) {
-        int l = i == 0 ? 11 : 16;
-        m3 R;
-        v3 p;
-        link_frame(k, l, 1, R, p);
-        v3 c = vadd(mv(R, V(UG_LINK_AABB_C[3 * l], UG_LINK_AABB_C[3 * l + 1], UG_LINK_AABB_C[3 * l + 2])), p);
-        v3 h = V(UG_LINK_AABB_H[3 * l], UG_LINK_AABB_H[3 * l + 1], UG_LINK_AABB_H[3 * l + 2]);
-        const double* r = R.m;
-        v3 ext = V(ug_fabs(r[0]) * h.x + ug_fabs(r[1]) * h.y + ug_fabs(r[2]) * h.z,
-                   ug_fabs(r[3]) * h.x + ug_fabs(r[4]) * h.y + ug_fabs(r[5]) * h.z,
-                   ug_fabs(r[6]) * h.x + ug_fabs(r[7]) * h.y + ug_fabs(r[8]) * h.z);
-        v3 mn = vsub(c, ext), mx = vadd(c, ext);
-        lo = V(ug_min(lo.x, mn.x), ug_min(lo.y, mn.y), ug_min(lo.z, mn.z));
-        hi = V(ug_max(hi.x, mx.x), ug_max(hi.y, mx.y), ug_max(hi.z, mx.z));
-    }
-    return V((hi.x + lo.x) / 2.0, (hi.y + lo.y) / 2.0, (hi.z + lo.z) / 2.0);
-}
-DF void remove_object(Env& e, int o) {
-    e.oactive[o] = 0;
-    int ci = e.sc->ocol[o];
-    for (int m = e.nman - 1; m >= 0; m--) {
-        const PairDef& P = e.sc->pair[e.man[m].pair];
-        if (P.a == ci || P.b == ci) {
-            int last = e.nman - 1;
-            if (m != last) e.man[m] = e.man[last];
-            e.nman--;
-        }
-    }
-}
-DFI void place_object(Env& e, int o, v3 pos, q4 orn) {
-    e.oactive[o] = 1;
-    e.opos[o] = pos;
-    e.oquat[o] = orn;
-    e.ov[o] = V(0, 0, 0);
-    e.ow[o] = V(0, 0, 0);
-}
-DF int robot_reset(Env& e, RowSet& rs) {
-    for (int i = 0; i < 6; i++) { e.q[i] = UG_ARM_REST[i]; e.qd[i] = 0.0; }
-    for (int i = 0; i < 10; i++) substep(e, rs);
-    open_gripper(e, 100.0);
-    return 10;
-}
-
-/* ---------------- tasks ---------------- */
-/* draws: source of random.random() values for resets: device MT19937 or caller-supplied */
-struct Draws {
-    const Rng* rng;
-    const double* given;  /* n x ndraw or null */
-    int k;
-    __device__ double next() { return given ? given[k++] : mt_random(*rng); }
-};
-DFI double uniform(Draws& d, double a, double b) { return a + (b - a) * d.next(); }
-
-DF void bb_obs(const Env& e, double* obs) {
-    v3 eu = euler_from_quat(e.oquat[0]);
-    obs[0] = eu.x; obs[1] = eu.y; obs[2] = eu.z;
-    obs[3] = e.opos[0].x - e.opos[1].x;
-    obs[4] = e.opos[0].y - e.opos[1].y;
-    obs[5] = e.opos[0].z - e.opos[1].z;
-}
-/* create_ball (env_ball_balance_v0.py:186-205) */
-DF v3 bb_ball_position(Draws& dr, v3 paddle) {
-    v3 bp = V(paddle.x, paddle.y, paddle.z + 0.2 + UG_BB_BALL_R);
-    bp.x += uniform(dr, -0.03, 0.03);
-    bp.y += uniform(dr, -0.08, 0.02);
-    return bp;
-}
-DF int bb_reset(Env& e, RowSet& rs, Draws& dr, double* obs) {
-    int n = robot_reset(e, rs);
-    remove_object(e, 0);
-    remove_object(e, 1);
-    move_ee_end(e, V(0.0, -0.60, 0.60), Q(0.50, -0.50, -0.50, 0.50));
-    open_gripper(e, 20.0);
-    n += wait_until_stable(e, rs);
-    v3 pe;
-    q4 oe;
-    link_state(e, UG_EE_LINK, pe, oe);
-    v3 gc = gripper_center(e);
-    v3 pose = V(pe.x, pe.y - 0.2, gc.z);
-    place_object(e, 0, pose, Q(0, 0, 0, 1));
-    place_object(e, 1, bb_ball_position(dr, pose), e.oquat[0]);
-    close_gripper(e, 100.0);
-    n += wait_until_stable(e, rs);
-    bb_obs(e, obs);
-    return n;
-}
-DF int bb_step(Env& e, RowSet& rs, const float* a, double* obs, double* rew, int* term, int* succ) {
-    v3 pe;
-    q4 oe;
-    link_state(e, UG_EE_LINK, pe, oe);
-    v3 eu = euler_from_quat(oe);
-    eu.x += (double)a[0]; eu.y += (double)a[1]; eu.z += (double)a[2];
-    q4 qn = quat_from_euler(eu);
-    move_ee_end(e, pe, qn);
-    int n = wait_until_stable(e, rs);
-    *rew = 1.0;
-    *term = e.opos[1].z < e.opos[0].z;
-    *succ = 0;
-    bb_obs(e, obs);
-    return n;
-}
-DF int task_reset(Env& e, RowSet& rs, Draws& dr, double* obs) {
-    e.goal_approached = e.goal_grasped = 0;
-    if (e.sc->task == UG_TASK_BALLBALANCE) return bb_reset(e, rs, dr, obs);
-    return 0;
-}
-DF int task_step(Env& e, RowSet& rs, const float* a, double* obs, double* rew, int* term, int* succ) {
-    if (e.sc->task == UG_TASK_BALLBALANCE) return bb_step(e, rs, a, obs, rew, term, succ);
-    return 0;
 }
 
 }  // namespace ugd

@@ -1,11 +1,11 @@
 /* ug_layout.h -- per-environment state layout of the MI355X simulator.
  *
- * Device memory holds every field structure-of-arrays: field f of env i lives
- * at state[f * n_envs + i] (FP64), so a wavefront loading one field touches
- * 64 consecutive doubles (512 B, fully coalesced).  urgym_get_state /
- * urgym_set_state exchange the same fields per env (array-of-structs,
- * UG_STATE_DIM doubles per env) -- the canonical layout also used by the CPU
- * restatement's ugo_get_state, so parity tests compare states directly.
+ * Device memory holds one contiguous record of UG_STATE_DIM doubles per env
+ * (array-of-structs): the wavefront that owns env i copies state[i * DIM ..]
+ * into LDS with 64-lane coalesced loads at kernel start and back at the end.
+ * urgym_get_state / urgym_set_state exchange exactly these records -- the
+ * canonical layout also used by the CPU restatement's ugo_get_state, so parity
+ * tests compare states directly.
  */
 #ifndef UG_LAYOUT_H
 #define UG_LAYOUT_H
@@ -28,6 +28,6 @@
 #define UG_F_TASK (UG_F_MAN + UG_MAXMAN * UG_MAN_DOUBLES)   /* approached, grasped, overflow, spare */
 #define UG_STATE_DIM (UG_F_TASK + 4)
 
-#define UG_MT_WORDS 625      /* MT19937 state (624) + index, uint32 SoA */
+#define UG_MT_WORDS 625      /* MT19937 state (624) + index, uint32, contiguous per env */
 
 #endif

@@ -1,0 +1,1020 @@
+/* ug_team.h -- one wavefront per environment ("team") implementation of the hot path.
+ *
+ * Why: the env-step is a long sequential chain (<=480 substeps, each a projected
+ * Gauss-Seidel over ~90 constraint rows x 50 iterations).  One env per lane left
+ * the PGS rows (48 doubles each) streaming through scratch and used 64 of the
+ * chip's 1024 SIMDs at 4096 envs.  Here a 64-lane wavefront owns one env:
+ *
+ *  - the env state (canonical layout, ug_layout.h) lives in LDS for the whole launch;
+ *  - collision: lane per collider (transforms, AABBs), lane per pair (broadphase,
+ *    box/sphere narrowphase, manifold update), the whole wave per hull-box pair
+ *    (lane per hull vertex, 8 lanes per box corner over the hull's face planes,
+ *    wave-wide arg-min/arg-max for the 4-point reduction);
+ *  - constraint rows: lane per row (Jacobian, M^-1 J^T, rhs), staged through LDS;
+ *  - PGS: row p lives in the VGPRs of half (p & 1) of the wave (lane d holds
+ *    J[d], M^-1J[d] of that row, d = dof slot 0..31), the velocity delta is
+ *    replicated in both halves; a row update is a 16-lane DPP tree reduction,
+ *    two readlanes, the clamp, and a permlane32 broadcast of M^-1J * delta;
+ *  - the remaining sequential pieces (FK, CRBA/RNEA/LDL^T, IK, integration,
+ *    task glue) run on lane 0 with their data in LDS.
+ * Arithmetic order is that of oracle/ug_oracle.c (the pairwise tree of the DPP
+ * reduction included), so results stay bit-identical to the CPU restatement.
+ */
+#ifndef UG_TEAM_H
+#define UG_TEAM_H
+
+#include "ug_device.h"
+
+namespace ugd {
+
+#define TEAM 64
+#define NVP 32
+#define NSLOT (MAXROWS / 2)
+#define STAGE 24
+#define MAXOV 40
+
+/* ---------------- env state (canonical layout) ---------------- */
+struct StObj { v3 pos; q4 quat; v3 v, w; };
+struct StPt { v3 lpA, lpB, n; double dist, imp, imp1, imp2; };
+struct StMan { double pair, npts; StPt pt[4]; };
+struct EnvState {
+    double q[NB], qd[NB], mtarget[7], mon[7], oactive[MAXOBJ];
+    StObj obj[MAXOBJ];
+    double nman;
+    StMan man[MAXMAN];
+    double goal_approached, goal_grasped, overflow, spare;
+};
+static_assert(sizeof(EnvState) == UG_STATE_DIM * sizeof(double), "EnvState must match ug_layout.h");
+
+struct RowS {
+    double invD, rinv, rhs, rhsPen, lo, hi, imp, impPen, fric; /* rinv = invD == 0 ? 0 : 1 / invD */
+    int kind; /* 0 limit, 1 motor, 2 gear, 3 normal, 4/5 friction dir 1/2 */
+    int a, b; /* limit: dof, side | motor: m | gear: g | contact: manifold, point */
+    int nrow; /* friction: position of its normal row */
+};
+
+struct Shared {
+    EnvState e;
+    Kin kin;
+    double LDL[NB * NB];
+    double v0[NVP];
+    double dvout[NVP], dvsout[NVP];
+    XF O[MAXCOL];
+    v3 lo[MAXCOL], hi[MAXCOL];
+    int nov, ov[MAXPAIR];
+    int nrows, nnc, nn, nf, split;
+    RowS rs[MAXROWS];
+    union {
+        double stage[STAGE][48];
+        struct { Cand c[MAXOV][4]; int n[MAXOV]; } cand;
+    } u;
+    Cand hc[64];
+    double a12[NB];
+    double fs[8];
+    int is[8];
+};
+
+/* ---------------- wave helpers ---------------- */
+template <int CTRL>
+__device__ __forceinline__ double dpp(double x) {
+    int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xF, 0xF, false);
+    int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int x) { return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, false); }
+/* pairwise tree over each 16-lane row: quad xor1, quad xor2, half-row mirror, row mirror.
+ * Every lane of the row ends with ((x0+x1)+(x2+x3))+... -- oracle tree16(). */
+__device__ __forceinline__ double reduce16(double x) {
+    x = x + dpp<0xB1>(x);
+    x = x + dpp<0x4E>(x);
+    x = x + dpp<0x141>(x);
+    x = x + dpp<0x140>(x);
+    return x;
+}
+__device__ __forceinline__ double readlane_d(double x, int l) {
+    int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+    int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+    return __hiloint2double(hi, lo);
+}
+/* every lane l receives x from lane (32*h + (l & 31)) */
+__device__ __forceinline__ double half_bcast(double x, int h) {
+    int lo = __double2loint(x), hi = __double2hiint(x);
+    auto plo = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    auto phi = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    return h == 0 ? __hiloint2double(phi[0], plo[0]) : __hiloint2double(phi[1], plo[1]);
+}
+__device__ __forceinline__ unsigned long long ballot(int p) { return __ballot(p); }
+__device__ __forceinline__ int lane_prefix(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
+}
+/* wave-wide best (value, index): want_max picks the larger value, else the smaller; ties -> lower index;
+ * invalid lanes pass idx = 0x7fffffff.  Result is uniform. */
+__device__ __forceinline__ bool better(double v, int i, double w, int j, bool want_max) {
+    if (j == 0x7fffffff) return true;
+    if (i == 0x7fffffff) return false;
+    if (v != w) return want_max ? v > w : v < w;
+    return i < j;
+}
+__device__ __forceinline__ void wave_best(double& v, int& idx, bool want_max) {
+#define STEP(CTRL)                                             \
+    {                                                          \
+        double w = dpp<CTRL>(v);                               \
+        int j = dppi<CTRL>(idx);                               \
+        if (!better(v, idx, w, j, want_max)) { v = w; idx = j; } \
+    }
+    STEP(0xB1) STEP(0x4E) STEP(0x141) STEP(0x140)
+#undef STEP
+    double bv = readlane_d(v, 0);
+    int bi = __builtin_amdgcn_readlane(idx, 0);
+    for (int r = 16; r < 64; r += 16) {
+        double w = readlane_d(v, r);
+        int j = __builtin_amdgcn_readlane(idx, r);
+        if (!better(bv, bi, w, j, want_max)) { bv = w; bi = j; }
+    }
+    v = bv;
+    idx = bi;
+}
+
+/* ---------------- env-state helpers (lane-serial) ---------------- */
+__device__ static XF owner_xf(const EnvState& e, const Kin& k, int owner) {
+    XF T;
+    if (owner >= 0) { T.R = k.R[owner]; T.p = k.p[owner]; }
+    else if (owner <= -2 && owner > -100) { int o = -2 - owner; T.R = qmat(e.obj[o].quat); T.p = e.obj[o].pos; }
+    else { T.R = mident(); T.p = V(0, 0, 0); }
+    return T;
+}
+__device__ static inline int collider_active(const EnvState& e, const Collider& c) {
+    if (c.owner <= -2 && c.owner > -100) return e.oactive[-2 - c.owner] != 0.0;
+    return 1;
+}
+__device__ static inline void man_from_st(Manifold& M, const StMan& S) {
+    M.pair = (int)S.pair;
+    M.npts = (int)S.npts;
+    for (int p = 0; p < 4; p++) {
+        const StPt& s = S.pt[p];
+        M.pt[p].lpA = s.lpA; M.pt[p].lpB = s.lpB; M.pt[p].n = s.n;
+        M.pt[p].dist = s.dist; M.pt[p].imp = s.imp; M.pt[p].imp1 = s.imp1; M.pt[p].imp2 = s.imp2;
+    }
+}
+__device__ static inline void man_to_st(StMan& S, const Manifold& M) {
+    S.pair = (double)M.pair;
+    S.npts = (double)M.npts;
+    for (int p = 0; p < 4; p++) {
+        StPt& s = S.pt[p];
+        bool live = p < M.npts;
+        s.lpA = live ? M.pt[p].lpA : V(0, 0, 0);
+        s.lpB = live ? M.pt[p].lpB : V(0, 0, 0);
+        s.n = live ? M.pt[p].n : V(0, 0, 0);
+        s.dist = live ? M.pt[p].dist : 0.0;
+        s.imp = live ? M.pt[p].imp : 0.0;
+        s.imp1 = live ? M.pt[p].imp1 : 0.0;
+        s.imp2 = live ? M.pt[p].imp2 : 0.0;
+    }
+}
+
+/* ---------------- collision ---------------- */
+/* hull (A, robot link) vs box (B): the whole wave.  Produces cand k (<= 4 points) in sh.u.cand. */
+__device__ static void team_hull_box(Shared& sh, const Collider& A, const Collider& B, const XF& TA, const XF& TB,
+                                     double thr, int k) {
+    const int lane = threadIdx.x;
+    m3 RAB = mtm(TB.R, TA.R);
+    v3 pAB = mtv(TB.R, vsub(TA.p, TB.p));
+    v3 h = V(B.half[0], B.half[1], B.half[2]);
+    double mA = A.margin;
+    /* vertices (lane i = vertex i) */
+    int vvalid = 0;
+    Cand vc;
+    if (lane < A.nv) {
+        const double* vv = &UG_HULL_V[3 * (A.v0 + lane)];
+        v3 x = vadd(mv(RAB, V(vv[0], vv[1], vv[2])), pAB);
+        v3 d = V(ug_fabs(x.x) - h.x, ug_fabs(x.y) - h.y, ug_fabs(x.z) - h.z);
+        double dist = 0.0;
+        v3 nl = V(0, 0, 0), pl = V(0, 0, 0);
+        int ok = 1;
+        if (d.x < 0 && d.y < 0 && d.z < 0) {
+            int kk = 0;
+            double dm = d.x;
+            if (d.y > dm) { dm = d.y; kk = 1; }
+            if (d.z > dm) { dm = d.z; kk = 2; }
+            dist = dm;
+            double sg = vget(x, kk) < 0 ? -1.0 : 1.0;
+            vsetc(nl, kk, sg);
+            pl = x; vsetc(pl, kk, sg * vget(h, kk));
+        } else {
+            v3 q = V(ug_max(-h.x, ug_min(h.x, x.x)), ug_max(-h.y, ug_min(h.y, x.y)), ug_max(-h.z, ug_min(h.z, x.z)));
+            v3 df = vsub(x, q);
+            double dl = vlen(df);
+            if (dl - mA >= thr) ok = 0;
+            else { dist = dl; nl = vscale(df, 1.0 / dl); pl = q; }
+        }
+        double depth = dist - mA;
+        if (ok && depth < thr) {
+            vvalid = 1;
+            vc.n = mv(TB.R, nl);
+            vc.pB = xf_apply(TB, pl);
+            vc.d = depth;
+        }
+    }
+    /* box corners: 8 lanes per corner, faces strided over the group, then a group arg-max */
+    int c = lane >> 3, j = lane & 7;
+    m3 RBA = mtm(TA.R, TB.R);
+    v3 pBA = mtv(TA.R, vsub(TB.p, TA.p));
+    v3 cl = V((c & 1) ? h.x : -h.x, (c & 2) ? h.y : -h.y, (c & 4) ? h.z : -h.z);
+    v3 y = vadd(mv(RBA, cl), pBA);
+    double smax = -1e300;
+    int fm = 0x7fffffff;
+    for (int f = j; f < A.nf; f += 8) {
+        const double* F = &UG_HULL_F[4 * (A.f0 + f)];
+        double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
+        if (sd > smax) { smax = sd; fm = f; }
+    }
+    {
+        double w; int jj;
+        w = dpp<0xB1>(smax); jj = dppi<0xB1>(fm);
+        if (!better(smax, fm, w, jj, true)) { smax = w; fm = jj; }
+        w = dpp<0x4E>(smax); jj = dppi<0x4E>(fm);
+        if (!better(smax, fm, w, jj, true)) { smax = w; fm = jj; }
+        w = dpp<0x141>(smax); jj = dppi<0x141>(fm);
+        if (!better(smax, fm, w, jj, true)) { smax = w; fm = jj; }
+    }
+    int cvalid = 0;
+    Cand cc;
+    if (j == 0 && fm != 0x7fffffff) {
+        double depth = smax - mA;
+        if (depth < thr) {
+            const double* F = &UG_HULL_F[4 * (A.f0 + fm)];
+            v3 nw = mv(TA.R, V(F[0], F[1], F[2]));
+            cvalid = 1;
+            cc.n = vneg(nw);
+            cc.pB = xf_apply(TB, cl);
+            cc.d = depth;
+        }
+    }
+    /* collect in canonical order: vertices by index, then corners by index */
+    unsigned long long vb = ballot(vvalid), cb = ballot(cvalid);
+    int nv = __popcll(vb), nc = __popcll(cb);
+    if (vvalid) sh.hc[lane_prefix(vb)] = vc;
+    if (cvalid) sh.hc[nv + lane_prefix(cb)] = cc;
+    __syncthreads();
+    int n = nv + nc;
+    if (n <= 4) {
+        if (lane < n) sh.u.cand.c[k][lane] = sh.hc[lane];
+        if (lane == 0) sh.u.cand.n[k] = n;
+        __syncthreads();
+        return;
+    }
+    /* reduce4: deepest first, then farthest-spread (oracle reduce4) */
+    Cand mine;
+    if (lane < n) mine = sh.hc[lane];
+    double v = lane < n ? mine.d : 0.0;
+    int idx = lane < n ? lane : 0x7fffffff;
+    wave_best(v, idx, false);
+    int sel[4];
+    sel[0] = idx;
+    for (int s = 1; s < 4; s++) {
+        double md = 1e300;
+        for (int t = 0; t < s; t++) {
+            const Cand& st = sh.hc[sel[t]];
+            v3 dd = vsub(mine.pB, st.pB);
+            double x = vdot(dd, dd);
+            if (x < md) md = x;
+        }
+        bool used = false;
+        for (int t = 0; t < s; t++) used = used || (sel[t] == lane);
+        double mv2 = md;
+        int mi = (lane < n && !used) ? lane : 0x7fffffff;
+        wave_best(mv2, mi, true);
+        sel[s] = mi;
+    }
+    if (lane < 4) sh.u.cand.c[k][lane] = sh.hc[sel[lane]];
+    if (lane == 0) sh.u.cand.n[k] = 4;
+    __syncthreads();
+}
+
+/* performDiscreteCollisionDetection (oracle collide()), team version.  ws: this env's global workspace. */
+__device__ static void team_collide(Shared& sh, const Scene* s, double* ws) {
+    const int lane = threadIdx.x;
+    EnvState& e = sh.e;
+    if (lane < s->ncol) {
+        const Collider& c = s->col[lane];
+        XF O = owner_xf(e, sh.kin, c.owner);
+        v3 lo, hi;
+        world_aabb(O, c, lo, hi);
+        sh.O[lane] = O;
+        sh.lo[lane] = vsub(lo, V(UG_AABB_PAD, UG_AABB_PAD, UG_AABB_PAD));
+        sh.hi[lane] = vadd(hi, V(UG_AABB_PAD, UG_AABB_PAD, UG_AABB_PAD));
+    }
+    /* live manifolds -> global workspace (read back per pair below; LDS list is rebuilt in place) */
+    int nold = (int)e.nman;
+    const double* src = (const double*)e.man;
+    for (int i = lane; i < nold * UG_MAN_DOUBLES; i += TEAM) ws[i] = src[i];
+    __threadfence_block();
+    __syncthreads();
+    /* broadphase: ordered list of overlapping pairs */
+    int base = 0;
+    for (int p0 = 0; p0 < s->npair; p0 += TEAM) {
+        int p = p0 + lane;
+        int ovl = 0;
+        if (p < s->npair) {
+            const PairDef& P = s->pair[p];
+            int a = P.a, b = P.b;
+            ovl = collider_active(e, s->col[a]) && collider_active(e, s->col[b]) &&
+                  !(sh.lo[a].x > sh.hi[b].x || sh.hi[a].x < sh.lo[b].x || sh.lo[a].y > sh.hi[b].y ||
+                    sh.hi[a].y < sh.lo[b].y || sh.lo[a].z > sh.hi[b].z || sh.hi[a].z < sh.lo[b].z);
+        }
+        unsigned long long m = ballot(ovl);
+        if (ovl) sh.ov[base + lane_prefix(m)] = p;
+        base += __popcll(m);
+    }
+    if (lane == 0) sh.nov = base;
+    __syncthreads();
+    int nov = base;
+    int nnew = 0;
+    for (int c0 = 0; c0 < nov; c0 += MAXOV) {
+        int cn = nov - c0 < MAXOV ? nov - c0 : MAXOV;
+        /* hull-box pairs of this chunk: cooperative narrowphase */
+        for (int k = 0; k < cn; k++) {
+            const PairDef& P = s->pair[sh.ov[c0 + k]];
+            const Collider& A = s->col[P.a];
+            const Collider& B = s->col[P.b];
+            if (A.kind == UG_SHAPE_HULL && B.kind == UG_SHAPE_BOX) {
+                XF TA = shape_xf(sh.O[P.a], A), TB = shape_xf(sh.O[P.b], B);
+                team_hull_box(sh, A, B, TA, TB, P.thr, k);
+            }
+        }
+        /* lane per pair: remaining narrowphases, manifold update */
+        Manifold M;
+        M.npts = 0;
+        int has = 0;
+        if (lane < cn) {
+            int p = sh.ov[c0 + lane];
+            const PairDef& P = s->pair[p];
+            const Collider& A = s->col[P.a];
+            const Collider& B = s->col[P.b];
+            M.pair = p;
+            for (int m = 0; m < nold; m++) {
+                if ((int)ws[m * UG_MAN_DOUBLES] == p) {
+                    StMan tmp;
+                    double* t = (double*)&tmp;
+                    for (int i = 0; i < UG_MAN_DOUBLES; i++) t[i] = ws[m * UG_MAN_DOUBLES + i];
+                    man_from_st(M, tmp);
+                    break;
+                }
+            }
+            XF TA = shape_xf(sh.O[P.a], A), TB = shape_xf(sh.O[P.b], B);
+            CandList L;
+            L.n = 0;
+            if (A.kind == UG_SHAPE_HULL && B.kind == UG_SHAPE_BOX) {
+                for (int i = 0; i < sh.u.cand.n[lane]; i++) cand_add(L, sh.u.cand.c[lane][i].n, sh.u.cand.c[lane][i].pB, sh.u.cand.c[lane][i].d);
+            } else if (A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_BOX) nc_sphere_box(TA, A, TB, B, P.thr, L);
+            else if (A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_SPHERE) nc_sphere_sphere(TA, A, TB, B, P.thr, L);
+            else if (A.kind == UG_SHAPE_BOX && B.kind == UG_SHAPE_BOX) nc_box_box(TA, A, TB, B, P.thr, L);
+            else if (A.kind == UG_SHAPE_HULL && B.kind == UG_SHAPE_SPHERE) nc_hull_sphere(TA, A, TB, B, P.thr, L);
+            else if (A.kind == UG_SHAPE_BOX && B.kind == UG_SHAPE_SPHERE) {
+                CandList L2;
+                L2.n = 0;
+                nc_sphere_box(TB, B, TA, A, P.thr, L2);
+                for (int i = 0; i < L2.n; i++)
+                    cand_add(L, vneg(L2.c[i].n), vadd(L2.c[i].pB, vscale(L2.c[i].n, L2.c[i].d)), L2.c[i].d);
+            }
+            for (int i = 0; i < L.n; i++) manifold_add(M, sh.O[P.a], sh.O[P.b], L.c[i], P.thr);
+            if (M.npts) manifold_refresh(M, sh.O[P.a], sh.O[P.b], P.thr);
+            has = M.npts > 0;
+        }
+        __syncthreads();
+        unsigned long long hm = ballot(has);
+        if (has) {
+            int pos = nnew + lane_prefix(hm);
+            if (pos < MAXMAN) man_to_st(e.man[pos], M);
+        }
+        nnew += __popcll(hm);
+        __syncthreads();
+    }
+    if (lane == 0) {
+        if (nnew > MAXMAN) e.overflow += (double)(nnew - MAXMAN);
+        e.nman = (double)(nnew < MAXMAN ? nnew : MAXMAN);
+    }
+    __syncthreads();
+}
+
+/* ---------------- rows ---------------- */
+__device__ static inline int ent_dofs(int ent) { return ent == 0 ? NB : 6; }
+__device__ static inline int ent_off(int ent) { return ent == 0 ? 0 : NB + 6 * (ent - 1); }
+__device__ static inline double ent_dot(int ent, const double* J, const double* v) {
+    int n = ent_dofs(ent), o = ent_off(ent);
+    double s = 0.0;
+    for (int i = 0; i < n; i++) s += J[i] * v[o + i];
+    return s;
+}
+__device__ static inline double ent_dot_local(int ent, const double* a, const double* b) {
+    int n = ent_dofs(ent);
+    double s = 0.0;
+    for (int i = 0; i < n; i++) s += a[i] * b[i];
+    return s;
+}
+__device__ static void point_jac(const Scene* sc, const EnvState& e, const Kin& k, int ent, int body, v3 p, v3 d,
+                                 double* J, double* MiJ, const double* LDL) {
+    if (ent == 0) {
+        for (int i = 0; i < NB; i++) {
+            J[i] = moves(i, body) ? vdot(d, vcross(k.a[i], vsub(p, k.p[i]))) : 0.0;
+            MiJ[i] = J[i];
+        }
+        ldlt_solve(LDL, NB, MiJ);
+    } else {
+        int o = ent - 1;
+        v3 r = vsub(p, e.obj[o].pos);
+        v3 rn = vcross(r, d);
+        J[0] = d.x; J[1] = d.y; J[2] = d.z; J[3] = rn.x; J[4] = rn.y; J[5] = rn.z;
+        double im = 1.0 / sc->omass[o];
+        m3 R = qmat(e.obj[o].quat);
+        v3 ir = mtv(R, rn);
+        ir = V(ir.x / sc->oinertia[o].x, ir.y / sc->oinertia[o].y, ir.z / sc->oinertia[o].z);
+        ir = mv(R, ir);
+        MiJ[0] = d.x * im; MiJ[1] = d.y * im; MiJ[2] = d.z * im; MiJ[3] = ir.x; MiJ[4] = ir.y; MiJ[5] = ir.z;
+    }
+}
+__device__ static inline int ent_of_collider(const Collider& c, int& body) {
+    body = -1;
+    if (c.owner >= 0) { body = c.owner; return 0; }
+    if (c.owner == -1) return -1;
+    if (c.owner > -100) return -1 - c.owner;
+    return -1;
+}
+__device__ static inline void put_seg(int ent, const double* src, double* dst) {
+    int n = ent_dofs(ent), o = ent_off(ent);
+    for (int i = 0; i < n; i++) dst[o + i] = src[i];
+}
+/* enumerate rows in solve order (lane 0): nc rows, then normals, then frictions */
+__device__ static void enumerate_rows(Shared& sh, const Scene* s) {
+    EnvState& e = sh.e;
+    int n = 0, nnc = 0, nn = 0, nf = 0;
+    /* first pass: counts and capacity decisions in the oracle's enumeration order */
+    int ncnt = 0;
+    for (int d = 0; d < NB; d++)
+        for (int side = 0; side < 2; side++) {
+            double pen = side == 0 ? e.q[d] - UG_DOF_LOWER[d] : UG_DOF_UPPER[d] - e.q[d];
+            if (pen > 0) continue;
+            if (ncnt >= MAXROWS) { e.overflow += 1.0; continue; }
+            RowS& r = sh.rs[nnc];
+            r.kind = 0; r.a = d; r.b = side;
+            nnc++; ncnt++;
+        }
+    for (int m = 0; m < 7; m++) {
+        if (e.mon[m] == 0.0) continue;
+        if (ncnt >= MAXROWS) { e.overflow += 1.0; continue; }
+        RowS& r = sh.rs[nnc];
+        r.kind = 1; r.a = m;
+        nnc++; ncnt++;
+    }
+    for (int g = 0; g < 5; g++) {
+        if (ncnt >= MAXROWS) { e.overflow += 1.0; continue; }
+        RowS& r = sh.rs[nnc];
+        r.kind = 2; r.a = g;
+        nnc++; ncnt++;
+    }
+    int nman = (int)e.nman;
+    /* contact points kept (capacity: 3 rows each) */
+    int npt = 0;
+    for (int m = 0; m < nman; m++) {
+        const PairDef& P = s->pair[(int)e.man[m].pair];
+        int bA, bB;
+        int eA = ent_of_collider(s->col[P.a], bA), eB = ent_of_collider(s->col[P.b], bB);
+        if (eA < 0 && eB < 0) continue;
+        for (int j = 0; j < (int)e.man[m].npts; j++) {
+            if (ncnt + 3 > MAXROWS) { e.overflow += 1.0; continue; }
+            ncnt += 3;
+            npt++;
+        }
+    }
+    nn = npt;
+    nf = 2 * npt;
+    int pn = nnc, pf = nnc + nn;
+    for (int m = 0; m < nman; m++) {
+        const PairDef& P = s->pair[(int)e.man[m].pair];
+        int bA, bB;
+        int eA = ent_of_collider(s->col[P.a], bA), eB = ent_of_collider(s->col[P.b], bB);
+        if (eA < 0 && eB < 0) continue;
+        for (int j = 0; j < (int)e.man[m].npts; j++) {
+            if (pn >= nnc + nn) break;
+            RowS& r = sh.rs[pn];
+            r.kind = 3; r.a = m; r.b = j;
+            for (int f = 0; f < 2; f++) {
+                RowS& q = sh.rs[pf + f];
+                q.kind = 4 + f; q.a = m; q.b = j; q.nrow = pn;
+            }
+            pn++;
+            pf += 2;
+        }
+    }
+    n = nnc + nn + nf;
+    sh.nrows = n; sh.nnc = nnc; sh.nn = nn; sh.nf = nf;
+}
+/* build row at position pos (one lane): J, M^-1 J^T into stage row sl, scalars into rs[pos] */
+__device__ static void build_row(Shared& sh, const Scene* s, int pos, int sl) {
+    const EnvState& e = sh.e;
+    const double dt = UG_DT;
+    RowS& r = sh.rs[pos];
+    double J[NVP], MJ[NVP];
+    for (int i = 0; i < NVP; i++) { J[i] = 0.0; MJ[i] = 0.0; }
+    double invD = 0.0, rhs = 0.0, rhsPen = 0.0, lo = 0.0, hi = 0.0, imp = 0.0, fric = 0.0;
+    if (r.kind <= 1) {
+        int d = r.kind == 0 ? r.a : (r.a < 6 ? r.a : UG_FINGER_DOF);
+        double sgn = (r.kind == 0 && r.b == 1) ? -1.0 : 1.0;
+        double Jl[NB], Ml[NB];
+        for (int i = 0; i < NB; i++) Jl[i] = 0.0;
+        Jl[d] = sgn;
+        for (int i = 0; i < NB; i++) Ml[i] = Jl[i];
+        ldlt_solve(sh.LDL, NB, Ml);
+        double den = ent_dot_local(0, Jl, Ml);
+        invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
+        put_seg(0, Jl, J);
+        put_seg(0, Ml, MJ);
+        double relv = ent_dot(0, Jl, sh.v0);
+        if (r.kind == 0) {
+            double pen = r.b == 0 ? e.q[d] - UG_DOF_LOWER[d] : UG_DOF_UPPER[d] - e.q[d];
+            double erp = (pen > UG_SPLIT_PEN_THR) ? UG_ERP : UG_ERP2;
+            double perr = -pen * erp / dt, verr = -relv;
+            double pimp = perr * invD, vimp = verr * invD;
+            rhs = (pen > UG_SPLIT_PEN_THR) ? pimp + vimp : vimp;
+            lo = 0.0; hi = UG_LIMIT_MAXIMP;
+        } else {
+            int m = r.a;
+            double maxImp = UG_DOF_MAXFORCE[d] * dt;
+            double qd = sh.v0[d];
+            double pst = 1.0 * (e.mtarget[m] - e.q[d]) / dt;
+            double verr = 0.0 - qd;
+            double des = UG_MOTOR_KP * pst + qd + UG_MOTOR_KD * verr;
+            double clamp = UG_DOF_MAXVEL[d];
+            if (des > clamp) des = clamp;
+            if (des < -clamp) des = -clamp;
+            rhs = 0.0 * invD + (des - relv) * invD;
+            lo = -maxImp; hi = maxImp;
+        }
+    } else if (r.kind == 2) {
+        int pa = UG_FINGER_DOF, cb = UG_GEAR_CHILD[r.a];
+        double ratio = UG_GEAR_RATIO[r.a];
+        double JA[NB], JB[NB], MA[NB], MB[NB];
+        for (int i = 0; i < NB; i++) { JA[i] = 0.0; JB[i] = 0.0; }
+        JA[pa] = 1.0;
+        JB[cb] = ratio;
+        for (int i = 0; i < NB; i++) { MA[i] = JA[i]; MB[i] = JB[i]; }
+        ldlt_solve(sh.LDL, NB, MA);
+        ldlt_solve(sh.LDL, NB, MB);
+        double den = ent_dot_local(0, JA, MA) + ent_dot_local(0, JB, MB);
+        invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
+        for (int i = 0; i < NB; i++) { J[i] = JA[i] + JB[i]; MJ[i] = MA[i] + MB[i]; }
+        double relv = ent_dot(0, JA, sh.v0) + ent_dot(0, JB, sh.v0);
+        double diff = e.q[cb] * ratio + e.q[pa];
+        double pen = -UG_GEAR_ERP * (0.0 - diff);
+        double perr = -pen * UG_ERP / dt, verr = 0.0 - relv;
+        rhs = perr * invD + verr * invD;
+        double maxImp = UG_GEAR_MAXF * dt;
+        lo = -maxImp; hi = maxImp;
+    } else {
+        const StMan& M = e.man[r.a];
+        const PairDef& P = s->pair[(int)M.pair];
+        int bodyA, bodyB;
+        int entA = ent_of_collider(s->col[P.a], bodyA);
+        int entB = ent_of_collider(s->col[P.b], bodyB);
+        XF OA = owner_xf(e, sh.kin, s->col[P.a].owner), OB = owner_xf(e, sh.kin, s->col[P.b].owner);
+        const StPt& cp = M.pt[r.b];
+        v3 pA = xf_apply(OA, cp.lpA), pB = xf_apply(OB, cp.lpB);
+        v3 n = cp.n;
+        v3 d = n;
+        if (r.kind >= 4) {
+            v3 t1, t2;
+            if (ug_fabs(n.z) > 0.7071067811865475244) {
+                double a = n.y * n.y + n.z * n.z, kk = 1.0 / ug_sqrt(a);
+                t1 = V(0, -n.z * kk, n.y * kk);
+                t2 = V(a * kk, -n.x * t1.z, n.x * t1.y);
+            } else {
+                double a = n.x * n.x + n.y * n.y, kk = 1.0 / ug_sqrt(a);
+                t1 = V(-n.y * kk, n.x * kk, 0);
+                t2 = V(-n.z * t1.y, n.z * t1.x, a * kk);
+            }
+            d = r.kind == 4 ? t1 : t2;
+        }
+        double JA[NB], MA[NB], JB[NB], MB[NB];
+        double dA = 0.0, dB = 0.0, relv = 0.0;
+        if (entA >= 0) {
+            point_jac(s, e, sh.kin, entA, bodyA, pA, d, JA, MA, sh.LDL);
+            dA = ent_dot_local(entA, JA, MA);
+            relv += ent_dot(entA, JA, sh.v0);
+            put_seg(entA, JA, J);
+            put_seg(entA, MA, MJ);
+        }
+        if (entB >= 0) {
+            point_jac(s, e, sh.kin, entB, bodyB, pB, vneg(d), JB, MB, sh.LDL);
+            dB = ent_dot_local(entB, JB, MB);
+            relv += ent_dot(entB, JB, sh.v0);
+            put_seg(entB, JB, J);
+            put_seg(entB, MB, MJ);
+        }
+        double den = dA + dB;
+        invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
+        if (r.kind == 3) {
+            double pen = cp.dist + UG_LINEAR_SLOP;
+            double rest = 0.0;
+            if (!(ug_fabs(relv) < UG_REST_VEL_THR)) rest = P.restitution * -relv;
+            if (rest <= 0.0) rest = 0.0;
+            double verr = rest - relv, perr;
+            double erp = (pen > UG_SPLIT_PEN_THR) ? UG_ERP : UG_ERP2;
+            if (pen > 0) { perr = 0.0; verr -= pen / UG_DT; }
+            else perr = -pen * erp / UG_DT;
+            double pimp = perr * invD, vimp = verr * invD;
+            if (pen > UG_SPLIT_PEN_THR) { rhs = pimp + vimp; rhsPen = 0.0; }
+            else { rhs = vimp; rhsPen = pimp; }
+            lo = 0.0; hi = 1e10;
+            imp = cp.imp * UG_WARMSTART;
+        } else {
+            rhs = 0.0 * invD + (0.0 - relv) * invD;
+            fric = P.friction;
+        }
+    }
+    r.invD = invD; r.rinv = invD == 0.0 ? 0.0 : 1.0 / invD; r.rhs = rhs; r.rhsPen = rhsPen; r.lo = lo; r.hi = hi; r.imp = imp; r.impPen = 0.0; r.fric = fric;
+    for (int i = 0; i < 24; i++) { sh.u.stage[sl][i] = J[i]; sh.u.stage[sl][24 + i] = MJ[i]; }
+}
+
+/* ---------------- PGS (btMultiBodyConstraintSolver) ---------------- */
+struct Regs {
+    double J[NSLOT], M[NSLOT];
+};
+/* one row update; p = position, s = slot (compile-time at the call site), h = half */
+__device__ __forceinline__ void pgs_row(Shared& sh, const double& Js, const double& Ms, int p, int h, double& dv,
+                                        double& res, int pen) {
+    RowS& r = sh.rs[p];
+    double lo = r.lo, hi = r.hi;
+    if (!pen && r.kind >= 4) {
+        double tot = sh.rs[r.nrow].imp;
+        if (!(tot > 0.0)) return;
+        lo = -(r.fric * tot);
+        hi = r.fric * tot;
+    }
+    double prod = Js * dv;
+    double red = reduce16(prod);
+    double dot = readlane_d(red, 32 * h) + readlane_d(red, 32 * h + 16);
+    double imp = pen ? r.impPen : r.imp;
+    double invD = r.invD;
+    double di = (pen ? r.rhsPen : r.rhs) - imp * 0.0;
+    di -= dot * invD;
+    double sum = imp + di;
+    if (sum < lo) { di = lo - imp; imp = lo; }
+    else if (sum > hi) { di = hi - imp; imp = hi; }
+    else imp = sum;
+    if (threadIdx.x == 0) {
+        if (pen) r.impPen = imp;
+        else r.imp = imp;
+    }
+    double c = Ms * di;
+    dv = dv + half_bcast(c, h);
+    double x = di * r.rinv;
+    x = x * x;
+    res = res > x ? res : x;
+}
+
+
+/* ---------------- one p.stepSimulation() (oracle substep()) ---------------- */
+__device__ static void team_substep(Shared& sh, const Scene* s, double* ws) {
+    const int lane = threadIdx.x;
+    const int h = lane >> 5, d = lane & 31;
+    EnvState& e = sh.e;
+    const double dt = UG_DT;
+    if (lane == 0) fk(e.q, sh.kin);
+    __syncthreads();
+    team_collide(sh, s, ws);
+    if (lane == 0) {
+        double C[NB];
+        robot_dynamics(e.qd, sh.kin, s->gravity, sh.LDL, C);
+        ldlt(sh.LDL, NB);
+        double qdd[NB];
+        for (int i = 0; i < NB; i++) qdd[i] = -C[i];
+        ldlt_solve(sh.LDL, NB, qdd);
+        for (int i = 0; i < NVP; i++) sh.v0[i] = 0.0;
+        for (int i = 0; i < NB; i++) { e.qd[i] = e.qd[i] + qdd[i] * dt; sh.v0[i] = e.qd[i]; }
+        for (int o = 0; o < s->nobj; o++) {
+            if (e.oactive[o] == 0.0) continue;
+            StObj& ob = e.obj[o];
+            v3 v = ob.v;
+            double vn = vlen(v);
+            v3 a = vsub(V(0, 0, s->gravity), vscale(v, UG_LIN_DAMP + UG_LIN_DAMP * vn));
+            ob.v = vadd(v, vscale(a, dt));
+            m3 R = qmat(ob.quat);
+            v3 wl = mtv(R, ob.w);
+            v3 I = s->oinertia[o];
+            v3 Iw = V(I.x * wl.x, I.y * wl.y, I.z * wl.z);
+            double wn = vlen(wl);
+            v3 z = vadd(vscale(Iw, UG_ANG_DAMP + UG_ANG_DAMP * wn), vcross(wl, Iw));
+            v3 al = V(-z.x / I.x, -z.y / I.y, -z.z / I.z);
+            ob.w = vadd(ob.w, vscale(mv(R, al), dt));
+            int off = NB + 6 * o;
+            sh.v0[off] = ob.v.x; sh.v0[off + 1] = ob.v.y; sh.v0[off + 2] = ob.v.z;
+            sh.v0[off + 3] = ob.w.x; sh.v0[off + 4] = ob.w.y; sh.v0[off + 5] = ob.w.z;
+        }
+        enumerate_rows(sh, s);
+    }
+    __syncthreads();
+    const int n = sh.nrows, nnc = sh.nnc, nn = sh.nn;
+    /* rows: built lane-per-row in batches, then moved into the register slots of their half */
+    double RJ[NSLOT], RM[NSLOT];
+    for (int base = 0; base < n; base += STAGE) {
+        int cnt = n - base < STAGE ? n - base : STAGE;
+        if (lane < cnt) build_row(sh, s, base + lane, lane);
+        __syncthreads();
+#pragma unroll
+        for (int sl = 0; sl < NSLOT; sl++) {
+            if (2 * sl + 1 < base || 2 * sl >= base + cnt) continue;
+            int r = 2 * sl + h - base;
+            bool in = r >= 0 && r < cnt;
+            int rr = in ? r : 0;
+            int dd = d < 24 ? d : 0;
+            double vj = sh.u.stage[rr][dd], vm = sh.u.stage[rr][24 + dd];
+            if (in) {
+                RJ[sl] = d < 24 ? vj : 0.0;
+                RM[sl] = d < 24 ? vm : 0.0;
+            }
+        }
+        __syncthreads();
+    }
+    /* PGS: warm start (normals), iterations; split-impulse pass */
+    double dv = 0.0, dvs = 0.0;
+#pragma unroll
+    for (int sl = 0; sl < NSLOT; sl++) {
+        if (2 * sl + 1 < nnc || 2 * sl >= nnc + nn) continue;
+#pragma unroll
+        for (int hh = 0; hh < 2; hh++) {
+            int p = 2 * sl + hh;
+            if (p < nnc || p >= nnc + nn) continue;
+            double imp = sh.rs[p].imp;
+            if (imp != 0.0) dv = dv + half_bcast(RM[sl] * imp, hh);
+        }
+    }
+    for (int it = 0; it < UG_PGS_ITERS; it++) {
+        double res = 0.0;
+        int start = 0;
+        if (!(it & 1)) {
+#pragma unroll
+            for (int sl = NSLOT - 1; sl >= 0; sl--) {
+                if (2 * sl >= nnc) continue;
+#pragma unroll
+                for (int hh = 1; hh >= 0; hh--) {
+                    int p = 2 * sl + hh;
+                    if (p < nnc) pgs_row(sh, RJ[sl], RM[sl], p, hh, dv, res, 0);
+                }
+            }
+            start = nnc;
+        }
+#pragma unroll
+        for (int sl = 0; sl < NSLOT; sl++) {
+            if (2 * sl + 1 < start || 2 * sl >= n) continue;
+#pragma unroll
+            for (int hh = 0; hh < 2; hh++) {
+                int p = 2 * sl + hh;
+                if (p >= start && p < n) pgs_row(sh, RJ[sl], RM[sl], p, hh, dv, res, 0);
+            }
+        }
+        if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
+    }
+    int anypen = 0;
+    for (int p = nnc + lane; p < nnc + nn; p += TEAM) anypen |= sh.rs[p].rhsPen != 0.0;
+    int split = ballot(anypen) != 0ull;
+    if (split) {
+        for (int it = 0; it < UG_PGS_ITERS; it++) {
+            double res = 0.0;
+#pragma unroll
+            for (int sl = 0; sl < NSLOT; sl++) {
+                if (2 * sl + 1 < nnc || 2 * sl >= nnc + nn) continue;
+#pragma unroll
+                for (int hh = 0; hh < 2; hh++) {
+                    int p = 2 * sl + hh;
+                    if (p >= nnc && p < nnc + nn) pgs_row(sh, RJ[sl], RM[sl], p, hh, dvs, res, 1);
+                }
+            }
+            if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
+        }
+    }
+    if (lane < NVP) { sh.dvout[lane] = dv; sh.dvsout[lane] = dvs; }
+    /* impulses back into the manifold points (lane per row) */
+    for (int p = nnc + lane; p < n; p += TEAM) {
+        const RowS& r = sh.rs[p];
+        StPt& pt = e.man[r.a].pt[r.b];
+        if (r.kind == 3) pt.imp = r.imp;
+        else if (r.kind == 4) pt.imp1 = r.imp;
+        else pt.imp2 = r.imp;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        const double* DV = sh.dvout;
+        const double* DVS = sh.dvsout;
+        for (int i = 0; i < NB; i++) {
+            e.qd[i] = e.qd[i] + DV[i];
+            double vi = split ? e.qd[i] + DVS[i] : e.qd[i];
+            e.q[i] = e.q[i] + vi * dt;
+        }
+        for (int o = 0; o < s->nobj; o++) {
+            if (e.oactive[o] == 0.0) continue;
+            StObj& ob = e.obj[o];
+            int off = NB + 6 * o;
+            ob.v = vadd(ob.v, V(DV[off], DV[off + 1], DV[off + 2]));
+            ob.w = vadd(ob.w, V(DV[off + 3], DV[off + 4], DV[off + 5]));
+            v3 vl = ob.v, wa = ob.w;
+            if (split) {
+                vl = vadd(vl, V(DVS[off], DVS[off + 1], DVS[off + 2]));
+                wa = vadd(wa, V(DVS[off + 3], DVS[off + 4], DVS[off + 5]));
+            }
+            ob.pos = vadd(ob.pos, vscale(vl, dt));
+            double ang = vlen(wa);
+            if (ang * dt > UG_ANGULAR_MOTION_THR) ang = UG_ANGULAR_MOTION_THR / dt;
+            v3 ax;
+            if (ang < 0.001) ax = vscale(wa, 0.5 * dt - (dt * dt * dt) * 0.020833333333 * ang * ang);
+            else ax = vscale(wa, ug_sin(0.5 * ang * dt) / ang);
+            q4 dq = Q(ax.x, ax.y, ax.z, ug_cos(0.5 * ang * dt));
+            ob.quat = qnormalize(qmul(dq, ob.quat));
+        }
+    }
+    __syncthreads();
+}
+
+/* wait_until_stable (env_ball_balance_v0.py:94-103): returns substeps taken */
+__device__ static int team_wait(Shared& sh, const Scene* s, double* ws) {
+    const int lane = threadIdx.x;
+    double pos = lane < NB ? sh.e.q[lane] : 0.0;
+    for (int i = 0; i < UG_STABLE_STEPS; i++) {
+        team_substep(sh, s, ws);
+        double qn = lane < NB ? sh.e.q[lane] : 0.0;
+        if (lane < NB) sh.a12[lane] = ug_fabs(pos - qn);
+        __syncthreads();
+        if (lane == 0) sh.is[0] = np_sum12(sh.a12) < UG_STABLE_EPS;
+        __syncthreads();
+        if (sh.is[0]) return i + 1;
+        pos = qn;
+    }
+    return UG_STABLE_STEPS;
+}
+
+/* ---------------- robot control + BallBalance glue (lane 0 unless noted) ---------------- */
+__device__ static inline void set_gripper(EnvState& e, double L) {
+    e.mtarget[6] = gripper_angle(L);
+    e.mon[6] = 1.0;
+}
+__device__ static inline void open_gripper(EnvState& e, double pct) {
+    set_gripper(e, UG_GRIP_MIN + (UG_GRIP_MAX - UG_GRIP_MIN) * (pct / 100.0));
+}
+__device__ static inline void close_gripper(EnvState& e, double pct) {
+    set_gripper(e, UG_GRIP_MAX - (UG_GRIP_MAX - UG_GRIP_MIN) * (pct / 100.0));
+}
+__device__ static void move_ee_end(EnvState& e, v3 pos, q4 orn) {
+    double qt[NB];
+    ik_solve(e.q, pos, orn, qt);
+    for (int i = 0; i < 6; i++) { e.mtarget[i] = qt[i]; e.mon[i] = 1.0; }
+}
+__device__ static void link_state_of(const double* q, int l, v3& p, q4& o) {
+    Kin k;
+    fk(q, k);
+    m3 R;
+    link_frame(k, l, 1, R, p);
+    o = mquat(R);
+}
+__device__ static v3 gripper_center(const double* q) {
+    Kin k;
+    fk(q, k);
+    v3 lo = V(1e300, 1e300, 1e300), hi = V(-1e300, -1e300, -1e300);
+    const int links[2] = {11, 16};
+    for (int i = 0; i < 2; i++) {
+        int l = links[i];
+        m3 R;
+        v3 p;
+        link_frame(k, l, 1, R, p);
+        v3 c = vadd(mv(R, V(UG_LINK_AABB_C[3 * l], UG_LINK_AABB_C[3 * l + 1], UG_LINK_AABB_C[3 * l + 2])), p);
+        v3 hh = V(UG_LINK_AABB_H[3 * l], UG_LINK_AABB_H[3 * l + 1], UG_LINK_AABB_H[3 * l + 2]);
+        const double* r = R.m;
+        v3 ext = V(ug_fabs(r[0]) * hh.x + ug_fabs(r[1]) * hh.y + ug_fabs(r[2]) * hh.z,
+                   ug_fabs(r[3]) * hh.x + ug_fabs(r[4]) * hh.y + ug_fabs(r[5]) * hh.z,
+                   ug_fabs(r[6]) * hh.x + ug_fabs(r[7]) * hh.y + ug_fabs(r[8]) * hh.z);
+        v3 mn = vsub(c, ext), mx = vadd(c, ext);
+        lo = V(ug_min(lo.x, mn.x), ug_min(lo.y, mn.y), ug_min(lo.z, mn.z));
+        hi = V(ug_max(hi.x, mx.x), ug_max(hi.y, mx.y), ug_max(hi.z, mx.z));
+    }
+    return V((hi.x + lo.x) / 2.0, (hi.y + lo.y) / 2.0, (hi.z + lo.z) / 2.0);
+}
+__device__ static void remove_object(EnvState& e, const Scene* s, int o) {
+    e.oactive[o] = 0.0;
+    int ci = s->ocol[o];
+    int k = 0, nm = (int)e.nman;
+    for (int m = 0; m < nm; m++) {
+        const PairDef& P = s->pair[(int)e.man[m].pair];
+        if (P.a == ci || P.b == ci) continue;
+        if (k != m) e.man[k] = e.man[m];
+        k++;
+    }
+    e.nman = (double)k;
+}
+__device__ static void place_object(EnvState& e, int o, v3 pos, q4 orn) {
+    e.oactive[o] = 1.0;
+    e.obj[o].pos = pos;
+    e.obj[o].quat = orn;
+    e.obj[o].v = V(0, 0, 0);
+    e.obj[o].w = V(0, 0, 0);
+}
+/* random.uniform(a, b) from the env's stream, or from a caller-supplied draw in [0,1) */
+struct Draws {
+    Rng rng;
+    const double* given;
+    int k;
+    __device__ double uniform(double a, double b) {
+        double u = given ? given[k++] : mt_random(rng);
+        return a + (b - a) * u;
+    }
+};
+__device__ static void bb_obs(const EnvState& e, double* obs) {
+    v3 eu = euler_from_quat(e.obj[0].quat);
+    obs[0] = eu.x; obs[1] = eu.y; obs[2] = eu.z;
+    obs[3] = e.obj[0].pos.x - e.obj[1].pos.x;
+    obs[4] = e.obj[0].pos.y - e.obj[1].pos.y;
+    obs[5] = e.obj[0].pos.z - e.obj[1].pos.z;
+}
+/* env_ball_balance_v0.py:145-170 (obs written by lane 0) */
+__device__ static int team_bb_reset(Shared& sh, const Scene* s, double* ws, Draws& dr, double* obs) {
+    const int lane = threadIdx.x;
+    EnvState& e = sh.e;
+    if (lane == 0) {
+        e.goal_approached = 0.0;
+        e.goal_grasped = 0.0;
+        for (int i = 0; i < 6; i++) { e.q[i] = UG_ARM_REST[i]; e.qd[i] = 0.0; }
+    }
+    __syncthreads();
+    int n = 0;
+    for (int i = 0; i < 10; i++) team_substep(sh, s, ws);
+    n += 10;
+    if (lane == 0) {
+        open_gripper(e, 100.0);
+        remove_object(e, s, 0);
+        remove_object(e, s, 1);
+        move_ee_end(e, V(0.0, -0.60, 0.60), Q(0.50, -0.50, -0.50, 0.50));
+        open_gripper(e, 20.0);
+    }
+    __syncthreads();
+    n += team_wait(sh, s, ws);
+    if (lane == 0) {
+        v3 pe;
+        q4 oe;
+        link_state_of(e.q, UG_EE_LINK, pe, oe);
+        v3 gc = gripper_center(e.q);
+        v3 pose = V(pe.x, pe.y - 0.2, gc.z);
+        place_object(e, 0, pose, Q(0, 0, 0, 1));
+        v3 bp = V(pose.x, pose.y, pose.z + 0.2 + UG_BB_BALL_R);
+        bp.x += dr.uniform(-0.03, 0.03);
+        bp.y += dr.uniform(-0.08, 0.02);
+        place_object(e, 1, bp, e.obj[0].quat);
+        close_gripper(e, 100.0);
+    }
+    __syncthreads();
+    n += team_wait(sh, s, ws);
+    if (lane == 0) bb_obs(e, obs);
+    return n;
+}
+/* env_ball_balance_v0.py:105-134 */
+__device__ static int team_bb_step(Shared& sh, const Scene* s, double* ws, const float* a, double* obs, double* rew,
+                                   int* term, int* succ) {
+    const int lane = threadIdx.x;
+    EnvState& e = sh.e;
+    if (lane == 0) {
+        v3 pe;
+        q4 oe;
+        link_state_of(e.q, UG_EE_LINK, pe, oe);
+        v3 eu = euler_from_quat(oe);
+        eu.x += (double)a[0]; eu.y += (double)a[1]; eu.z += (double)a[2];
+        q4 qn = quat_from_euler(eu);
+        move_ee_end(e, pe, qn);
+    }
+    __syncthreads();
+    int n = team_wait(sh, s, ws);
+    *rew = 1.0;
+    *term = e.obj[1].pos.z < e.obj[0].pos.z;
+    *succ = 0;
+    if (lane == 0) bb_obs(e, obs);
+    return n;
+}
+
+/* ---------------- state in/out (cooperative, canonical layout) ---------------- */
+__device__ static void team_load(Shared& sh, const double* S) {
+    double* dst = (double*)&sh.e;
+    for (int i = threadIdx.x; i < UG_STATE_DIM; i += TEAM) dst[i] = S[i];
+    __syncthreads();
+}
+/* manifold slots beyond nman are written as (pair -1, zeros), as ugo_get_state does */
+__device__ static void team_store(const Shared& sh, double* S) {
+    const double* src = (const double*)&sh.e;
+    int nm = (int)sh.e.nman;
+    for (int i = threadIdx.x; i < UG_STATE_DIM; i += TEAM) {
+        double v = src[i];
+        if (i >= UG_F_MAN && i < UG_F_TASK) {
+            int m = (i - UG_F_MAN) / UG_MAN_DOUBLES, f = (i - UG_F_MAN) % UG_MAN_DOUBLES;
+            if (m >= nm) v = f == 0 ? -1.0 : 0.0;
+        }
+        S[i] = v;
+    }
+}
+
+}  // namespace ugd
+#endif
