@@ -100,6 +100,10 @@ int urgym_ik(urgym_handle* h, const double* target, double* q_out);
 /* Device time (ms) of the most recent step/reset kernel, measured with HIP events on the
  * handle's stream (bench.py roofline). */
 double urgym_last_kernel_ms(const urgym_handle* h);
+/* Development aid, no reference counterpart: phase cycle counters of the step/reset kernels
+ * (collision, dynamics, row build, PGS, split, integration, glue, total, then event counts).
+ * Returns -1 unless the library was built with -DUG_PROF. */
+int urgym_debug_prof(urgym_handle* h, unsigned long long* out16, int reset);
 
 #ifdef __cplusplus
 }

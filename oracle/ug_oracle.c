@@ -1389,7 +1389,7 @@ static void build_rows(ugo_env* e, const kin* k, const double* LDL, const double
 /* resolveSingleConstraintRowGeneric [ext] over the full generalized vector */
 static double solve_row(row* r, double* dv, int pen) {
     double imp = pen ? r->impPen : r->imp;
-    double di = (pen ? r->rhsPen : r->rhs) - imp * 0.0;
+    double di = pen ? r->rhsPen : r->rhs; /* - imp * cfm, cfm = 0 */
     di -= pdot(r->J, dv) * r->invD;
     double sum = imp + di;
     if (sum < r->lo) { di = r->lo - imp; imp = r->lo; }

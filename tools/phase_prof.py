@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Per-phase cycle breakdown of the team kernels (development aid).
+
+Needs the instrumented library: hipcc ... -DUG_PROF -o urgym_amd/_lib/liburgym_prof.so
+(tools/build_prof.sh).  Runs BallBalance x N envs with autoreset for K steps and prints
+cycles per phase per env-step, plus substeps / rows / PGS iterations per substep.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("URGYM_LIB", os.path.join(ROOT, "urgym_amd", "_lib", "liburgym_prof.so"))
+
+NAMES = ["collide", "dyn+enum", "rows", "pgs", "split", "integrate", "glue", "total",
+         "substeps", "nrows", "pgs_iters", "overlap_pairs", "hull_pairs", "manifolds"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--steps", type=int, default=5)
+    a = ap.parse_args()
+    from urgym_amd._native import Sim
+    sim = Sim(0, a.envs, seed=20241220)
+    sim.set_autoreset(True, 500)
+    buf = np.zeros(16, np.uint64)
+    sim.reset()
+    sim.sync()
+    rc = sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
+    assert rc == 0, "library not built with -DUG_PROF"
+    print("reset:", json.dumps(dict(zip(NAMES, (int(x) for x in buf[:14])))))
+    rng = np.random.default_rng(1)
+    for _ in range(a.steps):
+        sim.step(rng.uniform(-0.1, 0.1, size=(a.envs, 3)).astype(np.float32))
+    sim.sync()
+    sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
+    es = a.envs * a.steps
+    d = {k: float(v) for k, v in zip(NAMES, buf[:14])}
+    out = {"per_env_step_cycles": {k: d[k] / es for k in NAMES[:8]},
+           "substeps_per_env_step": d["substeps"] / es,
+           "rows_per_substep": d["nrows"] / max(d["substeps"], 1),
+           "pgs_iters_per_substep": d["pgs_iters"] / max(d["substeps"], 1),
+           "pgs_cycles_per_row_update": d["pgs"] / max(d["nrows"] * d["pgs_iters"] / max(d["substeps"], 1), 1),
+           "collide_cycles_per_substep": d["collide"] / max(d["substeps"], 1),
+           "overlap_pairs_per_substep": d["overlap_pairs"] / max(d["substeps"], 1),
+           "hull_pairs_per_substep": d["hull_pairs"] / max(d["substeps"], 1),
+           "manifolds_per_substep": d["manifolds"] / max(d["substeps"], 1)}
+    for k in ("dyn+enum", "rows", "pgs", "split", "integrate"):
+        out[k + "_cycles_per_substep"] = d[k] / max(d["substeps"], 1)
+    print(json.dumps(out, indent=1))
+    sim.close()
+
+
+if __name__ == "__main__":
+    main()

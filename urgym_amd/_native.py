@@ -9,14 +9,14 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "liburgym.so")
+LIB_PATH = os.environ.get("URGYM_LIB") or os.path.join(_HERE, "_lib", "liburgym.so")
 
 # C-ABI symbols declared in include/urgym.h (checked by tests/test_capi_symbols.py)
 SYMBOLS = [
     "urgym_create", "urgym_destroy", "urgym_last_error", "urgym_obs_dim", "urgym_act_dim", "urgym_state_dim",
     "urgym_num_envs", "urgym_set_autoreset", "urgym_reset", "urgym_num_draws", "urgym_step", "urgym_step_device",
     "urgym_reset_device", "urgym_sync", "urgym_stream", "urgym_get_state", "urgym_set_state", "urgym_substep",
-    "urgym_link_state", "urgym_ik", "urgym_last_kernel_ms",
+    "urgym_link_state", "urgym_ik", "urgym_last_kernel_ms", "urgym_debug_prof",
 ]
 
 _lib = None
@@ -54,6 +54,7 @@ def lib():
     L.urgym_ik.argtypes = [P, P, P]
     L.urgym_last_kernel_ms.restype = D
     L.urgym_last_kernel_ms.argtypes = [P]
+    L.urgym_debug_prof.argtypes = [P, P, I]
     _lib = L
     return L
 

@@ -138,7 +138,6 @@ __global__ void k_build_scene(Scene* s, int task) {
 // ---------------------------------------------------------------------------
 // kernels: one wavefront (block of 64) per environment, state resident in LDS
 // ---------------------------------------------------------------------------
-#define WS_DOUBLES (UG_MAXMAN * UG_MAN_DOUBLES)   // per-env global workspace (old manifolds)
 
 static __device__ int task_obs_dim(int task) { return task == UG_TASK_BALLBALANCE ? 6 : (task == UG_TASK_CUBESGRASP ? 17 : 9); }
 static __device__ int task_act_dim(int task) { return task == UG_TASK_CUBESGRASP ? 9 : 3; }
@@ -147,17 +146,23 @@ static __device__ int task_ndraw(int task) { return task == UG_TASK_CUBESPUSH ? 
 __global__ void __launch_bounds__(TEAM, 1) k_reset(const Scene* sc, double* S, uint32_t* mt, int* elapsed, double* ws,
                                                    int n, const uint8_t* mask, const double* draws, double* obs,
                                                    int32_t* substeps) {
-    __shared__ Shared sh;
     const int i = blockIdx.x;
     if (i >= n) return;
     if (mask && !mask[i]) return;
     double* Si = S + (size_t)i * UG_STATE_DIM;
-    double* wsi = ws + (size_t)i * WS_DOUBLES;
-    team_load(sh, Si);
-    Draws dr{Rng{mt + (size_t)i * UG_MT_WORDS, 1, 0}, draws ? draws + (size_t)i * task_ndraw(sc->task) : nullptr, 0};
-    int O = task_obs_dim(sc->task);
-    int ns = team_bb_reset(sh, sc, wsi, dr, obs + (size_t)i * O);
-    team_store(sh, Si);
+    team_load(Si);
+    RunIO io;
+    io.act = nullptr;
+    io.obs = obs + (size_t)i * task_obs_dim(sc->task);
+    io.final_obs = nullptr;
+    io.dr = Draws{Rng{mt + (size_t)i * UG_MT_WORDS, 1, 0}, draws ? draws + (size_t)i * task_ndraw(sc->task) : nullptr, 0};
+    io.autoreset = 0;
+    io.trunc = 0;
+    PROF_T0(t_tot);
+    int ns = team_run(sc, ws + (size_t)i * WS_DOUBLES, G_RESET, io);
+    PROF_ADD(PF_TOTAL, t_tot);
+    team_store(Si);
+    team_prof_flush();
     if (threadIdx.x == 0) {
         elapsed[i] = 0;
         if (substeps) substeps[i] = ns;
@@ -168,45 +173,42 @@ __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, ui
                                                   int n, const float* act, double* obs, double* final_obs, double* rew,
                                                   uint8_t* term, uint8_t* trunc, uint8_t* succ, int32_t* substeps,
                                                   int autoreset, int max_steps) {
-    __shared__ Shared sh;
     const int i = blockIdx.x;
     if (i >= n) return;
     double* Si = S + (size_t)i * UG_STATE_DIM;
-    double* wsi = ws + (size_t)i * WS_DOUBLES;
-    team_load(sh, Si);
-    int O = task_obs_dim(sc->task), A = task_act_dim(sc->task);
-    double* ob = obs + (size_t)i * O;
-    double r = 0.0;
-    int t = 0, su = 0;
-    int ns = team_bb_step(sh, sc, wsi, act + (size_t)i * A, ob, &r, &t, &su);
-    int el = elapsed[i] + 1;
-    int tr = (max_steps > 0 && el >= max_steps) ? 1 : 0;
-    if (autoreset && (t || tr)) {
-        if (final_obs && threadIdx.x == 0)
-            for (int j = 0; j < O; j++) final_obs[(size_t)i * O + j] = ob[j];
-        Draws dr{Rng{mt + (size_t)i * UG_MT_WORDS, 1, 0}, nullptr, 0};
-        ns += team_bb_reset(sh, sc, wsi, dr, ob);
-        el = 0;
-    }
-    team_store(sh, Si);
+    team_load(Si);
+    const int O = task_obs_dim(sc->task), A = task_act_dim(sc->task);
+    const int el = elapsed[i] + 1;
+    RunIO io;
+    io.act = act + (size_t)i * A;
+    io.obs = obs + (size_t)i * O;
+    io.final_obs = final_obs ? final_obs + (size_t)i * O : nullptr;
+    io.dr = Draws{Rng{mt + (size_t)i * UG_MT_WORDS, 1, 0}, nullptr, 0};
+    io.autoreset = autoreset;
+    io.trunc = (max_steps > 0 && el >= max_steps) ? 1 : 0;
+    io.reset_done = 0;
+    PROF_T0(t_tot);
+    int ns = team_run(sc, ws + (size_t)i * WS_DOUBLES, G_STEP, io);
+    PROF_ADD(PF_TOTAL, t_tot);
+    team_store(Si);
+    team_prof_flush();
     if (threadIdx.x == 0) {
-        elapsed[i] = el;
-        if (rew) rew[i] = r;
-        if (term) term[i] = (uint8_t)t;
-        if (trunc) trunc[i] = (uint8_t)tr;
-        if (succ) succ[i] = (uint8_t)su;
+        elapsed[i] = io.reset_done ? 0 : el;
+        if (rew) rew[i] = io.rew;
+        if (term) term[i] = (uint8_t)io.term;
+        if (trunc) trunc[i] = (uint8_t)io.trunc;
+        if (succ) succ[i] = (uint8_t)io.succ;
         if (substeps) substeps[i] = ns;
     }
 }
 
 __global__ void __launch_bounds__(TEAM, 1) k_substep(const Scene* sc, double* S, double* ws, int n) {
-    __shared__ Shared sh;
     const int i = blockIdx.x;
     if (i >= n) return;
     double* Si = S + (size_t)i * UG_STATE_DIM;
-    team_load(sh, Si);
-    team_substep(sh, sc, ws + (size_t)i * WS_DOUBLES);
-    team_store(sh, Si);
+    team_load(Si);
+    team_substep(sc, ws + (size_t)i * WS_DOUBLES);
+    team_store(Si);
 }
 
 // getLinkState / calculateInverseKinematics queries: one env per lane (not on the step path)
@@ -505,6 +507,25 @@ int urgym_ik(urgym_handle* h, const double* target, double* q_out) {
     HIPCHK(h, hipMemcpyAsync(q_out, d_q, sizeof(double) * NB * N, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
+}
+
+// Phase cycle counters of the team kernels (only a -DUG_PROF build records them):
+// out16 receives the 16 accumulators (ug_team.h PF_* / PC_*); reset != 0 zeroes them.
+int urgym_debug_prof(urgym_handle* h, unsigned long long* out16, int reset) {
+#ifdef UG_PROF
+    if (!h || !out16) return -1;
+    HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16));
+    if (reset) {
+        unsigned long long z[16] = {0};
+        HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
+    }
+    return 0;
+#else
+    (void)h; (void)out16; (void)reset;
+    return -1;
+#endif
 }
 
 }  // extern "C"

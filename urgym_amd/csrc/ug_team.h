@@ -23,13 +23,20 @@
 #ifndef UG_TEAM_H
 #define UG_TEAM_H
 
+#include <utility>
+
 #include "ug_device.h"
 
 namespace ugd {
 
 #define TEAM 64
 #define NVP 32
-#define NSLOT (MAXROWS / 2)
+#define REGROWS 96          /* rows held in VGPR slots; rows beyond stream from the global workspace */
+#define NSLOT (REGROWS / 2)
+/* per-env global workspace (L2-resident): old manifolds (collision), then every row's J | M^-1 J^T
+ * (24 + 24 doubles), written lane-per-row by the row build and read back into the register slots */
+#define WS_ROWS (UG_MAXMAN * UG_MAN_DOUBLES)
+#define WS_DOUBLES (WS_ROWS + MAXROWS * 48)
 #define STAGE 24
 #define MAXOV 40
 
@@ -72,7 +79,33 @@ struct Shared {
     double a12[NB];
     double fs[8];
     int is[8];
+#ifdef UG_PROF
+    unsigned long long prof[16];
+#endif
 };
+
+/* the env's LDS image: one per workgroup; a namespace-scope object gives every access a constant address */
+static __shared__ Shared g_sh;
+
+/* phase timers (build with -DUG_PROF; read back with urgym_debug_prof) */
+#ifdef UG_PROF
+__device__ unsigned long long g_prof[16];
+#define PROF_T0(v) unsigned long long v = __builtin_readcyclecounter()
+#define PROF_ADD(k, v)                                                   \
+    do {                                                                 \
+        if (threadIdx.x == 0) g_sh.prof[k] += __builtin_readcyclecounter() - (v); \
+    } while (0)
+#define PROF_CNT(k, val)                                 \
+    do {                                               \
+        if (threadIdx.x == 0) g_sh.prof[k] += (unsigned long long)(val); \
+    } while (0)
+#else
+#define PROF_T0(v)
+#define PROF_ADD(k, v)
+#define PROF_CNT(k, x)
+#endif
+enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_TOTAL,
+       PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -175,8 +208,9 @@ __device__ static inline void man_to_st(StMan& S, const Manifold& M) {
 
 /* ---------------- collision ---------------- */
 /* hull (A, robot link) vs box (B): the whole wave.  Produces cand k (<= 4 points) in sh.u.cand. */
-__device__ static void team_hull_box(Shared& sh, const Collider& A, const Collider& B, const XF& TA, const XF& TB,
+__device__ __noinline__ static void team_hull_box(const Collider& A, const Collider& B, const XF& TA, const XF& TB,
                                      double thr, int k) {
+    Shared& sh = g_sh;
     const int lane = threadIdx.x;
     m3 RAB = mtm(TB.R, TA.R);
     v3 pAB = mtv(TB.R, vsub(TA.p, TB.p));
@@ -293,7 +327,8 @@ __device__ static void team_hull_box(Shared& sh, const Collider& A, const Collid
 }
 
 /* performDiscreteCollisionDetection (oracle collide()), team version.  ws: this env's global workspace. */
-__device__ static void team_collide(Shared& sh, const Scene* s, double* ws) {
+__device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
+    Shared& sh = g_sh;
     const int lane = threadIdx.x;
     EnvState& e = sh.e;
     if (lane < s->ncol) {
@@ -340,7 +375,8 @@ __device__ static void team_collide(Shared& sh, const Scene* s, double* ws) {
             const Collider& B = s->col[P.b];
             if (A.kind == UG_SHAPE_HULL && B.kind == UG_SHAPE_BOX) {
                 XF TA = shape_xf(sh.O[P.a], A), TB = shape_xf(sh.O[P.b], B);
-                team_hull_box(sh, A, B, TA, TB, P.thr, k);
+                team_hull_box(A, B, TA, TB, P.thr, k);
+                PROF_CNT(PC_HULL, 1);
             }
         }
         /* lane per pair: remaining narrowphases, manifold update */
@@ -511,7 +547,8 @@ __device__ static void enumerate_rows(Shared& sh, const Scene* s) {
     sh.nrows = n; sh.nnc = nnc; sh.nn = nn; sh.nf = nf;
 }
 /* build row at position pos (one lane): J, M^-1 J^T into stage row sl, scalars into rs[pos] */
-__device__ static void build_row(Shared& sh, const Scene* s, int pos, int sl) {
+__device__ __noinline__ static void build_row(const Scene* s, int pos, double* wrow) {
+    Shared& sh = g_sh;
     const EnvState& e = sh.e;
     const double dt = UG_DT;
     RowS& r = sh.rs[pos];
@@ -633,56 +670,180 @@ __device__ static void build_row(Shared& sh, const Scene* s, int pos, int sl) {
         }
     }
     r.invD = invD; r.rinv = invD == 0.0 ? 0.0 : 1.0 / invD; r.rhs = rhs; r.rhsPen = rhsPen; r.lo = lo; r.hi = hi; r.imp = imp; r.impPen = 0.0; r.fric = fric;
-    for (int i = 0; i < 24; i++) { sh.u.stage[sl][i] = J[i]; sh.u.stage[sl][24 + i] = MJ[i]; }
+    for (int i = 0; i < 24; i++) { wrow[i] = J[i]; wrow[24 + i] = MJ[i]; }
 }
 
-/* ---------------- PGS (btMultiBodyConstraintSolver) ---------------- */
-struct Regs {
-    double J[NSLOT], M[NSLOT];
+/* ---------------- PGS (btMultiBodyConstraintSolver) ----------------
+ * Row positions are template parameters, so the register slots RJ[P >> 1] / RM[P >> 1] are
+ * addressed with constants (the arrays stay in VGPRs) and every row-range test is a scalar
+ * branch.  Each row's scalars (rhs, 1/D, bounds, impulse) are fetched from LDS one row ahead. */
+#define NCMAX (2 * NB + 12) /* limits (both sides) + 7 motors + 5 gears */
+struct RowPre {
+    double rhs, invD, rinv, imp, lo, hi, tot;
+    int skip; /* friction row whose normal carries no impulse: not solved this pass */
 };
-/* one row update; p = position, s = slot (compile-time at the call site), h = half */
-__device__ __forceinline__ void pgs_row(Shared& sh, const double& Js, const double& Ms, int p, int h, double& dv,
-                                        double& res, int pen) {
-    RowS& r = sh.rs[p];
-    double lo = r.lo, hi = r.hi;
-    if (!pen && r.kind >= 4) {
-        double tot = sh.rs[r.nrow].imp;
-        if (!(tot > 0.0)) return;
-        lo = -(r.fric * tot);
-        hi = r.fric * tot;
+
+template <int PEN>
+__device__ __forceinline__ RowPre row_fetch(const Shared& sh, int p, int nnc, int fb) {
+    const RowS& r = sh.rs[p];
+    RowPre x;
+    x.invD = r.invD;
+    x.rinv = r.rinv;
+    x.lo = r.lo;
+    x.hi = r.hi;
+    x.tot = 0.0;
+    x.skip = 0;
+    if (PEN) {
+        x.rhs = r.rhsPen; x.imp = r.impPen;
+    } else {
+        x.rhs = r.rhs; x.imp = r.imp;
+        if (p >= fb) {
+            double tot = sh.rs[nnc + ((p - fb) >> 1)].imp, fric = r.fric;
+            x.tot = tot;
+            x.lo = -(fric * tot);
+            x.hi = fric * tot;
+            x.skip = !(tot > 0.0);
+        }
     }
-    double prod = Js * dv;
-    double red = reduce16(prod);
-    double dot = readlane_d(red, 32 * h) + readlane_d(red, 32 * h + 16);
-    double imp = pen ? r.impPen : r.imp;
-    double invD = r.invD;
-    double di = (pen ? r.rhsPen : r.rhs) - imp * 0.0;
-    di -= dot * invD;
-    double sum = imp + di;
-    if (sum < lo) { di = lo - imp; imp = lo; }
-    else if (sum > hi) { di = hi - imp; imp = hi; }
-    else imp = sum;
-    if (threadIdx.x == 0) {
-        if (pen) r.impPen = imp;
-        else r.imp = imp;
-    }
-    double c = Ms * di;
-    dv = dv + half_bcast(c, h);
-    double x = di * r.rinv;
-    x = x * x;
-    res = res > x ? res : x;
+    return x;
+}
+__device__ __forceinline__ void fric_bounds(const Shared& sh, int p, RowPre& x, double tot) {
+    double fric = sh.rs[p].fric;
+    x.tot = tot;
+    x.lo = -(fric * tot);
+    x.hi = fric * tot;
+    x.skip = !(tot > 0.0);
 }
 
+/* lane l of half h gets rowsum(2h) + rowsum(2h+1) of a reduce16 result: its half's 32-slot dot */
+__device__ __forceinline__ double half_dot(double red) {
+    int lo = __double2loint(red), hi = __double2hiint(red);
+    auto plo = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    auto phi = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    double a = __hiloint2double(phi[0], plo[0]);
+    double b = __hiloint2double(phi[1], plo[1]);
+    return a + b;
+}
 
-/* ---------------- one p.stepSimulation() (oracle substep()) ---------------- */
-__device__ static void team_substep(Shared& sh, const Scene* s, double* ws) {
-    const int lane = threadIdx.x;
-    const int h = lane >> 5, d = lane & 31;
+/* resolveSingleConstraintRowGeneric [ext] (oracle solve_row) for the row held by half H.  Lanes of the
+ * other half compute with their own (unrelated) dot and are ignored: the impulse change reaches dv
+ * through a half-H broadcast, the new impulse is valid in half H, the residual is kept per half. */
+template <int H>
+__device__ __forceinline__ double pgs_update(double Js, double Ms, const RowPre& c, double& dv, double& res) {
+    double dot = half_dot(reduce16(Js * dv));
+    double imp = c.imp;
+    double di = c.rhs - dot * c.invD;
+    double sum = imp + di;
+    bool below = sum < c.lo, above = sum > c.hi;
+    double dn = below ? c.lo - imp : (above ? c.hi - imp : di);
+    double in = below ? c.lo : (above ? c.hi : sum);
+    dv = dv + half_bcast(Ms * dn, H);
+    double x = dn * c.rinv;
+    x = x * x;
+    double rn = res > x ? res : x;
+    bool inH = (int)(threadIdx.x >> 5) == H;
+    res = inH ? rn : res;
+    return in;
+}
+
+template <int P>
+__device__ __forceinline__ void row_jm(const double (&RJ)[NSLOT], const double (&RM)[NSLOT], const double* ws, int d,
+                                       double& Js, double& Ms) {
+    if constexpr (P < REGROWS) {
+        Js = RJ[P >> 1];
+        Ms = RM[P >> 1];
+    } else {
+        const double* x = ws + WS_ROWS + P * 48;
+        int dd = d < 24 ? d : 0;
+        double a = x[dd], b = x[24 + dd];
+        Js = d < 24 ? a : 0.0;
+        Ms = d < 24 ? b : 0.0;
+    }
+}
+/* rows [start, end) in increasing position; cur = fetched data of row max(P, start) */
+template <int P, int PEN>
+__device__ __forceinline__ void pgs_fwd(Shared& sh, const double (&RJ)[NSLOT], const double (&RM)[NSLOT], const double* ws,
+                                        int d, int start, int end, int nnc, int fb, double& dv, double& res, RowPre cur) {
+    if constexpr (P < MAXROWS) {
+        if (P < end) {
+            RowPre next = cur;
+            if (P >= start) {
+                RowPre nxt = row_fetch<PEN>(sh, P + 1 < MAXROWS ? P + 1 : P, nnc, fb);
+                if (PEN || !__builtin_amdgcn_readfirstlane(cur.skip)) {
+                    double Js, Ms;
+                    row_jm<P>(RJ, RM, ws, d, Js, Ms);
+                    double imp = pgs_update<P & 1>(Js, Ms, cur, dv, res);
+                    if (threadIdx.x == 32 * (P & 1)) {
+                        if (PEN) sh.rs[P].impPen = imp;
+                        else sh.rs[P].imp = imp;
+                    }
+                    /* the next row's bound source may be this very normal (fetched before the store) */
+                    if (!PEN && P >= nnc && P < fb && P + 1 >= fb && nnc + ((P + 1 - fb) >> 1) == P)
+                        fric_bounds(sh, P + 1, nxt, readlane_d(imp, 32 * (P & 1)));
+                }
+                next = nxt;
+            }
+            pgs_fwd<P + 1, PEN>(sh, RJ, RM, ws, d, start, end, nnc, fb, dv, res, next);
+        }
+    }
+}
+/* non-contact rows in decreasing position (even iterations); cur = fetched data of row min(P, nnc-1) */
+template <int P>
+__device__ __forceinline__ void pgs_rev(Shared& sh, const double (&RJ)[NSLOT], const double (&RM)[NSLOT], int nnc,
+                                        double& dv, double& res, RowPre cur) {
+    if constexpr (P >= 0) {
+        RowPre next = cur;
+        if (P < nnc) {
+            next = row_fetch<0>(sh, P > 0 ? P - 1 : 0, nnc, MAXROWS);
+            double imp = pgs_update<P & 1>(RJ[P >> 1], RM[P >> 1], cur, dv, res);
+            if (threadIdx.x == 32 * (P & 1)) sh.rs[P].imp = imp;
+        }
+        pgs_rev<P - 1>(sh, RJ, RM, nnc, dv, res, next);
+    }
+}
+/* warm start: normal rows with a carried impulse */
+template <int P>
+__device__ __forceinline__ void pgs_warm(Shared& sh, const double (&RJ)[NSLOT], const double (&RM)[NSLOT],
+                                         const double* ws, int d, int nnc, int fb, double& dv) {
+    if constexpr (P < MAXROWS) {
+        if (P < fb) {
+            if (P >= nnc) {
+                double imp = sh.rs[P].imp;
+                double Js, Ms;
+                row_jm<P>(RJ, RM, ws, d, Js, Ms);
+                double bc = half_bcast(Ms * imp, P & 1);
+                double dvn = dv + bc;
+                dv = imp != 0.0 ? dvn : dv;
+            }
+            pgs_warm<P + 1>(sh, RJ, RM, ws, d, nnc, fb, dv);
+        }
+    }
+}
+/* rows (global workspace) -> register slots of their half: lane d of half h holds J[d], M^-1J[d] of row 2*SL+h */
+template <int SL>
+__device__ __forceinline__ void load_slots(const double* ws, double (&RJ)[NSLOT], double (&RM)[NSLOT], int n, int h,
+                                           int d) {
+    if constexpr (SL < NSLOT) {
+        if (2 * SL < n) {
+            int p = 2 * SL + h;
+            bool in = p < n && d < 24;
+            const double* x = ws + WS_ROWS + (p < n ? p : 0) * 48 + (d < 24 ? d : 0);
+            double vj = x[0], vm = x[24];
+            RJ[SL] = in ? vj : 0.0;
+            RM[SL] = in ? vm : 0.0;
+            load_slots<SL + 1>(ws, RJ, RM, n, h, d);
+        }
+    }
+}
+__device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+/* lane 0: external forces (robot gravity/gyroscopic/damping via CRBA + RNEA, free objects), the LDL^T of
+ * the mass matrix, and the row enumeration */
+__device__ __noinline__ static void serial_pre(const Scene* s) {
+    Shared& sh = g_sh;
     EnvState& e = sh.e;
     const double dt = UG_DT;
-    if (lane == 0) fk(e.q, sh.kin);
-    __syncthreads();
-    team_collide(sh, s, ws);
+    const int lane = threadIdx.x;
     if (lane == 0) {
         double C[NB];
         robot_dynamics(e.qd, sh.kin, s->gravity, sh.LDL, C);
@@ -713,96 +874,13 @@ __device__ static void team_substep(Shared& sh, const Scene* s, double* ws) {
         }
         enumerate_rows(sh, s);
     }
-    __syncthreads();
-    const int n = sh.nrows, nnc = sh.nnc, nn = sh.nn;
-    /* rows: built lane-per-row in batches, then moved into the register slots of their half */
-    double RJ[NSLOT], RM[NSLOT];
-    for (int base = 0; base < n; base += STAGE) {
-        int cnt = n - base < STAGE ? n - base : STAGE;
-        if (lane < cnt) build_row(sh, s, base + lane, lane);
-        __syncthreads();
-#pragma unroll
-        for (int sl = 0; sl < NSLOT; sl++) {
-            if (2 * sl + 1 < base || 2 * sl >= base + cnt) continue;
-            int r = 2 * sl + h - base;
-            bool in = r >= 0 && r < cnt;
-            int rr = in ? r : 0;
-            int dd = d < 24 ? d : 0;
-            double vj = sh.u.stage[rr][dd], vm = sh.u.stage[rr][24 + dd];
-            if (in) {
-                RJ[sl] = d < 24 ? vj : 0.0;
-                RM[sl] = d < 24 ? vm : 0.0;
-            }
-        }
-        __syncthreads();
-    }
-    /* PGS: warm start (normals), iterations; split-impulse pass */
-    double dv = 0.0, dvs = 0.0;
-#pragma unroll
-    for (int sl = 0; sl < NSLOT; sl++) {
-        if (2 * sl + 1 < nnc || 2 * sl >= nnc + nn) continue;
-#pragma unroll
-        for (int hh = 0; hh < 2; hh++) {
-            int p = 2 * sl + hh;
-            if (p < nnc || p >= nnc + nn) continue;
-            double imp = sh.rs[p].imp;
-            if (imp != 0.0) dv = dv + half_bcast(RM[sl] * imp, hh);
-        }
-    }
-    for (int it = 0; it < UG_PGS_ITERS; it++) {
-        double res = 0.0;
-        int start = 0;
-        if (!(it & 1)) {
-#pragma unroll
-            for (int sl = NSLOT - 1; sl >= 0; sl--) {
-                if (2 * sl >= nnc) continue;
-#pragma unroll
-                for (int hh = 1; hh >= 0; hh--) {
-                    int p = 2 * sl + hh;
-                    if (p < nnc) pgs_row(sh, RJ[sl], RM[sl], p, hh, dv, res, 0);
-                }
-            }
-            start = nnc;
-        }
-#pragma unroll
-        for (int sl = 0; sl < NSLOT; sl++) {
-            if (2 * sl + 1 < start || 2 * sl >= n) continue;
-#pragma unroll
-            for (int hh = 0; hh < 2; hh++) {
-                int p = 2 * sl + hh;
-                if (p >= start && p < n) pgs_row(sh, RJ[sl], RM[sl], p, hh, dv, res, 0);
-            }
-        }
-        if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
-    }
-    int anypen = 0;
-    for (int p = nnc + lane; p < nnc + nn; p += TEAM) anypen |= sh.rs[p].rhsPen != 0.0;
-    int split = ballot(anypen) != 0ull;
-    if (split) {
-        for (int it = 0; it < UG_PGS_ITERS; it++) {
-            double res = 0.0;
-#pragma unroll
-            for (int sl = 0; sl < NSLOT; sl++) {
-                if (2 * sl + 1 < nnc || 2 * sl >= nnc + nn) continue;
-#pragma unroll
-                for (int hh = 0; hh < 2; hh++) {
-                    int p = 2 * sl + hh;
-                    if (p >= nnc && p < nnc + nn) pgs_row(sh, RJ[sl], RM[sl], p, hh, dvs, res, 1);
-                }
-            }
-            if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
-        }
-    }
-    if (lane < NVP) { sh.dvout[lane] = dv; sh.dvsout[lane] = dvs; }
-    /* impulses back into the manifold points (lane per row) */
-    for (int p = nnc + lane; p < n; p += TEAM) {
-        const RowS& r = sh.rs[p];
-        StPt& pt = e.man[r.a].pt[r.b];
-        if (r.kind == 3) pt.imp = r.imp;
-        else if (r.kind == 4) pt.imp1 = r.imp;
-        else pt.imp2 = r.imp;
-    }
-    __syncthreads();
+}
+/* lane 0: velocities += solver delta, positions integrate (v + split velocity) */
+__device__ __noinline__ static void serial_post(const Scene* s, int split) {
+    Shared& sh = g_sh;
+    EnvState& e = sh.e;
+    const double dt = UG_DT;
+    const int lane = threadIdx.x;
     if (lane == 0) {
         const double* DV = sh.dvout;
         const double* DVS = sh.dvsout;
@@ -832,24 +910,95 @@ __device__ static void team_substep(Shared& sh, const Scene* s, double* ws) {
             ob.quat = qnormalize(qmul(dq, ob.quat));
         }
     }
-    __syncthreads();
+}
+__device__ __noinline__ static void serial_fk() {
+    if (threadIdx.x == 0) fk(g_sh.e.q, g_sh.kin);
 }
 
-/* wait_until_stable (env_ball_balance_v0.py:94-103): returns substeps taken */
-__device__ static int team_wait(Shared& sh, const Scene* s, double* ws) {
+/* ---------------- one p.stepSimulation() (oracle substep()) ---------------- */
+__device__ __forceinline__ static void team_substep(const Scene* s, double* ws) {
+    Shared& sh = g_sh;
     const int lane = threadIdx.x;
-    double pos = lane < NB ? sh.e.q[lane] : 0.0;
-    for (int i = 0; i < UG_STABLE_STEPS; i++) {
-        team_substep(sh, s, ws);
-        double qn = lane < NB ? sh.e.q[lane] : 0.0;
-        if (lane < NB) sh.a12[lane] = ug_fabs(pos - qn);
-        __syncthreads();
-        if (lane == 0) sh.is[0] = np_sum12(sh.a12) < UG_STABLE_EPS;
-        __syncthreads();
-        if (sh.is[0]) return i + 1;
-        pos = qn;
+    const int h = lane >> 5, d = lane & 31;
+    EnvState& e = sh.e;
+    const double dt = UG_DT;
+    PROF_T0(t_col);
+    serial_fk();
+    __syncthreads();
+    team_collide(s, ws);
+    PROF_ADD(PF_COLLIDE, t_col);
+    PROF_T0(t_dyn);
+    serial_pre(s);
+    __syncthreads();
+    PROF_ADD(PF_DYN, t_dyn);
+    PROF_T0(t_rows);
+    const int n = uniform(sh.nrows), nnc = uniform(sh.nnc), nn = uniform(sh.nn);
+    const int fb = nnc + nn;
+    PROF_CNT(PC_SUBSTEPS, 1);
+    PROF_CNT(PC_ROWS, n);
+    PROF_CNT(PC_OVL, sh.nov);
+    PROF_CNT(PC_NMAN, (int)e.nman);
+    /* rows: built lane-per-row in batches, then moved into the register slots of their half */
+    for (int p = lane; p < n; p += TEAM) build_row(s, p, ws + WS_ROWS + p * 48);
+    __threadfence_block();
+    __syncthreads();
+    double RJ[NSLOT], RM[NSLOT];
+#pragma unroll
+    for (int sl = 0; sl < NSLOT; sl++) { RJ[sl] = 0.0; RM[sl] = 0.0; }
+    load_slots<0>(ws, RJ, RM, n, h, d);
+    PROF_ADD(PF_ROWS, t_rows);
+    PROF_T0(t_pgs);
+    /* PGS: warm start (normals), iterations; split-impulse pass */
+    double dv = 0.0, dvs = 0.0;
+    pgs_warm<0>(sh, RJ, RM, ws, d, nnc, fb, dv);
+    for (int it = 0; it < UG_PGS_ITERS; it++) {
+        double res = 0.0;
+        /* opaque per-iteration copies: keeps the per-row scalar tests inside the loop instead of
+         * hoisting ~128 of them into (spilled) SGPRs */
+        int o_n = n, o_nnc = nnc, o_fb = fb;
+        asm volatile("" : "+s"(o_n), "+s"(o_nnc), "+s"(o_fb));
+        int start = 0;
+        if (!(it & 1)) {
+            if (o_nnc > 0) pgs_rev<NCMAX - 1>(sh, RJ, RM, o_nnc, dv, res, row_fetch<0>(sh, o_nnc - 1, o_nnc, MAXROWS));
+            start = o_nnc;
+        }
+        if (start < o_n) pgs_fwd<0, 0>(sh, RJ, RM, ws, d, start, o_n, o_nnc, o_fb, dv, res, row_fetch<0>(sh, start, o_nnc, o_fb));
+        PROF_CNT(PC_ITERS, 1);
+        double r0 = readlane_d(res, 0), r1 = readlane_d(res, 32);
+        double rall = r0 > r1 ? r0 : r1;
+        if (rall <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
     }
-    return UG_STABLE_STEPS;
+    PROF_ADD(PF_PGS, t_pgs);
+    PROF_T0(t_split);
+    int anypen = 0;
+    for (int p = nnc + lane; p < fb; p += TEAM) anypen |= sh.rs[p].rhsPen != 0.0;
+    int split = ballot(anypen) != 0ull;
+    if (split) {
+        for (int it = 0; it < UG_PGS_ITERS; it++) {
+            double res = 0.0;
+            int o_nnc = nnc, o_fb = fb;
+            asm volatile("" : "+s"(o_nnc), "+s"(o_fb));
+            pgs_fwd<0, 1>(sh, RJ, RM, ws, d, o_nnc, o_fb, o_nnc, o_fb, dvs, res, row_fetch<1>(sh, o_nnc, o_nnc, o_fb));
+            double r0 = readlane_d(res, 0), r1 = readlane_d(res, 32);
+            double rall = r0 > r1 ? r0 : r1;
+            if (rall <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
+        }
+    }
+    PROF_ADD(PF_SPLIT, t_split);
+    PROF_T0(t_int);
+    if (lane < NVP) { sh.dvout[lane] = dv; sh.dvsout[lane] = dvs; }
+    /* impulses back into the manifold points (lane per row) */
+    for (int p = nnc + lane; p < n; p += TEAM) {
+        const RowS& r = sh.rs[p];
+        StPt& pt = e.man[r.a].pt[r.b];
+        if (r.kind == 3) pt.imp = r.imp;
+        else if (r.kind == 4) pt.imp1 = r.imp;
+        else pt.imp2 = r.imp;
+    }
+    __syncthreads();
+    serial_post(s, split);
+    __syncthreads();
+    PROF_ADD(PF_INTEG, t_int);
 }
 
 /* ---------------- robot control + BallBalance glue (lane 0 unless noted) ---------------- */
@@ -933,77 +1082,147 @@ __device__ static void bb_obs(const EnvState& e, double* obs) {
     obs[4] = e.obj[0].pos.y - e.obj[1].pos.y;
     obs[5] = e.obj[0].pos.z - e.obj[1].pos.z;
 }
-/* env_ball_balance_v0.py:145-170 (obs written by lane 0) */
-__device__ static int team_bb_reset(Shared& sh, const Scene* s, double* ws, Draws& dr, double* obs) {
-    const int lane = threadIdx.x;
-    EnvState& e = sh.e;
-    if (lane == 0) {
-        e.goal_approached = 0.0;
-        e.goal_grasped = 0.0;
-        for (int i = 0; i < 6; i++) { e.q[i] = UG_ARM_REST[i]; e.qd[i] = 0.0; }
+/* ---------------- the env program: step / reset as one substep loop ----------------
+ * The reference's control flow (env_ball_balance_v0.py: step 105-134, reset 145-170, wait_until_stable
+ * 94-103, robot.reset 89-106) is a sequence of glue actions separated by physics loops.  It runs here as
+ * a small state machine around a single inlined team_substep(), so the PGS register slots exist once. */
+enum { G_STEP = 0, G_STEP_DONE, G_RESET, G_RESET_ROBOT, G_RESET_PLACE, G_RESET_DONE, G_END };
+enum { L_NONE = 0, L_FIXED10, L_WAIT };
+struct RunIO {
+    const float* act;    /* step action (task act_dim floats) */
+    double* obs;         /* obs row */
+    double* final_obs;   /* final obs row (autoreset) or null */
+    Draws dr;            /* reset draws */
+    int autoreset, trunc;
+    double rew;
+    int term, succ, reset_done;
+};
+/* lane-0 glue of one program point; returns the physics loop to run next and sets *next */
+__device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* next) {
+    EnvState& e = g_sh.e;
+    switch (pc) {
+        case G_STEP: { /* env_ball_balance_v0.py:105-118: move_ee(end pose + action) */
+            v3 pe;
+            q4 oe;
+            link_state_of(e.q, UG_EE_LINK, pe, oe);
+            v3 eu = euler_from_quat(oe);
+            eu.x += (double)io.act[0]; eu.y += (double)io.act[1]; eu.z += (double)io.act[2];
+            move_ee_end(e, pe, quat_from_euler(eu));
+            *next = G_STEP_DONE;
+            return L_WAIT;
+        }
+        case G_STEP_DONE: /* :119-134 reward 1, terminated when the ball falls below the paddle */
+            io.rew = 1.0;
+            io.term = e.obj[1].pos.z < e.obj[0].pos.z;
+            io.succ = 0;
+            bb_obs(e, io.obs);
+            if (io.autoreset && (io.term || io.trunc)) {
+                if (io.final_obs)
+                    for (int j = 0; j < 6; j++) io.final_obs[j] = io.obs[j];
+                *next = G_RESET;
+                return L_NONE;
+            }
+            *next = G_END;
+            return L_NONE;
+        case G_RESET: /* robot.reset(): reset_arm (rest pose) + 10 substeps */
+            e.goal_approached = 0.0;
+            e.goal_grasped = 0.0;
+            for (int i = 0; i < 6; i++) { e.q[i] = UG_ARM_REST[i]; e.qd[i] = 0.0; }
+            *next = G_RESET_ROBOT;
+            return L_FIXED10;
+        case G_RESET_ROBOT: /* open_gripper; remove paddle/ball; move_ee(start pose); open 20% */
+            open_gripper(e, 100.0);
+            remove_object(e, s, 0);
+            remove_object(e, s, 1);
+            move_ee_end(e, V(0.0, -0.60, 0.60), Q(0.50, -0.50, -0.50, 0.50));
+            open_gripper(e, 20.0);
+            *next = G_RESET_PLACE;
+            return L_WAIT;
+        case G_RESET_PLACE: { /* create paddle between the fingers, ball above it; close gripper */
+            v3 pe;
+            q4 oe;
+            link_state_of(e.q, UG_EE_LINK, pe, oe);
+            v3 gc = gripper_center(e.q);
+            v3 pose = V(pe.x, pe.y - 0.2, gc.z);
+            place_object(e, 0, pose, Q(0, 0, 0, 1));
+            v3 bp = V(pose.x, pose.y, pose.z + 0.2 + UG_BB_BALL_R);
+            bp.x += io.dr.uniform(-0.03, 0.03);
+            bp.y += io.dr.uniform(-0.08, 0.02);
+            place_object(e, 1, bp, e.obj[0].quat);
+            close_gripper(e, 100.0);
+            *next = G_RESET_DONE;
+            return L_WAIT;
+        }
+        case G_RESET_DONE:
+            bb_obs(e, io.obs);
+            io.reset_done = 1;
+            *next = G_END;
+            return L_NONE;
     }
-    __syncthreads();
-    int n = 0;
-    for (int i = 0; i < 10; i++) team_substep(sh, s, ws);
-    n += 10;
-    if (lane == 0) {
-        open_gripper(e, 100.0);
-        remove_object(e, s, 0);
-        remove_object(e, s, 1);
-        move_ee_end(e, V(0.0, -0.60, 0.60), Q(0.50, -0.50, -0.50, 0.50));
-        open_gripper(e, 20.0);
-    }
-    __syncthreads();
-    n += team_wait(sh, s, ws);
-    if (lane == 0) {
-        v3 pe;
-        q4 oe;
-        link_state_of(e.q, UG_EE_LINK, pe, oe);
-        v3 gc = gripper_center(e.q);
-        v3 pose = V(pe.x, pe.y - 0.2, gc.z);
-        place_object(e, 0, pose, Q(0, 0, 0, 1));
-        v3 bp = V(pose.x, pose.y, pose.z + 0.2 + UG_BB_BALL_R);
-        bp.x += dr.uniform(-0.03, 0.03);
-        bp.y += dr.uniform(-0.08, 0.02);
-        place_object(e, 1, bp, e.obj[0].quat);
-        close_gripper(e, 100.0);
-    }
-    __syncthreads();
-    n += team_wait(sh, s, ws);
-    if (lane == 0) bb_obs(e, obs);
-    return n;
+    *next = G_END;
+    return L_NONE;
 }
-/* env_ball_balance_v0.py:105-134 */
-__device__ static int team_bb_step(Shared& sh, const Scene* s, double* ws, const float* a, double* obs, double* rew,
-                                   int* term, int* succ) {
+/* runs the program from pc0 to the end; returns physics substeps taken */
+__device__ __forceinline__ static int team_run(const Scene* s, double* ws, int pc0, RunIO& io) {
+    Shared& sh = g_sh;
     const int lane = threadIdx.x;
-    EnvState& e = sh.e;
-    if (lane == 0) {
-        v3 pe;
-        q4 oe;
-        link_state_of(e.q, UG_EE_LINK, pe, oe);
-        v3 eu = euler_from_quat(oe);
-        eu.x += (double)a[0]; eu.y += (double)a[1]; eu.z += (double)a[2];
-        q4 qn = quat_from_euler(eu);
-        move_ee_end(e, pe, qn);
+    int pc = pc0, ns = 0;
+    while (true) {
+        PROF_T0(t_glue);
+        if (lane == 0) {
+            int next;
+            sh.is[1] = glue(s, pc, io, &next);
+            sh.is[2] = next;
+        }
+        __syncthreads();
+        PROF_ADD(PF_GLUE, t_glue);
+        int loop = uniform(sh.is[1]);
+        pc = uniform(sh.is[2]);
+        if (loop == L_NONE) {
+            if (pc == G_END) break;
+            continue;
+        }
+        /* physics: 10 fixed substeps, or wait_until_stable (<= 480 substeps until sum|dq| < eps) */
+        double pos = lane < NB ? sh.e.q[lane] : 0.0;
+        for (int i = 0;; i++) {
+            team_substep(s, ws);
+            ns++;
+            if (loop == L_FIXED10) {
+                if (i + 1 == 10) break;
+                continue;
+            }
+            double qn = lane < NB ? sh.e.q[lane] : 0.0;
+            if (lane < NB) sh.a12[lane] = ug_fabs(pos - qn);
+            __syncthreads();
+            if (lane == 0) sh.is[0] = np_sum12(sh.a12) < UG_STABLE_EPS;
+            __syncthreads();
+            if (uniform(sh.is[0]) || i + 1 == UG_STABLE_STEPS) break;
+            pos = qn;
+        }
     }
-    __syncthreads();
-    int n = team_wait(sh, s, ws);
-    *rew = 1.0;
-    *term = e.obj[1].pos.z < e.obj[0].pos.z;
-    *succ = 0;
-    if (lane == 0) bb_obs(e, obs);
-    return n;
+    return ns;
 }
 
 /* ---------------- state in/out (cooperative, canonical layout) ---------------- */
-__device__ static void team_load(Shared& sh, const double* S) {
+__device__ static void team_load(const double* S) {
+    Shared& sh = g_sh;
     double* dst = (double*)&sh.e;
     for (int i = threadIdx.x; i < UG_STATE_DIM; i += TEAM) dst[i] = S[i];
+#ifdef UG_PROF
+    if (threadIdx.x < 16) sh.prof[threadIdx.x] = 0;
+#endif
     __syncthreads();
 }
+__device__ static void team_prof_flush() {
+    Shared& sh = g_sh;
+#ifdef UG_PROF
+    __syncthreads();
+    if (threadIdx.x < 16) atomicAdd(&g_prof[threadIdx.x], sh.prof[threadIdx.x]);
+#endif
+}
 /* manifold slots beyond nman are written as (pair -1, zeros), as ugo_get_state does */
-__device__ static void team_store(const Shared& sh, double* S) {
+__device__ static void team_store(double* S) {
+    const Shared& sh = g_sh;
     const double* src = (const double*)&sh.e;
     int nm = (int)sh.e.nman;
     for (int i = threadIdx.x; i < UG_STATE_DIM; i += TEAM) {
