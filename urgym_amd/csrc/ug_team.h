@@ -32,7 +32,7 @@ namespace ugd {
 #define TEAM 64
 #define NVP 32
 #define REGROWS 96          /* rows held in VGPR slots; rows beyond stream from the global workspace */
-#define NSLOT (REGROWS / 2)
+#define NSLOT REGROWS       /* one row per register slot: lane d holds J[d], M^-1J[d] */
 /* per-env global workspace (L2-resident): old manifolds (collision), then every row's J | M^-1 J^T
  * (24 + 24 doubles), written lane-per-row by the row build and read back into the register slots */
 #define WS_ROWS (UG_MAXMAN * UG_MAN_DOUBLES)
@@ -674,75 +674,65 @@ __device__ __noinline__ static void build_row(const Scene* s, int pos, double* w
 }
 
 /* ---------------- PGS (btMultiBodyConstraintSolver) ----------------
- * Row positions are template parameters, so the register slots RJ[P >> 1] / RM[P >> 1] are
+ * Row positions are template parameters, so the register slots RJ[P] / RM[P] are
  * addressed with constants (the arrays stay in VGPRs) and every row-range test is a scalar
  * branch.  Each row's scalars (rhs, 1/D, bounds, impulse) are fetched from LDS one row ahead. */
 #define NCMAX (2 * NB + 12) /* limits (both sides) + 7 motors + 5 gears */
 struct RowPre {
-    double rhs, invD, rinv, imp, lo, hi, tot;
-    int skip; /* friction row whose normal carries no impulse: not solved this pass */
+    double rhs, invD, rinv, lo, hi, fric; /* LDS values, fetched one row ahead */
 };
+/* row impulses, lane-distributed in two VGPR pairs: row r's impulse sits in lane (r & 63) of v[r >> 6]
+ * (read with v_readlane, written with a lane-select: no LDS traffic inside the iteration loop) */
+struct Imps {
+    double v[2];
+};
+template <int P>
+__device__ __forceinline__ double imp_get(const Imps& I) { return readlane_d(I.v[P >> 6], P & 63); }
+__device__ __forceinline__ double imp_get_dyn(const Imps& I, int r) {
+    double src = r >= 64 ? I.v[1] : I.v[0];
+    return readlane_d(src, r & 63);
+}
+template <int P>
+__device__ __forceinline__ void imp_set(Imps& I, double x) {
+    I.v[P >> 6] = (int)threadIdx.x == (P & 63) ? x : I.v[P >> 6];
+}
 
 template <int PEN>
-__device__ __forceinline__ RowPre row_fetch(const Shared& sh, int p, int nnc, int fb) {
+__device__ __forceinline__ RowPre row_fetch(const Shared& sh, int p) {
     const RowS& r = sh.rs[p];
     RowPre x;
     x.invD = r.invD;
     x.rinv = r.rinv;
     x.lo = r.lo;
     x.hi = r.hi;
-    x.tot = 0.0;
-    x.skip = 0;
-    if (PEN) {
-        x.rhs = r.rhsPen; x.imp = r.impPen;
-    } else {
-        x.rhs = r.rhs; x.imp = r.imp;
-        if (p >= fb) {
-            double tot = sh.rs[nnc + ((p - fb) >> 1)].imp, fric = r.fric;
-            x.tot = tot;
-            x.lo = -(fric * tot);
-            x.hi = fric * tot;
-            x.skip = !(tot > 0.0);
-        }
-    }
+    x.rhs = PEN ? r.rhsPen : r.rhs;
+    x.fric = PEN ? 0.0 : r.fric;
     return x;
 }
-__device__ __forceinline__ void fric_bounds(const Shared& sh, int p, RowPre& x, double tot) {
-    double fric = sh.rs[p].fric;
-    x.tot = tot;
-    x.lo = -(fric * tot);
-    x.hi = fric * tot;
-    x.skip = !(tot > 0.0);
-}
 
-/* lane l of half h gets rowsum(2h) + rowsum(2h+1) of a reduce16 result: its half's 32-slot dot */
-__device__ __forceinline__ double half_dot(double red) {
-    int lo = __double2loint(red), hi = __double2hiint(red);
-    auto plo = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-    auto phi = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-    double a = __hiloint2double(phi[0], plo[0]);
-    double b = __hiloint2double(phi[1], plo[1]);
-    return a + b;
+/* branch-free select on the bit patterns (keeps the clamp out of control flow) */
+__device__ __forceinline__ double bsel(bool c, double a, double b) {
+    unsigned long long m = 0ull - (unsigned long long)c;
+    unsigned long long r = (__double_as_longlong(a) & m) | (__double_as_longlong(b) & ~m);
+    return __longlong_as_double(r);
 }
-
-/* resolveSingleConstraintRowGeneric [ext] (oracle solve_row) for the row held by half H.  Lanes of the
- * other half compute with their own (unrelated) dot and are ignored: the impulse change reaches dv
- * through a half-H broadcast, the new impulse is valid in half H, the residual is kept per half. */
-template <int H>
-__device__ __forceinline__ double pgs_update(double Js, double Ms, const RowPre& c, double& dv, double& res) {
-    double dot = half_dot(reduce16(Js * dv));
-    double imp = c.imp;
+/* resolveSingleConstraintRowGeneric [ext] (oracle solve_row).  Lane d owns generalized-velocity slot d
+ * (both halves hold the same slots): the dot is a 16-lane DPP tree per row of lanes plus two readlanes,
+ * after which the row's scalar math is wave-uniform and the velocity update is lane-local. */
+__device__ __forceinline__ double pgs_update(double Js, double Ms, const RowPre& c, double imp, double& dv,
+                                             double& res) {
+    double red = reduce16(Js * dv);
+    double dot = readlane_d(red, 0) + readlane_d(red, 16);
     double di = c.rhs - dot * c.invD;
     double sum = imp + di;
     bool below = sum < c.lo, above = sum > c.hi;
-    double dn = below ? c.lo - imp : (above ? c.hi - imp : di);
-    double in = below ? c.lo : (above ? c.hi : sum);
-    dv = dv + half_bcast(Ms * dn, H);
+    double dlo = c.lo - imp, dhi = c.hi - imp;
+    double dn = bsel(below, dlo, bsel(above, dhi, di));
+    double in = bsel(below, c.lo, bsel(above, c.hi, sum));
+    dv = dv + Ms * dn;
     double x = dn * c.rinv;
     x = x * x;
-    double rn = res > x ? res : x;
-    bool inH = (int)(threadIdx.x >> 5) == H;
-    res = inH ? rn : res;
+    res = res > x ? res : x;
     return in;
 }
 
@@ -750,8 +740,8 @@ template <int P>
 __device__ __forceinline__ void row_jm(const double (&RJ)[NSLOT], const double (&RM)[NSLOT], const double* ws, int d,
                                        double& Js, double& Ms) {
     if constexpr (P < REGROWS) {
-        Js = RJ[P >> 1];
-        Ms = RM[P >> 1];
+        Js = RJ[P];
+        Ms = RM[P];
     } else {
         const double* x = ws + WS_ROWS + P * 48;
         int dd = d < 24 ? d : 0;
@@ -760,78 +750,78 @@ __device__ __forceinline__ void row_jm(const double (&RJ)[NSLOT], const double (
         Ms = d < 24 ? b : 0.0;
     }
 }
-/* rows [start, end) in increasing position; cur = fetched data of row max(P, start) */
+/* rows [start, end) in increasing position; cur = fetched data of row max(P, start).  Friction rows
+ * (P >= fb) take bounds +-mu * (their normal's current impulse) and are skipped while it is not positive */
 template <int P, int PEN>
 __device__ __forceinline__ void pgs_fwd(Shared& sh, const double (&RJ)[NSLOT], const double (&RM)[NSLOT], const double* ws,
-                                        int d, int start, int end, int nnc, int fb, double& dv, double& res, RowPre cur) {
+                                        int d, int start, int end, int nnc, int fb, Imps& I, double& dv, double& res,
+                                        RowPre cur) {
     if constexpr (P < MAXROWS) {
         if (P < end) {
             RowPre next = cur;
-            if (P >= start) {
-                RowPre nxt = row_fetch<PEN>(sh, P + 1 < MAXROWS ? P + 1 : P, nnc, fb);
-                if (PEN || !__builtin_amdgcn_readfirstlane(cur.skip)) {
+            /* start is 0 or nnc <= NCMAX: rows from NCMAX on are always inside the range */
+            if (P >= NCMAX || P >= start) {
+                RowPre nxt = row_fetch<PEN>(sh, P + 1 < MAXROWS ? P + 1 : P);
+                double imp = imp_get<P>(I);
+                bool skip = false;
+                if (!PEN && P >= fb) {
+                    double tot = imp_get_dyn(I, nnc + ((P - fb) >> 1));
+                    cur.lo = -(cur.fric * tot);
+                    cur.hi = cur.fric * tot;
+                    skip = __builtin_amdgcn_readfirstlane((int)!(tot > 0.0)) != 0;
+                }
+                if (!skip) {
                     double Js, Ms;
                     row_jm<P>(RJ, RM, ws, d, Js, Ms);
-                    double imp = pgs_update<P & 1>(Js, Ms, cur, dv, res);
-                    if (threadIdx.x == 32 * (P & 1)) {
-                        if (PEN) sh.rs[P].impPen = imp;
-                        else sh.rs[P].imp = imp;
-                    }
-                    /* the next row's bound source may be this very normal (fetched before the store) */
-                    if (!PEN && P >= nnc && P < fb && P + 1 >= fb && nnc + ((P + 1 - fb) >> 1) == P)
-                        fric_bounds(sh, P + 1, nxt, readlane_d(imp, 32 * (P & 1)));
+                    imp_set<P>(I, pgs_update(Js, Ms, cur, imp, dv, res));
                 }
                 next = nxt;
             }
-            pgs_fwd<P + 1, PEN>(sh, RJ, RM, ws, d, start, end, nnc, fb, dv, res, next);
+            pgs_fwd<P + 1, PEN>(sh, RJ, RM, ws, d, start, end, nnc, fb, I, dv, res, next);
         }
     }
 }
 /* non-contact rows in decreasing position (even iterations); cur = fetched data of row min(P, nnc-1) */
 template <int P>
 __device__ __forceinline__ void pgs_rev(Shared& sh, const double (&RJ)[NSLOT], const double (&RM)[NSLOT], int nnc,
-                                        double& dv, double& res, RowPre cur) {
+                                        Imps& I, double& dv, double& res, RowPre cur) {
     if constexpr (P >= 0) {
         RowPre next = cur;
         if (P < nnc) {
-            next = row_fetch<0>(sh, P > 0 ? P - 1 : 0, nnc, MAXROWS);
-            double imp = pgs_update<P & 1>(RJ[P >> 1], RM[P >> 1], cur, dv, res);
-            if (threadIdx.x == 32 * (P & 1)) sh.rs[P].imp = imp;
+            next = row_fetch<0>(sh, P > 0 ? P - 1 : 0);
+            imp_set<P>(I, pgs_update(RJ[P], RM[P], cur, imp_get<P>(I), dv, res));
         }
-        pgs_rev<P - 1>(sh, RJ, RM, nnc, dv, res, next);
+        pgs_rev<P - 1>(sh, RJ, RM, nnc, I, dv, res, next);
     }
 }
 /* warm start: normal rows with a carried impulse */
 template <int P>
-__device__ __forceinline__ void pgs_warm(Shared& sh, const double (&RJ)[NSLOT], const double (&RM)[NSLOT],
-                                         const double* ws, int d, int nnc, int fb, double& dv) {
+__device__ __forceinline__ void pgs_warm(const double (&RJ)[NSLOT], const double (&RM)[NSLOT], const double* ws,
+                                         int d, int nnc, int fb, const Imps& I, double& dv) {
     if constexpr (P < MAXROWS) {
         if (P < fb) {
             if (P >= nnc) {
-                double imp = sh.rs[P].imp;
+                double imp = imp_get<P>(I);
                 double Js, Ms;
                 row_jm<P>(RJ, RM, ws, d, Js, Ms);
-                double bc = half_bcast(Ms * imp, P & 1);
-                double dvn = dv + bc;
+                double dvn = dv + Ms * imp;
                 dv = imp != 0.0 ? dvn : dv;
             }
-            pgs_warm<P + 1>(sh, RJ, RM, ws, d, nnc, fb, dv);
+            pgs_warm<P + 1>(RJ, RM, ws, d, nnc, fb, I, dv);
         }
     }
 }
 /* rows (global workspace) -> register slots of their half: lane d of half h holds J[d], M^-1J[d] of row 2*SL+h */
 template <int SL>
-__device__ __forceinline__ void load_slots(const double* ws, double (&RJ)[NSLOT], double (&RM)[NSLOT], int n, int h,
-                                           int d) {
+__device__ __forceinline__ void load_slots(const double* ws, double (&RJ)[NSLOT], double (&RM)[NSLOT], int n, int d) {
     if constexpr (SL < NSLOT) {
-        if (2 * SL < n) {
-            int p = 2 * SL + h;
-            bool in = p < n && d < 24;
-            const double* x = ws + WS_ROWS + (p < n ? p : 0) * 48 + (d < 24 ? d : 0);
+        if (SL < n) {
+            bool in = d < 24;
+            const double* x = ws + WS_ROWS + SL * 48 + (in ? d : 0);
             double vj = x[0], vm = x[24];
             RJ[SL] = in ? vj : 0.0;
             RM[SL] = in ? vm : 0.0;
-            load_slots<SL + 1>(ws, RJ, RM, n, h, d);
+            load_slots<SL + 1>(ws, RJ, RM, n, d);
         }
     }
 }
@@ -915,6 +905,57 @@ __device__ __noinline__ static void serial_fk() {
     if (threadIdx.x == 0) fk(g_sh.e.q, g_sh.kin);
 }
 
+/* PGS over the rows in the register slots: warm start (normals), iterations (residual early-out), and
+ * the split-impulse pass; returns whether the split pass ran (dvs valid) */
+__device__ __forceinline__ static int team_pgs(const double* ws, int n, int nnc, int nn, int d,
+                                               const double (&RJ)[NSLOT], const double (&RM)[NSLOT], double& dv,
+                                               double& dvs) {
+    Shared& sh = g_sh;
+    const int lane = threadIdx.x;
+    const int fb = nnc + nn;
+    dv = 0.0;
+    dvs = 0.0;
+    Imps I;
+    I.v[0] = lane < n ? sh.rs[lane].imp : 0.0;
+    I.v[1] = lane + 64 < n ? sh.rs[lane + 64].imp : 0.0;
+    pgs_warm<0>(RJ, RM, ws, d, nnc, fb, I, dv);
+    for (int it = 0; it < UG_PGS_ITERS; it++) {
+        double res = 0.0;
+        /* opaque per-iteration copies: keeps the per-row scalar tests inside the loop instead of
+         * hoisting ~128 of them into (spilled) SGPRs */
+        int o_n = n, o_nnc = nnc, o_fb = fb;
+        const double* o_ws = ws;
+        asm volatile("" : "+s"(o_n), "+s"(o_nnc), "+s"(o_fb), "+s"(o_ws));
+        int start = 0;
+        if (!(it & 1)) {
+            if (o_nnc > 0) pgs_rev<NCMAX - 1>(sh, RJ, RM, o_nnc, I, dv, res, row_fetch<0>(sh, o_nnc - 1));
+            start = o_nnc;
+        }
+        if (start < o_n) pgs_fwd<0, 0>(sh, RJ, RM, o_ws, d, start, o_n, o_nnc, o_fb, I, dv, res, row_fetch<0>(sh, start));
+        PROF_CNT(PC_ITERS, 1);
+        if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
+    }
+    if (lane < n) sh.rs[lane].imp = I.v[0];
+    if (lane + 64 < n) sh.rs[lane + 64].imp = I.v[1];
+    int anypen = 0;
+    for (int p = nnc + lane; p < fb; p += TEAM) anypen |= sh.rs[p].rhsPen != 0.0;
+    int split = ballot(anypen) != 0ull;
+    if (split) {
+        Imps IP;
+        IP.v[0] = 0.0;
+        IP.v[1] = 0.0;
+        for (int it = 0; it < UG_PGS_ITERS; it++) {
+            double res = 0.0;
+            int o_nnc = nnc, o_fb = fb;
+            const double* o_ws = ws;
+            asm volatile("" : "+s"(o_nnc), "+s"(o_fb), "+s"(o_ws));
+            pgs_fwd<0, 1>(sh, RJ, RM, o_ws, d, o_nnc, o_fb, o_nnc, o_fb, IP, dvs, res, row_fetch<1>(sh, o_nnc));
+            if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
+        }
+    }
+    return split;
+}
+
 /* ---------------- one p.stepSimulation() (oracle substep()) ---------------- */
 __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) {
     Shared& sh = g_sh;
@@ -945,45 +986,13 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     double RJ[NSLOT], RM[NSLOT];
 #pragma unroll
     for (int sl = 0; sl < NSLOT; sl++) { RJ[sl] = 0.0; RM[sl] = 0.0; }
-    load_slots<0>(ws, RJ, RM, n, h, d);
+    load_slots<0>(ws, RJ, RM, n, d);
     PROF_ADD(PF_ROWS, t_rows);
     PROF_T0(t_pgs);
-    /* PGS: warm start (normals), iterations; split-impulse pass */
-    double dv = 0.0, dvs = 0.0;
-    pgs_warm<0>(sh, RJ, RM, ws, d, nnc, fb, dv);
-    for (int it = 0; it < UG_PGS_ITERS; it++) {
-        double res = 0.0;
-        /* opaque per-iteration copies: keeps the per-row scalar tests inside the loop instead of
-         * hoisting ~128 of them into (spilled) SGPRs */
-        int o_n = n, o_nnc = nnc, o_fb = fb;
-        asm volatile("" : "+s"(o_n), "+s"(o_nnc), "+s"(o_fb));
-        int start = 0;
-        if (!(it & 1)) {
-            if (o_nnc > 0) pgs_rev<NCMAX - 1>(sh, RJ, RM, o_nnc, dv, res, row_fetch<0>(sh, o_nnc - 1, o_nnc, MAXROWS));
-            start = o_nnc;
-        }
-        if (start < o_n) pgs_fwd<0, 0>(sh, RJ, RM, ws, d, start, o_n, o_nnc, o_fb, dv, res, row_fetch<0>(sh, start, o_nnc, o_fb));
-        PROF_CNT(PC_ITERS, 1);
-        double r0 = readlane_d(res, 0), r1 = readlane_d(res, 32);
-        double rall = r0 > r1 ? r0 : r1;
-        if (rall <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
-    }
+    double dv, dvs;
+    int split = team_pgs(ws, n, nnc, nn, d, RJ, RM, dv, dvs);
     PROF_ADD(PF_PGS, t_pgs);
     PROF_T0(t_split);
-    int anypen = 0;
-    for (int p = nnc + lane; p < fb; p += TEAM) anypen |= sh.rs[p].rhsPen != 0.0;
-    int split = ballot(anypen) != 0ull;
-    if (split) {
-        for (int it = 0; it < UG_PGS_ITERS; it++) {
-            double res = 0.0;
-            int o_nnc = nnc, o_fb = fb;
-            asm volatile("" : "+s"(o_nnc), "+s"(o_fb));
-            pgs_fwd<0, 1>(sh, RJ, RM, ws, d, o_nnc, o_fb, o_nnc, o_fb, dvs, res, row_fetch<1>(sh, o_nnc, o_nnc, o_fb));
-            double r0 = readlane_d(res, 0), r1 = readlane_d(res, 32);
-            double rall = r0 > r1 ? r0 : r1;
-            if (rall <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
-        }
-    }
     PROF_ADD(PF_SPLIT, t_split);
     PROF_T0(t_int);
     if (lane < NVP) { sh.dvout[lane] = dv; sh.dvsout[lane] = dvs; }
