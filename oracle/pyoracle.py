@@ -29,6 +29,23 @@ def lib():
         L.ugo_act_dim.argtypes = [I]
         L.ugo_state_dim.argtypes = []
         L.ugo_reset.argtypes = [P, P]
+        L.ugo_reset_draws.argtypes = [P, P, P]
+        L.ugo_robot_contact.argtypes = [P, I, I, I]
+        L.ugo_gripper_opening.argtypes = [P]
+        L.ugo_gripper_opening.restype = D
+        L.ugo_gripper_center.argtypes = [P, P]
+        L.ugo_choose.argtypes = [P, ctypes.c_float, ctypes.c_float]
+        L.ugo_norm3.argtypes = [P]
+        L.ugo_norm3.restype = D
+        L.ugo_g_cp_cube1_x.argtypes = [D]
+        L.ugo_g_cp_cube1_x.restype = D
+        L.ugo_g_cp_reward.argtypes = [I, I, P, P, P]
+        L.ugo_g_cg_cube_xy.argtypes = [D, D, P]
+        L.ugo_g_cg_choose.argtypes = [ctypes.c_float, ctypes.c_float, D]
+        L.ugo_g_cg_opening.argtypes = [D]
+        L.ugo_g_cg_opening.restype = D
+        L.ugo_g_cg_reward.argtypes = [P, D, D, I, D, P]
+        L.ugo_g_union_center.argtypes = [P, P]
         L.ugo_step.argtypes = [P, P, P, P, P, P]
         L.ugo_get_state.argtypes = [P, P]
         L.ugo_set_state.argtypes = [P, P]
@@ -76,10 +93,28 @@ class OracleEnv:
         except Exception:
             pass
 
-    def reset(self):
+    def reset(self, draws=None):
         obs = np.zeros(self.obs_dim)
-        n = self.L.ugo_reset(self.h, _p(obs))
+        if draws is None:
+            n = self.L.ugo_reset(self.h, _p(obs))
+        else:
+            d = np.ascontiguousarray(draws, dtype=np.float64)
+            n = self.L.ugo_reset_draws(self.h, _p(d), _p(obs))
         return obs, n
+
+    def robot_contact(self, obj_or_static, lmin, lmax):
+        return bool(self.L.ugo_robot_contact(self.h, obj_or_static, lmin, lmax))
+
+    def gripper_opening(self):
+        return self.L.ugo_gripper_opening(self.h)
+
+    def gripper_center(self):
+        out = np.zeros(3)
+        self.L.ugo_gripper_center(self.h, _p(out))
+        return out
+
+    def choose(self, w0, w1):
+        return self.L.ugo_choose(self.h, w0, w1)
 
     def step(self, action):
         a = np.ascontiguousarray(action, dtype=np.float32)
@@ -130,6 +165,10 @@ class OracleEnv:
         q = np.zeros(12)
         self.L.ugo_ik(self.h, _p(np.asarray(pos, np.float64)), _p(np.asarray(orn, np.float64)), _p(q))
         return q
+
+
+def norm3(v):
+    return lib().ugo_norm3(_p(np.ascontiguousarray(v, dtype=np.float64)))
 
 
 def gdr(v, s, m):

@@ -16,6 +16,7 @@
 #include "../urgym_amd/csrc/model_data.h"
 #include "../urgym_amd/csrc/scene_data.h"
 #include "../urgym_amd/csrc/ug_detmath.h"
+#include "../urgym_amd/csrc/ug_glue.h"
 
 #define NB UG_NB
 #define MAXOBJ 2
@@ -351,6 +352,30 @@ static void build_scene(scene* s, int task) {
         c->disc = ug_sqrt(3.0) * r;
         c->owner = -3; c->ent = 2;
         s->ocol[1] = s->ncol++;
+    }
+    if (task == UG_TASK_CUBESPUSH || task == UG_TASK_CUBESGRASP) {
+        /* cube.urdf x 0.04 (env_cubes_push_v0.py:232-246: two; env_cubes_grasp_v0.py:300-330: one):
+         * URDF box, default URDF margin, inertia from the shape's box [ext] */
+        s->nobj = task == UG_TASK_CUBESPUSH ? 2 : 1;
+        for (int o = 0; o < s->nobj; o++) {
+            double h = UG_CUBE_HALF, m = UG_CUBE_MASS;
+            s->omass[o] = m;
+            double ii = m / 12.0 * (4.0 * h * h + 4.0 * h * h);
+            s->oinertia[o] = V(ii, ii, ii);
+            collider* c = &s->col[s->ncol];
+            box_collider(c, h, h, h, UG_URDF_MARGIN, UG_CUBE_FRICTION);
+            c->owner = -2 - o; c->ent = 1 + o;
+            s->ocol[o] = s->ncol++;
+        }
+    }
+    if (task == UG_TASK_CUBESGRASP) {
+        /* plane.urdf at the origin, no table (env_cubes_grasp_v0.py:48) */
+        collider* c = &s->col[s->ncol];
+        box_collider(c, UG_PLANE_HALF_XY, UG_PLANE_HALF_XY, UG_PLANE_HALF_Z, UG_URDF_MARGIN, UG_PLANE_FRICTION);
+        c->P = V(0.0, 0.0, -UG_PLANE_HALF_Z); c->aP = c->P;
+        c->disc = ug_sqrt(15.0 * 15.0 * 2.0 + 25.0) + 5.0;
+        c->owner = -100; c->ent = 11;
+        statics[nstat++] = s->ncol++;
     }
     if (task == UG_TASK_BALLBALANCE || task == UG_TASK_CUBESPUSH || task == UG_TASK_GOLF) {
         /* table (env_ball_balance_v0.py:71,216-247) and plane at z=-0.5 (:70) */
@@ -1654,7 +1679,7 @@ static void link_state(const ugo_env* e, int l, v3* p, q4* o) {
 static v3 gripper_center(const ugo_env* e) {
     kin k;
     fk(e->q, &k);
-    v3 lo = V(1e300, 1e300, 1e300), hi = V(-1e300, -1e300, -1e300);
+    double bl[2][3], bh[2][3];
     const int links[2] = {11, 16};
     for (int i = 0; i < 2; i++) {
         int l = links[i];
@@ -1668,10 +1693,12 @@ static v3 gripper_center(const ugo_env* e) {
                    ug_fabs(r[3]) * h.x + ug_fabs(r[4]) * h.y + ug_fabs(r[5]) * h.z,
                    ug_fabs(r[6]) * h.x + ug_fabs(r[7]) * h.y + ug_fabs(r[8]) * h.z);
         v3 mn = vsub(c, ext), mx = vadd(c, ext);
-        lo = V(ug_min(lo.x, mn.x), ug_min(lo.y, mn.y), ug_min(lo.z, mn.z));
-        hi = V(ug_max(hi.x, mx.x), ug_max(hi.y, mx.y), ug_max(hi.z, mx.z));
+        bl[i][0] = mn.x; bl[i][1] = mn.y; bl[i][2] = mn.z;
+        bh[i][0] = mx.x; bh[i][1] = mx.y; bh[i][2] = mx.z;
     }
-    return V((hi.x + lo.x) / 2.0, (hi.y + lo.y) / 2.0, (hi.z + lo.z) / 2.0);
+    double ctr[3];
+    ugg_union_center(bl[0], bh[0], bl[1], bh[1], ctr);
+    return V(ctr[0], ctr[1], ctr[2]);
 }
 static void remove_object(ugo_env* e, int o) {
     e->oactive[o] = 0;
@@ -1716,13 +1743,13 @@ static void bb_obs(const ugo_env* e, double* obs) {
     obs[5] = e->opos[0].z - e->opos[1].z;
 }
 /* create_ball (env_ball_balance_v0.py:186-205): 0.2 m + r above the paddle, x += U(-0.03,0.03), y += U(-0.08,0.02) */
-static v3 bb_ball_position(ugo_env* e, v3 paddle) {
+static v3 bb_ball_position(ugo_env* e, const double* draws, v3 paddle) {
     v3 bp = V(paddle.x, paddle.y, paddle.z + 0.2 + UG_BB_BALL_R);
-    bp.x += mt_uniform(&e->rng, -0.03, 0.03);
-    bp.y += mt_uniform(&e->rng, -0.08, 0.02);
+    bp.x += draws ? -0.03 + (0.03 - -0.03) * draws[0] : mt_uniform(&e->rng, -0.03, 0.03);
+    bp.y += draws ? -0.08 + (0.02 - -0.08) * draws[1] : mt_uniform(&e->rng, -0.08, 0.02);
     return bp;
 }
-static int bb_reset(ugo_env* e, double* obs) {
+static int bb_reset(ugo_env* e, const double* draws, double* obs) {
     /* env_ball_balance_v0.py:145-170 */
     int n = robot_reset(e);
     remove_object(e, 0);
@@ -1736,7 +1763,7 @@ static int bb_reset(ugo_env* e, double* obs) {
     v3 gc = gripper_center(e);
     v3 pose = V(pe.x, pe.y - 0.2, gc.z);
     place_object(e, 0, pose, Q(0, 0, 0, 1));
-    place_object(e, 1, bb_ball_position(e, pose), e->oquat[0]);
+    place_object(e, 1, bb_ball_position(e, draws, pose), e->oquat[0]);
     close_gripper(e, 100.0);
     n += wait_until_stable(e);
     bb_obs(e, obs);
@@ -1759,6 +1786,142 @@ static int bb_step(ugo_env* e, const float* a, double* obs, double* rew, uint8_t
     return n;
 }
 
+/* ---- contact predicates over the manifold cache (p.getContactPoints existence) ---- */
+/* any point between a robot link in [lmin, lmax] and the collider cb */
+static int robot_contact(const ugo_env* e, int cb, int lmin, int lmax) {
+    const scene* s = &e->sc;
+    for (int m = 0; m < e->nman; m++) {
+        const pairdef* P = &s->pair[e->man[m].pair];
+        if (e->man[m].npts <= 0 || P->b != cb) continue;
+        int l = s->col[P->a].link;
+        if (l >= lmin && l <= lmax) return 1;
+    }
+    return 0;
+}
+static int static_collider(const scene* s, int ent) {
+    for (int i = 0; i < s->ncol; i++)
+        if (s->col[i].ent == ent) return i;
+    return -1;
+}
+
+/* ---- CubesPush (env_cubes_push_v0.py) ---- */
+static void cp_obs(const ugo_env* e, double* obs) {
+    /* :198-205 ee position (link 7 COM) + both cube positions */
+    v3 pe;
+    q4 oe;
+    link_state(e, UG_EE_LINK, &pe, &oe);
+    obs[0] = pe.x; obs[1] = pe.y; obs[2] = pe.z;
+    for (int o = 0; o < 2; o++) { obs[3 + 3 * o] = e->opos[o].x; obs[4 + 3 * o] = e->opos[o].y; obs[5 + 3 * o] = e->opos[o].z; }
+}
+static int cp_reset(ugo_env* e, const double* draws, double* obs) {
+    /* :207-227 */
+    int n = robot_reset(e);
+    remove_object(e, 0);
+    remove_object(e, 1);
+    place_object(e, 0, V(0.0, -0.5, 0.1), Q(0, 0, 0, 1));
+    double x = ugg_cp_cube1_x(draws ? draws[0] : mt_random(&e->rng));
+    place_object(e, 1, V(x, -0.7, 0.1), Q(0, 0, 0, 1));
+    move_ee_end(e, V(x, -0.7, 0.1 + UG_CP_EE_DZ), Q(0.0, UG_VQ_S, 0.0, UG_VQ_C));
+    close_gripper(e, 100.0);
+    n += wait_until_stable(e);
+    cp_obs(e, obs);
+    return n;
+}
+static int cp_step(ugo_env* e, const float* a, double* obs, double* rew, uint8_t* term, uint8_t* succ) {
+    /* :115-150 */
+    v3 pe;
+    q4 oe;
+    link_state(e, UG_EE_LINK, &pe, &oe);
+    move_ee_end(e, V(pe.x + (double)a[0], pe.y + (double)a[1], pe.z + (double)a[2]), Q(0.0, UG_VQ_S, 0.0, UG_VQ_C));
+    int n = wait_until_stable(e);
+    int table = robot_contact(e, static_collider(&e->sc, 10), 1, UG_NL - 1); /* :176-183 robot link != 0 */
+    int touched = robot_contact(e, e->sc.ocol[1], 9, 18);                    /* :185-194 fingers 9..18 */
+    double r;
+    int success = ugg_cp_reward(table, touched, e->opos[0].x, e->opos[0].y, e->opos[0].z, e->opos[1].x,
+                                e->opos[1].y, e->opos[1].z, &r);
+    *rew = r;
+    *term = (uint8_t)success;
+    *succ = (uint8_t)success;
+    cp_obs(e, obs);
+    return n;
+}
+
+/* ---- CubesGrasp (env_cubes_grasp_v0.py) ---- */
+/* get_gripper_opening_length (:349-376): link frames 11 and 16, distance - 0.052, clamp, normalise */
+static double cg_opening(const ugo_env* e) {
+    kin k;
+    fk(e->q, &k);
+    m3 R1, R2;
+    v3 p1, p2;
+    link_frame(&k, 11, 0, &R1, &p1);
+    link_frame(&k, 16, 0, &R2, &p2);
+    return ugg_cg_opening(ug_norm3(p2.x - p1.x, p2.y - p1.y, p2.z - p1.z));
+}
+static double cg_distance(const ugo_env* e) {
+    /* distance_to_target (:199-204): gripper geometric centre to the cube position */
+    v3 gc = gripper_center(e);
+    return ug_norm3(gc.x - e->opos[0].x, gc.y - e->opos[0].y, gc.z - e->opos[0].z);
+}
+static int cg_grasped(const ugo_env* e) {
+    /* object_grasped (:211-228): a point on a left link {11,12,13} and one on a right link {16,17,18} */
+    return robot_contact(e, e->sc.ocol[0], 11, 13) && robot_contact(e, e->sc.ocol[0], 16, 18);
+}
+static void cg_obs(const ugo_env* e, double* obs) {
+    /* :268-287 subgoal flags, ee pose (7), opening, cube pose (7) */
+    v3 pe;
+    q4 oe;
+    link_state(e, UG_EE_LINK, &pe, &oe);
+    obs[0] = e->goal_approached; obs[1] = e->goal_grasped;
+    obs[2] = pe.x; obs[3] = pe.y; obs[4] = pe.z; obs[5] = oe.x; obs[6] = oe.y; obs[7] = oe.z; obs[8] = oe.w;
+    obs[9] = cg_opening(e);
+    obs[10] = e->opos[0].x; obs[11] = e->opos[0].y; obs[12] = e->opos[0].z;
+    obs[13] = e->oquat[0].x; obs[14] = e->oquat[0].y; obs[15] = e->oquat[0].z; obs[16] = e->oquat[0].w;
+}
+static int cg_reset(ugo_env* e, const double* draws, double* obs) {
+    /* :289-307 robot.reset, create_cubes (:310-330), move_ee(get_ee_pose) and settle */
+    int n = robot_reset(e);
+    remove_object(e, 0);
+    double u0 = draws ? draws[0] : mt_random(&e->rng);
+    double u1 = draws ? draws[1] : mt_random(&e->rng);
+    double x, y;
+    ugg_cg_cube_xy(u0, u1, &x, &y);
+    place_object(e, 0, V(x, y, 0.1), Q(0, 0, 0, 1));
+    v3 pe;
+    q4 oe;
+    link_state(e, UG_EE_LINK, &pe, &oe);
+    move_ee_end(e, pe, oe);
+    n += wait_until_stable(e);
+    e->goal_approached = e->goal_grasped = 0;
+    cg_obs(e, obs);
+    return n;
+}
+static int cg_choose(ugo_env* e, float w0, float w1) { return ugg_cg_choose(w0, w1, mt_random(&e->rng)); }
+static int cg_step(ugo_env* e, const float* a, double* obs, double* rew, uint8_t* term, uint8_t* succ) {
+    /* :132-192 */
+    int sel = cg_choose(e, a[0], a[1]);
+    if (sel == 0) {
+        double q6[6];
+        for (int i = 0; i < 6; i++) q6[i] = (double)a[2 + i];
+        move_ee_joint(e, q6);
+    } else if (a[8] < 0.5f) {
+        open_gripper(e, 100.0);
+    } else {
+        close_gripper(e, 100.0);
+    }
+    int n = wait_until_stable(e);
+    int app = e->goal_approached, gr = e->goal_grasped;
+    double d = cg_distance(e);
+    double r;
+    int success = ugg_cg_reward(&app, &gr, d, cg_opening(e), cg_grasped(e), e->opos[0].z, &r);
+    e->goal_approached = app;
+    e->goal_grasped = gr;
+    *rew = r;
+    *term = (uint8_t)success;
+    *succ = (uint8_t)success;
+    cg_obs(e, obs);
+    return n;
+}
+
 /* ======================================================================== */
 /* public API                                                                */
 /* ======================================================================== */
@@ -1770,13 +1933,22 @@ ugo_env* ugo_create(int task, uint32_t seed) {
 }
 void ugo_destroy(ugo_env* e) { free(e); }
 void ugo_substep(ugo_env* e) { substep(e); }
-int ugo_reset(ugo_env* e, double* obs) {
+int ugo_reset(ugo_env* e, double* obs) { return ugo_reset_draws(e, NULL, obs); }
+int ugo_reset_draws(ugo_env* e, const double* draws, double* obs) {
     e->goal_approached = e->goal_grasped = 0;
-    if (e->sc.task == UG_TASK_BALLBALANCE) return bb_reset(e, obs);
+    switch (e->sc.task) {
+        case UG_TASK_BALLBALANCE: return bb_reset(e, draws, obs);
+        case UG_TASK_CUBESPUSH: return cp_reset(e, draws, obs);
+        case UG_TASK_CUBESGRASP: return cg_reset(e, draws, obs);
+    }
     return -1;
 }
 int ugo_step(ugo_env* e, const float* action, double* obs, double* reward, uint8_t* terminated, uint8_t* success) {
-    if (e->sc.task == UG_TASK_BALLBALANCE) return bb_step(e, action, obs, reward, terminated, success);
+    switch (e->sc.task) {
+        case UG_TASK_BALLBALANCE: return bb_step(e, action, obs, reward, terminated, success);
+        case UG_TASK_CUBESPUSH: return cp_step(e, action, obs, reward, terminated, success);
+        case UG_TASK_CUBESGRASP: return cg_step(e, action, obs, reward, terminated, success);
+    }
     return -1;
 }
 void ugo_get_state(const ugo_env* e, double* s) {
@@ -1843,13 +2015,7 @@ void ugo_set_state(ugo_env* e, const double* s) {
 }
 void ugo_rng_seed(ugo_env* e, uint32_t seed) { mt_seed(&e->rng, seed); }
 double ugo_rng_random(ugo_env* e) { return mt_random(&e->rng); }
-double ugo_gdr(double value, double ts, double tm) {
-    /* geometric_distance_reward (utilities.py:192-207) */
-    value = value > 1e-10 ? value : 1e-10;
-    double f1 = (value - ts) / value;
-    double f2 = (tm - value) > 1e-10 ? (tm - value) : 1e-10;
-    return -ug_tanh(f1 / f2);
-}
+double ugo_gdr(double value, double ts, double tm) { return ugg_gdr(value, ts, tm); }
 void ugo_euler_from_quat(const double* q, double* rpy) {
     v3 r = euler_from_quat(Q(q[0], q[1], q[2], q[3]));
     rpy[0] = r.x; rpy[1] = r.y; rpy[2] = r.z;
@@ -1890,14 +2056,42 @@ long ugo_batch_step(ugo_env** envs, int n, const float* actions, double* obs, do
 
 /* ---- hooks for known-answer / golden tests ---- */
 void ugo_bb_ball_position(ugo_env* e, const double* paddle, double* out) {
-    v3 b = bb_ball_position(e, V(paddle[0], paddle[1], paddle[2]));
+    v3 b = bb_ball_position(e, NULL, V(paddle[0], paddle[1], paddle[2]));
     out[0] = b.x; out[1] = b.y; out[2] = b.z;
 }
 double ugo_stable_sum(const double* a12) { return np_sum12(a12); }
 void ugo_observe(const ugo_env* e, double* obs) {
-    if (e->sc.task == UG_TASK_BALLBALANCE) bb_obs(e, obs);
+    switch (e->sc.task) {
+        case UG_TASK_BALLBALANCE: bb_obs(e, obs); break;
+        case UG_TASK_CUBESPUSH: cp_obs(e, obs); break;
+        case UG_TASK_CUBESGRASP: cg_obs(e, obs); break;
+    }
 }
 int ugo_terminated(const ugo_env* e) {
     if (e->sc.task == UG_TASK_BALLBALANCE) return e->opos[1].z < e->opos[0].z;
     return 0;
 }
+/* contact predicates and gripper geometry (A12/A13) for the golden and parity tests */
+int ugo_robot_contact(const ugo_env* e, int obj_or_static, int lmin, int lmax) {
+    int cb = obj_or_static >= 10 ? static_collider(&e->sc, obj_or_static) : e->sc.ocol[obj_or_static];
+    return cb < 0 ? 0 : robot_contact(e, cb, lmin, lmax);
+}
+double ugo_gripper_opening(const ugo_env* e) { return cg_opening(e); }
+void ugo_gripper_center(const ugo_env* e, double* out3) {
+    v3 c = gripper_center(e);
+    out3[0] = c.x; out3[1] = c.y; out3[2] = c.z;
+}
+int ugo_choose(ugo_env* e, float w0, float w1) { return cg_choose(e, w0, w1); }
+double ugo_norm3(const double* v) { return ug_norm3(v[0], v[1], v[2]); }
+/* the shared task glue (ug_glue.h), exported for the golden tests */
+double ugo_g_cp_cube1_x(double u) { return ugg_cp_cube1_x(u); }
+int ugo_g_cp_reward(int table, int touched, const double* c0, const double* c1, double* r) {
+    return ugg_cp_reward(table, touched, c0[0], c0[1], c0[2], c1[0], c1[1], c1[2], r);
+}
+void ugo_g_cg_cube_xy(double u0, double u1, double* xy) { ugg_cg_cube_xy(u0, u1, &xy[0], &xy[1]); }
+int ugo_g_cg_choose(float w0, float w1, double u) { return ugg_cg_choose(w0, w1, u); }
+double ugo_g_cg_opening(double d) { return ugg_cg_opening(d); }
+int ugo_g_cg_reward(int* flags, double dist, double opening, int grasp, double cube_z, double* r) {
+    return ugg_cg_reward(&flags[0], &flags[1], dist, opening, grasp, cube_z, r);
+}
+void ugo_g_union_center(const double* aabbs, double* c) { ugg_union_center(aabbs, aabbs + 3, aabbs + 6, aabbs + 9, c); }

@@ -33,6 +33,8 @@ int ugo_act_dim(int task);
 int ugo_state_dim(void);
 /* reset(): fills obs; returns substeps spent */
 int ugo_reset(ugo_env* e, double* obs);
+/* reset with caller-supplied uniforms in [0,1) replacing the env's random() draws (NULL: use the stream) */
+int ugo_reset_draws(ugo_env* e, const double* draws, double* obs);
 /* step(): action float32[act_dim]; returns substeps spent in wait_until_stable */
 int ugo_step(ugo_env* e, const float* action, double* obs, double* reward, uint8_t* terminated,
              uint8_t* success);
@@ -53,6 +55,21 @@ void ugo_bb_ball_position(ugo_env* e, const double* paddle, double* out);
 double ugo_stable_sum(const double* a12);
 void ugo_observe(const ugo_env* e, double* obs);
 int ugo_terminated(const ugo_env* e);
+/* contact predicate: a manifold point between a robot link in [lmin, lmax] and object i (0..) or the
+ * static with id obj_or_static (10 table, 11 plane) -- p.getContactPoints existence */
+int ugo_robot_contact(const ugo_env* e, int obj_or_static, int lmin, int lmax);
+double ugo_gripper_opening(const ugo_env* e);
+void ugo_gripper_center(const ugo_env* e, double* out3);
+int ugo_choose(ugo_env* e, float w0, float w1);
+double ugo_norm3(const double* v);
+/* shared task glue (urgym_amd/csrc/ug_glue.h) for the golden tests */
+double ugo_g_cp_cube1_x(double u);
+int ugo_g_cp_reward(int table, int touched, const double* c0, const double* c1, double* r);
+void ugo_g_cg_cube_xy(double u0, double u1, double* xy);
+int ugo_g_cg_choose(float w0, float w1, double u);
+double ugo_g_cg_opening(double d);
+int ugo_g_cg_reward(int* flags, double dist, double opening, int grasp, double cube_z, double* r);
+void ugo_g_union_center(const double* aabbs, double* c);
 /* batched CPU baseline: n envs, OpenMP over envs; returns total substeps */
 long ugo_batch_step(ugo_env** envs, int n, const float* actions, double* obs, double* reward,
                     uint8_t* terminated, uint8_t* success, int32_t* substeps, int autoreset,

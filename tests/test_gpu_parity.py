@@ -137,3 +137,60 @@ def test_full_config_properties(mods):
     out_b = b.step(act)
     assert np.array_equal(out["obs"], out_b["obs"])
     assert np.array_equal(b.get_state(), st)
+
+
+def _task_actions(task, rng, n):
+    """uniform in the reference's action_space (SURVEY.md 8(d) synthetic inputs)"""
+    if task == 2:
+        lo = np.array([0, 0] + [-np.pi] * 6 + [0], np.float64)
+        hi = np.array([1, 1] + [np.pi] * 6 + [1], np.float64)
+        return rng.uniform(lo, hi, size=(n, 9)).astype(np.float32)
+    return rng.uniform(-0.1, 0.1, size=(n, 3)).astype(np.float32)
+
+
+@pytest.mark.parametrize("task,max_steps", [(1, 50), (2, 20)])
+def test_cube_tasks_bit_exact_with_autoreset(mods, task, max_steps):
+    """CubesPush / CubesGrasp: reset, steps with contact-predicate rewards,
+    subgoal flags, random.choices draws and same-step autoreset, bit-identical to the oracle."""
+    Sim, OracleEnv = mods
+    n, T = 32, 6
+    sim = Sim(task, n, seed=SEED)
+    sim.set_autoreset(True, max_steps)
+    obs = sim.reset()
+    ref = {i: OracleEnv(task, SEED + i) for i in range(n)}
+    for i, r in ref.items():
+        o, _ = r.reset()
+        assert np.array_equal(obs[i], o), (task, i)
+    rng = np.random.default_rng(SEED + task)
+    elapsed = np.zeros(n, int)
+    for t in range(T):
+        act = _task_actions(task, rng, n)
+        out = sim.step(act)
+        for i, r in ref.items():
+            o, rew, term, succ, ns = r.step(act[i])
+            elapsed[i] += 1
+            assert out["reward"][i] == rew, (task, t, i)
+            assert bool(out["terminated"][i]) == term and bool(out["success"][i]) == succ, (task, t, i)
+            if term or elapsed[i] >= max_steps:
+                assert np.array_equal(out["final_obs"][i], o), (task, t, i)
+                o, ns2 = r.reset()
+                ns += ns2
+                elapsed[i] = 0
+            assert np.array_equal(out["obs"][i], o), (task, t, i)
+            assert out["substeps"][i] == ns, (task, t, i)
+    st = sim.get_state()
+    for i, r in ref.items():
+        assert np.array_equal(st[i], r.get_state()), (task, i)
+
+
+@pytest.mark.parametrize("task", [1, 2])
+def test_cube_tasks_reset_draws(mods, task):
+    """urgym_reset with caller-supplied draws == oracle reset with the same draws"""
+    Sim, OracleEnv = mods
+    n = 8
+    sim = Sim(task, n, seed=SEED)
+    draws = np.random.default_rng(7).uniform(0, 1, size=(n, sim.ndraw))
+    obs = sim.reset(draws=draws)
+    for i in range(n):
+        o, _ = OracleEnv(task, SEED + i).reset(draws=draws[i])
+        assert np.array_equal(obs[i], o), (task, i)

@@ -156,7 +156,187 @@ def main():
     sums = [float(np.sum(np.abs(np.array(qs[k]) - np.array(qs[k + 1])))) for k in range(5)]
     json.dump({"positions": qs, "abs_sums": sums, "stable": bool(stable)},
               open(os.path.join(OUT, "wait_until_stable.json"), "w"), indent=1)
+    gen_cubes(p, rng)
     print("wrote", sorted(os.listdir(OUT)))
+
+
+def bullet_axis_angle(axis, angle):
+    """btQuaternion::setRotation (getQuaternionFromAxisAngle) -- the Bullet side, restated for the mock."""
+    d = math.sqrt(axis[0] ** 2 + axis[1] ** 2 + axis[2] ** 2)
+    s = math.sin(angle * 0.5) / d
+    return (axis[0] * s, axis[1] * s, axis[2] * s, math.cos(angle * 0.5))
+
+
+def contact(link_a, link_b):
+    """a getContactPoints tuple: only fields [3] (linkIndexA) and [4] (linkIndexB) are read by the glue"""
+    return (0, 1, 2, link_a, link_b) + (0.0,) * 9
+
+
+def gen_cubes(p, rng):
+    """CubesPush (env_cubes_push_v0.py) and CubesGrasp (env_cubes_grasp_v0.py) glue."""
+    from urgym.envs.env_cubes_push_v0 import CubesPush  # noqa: E402
+    from urgym.envs.env_cubes_grasp_v0 import CubesGrasp  # noqa: E402
+    out = {}
+    # -- CubesPush.reset: create_cubes draw -> positions, EE target above cube[1], vertical quaternion
+    resets = []
+    for seed in [0, 1, 7, 12345, 20241220]:
+        env = CubesPush.__new__(CubesPush)
+        env.visualize = False
+        env.cubes = []
+        calls = []
+        env.robot = types.SimpleNamespace(reset=lambda: None,
+                                          move_ee=lambda pose, m: calls.append(("move_ee", list(pose), m)),
+                                          close_gripper=lambda pct=100: calls.append(("close", pct)))
+        env.wait_until_stable = lambda: True
+        env.get_observation = lambda: None
+        p.reset_mock()
+        p.getQuaternionFromEuler.side_effect = lambda e: (0.0, 0.0, 0.0, 1.0)
+        ids = iter(range(100, 200))
+        p.loadURDF.side_effect = lambda *a, **k: next(ids)
+        placed = {}
+
+        def load(*a, **k):
+            i = next(ids)
+            placed[i] = list(a[1])
+            return i
+        p.loadURDF.side_effect = load
+        p.getBasePositionAndOrientation.side_effect = lambda i: (tuple(placed[i]), (0.0, 0.0, 0.0, 1.0))
+        p.getQuaternionFromAxisAngle.side_effect = bullet_axis_angle
+        random.seed(seed)
+        env.reset()
+        resets.append({"seed": seed, "cubes": [placed[i] for i in env.cubes], "calls": calls,
+                       "vertical_quaternion": list(env.vertical_quaternion)})
+    out["cubespush_reset"] = resets
+    # -- CubesPush.step: scripted EE pose, contacts and cube positions
+    steps = []
+    vq = resets[0]["vertical_quaternion"]
+    cases = [  # action, table contacts (robot links), cube[1] contacts (robot links), cube0, cube1
+        ((0.05, -0.02, 0.03), [3], [12], (0.0, -0.5, 0.02), (0.02, -0.6, 0.02)),
+        ((0.01, 0.0, -0.1), [0], [12], (0.0, -0.5, 0.02), (0.3, -0.6, 0.02)),
+        ((0.0, 0.1, 0.0), [], [16, 9], (0.0, -0.5, 0.02), (0.02, -0.52, 0.02)),
+        ((-0.1, 0.0, 0.02), [], [5], (0.0, -0.5, 0.02), (0.01, -0.51, 0.02)),
+        ((0.0, 0.0, 0.0), [], [], (0.0, -0.5, 0.02), (0.01, -0.51, 0.02)),
+        ((0.07, 0.03, -0.05), [0, 0], [18], (0.0, -0.5, 0.02), (0.06, -0.58, 0.021)),
+        ((0.02, 0.02, 0.02), [], [10], (0.1, -0.45, 0.02), (0.1, -0.7, 0.02)),
+    ]
+    for act, table_links, cube_links, c0, c1 in cases:
+        env = CubesPush.__new__(CubesPush)
+        env.visualize = False
+        env.reward_type = "dense"
+        env.positive_reward_radius = 0.1
+        env.vertical_quaternion = tuple(vq)
+        env.control_method = "end"
+        env.robot = types.SimpleNamespace(id=1)
+        env.table_id = 2
+        env.cubes = [10, 11]
+        ee_pose = (-0.05, -0.62, 0.21, 0.0, 0.7, 0.0, 0.7)
+        env.robot.get_ee_pose = lambda: ee_pose
+        env.robot.get_joint_obs = lambda: {"ee_pos": ee_pose}
+        moves = []
+        env.robot.move_ee = lambda pose, m: moves.append((list(pose), m))
+        env.wait_until_stable = lambda: True
+        p.reset_mock()
+        p.getBasePositionAndOrientation.side_effect = lambda i: ((c0 if i == 10 else c1), (0.0, 0.0, 0.0, 1.0))
+
+        def cps(*a, **k):
+            ba = k.get("bodyA", a[0] if a else None)
+            bb = k.get("bodyB", a[1] if len(a) > 1 else None)
+            if (ba, bb) == (1, 2):
+                return [contact(l, -1) for l in table_links]
+            if (ba, bb) == (11, 1):
+                return [contact(-1, l) for l in cube_links]
+            return []
+        p.getContactPoints.side_effect = cps
+        a = np.array(act, dtype=np.float32)
+        obs, rew, term, trunc, info = env.step(a)
+        steps.append({"action": a.tolist(), "ee_pose": list(ee_pose), "table_links": table_links,
+                      "cube1_links": cube_links, "cube0": list(c0), "cube1": list(c1), "ik_target": moves[0][0],
+                      "obs": [float(x) for x in obs], "reward": float(rew), "terminated": bool(term),
+                      "is_success": bool(info["is_success"])})
+    out["cubespush_step"] = steps
+    # -- CubesGrasp.create_cubes draws -> cube position
+    cg = []
+    for seed in [0, 1, 7, 12345, 20241220]:
+        env = CubesGrasp.__new__(CubesGrasp)
+        env.cubes = []
+        placed = []
+        p.reset_mock()
+        p.getQuaternionFromEuler.side_effect = lambda e: (0.0, 0.0, 0.0, 1.0)
+        p.loadURDF.side_effect = lambda *a, **k: placed.append(list(a[1])) or 100
+        random.seed(seed)
+        env.create_cubes()
+        cg.append({"seed": seed, "cube": placed[0], "next_random": random.random()})
+    out["cubesgrasp_create"] = cg
+    # -- CubesGrasp.step: random.choices on (w0, w1), action branch, subgoal rewards
+    rs = np.random.default_rng(5)
+    chooses = []
+    for k in range(40):
+        w = rs.uniform(0, 1, 2).astype(np.float32)
+        if k % 10 == 0:
+            w[:] = 0.0
+        seed = int(rs.integers(0, 2**31))
+        random.seed(seed)
+        u = random.random()
+        random.seed(seed)
+        # the reference's own guard (env_cubes_grasp_v0.py:144-147)
+        if w[0] + w[1] == 0:
+            sel = random.choices([0, 1], weights=[0.5, 0.5], k=1)[0]
+        else:
+            sel = random.choices([0, 1], weights=[w[0], w[1]], k=1)[0]
+        # numpy 1.26 promotion (float64 product) -- keep only draws where both promotions agree
+        tot = float(np.float32(w[0] + w[1]))
+        sel126 = (0 if u * 1.0 < 0.5 else 1) if np.float32(w[0] + w[1]) == 0 else (0 if u * tot < float(w[0]) else 1)
+        if sel == sel126:
+            chooses.append({"seed": seed, "w": [float(w[0]), float(w[1])], "u": u, "selected": int(sel)})
+    out["cubesgrasp_choose"] = chooses
+    steps = []
+    cases = [  # flags, gripper AABBs (link 11, 16), link frames 11/16, cube pos, robot links on cube
+        ({"approached": False, "grasped": False}, ((0.1, -0.5, 0.1), (0.12, -0.48, 0.15)), ((0.08, -0.5, 0.1), (0.1, -0.52, 0.16)),
+         (0.01, -0.5, 0.12), (0.16, -0.5, 0.12), (0.1, -0.49, 0.12), []),
+        ({"approached": False, "grasped": False}, ((0.1, -0.5, 0.1), (0.12, -0.48, 0.15)), ((0.08, -0.5, 0.1), (0.1, -0.52, 0.16)),
+         (0.01, -0.5, 0.12), (0.06, -0.5, 0.12), (0.4, -0.2, 0.12), []),
+        ({"approached": True, "grasped": False}, ((0.1, -0.5, 0.1), (0.12, -0.48, 0.15)), ((0.08, -0.5, 0.1), (0.1, -0.52, 0.16)),
+         (0.01, -0.5, 0.12), (0.16, -0.5, 0.12), (0.1, -0.49, 0.12), [12, 17]),
+        ({"approached": True, "grasped": False}, ((0.1, -0.5, 0.1), (0.12, -0.48, 0.15)), ((0.08, -0.5, 0.1), (0.1, -0.52, 0.16)),
+         (0.01, -0.5, 0.12), (0.16, -0.5, 0.12), (0.1, -0.49, 0.12), [12, 13]),
+        ({"approached": True, "grasped": True}, ((0.1, -0.5, 0.1), (0.12, -0.48, 0.15)), ((0.08, -0.5, 0.1), (0.1, -0.52, 0.16)),
+         (0.01, -0.5, 0.3), (0.16, -0.5, 0.3), (0.1, -0.49, 0.25), [11, 18]),
+        ({"approached": True, "grasped": True}, ((0.1, -0.5, 0.1), (0.12, -0.48, 0.15)), ((0.08, -0.5, 0.1), (0.1, -0.52, 0.16)),
+         (0.01, -0.5, 0.3), (0.16, -0.5, 0.3), (0.1, -0.49, 0.15), [11, 18]),
+        ({"approached": False, "grasped": False}, ((0.1, -0.5, 0.1), (0.12, -0.48, 0.15)), ((0.08, -0.5, 0.1), (0.1, -0.52, 0.16)),
+         (0.01, -0.5, 0.12), (0.2, -0.5, 0.12), (0.11, -0.49, 0.125), []),
+    ]
+    for flags, aabb11, aabb16, f11, f16, cube, links in cases:
+        env = CubesGrasp.__new__(CubesGrasp)
+        env.vis = False
+        env.camera = None
+        env.control_method = "joint"
+        env.subgoals_achieved = dict(flags)
+        env.target_id = 10
+        calls = []
+        ee_pose = (0.05, -0.5, 0.3, 0.0, 0.7, 0.0, 0.7)
+        env.robot = types.SimpleNamespace(id=1, gripper_range=[0, 0.085],
+                                          move_ee=lambda a, m: calls.append(("move_ee", [float(x) for x in a], m)),
+                                          open_gripper=lambda pct=100: calls.append(("open", pct)),
+                                          close_gripper=lambda pct=100: calls.append(("close", pct)),
+                                          get_joint_obs=lambda: {"ee_pos": ee_pose})
+        env.wait_until_stable = lambda: True
+        p.reset_mock()
+        p.getAABB.side_effect = lambda bid, l: (aabb11 if l == 11 else aabb16)
+        p.getLinkState.side_effect = lambda bid, l: ((0, 0, 0), (0, 0, 0, 1), (0, 0, 0), (0, 0, 0, 1),
+                                                     (f11 if l == 11 else f16), (0, 0, 0, 1))
+        p.getBasePositionAndOrientation.side_effect = lambda i: (cube, (0.0, 0.0, 0.0, 1.0))
+        p.getContactPoints.side_effect = lambda *a, **k: [contact(l, -1) for l in links]
+        act = np.array([0.9, 0.1, 0.1, -0.2, 0.3, -0.4, 0.5, -0.6, 0.7], dtype=np.float32)
+        random.seed(3)
+        obs, rew, term, trunc, info = env.step(act)
+        steps.append({"flags_in": flags, "aabb11": aabb11, "aabb16": aabb16, "frame11": f11, "frame16": f16,
+                      "cube": list(cube), "robot_links": links, "action": act.tolist(), "calls": calls,
+                      "flags_out": dict(env.subgoals_achieved), "obs": [float(x) for x in obs],
+                      "reward": float(rew), "terminated": bool(term), "is_success": bool(info["is_success"]),
+                      "distance": float(env.distance_to_target(10)), "opening": float(env.get_gripper_opening_length())})
+    out["cubesgrasp_step"] = steps
+    json.dump(out, open(os.path.join(OUT, "cubes_glue.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":

@@ -80,4 +80,24 @@ UG_CONST double UG_GEAR_RATIO[5] = {1.0, -1.0, -1.0, 1.0, -1.0};
 #define UG_CUBE_MASS 1.0
 #define UG_CUBE_FRICTION 1.0
 
+/* "vertical" EE orientation = quaternion_multiply((0,0,0,1), getQuaternionFromAxisAngle([0,1,0], pi/2))
+ * (env_cubes_push_v0.py:222-223, utilities.py:134-174): (0, sin(pi/4), 0, cos(pi/4)) with the libm
+ * values Bullet's btQuaternion::setRotation produces */
+#define UG_VQ_S 0.7071067811865475
+#define UG_VQ_C 0.7071067811865476
+
+/* CubesPush (env_cubes_push_v0.py) */
+#define UG_CP_RADIUS 0.1               /* :90 positive_reward_radius */
+#define UG_CP_DMAX 0.5                 /* :156 geometric_distance_reward(d, 0.1, 0.5) / 10 */
+#define UG_CP_CLOSE 0.05               /* :159 are_cubes_close(..., 0.05) */
+#define UG_CP_EE_DZ 0.2                /* :220 */
+
+/* CubesGrasp (env_cubes_grasp_v0.py) */
+#define UG_CG_RAISE 0.2                /* :20 OBJECT_RAISE_HEIGHT */
+#define UG_CG_APPROACH 0.05            /* :209 */
+#define UG_CG_OPEN_MIN 0.50            /* :209 */
+#define UG_CG_OPEN_OFF 0.052           /* :359 */
+#define UG_CG_RMIN 0.5                 /* :313 */
+#define UG_CG_RMAX 0.8                 /* :314 */
+
 #endif

@@ -108,6 +108,27 @@ __global__ void k_build_scene(Scene* s, int task) {
         c->owner = -3; c->ent = 2;
         s->ocol[1] = s->ncol++;
     }
+    if (task == UG_TASK_CUBESPUSH || task == UG_TASK_CUBESGRASP) {
+        s->nobj = task == UG_TASK_CUBESPUSH ? 2 : 1;
+        for (int o = 0; o < s->nobj; o++) {
+            double h = UG_CUBE_HALF, m = UG_CUBE_MASS;
+            s->omass[o] = m;
+            double ii = m / 12.0 * (4.0 * h * h + 4.0 * h * h);
+            s->oinertia[o] = V(ii, ii, ii);
+            Collider* c = &s->col[s->ncol];
+            box_collider(c, h, h, h, UG_URDF_MARGIN, UG_CUBE_FRICTION);
+            c->owner = -2 - o; c->ent = 1 + o;
+            s->ocol[o] = s->ncol++;
+        }
+    }
+    if (task == UG_TASK_CUBESGRASP) {
+        Collider* c = &s->col[s->ncol];
+        box_collider(c, UG_PLANE_HALF_XY, UG_PLANE_HALF_XY, UG_PLANE_HALF_Z, UG_URDF_MARGIN, UG_PLANE_FRICTION);
+        c->P = V(0.0, 0.0, -UG_PLANE_HALF_Z); c->aP = c->P;
+        c->disc = ug_sqrt(15.0 * 15.0 * 2.0 + 25.0) + 5.0;
+        c->owner = -100; c->ent = 11;
+        statics[nstat++] = s->ncol++;
+    }
     if (task == UG_TASK_BALLBALANCE || task == UG_TASK_CUBESPUSH || task == UG_TASK_GOLF) {
         Collider* c = &s->col[s->ncol];
         box_collider(c, 0.5, 1.0, 0.25, safe_margin(0.5, 1.0, 0.25), UG_DEFAULT_FRICTION);
@@ -338,8 +359,9 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
 }
 
 urgym_handle* urgym_create(int task, int n, int dev, int precision, uint32_t seed, int env_offset) {
-    if (task != URGYM_TASK_BALLBALANCE) {
-        fail(nullptr, "urgym_create: task " + std::to_string(task) + " not implemented in this build (BallBalance only)");
+    if (task < URGYM_TASK_BALLBALANCE || task > URGYM_TASK_CUBESGRASP) {
+        fail(nullptr, "urgym_create: task " + std::to_string(task) +
+                          " not implemented in this build (BallBalance, CubesPush, CubesGrasp)");
         return nullptr;
     }
     if (n <= 0) { fail(nullptr, "urgym_create: n_envs must be > 0"); return nullptr; }

@@ -1,0 +1,96 @@
+/* ug_glue.h -- the tasks' pure scalar glue (rewards, subgoals, draws -> placements, action choice),
+ * shared verbatim by the CPU restatement (oracle/ug_oracle.c) and the HIP kernels (ug_team.h), and
+ * pinned against the reference's own Python glue by tests/golden (tools/gen_golden.py).
+ * Inputs are the physics-derived quantities the reference queries through pybullet (contact
+ * predicates, poses, gripper geometry); the arithmetic order follows the cited Python lines.
+ */
+#ifndef UG_GLUE_H
+#define UG_GLUE_H
+
+#include "ug_detmath.h"
+
+/* geometric_distance_reward (utilities.py:192-207) */
+UG_HD double ugg_gdr(double value, double ts, double tm) {
+    value = value > 1e-10 ? value : 1e-10;
+    double f1 = (value - ts) / value;
+    double f2 = (tm - value) > 1e-10 ? (tm - value) : 1e-10;
+    return -ug_tanh(f1 / f2);
+}
+
+/* get_gripper_geometrical_center (env_ball_balance_v0.py:249-275): centre of the union of two AABBs */
+UG_HD void ugg_union_center(const double* lo1, const double* hi1, const double* lo2, const double* hi2, double* c) {
+    for (int i = 0; i < 3; i++) {
+        double lo = lo1[i] < lo2[i] ? lo1[i] : lo2[i];
+        double hi = hi1[i] > hi2[i] ? hi1[i] : hi2[i];
+        c[i] = (hi + lo) / 2.0;
+    }
+}
+
+/* random.uniform(a, b) = a + (b - a) * random() */
+UG_HD double ugg_uniform(double a, double b, double u) { return a + (b - a) * u; }
+
+/* ---- CubesPush (env_cubes_push_v0.py) ---- */
+/* create_cubes (:240-246): second cube x = uniform(-0.1, 0.1) */
+UG_HD double ugg_cp_cube1_x(double u) { return ugg_uniform(-0.1, 0.1, u); }
+/* step reward (:129-150 with update_reward :152-165, dense): returns success */
+UG_HD int ugg_cp_reward(int table_contact, int touched, double c0x, double c0y, double c0z, double c1x, double c1y,
+                        double c1z, double* reward) {
+    double r = 0.0;
+    int success = 0;
+    if (table_contact) {
+        r -= 0.01;
+    } else if (touched) {
+        double dist = ug_norm3(c0x - c1x, c0y - c1y, c0z - c1z);
+        double ur = 0.0 + ugg_gdr(dist, 0.1, 0.5) / 10.0;
+        if (dist < 0.05) { ur += 10.0; success = 1; }
+        r = ur + 0.1;
+    }
+    r -= 0.1;
+    *reward = r;
+    return success;
+}
+
+/* ---- CubesGrasp (env_cubes_grasp_v0.py) ---- */
+/* create_cubes (:310-330): r = uniform(0.5, 0.8), theta = uniform(-pi, 0), (r cos theta, r sin theta, 0.1) */
+UG_HD void ugg_cg_cube_xy(double u0, double u1, double* x, double* y) {
+    double r = ugg_uniform(0.5, 0.8, u0);
+    double th = ugg_uniform(-UG_PI, 0.0, u1);
+    *x = r * ug_cos(th);
+    *y = r * ug_sin(th);
+}
+/* random.choices([0, 1], weights=[w0, w1], k=1) (:141-147) with numpy 1.26 scalar promotion: float32
+ * cumulative weights, total promoted to float64, x = random() * total, bisect_right */
+UG_HD int ugg_cg_choose(float w0, float w1, double u) {
+    float sum = w0 + w1;
+    if (sum == 0.0f) return u * 1.0 < 0.5 ? 0 : 1;
+    double x = u * ((double)sum + 0.0);
+    return x < (double)w0 ? 0 : 1;
+}
+/* get_gripper_opening_length (:349-376) from the distance of link frames 11 and 16 */
+UG_HD double ugg_cg_opening(double frame_dist) {
+    double v = frame_dist - 0.052;
+    double lo = 0.0, hi = 0.085;
+    double t = v < hi ? v : hi;  /* min(max_opening, value) */
+    v = t > lo ? t : lo;         /* max(min_opening, ...) */
+    return (v - lo) / (hi - lo);
+}
+/* step reward and subgoal update (:156-192); flags in/out; returns success */
+UG_HD int ugg_cg_reward(int* approached, int* grasped, double dist, double opening, int grasp_contact, double cube_z,
+                        double* reward) {
+    double r = 0.0;
+    int success = 0;
+    if (!*approached) {
+        r += ugg_gdr(dist, 0.5, 2.0) / 4.0;
+        if (dist < 0.05 && opening > 0.50) { *approached = 1; r += 5.0; }
+    } else if (!*grasped) {
+        if (grasp_contact) { *grasped = 1; r += 5.0; }
+    } else if (grasp_contact && cube_z > 0.2) {
+        r += 10.0;
+        success = 1;
+    }
+    r -= 0.1;
+    *reward = r;
+    return success;
+}
+
+#endif

@@ -26,6 +26,7 @@
 #include <utility>
 
 #include "ug_device.h"
+#include "ug_glue.h"
 
 namespace ugd {
 
@@ -1079,10 +1080,9 @@ struct Draws {
     Rng rng;
     const double* given;
     int k;
-    __device__ double uniform(double a, double b) {
-        double u = given ? given[k++] : mt_random(rng);
-        return a + (b - a) * u;
-    }
+    /* one random.random(): the caller's reset draw when given, else the env's MT19937 stream */
+    __device__ double next() { return given ? given[k++] : mt_random(rng); }
+    __device__ double uniform(double a, double b) { return ugg_uniform(a, b, next()); }
 };
 __device__ static void bb_obs(const EnvState& e, double* obs) {
     v3 eu = euler_from_quat(e.obj[0].quat);
@@ -1090,6 +1090,60 @@ __device__ static void bb_obs(const EnvState& e, double* obs) {
     obs[3] = e.obj[0].pos.x - e.obj[1].pos.x;
     obs[4] = e.obj[0].pos.y - e.obj[1].pos.y;
     obs[5] = e.obj[0].pos.z - e.obj[1].pos.z;
+}
+/* p.getContactPoints existence: a manifold point between a robot link in [lmin, lmax]
+ * and collider cb (robot colliders are always side A of their pairs) */
+__device__ static int robot_contact(const EnvState& e, const Scene* s, int cb, int lmin, int lmax) {
+    int nm = (int)e.nman;
+    for (int m = 0; m < nm; m++) {
+        const PairDef& P = s->pair[(int)e.man[m].pair];
+        if (e.man[m].npts <= 0.0 || P.b != cb) continue;
+        int l = s->col[P.a].link;
+        if (l >= lmin && l <= lmax) return 1;
+    }
+    return 0;
+}
+__device__ static int static_collider(const Scene* s, int ent) {
+    for (int i = 0; i < s->ncol; i++)
+        if (s->col[i].ent == ent) return i;
+    return -1;
+}
+__device__ static void move_ee_joint(EnvState& e, const double* q6) {
+    for (int i = 0; i < 6; i++) { e.mtarget[i] = q6[i]; e.mon[i] = 1.0; }
+}
+/* CubesPush obs (env_cubes_push_v0.py:196-205) */
+__device__ static void cp_obs(const EnvState& e, double* obs) {
+    v3 pe;
+    q4 oe;
+    link_state_of(e.q, UG_EE_LINK, pe, oe);
+    obs[0] = pe.x; obs[1] = pe.y; obs[2] = pe.z;
+    for (int o = 0; o < 2; o++) { obs[3 + 3 * o] = e.obj[o].pos.x; obs[4 + 3 * o] = e.obj[o].pos.y; obs[5 + 3 * o] = e.obj[o].pos.z; }
+}
+/* CubesGrasp: opening from link frames 11/16 (env_cubes_grasp_v0.py:349-376) */
+__device__ static double cg_opening(const EnvState& e) {
+    Kin k;
+    fk(e.q, k);
+    m3 R1, R2;
+    v3 p1, p2;
+    link_frame(k, 11, 0, R1, p1);
+    link_frame(k, 16, 0, R2, p2);
+    return ugg_cg_opening(ug_norm3(p2.x - p1.x, p2.y - p1.y, p2.z - p1.z));
+}
+__device__ static void cg_obs(const EnvState& e, double* obs) {
+    /* :268-287 */
+    v3 pe;
+    q4 oe;
+    link_state_of(e.q, UG_EE_LINK, pe, oe);
+    obs[0] = e.goal_approached; obs[1] = e.goal_grasped;
+    obs[2] = pe.x; obs[3] = pe.y; obs[4] = pe.z; obs[5] = oe.x; obs[6] = oe.y; obs[7] = oe.z; obs[8] = oe.w;
+    obs[9] = cg_opening(e);
+    obs[10] = e.obj[0].pos.x; obs[11] = e.obj[0].pos.y; obs[12] = e.obj[0].pos.z;
+    obs[13] = e.obj[0].quat.x; obs[14] = e.obj[0].quat.y; obs[15] = e.obj[0].quat.z; obs[16] = e.obj[0].quat.w;
+}
+__device__ static void task_obs(const Scene* s, const EnvState& e, double* obs) {
+    if (s->task == UG_TASK_CUBESPUSH) cp_obs(e, obs);
+    else if (s->task == UG_TASK_CUBESGRASP) cg_obs(e, obs);
+    else bb_obs(e, obs);
 }
 /* ---------------- the env program: step / reset as one substep loop ----------------
  * The reference's control flow (env_ball_balance_v0.py: step 105-134, reset 145-170, wait_until_stable
@@ -1109,25 +1163,64 @@ struct RunIO {
 /* lane-0 glue of one program point; returns the physics loop to run next and sets *next */
 __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* next) {
     EnvState& e = g_sh.e;
+    const int task = s->task;
+    const int O = task == UG_TASK_BALLBALANCE ? 6 : (task == UG_TASK_CUBESGRASP ? 17 : 9);
     switch (pc) {
-        case G_STEP: { /* env_ball_balance_v0.py:105-118: move_ee(end pose + action) */
+        case G_STEP: {
             v3 pe;
             q4 oe;
-            link_state_of(e.q, UG_EE_LINK, pe, oe);
-            v3 eu = euler_from_quat(oe);
-            eu.x += (double)io.act[0]; eu.y += (double)io.act[1]; eu.z += (double)io.act[2];
-            move_ee_end(e, pe, quat_from_euler(eu));
+            if (task == UG_TASK_CUBESGRASP) {
+                /* env_cubes_grasp_v0.py:132-158: random.choices picks joint move or gripper command */
+                int sel = ugg_cg_choose(io.act[0], io.act[1], io.dr.next());
+                if (sel == 0) {
+                    double q6[6];
+                    for (int i = 0; i < 6; i++) q6[i] = (double)io.act[2 + i];
+                    move_ee_joint(e, q6);
+                } else if (io.act[8] < 0.5f) {
+                    open_gripper(e, 100.0);
+                } else {
+                    close_gripper(e, 100.0);
+                }
+            } else if (task == UG_TASK_CUBESPUSH) {
+                /* env_cubes_push_v0.py:115-127: EE position + action, vertical orientation */
+                link_state_of(e.q, UG_EE_LINK, pe, oe);
+                move_ee_end(e, V(pe.x + (double)io.act[0], pe.y + (double)io.act[1], pe.z + (double)io.act[2]),
+                            Q(0.0, UG_VQ_S, 0.0, UG_VQ_C));
+            } else {
+                /* env_ball_balance_v0.py:105-118: move_ee(end pose + action on the euler angles) */
+                link_state_of(e.q, UG_EE_LINK, pe, oe);
+                v3 eu = euler_from_quat(oe);
+                eu.x += (double)io.act[0]; eu.y += (double)io.act[1]; eu.z += (double)io.act[2];
+                move_ee_end(e, pe, quat_from_euler(eu));
+            }
             *next = G_STEP_DONE;
             return L_WAIT;
         }
-        case G_STEP_DONE: /* :119-134 reward 1, terminated when the ball falls below the paddle */
-            io.rew = 1.0;
-            io.term = e.obj[1].pos.z < e.obj[0].pos.z;
-            io.succ = 0;
-            bb_obs(e, io.obs);
+        case G_STEP_DONE:
+            if (task == UG_TASK_CUBESPUSH) { /* :129-150 */
+                int table = robot_contact(e, s, static_collider(s, 10), 1, UG_NL - 1);
+                int touched = robot_contact(e, s, s->ocol[1], 9, 18);
+                io.succ = ugg_cp_reward(table, touched, e.obj[0].pos.x, e.obj[0].pos.y, e.obj[0].pos.z, e.obj[1].pos.x,
+                                        e.obj[1].pos.y, e.obj[1].pos.z, &io.rew);
+                io.term = io.succ;
+            } else if (task == UG_TASK_CUBESGRASP) { /* :160-192 */
+                v3 gc = gripper_center(e.q);
+                double d = ug_norm3(gc.x - e.obj[0].pos.x, gc.y - e.obj[0].pos.y, gc.z - e.obj[0].pos.z);
+                int grasp = robot_contact(e, s, s->ocol[0], 11, 13) && robot_contact(e, s, s->ocol[0], 16, 18);
+                int app = (int)e.goal_approached, gr = (int)e.goal_grasped;
+                io.succ = ugg_cg_reward(&app, &gr, d, cg_opening(e), grasp, e.obj[0].pos.z, &io.rew);
+                e.goal_approached = (double)app;
+                e.goal_grasped = (double)gr;
+                io.term = io.succ;
+            } else { /* env_ball_balance_v0.py:119-134: reward 1, terminated when the ball falls below the paddle */
+                io.rew = 1.0;
+                io.term = e.obj[1].pos.z < e.obj[0].pos.z;
+                io.succ = 0;
+            }
+            task_obs(s, e, io.obs);
             if (io.autoreset && (io.term || io.trunc)) {
                 if (io.final_obs)
-                    for (int j = 0; j < 6; j++) io.final_obs[j] = io.obs[j];
+                    for (int j = 0; j < O; j++) io.final_obs[j] = io.obs[j];
                 *next = G_RESET;
                 return L_NONE;
             }
@@ -1139,15 +1232,32 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
             for (int i = 0; i < 6; i++) { e.q[i] = UG_ARM_REST[i]; e.qd[i] = 0.0; }
             *next = G_RESET_ROBOT;
             return L_FIXED10;
-        case G_RESET_ROBOT: /* open_gripper; remove paddle/ball; move_ee(start pose); open 20% */
+        case G_RESET_ROBOT: /* reset_gripper (open 100), then the task's scene and start pose */
             open_gripper(e, 100.0);
-            remove_object(e, s, 0);
-            remove_object(e, s, 1);
-            move_ee_end(e, V(0.0, -0.60, 0.60), Q(0.50, -0.50, -0.50, 0.50));
-            open_gripper(e, 20.0);
-            *next = G_RESET_PLACE;
+            for (int o = 0; o < s->nobj; o++) remove_object(e, s, o);
+            if (task == UG_TASK_CUBESPUSH) { /* env_cubes_push_v0.py:207-227, create_cubes :240-246 */
+                place_object(e, 0, V(0.0, -0.5, 0.1), Q(0, 0, 0, 1));
+                double x = ugg_cp_cube1_x(io.dr.next());
+                place_object(e, 1, V(x, -0.7, 0.1), Q(0, 0, 0, 1));
+                move_ee_end(e, V(x, -0.7, 0.1 + UG_CP_EE_DZ), Q(0.0, UG_VQ_S, 0.0, UG_VQ_C));
+                close_gripper(e, 100.0);
+                *next = G_RESET_DONE;
+            } else if (task == UG_TASK_CUBESGRASP) { /* env_cubes_grasp_v0.py:289-307, create_cubes :310-330 */
+                double u0 = io.dr.next(), u1 = io.dr.next(), x, y;
+                ugg_cg_cube_xy(u0, u1, &x, &y);
+                place_object(e, 0, V(x, y, 0.1), Q(0, 0, 0, 1));
+                v3 pe;
+                q4 oe;
+                link_state_of(e.q, UG_EE_LINK, pe, oe);
+                move_ee_end(e, pe, oe);
+                *next = G_RESET_DONE;
+            } else { /* env_ball_balance_v0.py:145-160: move_ee(start pose); open 20% */
+                move_ee_end(e, V(0.0, -0.60, 0.60), Q(0.50, -0.50, -0.50, 0.50));
+                open_gripper(e, 20.0);
+                *next = G_RESET_PLACE;
+            }
             return L_WAIT;
-        case G_RESET_PLACE: { /* create paddle between the fingers, ball above it; close gripper */
+        case G_RESET_PLACE: { /* BallBalance: paddle between the fingers, ball above it; close gripper */
             v3 pe;
             q4 oe;
             link_state_of(e.q, UG_EE_LINK, pe, oe);
@@ -1163,7 +1273,9 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
             return L_WAIT;
         }
         case G_RESET_DONE:
-            bb_obs(e, io.obs);
+            e.goal_approached = 0.0;
+            e.goal_grasped = 0.0;
+            task_obs(s, e, io.obs);
             io.reset_done = 1;
             *next = G_END;
             return L_NONE;

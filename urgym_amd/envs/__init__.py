@@ -64,4 +64,14 @@ def BallBalance(camera=None, reward_type="dense", render_mode="human", **kw):
     return URGymEnv(0, max_episode_steps=None, camera=camera, reward_type=reward_type, render_mode=render_mode, **kw)
 
 
-__all__ = ["make", "TASKS", "URGymEnv", "URGymVectorEnv", "BallBalance", "spaces_for"]
+def CubesPush(camera=None, reward_type="dense", render_mode="human", **kw):
+    """env_cubes_push_v0.CubesPush(camera, reward_type, render_mode) signature."""
+    return URGymEnv(1, max_episode_steps=None, camera=camera, reward_type=reward_type, render_mode=render_mode, **kw)
+
+
+def CubesGrasp(camera=None, reward_type="dense", render_mode="human", **kw):
+    """env_cubes_grasp_v0.CubesGrasp(camera, reward_type, render_mode) signature."""
+    return URGymEnv(2, max_episode_steps=None, camera=camera, reward_type=reward_type, render_mode=render_mode, **kw)
+
+
+__all__ = ["make", "TASKS", "URGymEnv", "URGymVectorEnv", "BallBalance", "CubesPush", "CubesGrasp", "spaces_for"]
