@@ -46,6 +46,8 @@ def lib():
         L.ugo_g_cg_opening.restype = D
         L.ugo_g_cg_reward.argtypes = [P, D, D, I, D, P]
         L.ugo_g_union_center.argtypes = [P, P]
+        L.ugo_g_gf_ball_xy.argtypes = [D, D, P]
+        L.ugo_g_gf_reward.argtypes = [P, P, P, I, I, I, P, P]
         L.ugo_step.argtypes = [P, P, P, P, P, P]
         L.ugo_get_state.argtypes = [P, P]
         L.ugo_set_state.argtypes = [P, P]

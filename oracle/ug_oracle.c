@@ -23,8 +23,8 @@
 #define NV (NB + 6 * MAXOBJ)
 #define MAXMAN 16
 #define MAXROWS 128
-#define MAXCOL 24
-#define MAXPAIR 96
+#define MAXCOL 28
+#define MAXPAIR 160
 #define MAXCAND 64
 #define PT_DOUBLES 13
 #define MAN_DOUBLES (2 + 4 * PT_DOUBLES)
@@ -228,13 +228,13 @@ typedef struct {
     m3 aR; v3 aP;     /* AABB frame in owner frame */
     v3 ac, ah;        /* AABB centre / half extents in the AABB frame */
     double disc;      /* angular motion disc */
-    double friction, restitution;
+    double friction, restitution, rolling;
     int owner;        /* >=0 robot body, -1 fixed robot base, -2-i object i, -100 static */
     int ent;          /* 0 robot, 1+i object i, 10+s static s */
     int link;         /* pybullet link index for robot colliders, -1 otherwise */
 } collider;
 
-typedef struct { int a, b; double thr, friction, restitution; } pairdef;
+typedef struct { int a, b; double thr, friction, restitution, rolling; } pairdef;
 
 typedef struct {
     int task;
@@ -244,7 +244,8 @@ typedef struct {
     v3 oinertia[MAXOBJ];
     int ncol;
     collider col[MAXCOL];
-    int ocol[MAXOBJ]; /* collider index of each object */
+    int ocol[MAXOBJ]; /* first collider of each object */
+    int oncol[MAXOBJ]; /* colliders of each object (consecutive) */
     int npair;
     pairdef pair[MAXPAIR];
 } scene;
@@ -298,6 +299,11 @@ static void add_pair(scene* s, int a, int b) {
     if (f > UG_MAX_FRICTION) f = UG_MAX_FRICTION;
     p->friction = f;
     p->restitution = s->col[a].restitution * s->col[b].restitution;
+    /* btManifoldResult::calculateCombinedRollingFriction [ext] */
+    double r = s->col[a].rolling * s->col[b].friction + s->col[a].friction * s->col[b].rolling;
+    if (r < -UG_MAX_FRICTION) r = -UG_MAX_FRICTION;
+    if (r > UG_MAX_FRICTION) r = UG_MAX_FRICTION;
+    p->rolling = r;
 }
 
 static void build_scene(scene* s, int task) {
@@ -377,6 +383,57 @@ static void build_scene(scene* s, int task) {
         c->owner = -100; c->ent = 11;
         statics[nstat++] = s->ncol++;
     }
+    if (task == UG_TASK_GOLF) {
+        /* club (env_golf_v0.py:289-332): one rigid body at the composite COM of its three 1 kg parts */
+        s->nobj = 2;
+        double m = UG_GF_PART_MASS, zc = UG_GF_ZC;
+        double bx = UG_GF_BASE_HX, bz = UG_GF_BASE_HZ, fx = UG_GF_FOOT_HX, fy = UG_GF_FOOT_HY;
+        double r = UG_CYL_R, hh = UG_CYL_HH;
+        /* part inertias: btBoxShape / btCylinderShapeZ calculateLocalInertia [ext] */
+        v3 Ib = V(m / 12.0 * (4.0 * bx * bx + 4.0 * bz * bz), m / 12.0 * (4.0 * bx * bx + 4.0 * bz * bz),
+                  m / 12.0 * (4.0 * bx * bx + 4.0 * bx * bx));
+        v3 If = V(m / 12.0 * (4.0 * fy * fy + 4.0 * fy * fy), m / 12.0 * (4.0 * fx * fx + 4.0 * fy * fy),
+                  m / 12.0 * (4.0 * fx * fx + 4.0 * fy * fy));
+        double ic = m / 12.0 * (4.0 * hh * hh) + m / 4.0 * (r * r);
+        v3 Ic = V(ic, ic, m / 2.0 * (r * r));
+        double d0 = 0.0 - zc, d1 = UG_GF_FOOT_Z - zc, d2 = UG_GF_DISC_Z - zc; /* offsets along z */
+        s->omass[0] = 3.0 * m;
+        s->oinertia[0] = V(Ib.x + m * d0 * d0 + If.x + m * d1 * d1 + Ic.x + m * d2 * d2,
+                           Ib.y + m * d0 * d0 + If.y + m * d1 * d1 + Ic.y + m * d2 * d2, Ib.z + If.z + Ic.z);
+        s->ocol[0] = s->ncol;
+        collider* c = &s->col[s->ncol++];
+        box_collider(c, bx, bx, bz, safe_margin(bx, bx, bz), UG_GF_BASE_FRICTION);
+        c->restitution = UG_GF_BASE_RESTITUTION;
+        c->P = V(0.0, 0.0, d0); c->aP = c->P;
+        c->owner = -2; c->ent = 1;
+        c = &s->col[s->ncol++];
+        box_collider(c, fx, fy, fy, safe_margin(fx, fy, fy), UG_DEFAULT_FRICTION);
+        c->P = V(0.0, 0.0, d1); c->aP = c->P;
+        c->owner = -2; c->ent = 1;
+        c = &s->col[s->ncol++];
+        box_collider(c, r, r, hh, UG_CYL_MARGIN, UG_DEFAULT_FRICTION);
+        c->kind = UG_SHAPE_HULL;
+        c->margin = UG_CYL_MARGIN;
+        c->v0 = UG_CYL_V0; c->nv = UG_CYL_NV; c->f0 = UG_CYL_F0; c->nf = UG_CYL_NF;
+        c->P = V(0.0, 0.0, d2); c->aP = c->P;
+        c->owner = -2; c->ent = 1;
+        s->oncol[0] = 3;
+        /* ball (:335-358) */
+        double rb = UG_GF_BALL_R, mb = UG_GF_BALL_MASS;
+        s->omass[1] = mb;
+        double ib = 0.4 * mb * rb * rb;
+        s->oinertia[1] = V(ib, ib, ib);
+        c = &s->col[s->ncol];
+        box_collider(c, rb, rb, rb, rb, UG_DEFAULT_FRICTION);
+        c->kind = UG_SHAPE_SPHERE;
+        c->half[1] = c->half[2] = 0.0;
+        c->disc = ug_sqrt(3.0) * rb;
+        c->restitution = UG_GF_BALL_RESTITUTION;
+        c->rolling = UG_GF_BALL_ROLLING;
+        c->owner = -3; c->ent = 2;
+        s->ocol[1] = s->ncol++;
+        s->oncol[1] = 1;
+    }
     if (task == UG_TASK_BALLBALANCE || task == UG_TASK_CUBESPUSH || task == UG_TASK_GOLF) {
         /* table (env_ball_balance_v0.py:71,216-247) and plane at z=-0.5 (:70) */
         collider* c = &s->col[s->ncol];
@@ -391,20 +448,35 @@ static void build_scene(scene* s, int task) {
         c->owner = -100; c->ent = 11;
         statics[nstat++] = s->ncol++;
     }
-    /* pairs: robot x objects, robot x statics, object x object, object x static */
+    if (task == UG_TASK_GOLF) {
+        /* pitch: static convex hull of golf_pitch.obj (a slab), margin outside (env_golf_v0.py:428-446) */
+        collider* c = &s->col[s->ncol];
+        box_collider(c, UG_GF_PITCH_HX + UG_URDF_MARGIN, UG_GF_PITCH_HX + UG_URDF_MARGIN,
+                     UG_GF_PITCH_HZ + UG_URDF_MARGIN, UG_URDF_MARGIN, UG_DEFAULT_FRICTION);
+        c->P = V(UG_GF_PITCH_X, UG_GF_PITCH_Y, UG_GF_PITCH_Z); c->aP = c->P;
+        c->owner = -100; c->ent = 12;
+        statics[nstat++] = s->ncol++;
+    }
     for (int o = 0; o < s->nobj; o++)
-        for (int l = 0; l < nrobot; l++) add_pair(s, l, s->ocol[o]);
+        if (s->oncol[o] == 0) s->oncol[o] = 1;
+    /* pairs: robot x objects, robot x statics, object x object, object x static (objects: each collider) */
+    for (int o = 0; o < s->nobj; o++)
+        for (int c = s->ocol[o]; c < s->ocol[o] + s->oncol[o]; c++)
+            for (int l = 0; l < nrobot; l++) add_pair(s, l, c);
     for (int t = 0; t < nstat; t++)
         for (int l = 0; l < nrobot; l++) add_pair(s, l, statics[t]);
     for (int o = 0; o < s->nobj; o++)
-        for (int p = o + 1; p < s->nobj; p++) {
-            int a = s->ocol[o], b = s->ocol[p];
-            /* canonical order for the narrowphase: sphere first, then box */
-            if (s->col[b].kind == UG_SHAPE_SPHERE && s->col[a].kind != UG_SHAPE_SPHERE) { int t = a; a = b; b = t; }
-            add_pair(s, a, b);
-        }
+        for (int p = o + 1; p < s->nobj; p++)
+            for (int ca = s->ocol[o]; ca < s->ocol[o] + s->oncol[o]; ca++)
+                for (int cb = s->ocol[p]; cb < s->ocol[p] + s->oncol[p]; cb++) {
+                    int a = ca, b = cb;
+                    /* canonical order for the narrowphase: sphere first */
+                    if (s->col[b].kind == UG_SHAPE_SPHERE && s->col[a].kind != UG_SHAPE_SPHERE) { int t = a; a = b; b = t; }
+                    add_pair(s, a, b);
+                }
     for (int o = 0; o < s->nobj; o++)
-        for (int t = 0; t < nstat; t++) add_pair(s, s->ocol[o], statics[t]);
+        for (int c = s->ocol[o]; c < s->ocol[o] + s->oncol[o]; c++)
+            for (int t = 0; t < nstat; t++) add_pair(s, c, statics[t]);
 }
 
 /* ======================================================================== */
@@ -1002,6 +1074,58 @@ static void nc_hull_box(const xf* TA, const collider* A, const xf* TB, const col
     reduce4(&L);
     for (int i = 0; i < L.n; i++) cand_add(out, L.c[i].n, L.c[i].pB, L.c[i].d);
 }
+/* hull (A, robot link) vs hull (B, club disc prism): vertex-in-hull both ways with the face planes
+ * (restated substitute for GJK/EPA, as nc_hull_box): A's vertices against B's planes, then B's vertices
+ * against A's planes, deepest + farthest-spread 4 points */
+static void nc_hull_hull(const xf* TA, const collider* A, const xf* TB, const collider* B, double thr, candlist* out) {
+    double mA = A->margin, mB = B->margin;
+    candlist L;
+    L.n = 0;
+    /* A vertex x in B's frame: max over B's faces of n.x - d */
+    m3 RAB = mtm(&TB->R, &TA->R);
+    v3 pAB = mtv(&TB->R, vsub(TA->p, TB->p));
+    for (int i = 0; i < A->nv; i++) {
+        const double* vv = &UG_HULL_V[3 * (A->v0 + i)];
+        v3 x = vadd(mv(&RAB, V(vv[0], vv[1], vv[2])), pAB);
+        double smax = -1e300;
+        int fm = -1;
+        for (int f = 0; f < B->nf; f++) {
+            const double* F = &UG_HULL_F[4 * (B->f0 + f)];
+            double sd = F[0] * x.x + F[1] * x.y + F[2] * x.z - F[3];
+            if (sd > smax) { smax = sd; fm = f; }
+        }
+        double depth = smax - mA - mB;
+        if (depth < thr) {
+            const double* F = &UG_HULL_F[4 * (B->f0 + fm)];
+            v3 nl = V(F[0], F[1], F[2]);
+            v3 pl = vsub(x, vscale(nl, smax));
+            cand_add(&L, mv(&TB->R, nl), xf_apply(TB, pl), depth);
+        }
+    }
+    /* B vertex y in A's frame against A's faces */
+    m3 RBA = mtm(&TA->R, &TB->R);
+    v3 pBA = mtv(&TA->R, vsub(TB->p, TA->p));
+    for (int i = 0; i < B->nv; i++) {
+        const double* vv = &UG_HULL_V[3 * (B->v0 + i)];
+        v3 yl = V(vv[0], vv[1], vv[2]);
+        v3 y = vadd(mv(&RBA, yl), pBA);
+        double smax = -1e300;
+        int fm = -1;
+        for (int f = 0; f < A->nf; f++) {
+            const double* F = &UG_HULL_F[4 * (A->f0 + f)];
+            double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
+            if (sd > smax) { smax = sd; fm = f; }
+        }
+        double depth = smax - mA - mB;
+        if (depth < thr) {
+            const double* F = &UG_HULL_F[4 * (A->f0 + fm)];
+            v3 nw = mv(&TA->R, V(F[0], F[1], F[2]));
+            cand_add(&L, vneg(nw), xf_apply(TB, yl), depth);
+        }
+    }
+    reduce4(&L);
+    for (int i = 0; i < L.n; i++) cand_add(out, L.c[i].n, L.c[i].pB, L.c[i].d);
+}
 /* hull (robot link, A) vs sphere (B): deepest face plane */
 static void nc_hull_sphere(const xf* TA, const collider* A, const xf* TB, const collider* B, double thr, candlist* out) {
     v3 y = mtv(&TA->R, vsub(TB->p, TA->p));
@@ -1134,6 +1258,15 @@ static void collide(ugo_env* e, const kin* k) {
         else if (A->kind == UG_SHAPE_BOX && B->kind == UG_SHAPE_BOX) nc_box_box(&TA, A, &TB, B, P->thr, &L);
         else if (A->kind == UG_SHAPE_HULL && B->kind == UG_SHAPE_BOX) nc_hull_box(&TA, A, &TB, B, P->thr, &L);
         else if (A->kind == UG_SHAPE_HULL && B->kind == UG_SHAPE_SPHERE) nc_hull_sphere(&TA, A, &TB, B, P->thr, &L);
+        else if (A->kind == UG_SHAPE_HULL && B->kind == UG_SHAPE_HULL) nc_hull_hull(&TA, A, &TB, B, P->thr, &L);
+        else if (A->kind == UG_SHAPE_SPHERE && B->kind == UG_SHAPE_HULL) {
+            /* hull-sphere with swapped roles: flip normal, move the point onto the sphere */
+            candlist L2;
+            L2.n = 0;
+            nc_hull_sphere(&TB, B, &TA, A, P->thr, &L2);
+            for (int i = 0; i < L2.n; i++)
+                cand_add(&L, vneg(L2.c[i].n), vadd(L2.c[i].pB, vscale(L2.c[i].n, L2.c[i].d)), L2.c[i].d);
+        }
         else if (A->kind == UG_SHAPE_BOX && B->kind == UG_SHAPE_SPHERE) {
             /* sphere-box with swapped roles: flip normal, move the point onto the sphere */
             candlist L2;
@@ -1163,14 +1296,14 @@ static void collide(ugo_env* e, const kin* k) {
 typedef struct {
     double J[UG_NVP], MiJ[UG_NVP];
     double invD, rhs, rhsPen, lo, hi, imp, impPen, fric;
-    int man, pt, kind;         /* kind 0 non-contact, 1 normal, 2 friction dir1, 3 friction dir2 */
+    int man, pt, kind;         /* kind 0 non-contact, 1 normal, 2/3 friction dir 1/2, 4/5 rolling axis 1/2 */
     int nrow;                  /* friction rows: index of their normal row */
 } row;
 
 typedef struct {
-    int n, nnc, nn, nf;
+    int n, nnc, nn, nf, nr;
     row r[MAXROWS];
-    int idx_nc[MAXROWS], idx_n[MAXROWS], idx_f[MAXROWS];
+    int idx_nc[MAXROWS], idx_n[MAXROWS], idx_f[MAXROWS], idx_r[MAXROWS];
 } rowset;
 
 static int ent_dofs(int ent) { return ent == 0 ? NB : 6; }
@@ -1229,6 +1362,24 @@ static void point_jac(const ugo_env* e, const kin* k, int ent, int body, v3 p, v
     }
 }
 
+/* Jacobian of an angular velocity component along u on entity ent (rolling friction rows) */
+static void ang_jac(const ugo_env* e, const kin* k, int ent, int body, v3 u, double* J, double* MiJ, const double* LDL) {
+    if (ent == 0) {
+        for (int i = 0; i < NB; i++) {
+            J[i] = moves(i, body) ? vdot(u, k->a[i]) : 0.0;
+            MiJ[i] = J[i];
+        }
+        ldlt_solve(LDL, NB, MiJ);
+    } else {
+        int o = ent - 1;
+        J[0] = 0.0; J[1] = 0.0; J[2] = 0.0; J[3] = u.x; J[4] = u.y; J[5] = u.z;
+        m3 R = qmat(e->oquat[o]);
+        v3 ir = mtv(&R, u);
+        ir = V(ir.x / e->sc.oinertia[o].x, ir.y / e->sc.oinertia[o].y, ir.z / e->sc.oinertia[o].z);
+        ir = mv(&R, ir);
+        MiJ[0] = 0.0; MiJ[1] = 0.0; MiJ[2] = 0.0; MiJ[3] = ir.x; MiJ[4] = ir.y; MiJ[5] = ir.z;
+    }
+}
 static int ent_of_collider(const collider* c, int* body) {
     *body = -1;
     if (c->owner >= 0) { *body = c->owner; return 0; }
@@ -1241,18 +1392,20 @@ static void row_clear(row* r) { memset(r, 0, sizeof(*r)); }
 
 /* contact-type row: J_A at pA along +d, J_B at pB along -d; returns relative velocity J.v0 */
 static double contact_row(const ugo_env* e, const kin* k, const double* LDL, const double* v0, row* r, int entA,
-                          int bodyA, int entB, int bodyB, v3 pA, v3 pB, v3 d) {
+                          int bodyA, int entB, int bodyB, v3 pA, v3 pB, v3 d, int ang) {
     double JA[NB], MiJA[NB], JB[NB], MiJB[NB];
     double dA = 0.0, dB = 0.0, relv = 0.0;
     if (entA >= 0) {
-        point_jac(e, k, entA, bodyA, pA, d, JA, MiJA, LDL);
+        if (ang) ang_jac(e, k, entA, bodyA, d, JA, MiJA, LDL);
+        else point_jac(e, k, entA, bodyA, pA, d, JA, MiJA, LDL);
         dA = ent_dot_local(entA, JA, MiJA);
         relv += ent_dot(entA, JA, v0);
         scatter(entA, JA, r->J);
         scatter(entA, MiJA, r->MiJ);
     }
     if (entB >= 0) {
-        point_jac(e, k, entB, bodyB, pB, vneg(d), JB, MiJB, LDL);
+        if (ang) ang_jac(e, k, entB, bodyB, vneg(d), JB, MiJB, LDL);
+        else point_jac(e, k, entB, bodyB, pB, vneg(d), JB, MiJB, LDL);
         dB = ent_dot_local(entB, JB, MiJB);
         relv += ent_dot(entB, JB, v0);
         scatter(entB, JB, r->J);
@@ -1277,7 +1430,7 @@ static double dof_row(const double* LDL, const double* v0, row* r, int d, double
 }
 
 static void build_rows(ugo_env* e, const kin* k, const double* LDL, const double* v0, rowset* rs) {
-    rs->n = rs->nnc = rs->nn = rs->nf = 0;
+    rs->n = rs->nnc = rs->nn = rs->nf = rs->nr = 0;
     const double dt = UG_DT;
     /* joint limits (btMultiBodyJointLimitConstraint, created at URDF load in link order) */
     for (int d = 0; d < NB; d++) {
@@ -1359,15 +1512,16 @@ static void build_rows(ugo_env* e, const kin* k, const double* LDL, const double
         int entB = ent_of_collider(&s->col[P->b], &bodyB);
         if (entA < 0 && entB < 0) continue;
         xf OA = owner_xf(e, k, s->col[P->a].owner), OB = owner_xf(e, k, s->col[P->b].owner);
+        int roll = P->rolling > 0.0; /* rolling friction: two more angular rows per point */
         for (int j = 0; j < M->npts; j++) {
-            if (rs->n + 3 > MAXROWS) { e->overflow++; continue; }
+            if (rs->n + (roll ? 5 : 3) > MAXROWS) { e->overflow++; continue; }
             const cpoint* cp = &M->pt[j];
             v3 pA = xf_apply(&OA, cp->lpA), pB = xf_apply(&OB, cp->lpB);
             v3 n = cp->n;
             int ni = rs->n;
             row* r = &rs->r[ni];
             row_clear(r);
-            double relv = contact_row(e, k, LDL, v0, r, entA, bodyA, entB, bodyB, pA, pB, n);
+            double relv = contact_row(e, k, LDL, v0, r, entA, bodyA, entB, bodyB, pA, pB, n, 0);
             /* a row with zero effective mass (e.g. a contact normal parallel to the only joint axis)
              * is kept as a no-op: rhs = 0, impulse stays 0, residual 0 (Bullet drops it) */
             double pen = cp->dist + UG_LINEAR_SLOP;
@@ -1399,13 +1553,26 @@ static void build_rows(ugo_env* e, const kin* k, const double* LDL, const double
             for (int fdir = 0; fdir < 2; fdir++) {
                 row* f = &rs->r[rs->n];
                 row_clear(f);
-                double frel = contact_row(e, k, LDL, v0, f, entA, bodyA, entB, bodyB, pA, pB, fdir == 0 ? t1 : t2);
+                double frel = contact_row(e, k, LDL, v0, f, entA, bodyA, entB, bodyB, pA, pB, fdir == 0 ? t1 : t2, 0);
                 f->rhs = 0.0 * f->invD + (0.0 - frel) * f->invD;
                 f->fric = P->friction;
                 f->lo = 0.0; f->hi = 0.0;
                 f->imp = 0.0;
                 f->kind = 2 + fdir; f->man = m; f->pt = j; f->nrow = ni;
                 rs->idx_f[rs->nf++] = rs->n++;
+            }
+            /* btMultiBodyConstraintSolver torsional (rolling) friction [ext]: angular rows about the two
+             * btPlaneSpace1 axes, bounds +-rolling * the normal impulse (restated as pyramid rows) */
+            for (int rdir = 0; roll && rdir < 2; rdir++) {
+                row* f = &rs->r[rs->n];
+                row_clear(f);
+                double frel = contact_row(e, k, LDL, v0, f, entA, bodyA, entB, bodyB, pA, pB, rdir == 0 ? t1 : t2, 1);
+                f->rhs = 0.0 * f->invD + (0.0 - frel) * f->invD;
+                f->fric = P->rolling;
+                f->lo = 0.0; f->hi = 0.0;
+                f->imp = 0.0;
+                f->kind = 4 + rdir; f->man = m; f->pt = j; f->nrow = ni;
+                rs->idx_r[rs->nr++] = rs->n++;
             }
         }
     }
@@ -1445,8 +1612,8 @@ static void pgs(rowset* rs, double* dv) {
             x = x * x;
             res = res > x ? res : x;
         }
-        for (int j = 0; j < rs->nf; j++) {
-            row* f = &rs->r[rs->idx_f[j]];
+        for (int j = 0; j < rs->nf + rs->nr; j++) {
+            row* f = &rs->r[j < rs->nf ? rs->idx_f[j] : rs->idx_r[j - rs->nf]];
             double tot = rs->r[f->nrow].imp;
             if (tot > 0.0) {
                 f->lo = -(f->fric * tot);
@@ -1702,11 +1869,11 @@ static v3 gripper_center(const ugo_env* e) {
 }
 static void remove_object(ugo_env* e, int o) {
     e->oactive[o] = 0;
-    int ci = e->sc.ocol[o];
+    int c0 = e->sc.ocol[o], c1 = c0 + e->sc.oncol[o];
     int k = 0;
     for (int m = 0; m < e->nman; m++) {
         const pairdef* P = &e->sc.pair[e->man[m].pair];
-        if (P->a == ci || P->b == ci) continue;
+        if ((P->a >= c0 && P->a < c1) || (P->b >= c0 && P->b < c1)) continue;
         if (k != m) e->man[k] = e->man[m];
         k++;
     }
@@ -1922,6 +2089,87 @@ static int cg_step(ugo_env* e, const float* a, double* obs, double* rew, uint8_t
     return n;
 }
 
+/* ---- Golf (env_golf_v0.py) ---- */
+/* any manifold point between a collider in [a0, a1) and one in [b0, b1) (either side of the pair) */
+static int pair_contact(const ugo_env* e, int a0, int a1, int b0, int b1) {
+    const scene* s = &e->sc;
+    for (int m = 0; m < e->nman; m++) {
+        const pairdef* P = &s->pair[e->man[m].pair];
+        if (e->man[m].npts <= 0) continue;
+        if ((P->a >= a0 && P->a < a1 && P->b >= b0 && P->b < b1) || (P->b >= a0 && P->b < a1 && P->a >= b0 && P->a < b1))
+            return 1;
+    }
+    return 0;
+}
+static void drop_manifolds_of(ugo_env* e, int ci) {
+    int k = 0;
+    for (int m = 0; m < e->nman; m++) {
+        const pairdef* P = &e->sc.pair[e->man[m].pair];
+        if (P->a == ci || P->b == ci) continue;
+        if (k != m) e->man[k] = e->man[m];
+        k++;
+    }
+    e->nman = k;
+}
+/* club reference points: composite COM + R * offset (offsets along the base z axis) */
+static v3 club_point(const ugo_env* e, double zoff) {
+    m3 R = qmat(e->oquat[0]);
+    return vadd(e->opos[0], mv(&R, V(0.0, 0.0, zoff - UG_GF_ZC)));
+}
+static void gf_obs(const ugo_env* e, double* obs) {
+    v3 st = club_point(e, UG_GF_FOOT_Z); /* getLinkState(stick, 0)[0] (:240-244) */
+    double stick[3] = {st.x, st.y, st.z}, ball[3] = {e->opos[1].x, e->opos[1].y, e->opos[1].z};
+    double hole[3] = {UG_GF_PITCH_X, UG_GF_PITCH_Y, UG_GF_PITCH_Z};
+    ugg_gf_obs(stick, ball, hole, obs);
+}
+static int gf_reset(ugo_env* e, const double* draws, double* obs) {
+    /* :238-267 */
+    int n = robot_reset(e);
+    remove_object(e, 0);
+    remove_object(e, 1);
+    drop_manifolds_of(e, static_collider(&e->sc, 12)); /* the pitch is removed and re-created (:246-248) */
+    move_ee_end(e, V(0.0, -0.60, 0.40), Q(0.0, 0.0, -0.70, 0.70));
+    open_gripper(e, 20.0);
+    n += wait_until_stable(e);
+    v3 gc = gripper_center(e);
+    /* create_stick(pose): base at the gripper centre - 0.05 z, identity orientation -> COM above by zc */
+    place_object(e, 0, V(gc.x, gc.y, gc.z - 0.05 + UG_GF_ZC), Q(0, 0, 0, 1));
+    double u0 = draws ? draws[0] : mt_random(&e->rng);
+    double u1 = draws ? draws[1] : mt_random(&e->rng);
+    double bx, by;
+    ugg_gf_ball_xy(u0, u1, &bx, &by);
+    place_object(e, 1, V(bx, by, 0.1), Q(0, 0, 0, 1));
+    close_gripper(e, 100.0);
+    n += wait_until_stable(e);
+    gf_obs(e, obs);
+    return n;
+}
+static int gf_step(ugo_env* e, const float* a, double* obs, double* rew, uint8_t* term, uint8_t* succ) {
+    /* :115-183 */
+    v3 pe;
+    q4 oe;
+    link_state(e, UG_EE_LINK, &pe, &oe);
+    move_ee_end(e, V(pe.x + (double)a[0], pe.y + (double)a[1], pe.z + (double)a[2]), Q(0.0, 0.0, -0.70, 0.70));
+    int n = wait_until_stable(e);
+    const scene* s = &e->sc;
+    int c0 = s->ocol[0], c1 = c0 + s->oncol[0], cb = s->ocol[1], cp = static_collider(s, 12);
+    int in_fingers = 0;
+    for (int c = c0; c < c1; c++) in_fingers |= robot_contact(e, c, 9, 18);          /* :199-208 */
+    int floor = robot_contact(e, cp, 0, UG_NL - 1) || pair_contact(e, c0, c1, cp, cp + 1); /* :185-197 */
+    int touched = pair_contact(e, cb, cb + 1, c0, c1);                               /* :199-203 */
+    v3 st = club_point(e, UG_GF_FOOT_Z);
+    double stick[3] = {st.x, st.y, st.z}, ball[3] = {e->opos[1].x, e->opos[1].y, e->opos[1].z};
+    double hole[3] = {UG_GF_PITCH_X, UG_GF_PITCH_Y, UG_GF_PITCH_Z};
+    double r;
+    int t;
+    int success = ugg_gf_reward(ball, hole, stick, in_fingers, floor, touched, &r, &t);
+    *rew = r;
+    *term = (uint8_t)t;
+    *succ = (uint8_t)success;
+    gf_obs(e, obs);
+    return n;
+}
+
 /* ======================================================================== */
 /* public API                                                                */
 /* ======================================================================== */
@@ -1940,6 +2188,7 @@ int ugo_reset_draws(ugo_env* e, const double* draws, double* obs) {
         case UG_TASK_BALLBALANCE: return bb_reset(e, draws, obs);
         case UG_TASK_CUBESPUSH: return cp_reset(e, draws, obs);
         case UG_TASK_CUBESGRASP: return cg_reset(e, draws, obs);
+        case UG_TASK_GOLF: return gf_reset(e, draws, obs);
     }
     return -1;
 }
@@ -1948,6 +2197,7 @@ int ugo_step(ugo_env* e, const float* action, double* obs, double* reward, uint8
         case UG_TASK_BALLBALANCE: return bb_step(e, action, obs, reward, terminated, success);
         case UG_TASK_CUBESPUSH: return cp_step(e, action, obs, reward, terminated, success);
         case UG_TASK_CUBESGRASP: return cg_step(e, action, obs, reward, terminated, success);
+        case UG_TASK_GOLF: return gf_step(e, action, obs, reward, terminated, success);
     }
     return -1;
 }
@@ -2065,6 +2315,7 @@ void ugo_observe(const ugo_env* e, double* obs) {
         case UG_TASK_BALLBALANCE: bb_obs(e, obs); break;
         case UG_TASK_CUBESPUSH: cp_obs(e, obs); break;
         case UG_TASK_CUBESGRASP: cg_obs(e, obs); break;
+        case UG_TASK_GOLF: gf_obs(e, obs); break;
     }
 }
 int ugo_terminated(const ugo_env* e) {
@@ -2095,3 +2346,8 @@ int ugo_g_cg_reward(int* flags, double dist, double opening, int grasp, double c
     return ugg_cg_reward(&flags[0], &flags[1], dist, opening, grasp, cube_z, r);
 }
 void ugo_g_union_center(const double* aabbs, double* c) { ugg_union_center(aabbs, aabbs + 3, aabbs + 6, aabbs + 9, c); }
+void ugo_g_gf_ball_xy(double u0, double u1, double* xy) { ugg_gf_ball_xy(u0, u1, &xy[0], &xy[1]); }
+int ugo_g_gf_reward(const double* ball, const double* hole, const double* stick, int in_fingers, int floor_contact,
+                    int touched, double* r, int* term) {
+    return ugg_gf_reward(ball, hole, stick, in_fingers, floor_contact, touched, r, term);
+}

@@ -70,6 +70,9 @@ int ugo_g_cg_choose(float w0, float w1, double u);
 double ugo_g_cg_opening(double d);
 int ugo_g_cg_reward(int* flags, double dist, double opening, int grasp, double cube_z, double* r);
 void ugo_g_union_center(const double* aabbs, double* c);
+void ugo_g_gf_ball_xy(double u0, double u1, double* xy);
+int ugo_g_gf_reward(const double* ball, const double* hole, const double* stick, int in_fingers, int floor_contact,
+                    int touched, double* r, int* term);
 /* batched CPU baseline: n envs, OpenMP over envs; returns total substeps */
 long ugo_batch_step(ugo_env** envs, int n, const float* actions, double* obs, double* reward,
                     uint8_t* terminated, uint8_t* success, int32_t* substeps, int autoreset,

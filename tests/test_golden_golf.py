@@ -1,0 +1,62 @@
+"""Golf glue (urgym_amd/csrc/ug_glue.h `ugg_gf_*`, shared by oracle and HIP kernels) pinned against
+fixtures recorded from the reference's own Golf methods (tools/gen_golden.py -> golf_glue.json):
+reset draw order and placements, EE target, termination precedence, rewards and the observation.
+Physics queries are scripted in the fixture.  Bar: bit-exact (tanh-based shaping within 2 ulp).
+"""
+import ctypes
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def L(built):
+    from oracle import pyoracle
+    return pyoracle.lib()
+
+
+def P(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def load():
+    with open(os.path.join(GOLD, "golf_glue.json")) as f:
+        return json.load(f)
+
+
+def test_golf_reset_sequence_and_placements(L):
+    for c in load()["golf_reset"]:
+        names = [x[0] for x in c["calls"]]
+        # robot.reset, move_ee(start pose), open 20 %, settle, close, settle (env_golf_v0.py:238-267)
+        assert names == ["robot_reset", "move_ee", "open", "wait", "close", "wait"]
+        assert c["calls"][1][1] == [0.0, -0.6, 0.4, 0.0, 0.0, -0.7, 0.7] and c["calls"][2][1] == 20
+        assert c["vertical_quaternion"] == [0.0, 0.0, -0.7, 0.7]
+        pitch, stick, ball = c["bodies"]
+        assert pitch["basePosition"] == [0.0, -0.6, 0.02]                     # re-created pitch
+        gc = c["gripper_center"]
+        assert stick["basePosition"] == [gc[0], gc[1], gc[2] - 0.05]          # :256-261
+        random.seed(c["seed"])
+        xy = np.zeros(2)
+        L.ugo_g_gf_ball_xy(random.random(), random.random(), P(xy))
+        assert ball["basePosition"] == [xy[0], xy[1], 0.1] and ball["args"] == [0.01]
+
+
+def test_golf_step_rewards_termination_obs(L):
+    for c in load()["golf_step"]:
+        a = np.array(c["action"], np.float32)
+        assert c["ik_target"] == [c["ee_pose"][i] + float(a[i]) for i in range(3)] + [0.0, 0.0, -0.7, 0.7]
+        in_fingers = any(9 <= l <= 18 for l in c["finger_links"])
+        floor = bool(c["robot_pitch_links"]) or c["stick_pitch"]
+        r = np.zeros(1)
+        t = np.zeros(1, np.int32)
+        succ = L.ugo_g_gf_reward(P(np.array(c["ball"])), P(np.array(c["hole"])), P(np.array(c["stick"])),
+                                 int(in_fingers), int(floor), int(c["touched"]), P(r), P(t))
+        assert r[0] == pytest.approx(c["reward"], rel=0, abs=4e-16), c
+        assert bool(t[0]) == c["terminated"] and bool(succ) == c["is_success"]
+        stick, ball, hole = np.array(c["stick"]), np.array(c["ball"]), np.array(c["hole"])
+        assert c["obs"] == list(stick) + list(stick - ball) + list(hole - ball)

@@ -148,10 +148,11 @@ def _task_actions(task, rng, n):
     return rng.uniform(-0.1, 0.1, size=(n, 3)).astype(np.float32)
 
 
-@pytest.mark.parametrize("task,max_steps", [(1, 50), (2, 20)])
+@pytest.mark.parametrize("task,max_steps", [(1, 50), (2, 20), (3, 100)])
 def test_cube_tasks_bit_exact_with_autoreset(mods, task, max_steps):
-    """CubesPush / CubesGrasp: reset, steps with contact-predicate rewards,
-    subgoal flags, random.choices draws and same-step autoreset, bit-identical to the oracle."""
+    """CubesPush / CubesGrasp / Golf: reset, steps with contact-predicate rewards,
+    subgoal flags, random.choices draws, the compound club, rolling friction and same-step autoreset,
+    bit-identical to the oracle."""
     Sim, OracleEnv = mods
     n, T = 32, 6
     sim = Sim(task, n, seed=SEED)
@@ -183,7 +184,7 @@ def test_cube_tasks_bit_exact_with_autoreset(mods, task, max_steps):
         assert np.array_equal(st[i], r.get_state()), (task, i)
 
 
-@pytest.mark.parametrize("task", [1, 2])
+@pytest.mark.parametrize("task", [1, 2, 3])
 def test_cube_tasks_reset_draws(mods, task):
     """urgym_reset with caller-supplied draws == oracle reset with the same draws"""
     Sim, OracleEnv = mods

@@ -345,6 +345,29 @@ def main():
                 shp_v0.append(len(V)); shp_nv.append(len(vv)); shp_f0.append(len(F)); shp_nf.append(len(s["planes"]))
                 V.extend(vv.tolist())
                 F.extend(s["planes"].tolist())
+    # Golf club disc (env_golf_v0.py:293-305: GEOM_CYLINDER r 0.04, height 0.01, Z axis): a 16-sided prism
+    # with the cylinder's safe margin (0.1 x min half extent) outside, so the outer extent is the cylinder's
+    # (hull vertices on the circle of radius r - m; restated substitute for btCylinderShapeZ + GJK)
+    cyl_r, cyl_h, cyl_m, nseg = 0.04, 0.005, 0.0005, 16
+    cyl_v0, cyl_f0 = len(V), len(F)
+    rr, hh = cyl_r - cyl_m, cyl_h - cyl_m
+    for zs in (-hh, hh):
+        for k in range(nseg):
+            th = 2.0 * np.pi * k / nseg
+            V.append([rr * np.cos(th), rr * np.sin(th), zs])
+    apo = rr * np.cos(np.pi / nseg)
+    for k in range(nseg):
+        th = 2.0 * np.pi * (k + 0.5) / nseg
+        F.append([np.cos(th), np.sin(th), 0.0, apo])
+    F.append([0.0, 0.0, 1.0, hh])
+    F.append([0.0, 0.0, -1.0, hh])
+    w("#define UG_CYL_V0 %d   /* golf club disc prism: 2 x %d vertices */" % (cyl_v0, nseg))
+    w("#define UG_CYL_NV %d" % (2 * nseg))
+    w("#define UG_CYL_F0 %d" % cyl_f0)
+    w("#define UG_CYL_NF %d" % (nseg + 2))
+    w("#define UG_CYL_R %.17g" % cyl_r)
+    w("#define UG_CYL_HH %.17g" % cyl_h)
+    w("#define UG_CYL_MARGIN %.17g" % cyl_m)
     w("#define UG_NSHAPE %d" % len(shp_link))
     w("#define UG_NHULLV %d" % len(V))
     w("#define UG_NHULLF %d" % len(F))

@@ -157,6 +157,7 @@ def main():
     json.dump({"positions": qs, "abs_sums": sums, "stable": bool(stable)},
               open(os.path.join(OUT, "wait_until_stable.json"), "w"), indent=1)
     gen_cubes(p, rng)
+    gen_golf(p)
     print("wrote", sorted(os.listdir(OUT)))
 
 
@@ -337,6 +338,95 @@ def gen_cubes(p, rng):
                       "distance": float(env.distance_to_target(10)), "opening": float(env.get_gripper_opening_length())})
     out["cubesgrasp_step"] = steps
     json.dump(out, open(os.path.join(OUT, "cubes_glue.json"), "w"), indent=1)
+
+
+
+def gen_golf(p):
+    """Golf (env_golf_v0.py) glue: reset draw order / stick placement / EE target, step termination
+    precedence, rewards and observation with scripted physics."""
+    from urgym.envs.env_golf_v0 import Golf  # noqa: E402
+    out = {}
+    resets = []
+    for seed in [0, 1, 7, 12345, 20241220]:
+        env = Golf.__new__(Golf)
+        env.visualize = False
+        env.stick_id = None
+        env.ball_id = None
+        env.pitch_id = 3
+        calls = []
+        ee = (0.01, -0.61, 0.41, 0.0, 0.0, -0.7, 0.7)
+        env.robot = types.SimpleNamespace(id=1, reset=lambda: calls.append(("robot_reset",)),
+                                          move_ee=lambda pose, m: calls.append(("move_ee", [float(x) for x in pose], m)),
+                                          open_gripper=lambda pct=100: calls.append(("open", pct)),
+                                          close_gripper=lambda pct=100: calls.append(("close", pct)),
+                                          get_joint_obs=lambda: {"ee_pos": ee})
+        env.wait_until_stable = lambda: calls.append(("wait",))
+        env.get_observation = lambda: None
+        gc = [0.012, -0.598, 0.231]
+        env.get_gripper_geometrical_center = lambda: list(gc)
+        p.reset_mock()
+        bodies = []
+
+        def cmb(*a, **k):
+            bodies.append({"args": [float(x) if isinstance(x, (int, float)) else None for x in a[:1]],
+                           "basePosition": [float(x) for x in (k.get("basePosition") if "basePosition" in k else a[3])]})
+            return 50 + len(bodies)
+        p.createMultiBody.side_effect = cmb
+        random.seed(seed)
+        env.reset()
+        resets.append({"seed": seed, "gripper_center": gc, "calls": calls, "bodies": bodies,
+                       "vertical_quaternion": list(env.vertical_quaternion)})
+    out["golf_reset"] = resets
+    steps = []
+    hole = (0.0, -0.6, 0.02)
+    cases = [  # ball, stick link0 COM, stick-finger links, robot-pitch links, stick-pitch?, ball-stick?
+        ((0.01, -0.61, 0.06), (0.05, -0.6, 0.07), [12], [], False, False),     # in hole
+        ((0.2, -0.7, 0.06), (0.05, -0.6, 0.07), [], [], False, False),         # stick fell
+        ((0.2, -0.7, -0.01), (0.05, -0.6, 0.07), [9], [], False, False),       # off pitch
+        ((0.2, -0.7, 0.06), (0.05, -0.6, 0.07), [16], [5], False, False),      # floor (robot) + dense
+        ((0.2, -0.7, 0.06), (0.05, -0.6, 0.07), [16], [], True, True),         # floor (stick) + touched
+        ((0.1, -0.65, 0.06), (0.08, -0.66, 0.07), [11, 18], [], False, True),  # touched
+        ((0.3, -0.9, 0.06), (0.05, -0.6, 0.07), [13], [], False, False),       # dense only
+    ]
+    for ball, stick, fingers, robot_pitch, stick_pitch, touched in cases:
+        env = Golf.__new__(Golf)
+        env.visualize = False
+        env.reward_type = "dense"
+        env.positive_reward_radius = 0.1
+        env.control_method = "end"
+        env.vertical_quaternion = [0.0, 0.0, -0.7, 0.7]
+        env.stick_id, env.ball_id, env.pitch_id = 20, 21, 3
+        ee = (0.02, -0.62, 0.35, 0.0, 0.0, -0.7, 0.7)
+        moves = []
+        env.robot = types.SimpleNamespace(id=1, get_ee_pose=lambda: ee,
+                                          move_ee=lambda pose, m: moves.append(([float(x) for x in pose], m)))
+        env.wait_until_stable = lambda: True
+        p.reset_mock()
+        p.getBasePositionAndOrientation.side_effect = lambda i: ((ball if i == 21 else hole), (0.0, 0.0, 0.0, 1.0))
+        p.getLinkState.side_effect = lambda bid, l: (stick, (0, 0, 0, 1))
+
+        def cps(*a, **k):
+            ba = k.get("bodyA", a[0] if a else None)
+            bb = k.get("bodyB", a[1] if len(a) > 1 else None)
+            if (ba, bb) == (1, 3):
+                return [contact(l, -1) for l in robot_pitch]
+            if (ba, bb) == (20, 3):
+                return [contact(-1, -1)] if stick_pitch else []
+            if (ba, bb) == (21, 20):
+                return [contact(-1, 0)] if touched else []
+            if (ba, bb) == (20, 1):
+                return [contact(0, l) for l in fingers]
+            return []
+        p.getContactPoints.side_effect = cps
+        a = np.array([0.03, -0.02, 0.01], np.float32)
+        obs, rew, term, trunc, info = env.step(a)
+        steps.append({"ball": list(ball), "hole": list(hole), "stick": list(stick), "finger_links": fingers,
+                      "robot_pitch_links": robot_pitch, "stick_pitch": stick_pitch, "touched": touched,
+                      "action": a.tolist(), "ee_pose": list(ee), "ik_target": moves[0][0],
+                      "obs": [float(x) for x in obs], "reward": float(rew), "terminated": bool(term),
+                      "is_success": bool(info["is_success"])})
+    out["golf_step"] = steps
+    json.dump(out, open(os.path.join(OUT, "golf_glue.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":

@@ -100,4 +100,30 @@ UG_CONST double UG_GEAR_RATIO[5] = {1.0, -1.0, -1.0, 1.0, -1.0};
 #define UG_CG_RMIN 0.5                 /* :313 */
 #define UG_CG_RMAX 0.8                 /* :314 */
 
+/* Golf (env_golf_v0.py).  Club = multibody: base box 0.03x0.03x0.15 (1 kg), fixed links: box 0.1x0.03x0.03
+ * (1 kg) at z -0.09 and cylinder r 0.04 h 0.01 (1 kg) at z +0.08 (:289-332); base friction 10, restitution
+ * 0.1 (:330).  Restated as one rigid body at the composite COM with the composite (diagonal) inertia. */
+#define UG_GF_BASE_HX 0.015
+#define UG_GF_BASE_HZ 0.075
+#define UG_GF_FOOT_HX 0.05
+#define UG_GF_FOOT_HY 0.015
+#define UG_GF_FOOT_Z (-(0.075 + 0.015)) /* :309 -(vertical/2 + transversal/2) */
+#define UG_GF_DISC_Z (0.075 + 0.005)    /* :310 vertical/2 + disc/2 */
+#define UG_GF_PART_MASS 1.0
+#define UG_GF_ZC ((0.0 + UG_GF_FOOT_Z + UG_GF_DISC_Z) / 3.0) /* composite COM height in the base frame */
+#define UG_GF_BASE_FRICTION 10.0
+#define UG_GF_BASE_RESTITUTION 0.1
+/* ball (:335-358): r 0.015, 0.01 kg, rolling friction 10, restitution 0.1, default lateral friction */
+#define UG_GF_BALL_R 0.015
+#define UG_GF_BALL_MASS 0.01
+#define UG_GF_BALL_ROLLING 10.0
+#define UG_GF_BALL_RESTITUTION 0.1
+/* pitch (:87, 428-446): convex hull of golf_pitch.obj = 0.8 x 0.8 x 0.05 slab at (0, -0.6, 0.02), static;
+ * mesh hull margin outside -> box half extents + margin */
+#define UG_GF_PITCH_X 0.0
+#define UG_GF_PITCH_Y (-0.6)
+#define UG_GF_PITCH_Z 0.02
+#define UG_GF_PITCH_HX 0.4
+#define UG_GF_PITCH_HZ 0.025
+
 #endif

@@ -35,6 +35,7 @@ __device__ static void box_collider(Collider* c, double hx, double hy, double hz
     c->disc = ug_sqrt(hx * hx + hy * hy + hz * hz);
     c->friction = friction;
     c->restitution = 0.0;
+    c->rolling = 0.0;
     c->owner = -100; c->ent = 0;
     c->link = -1;
 }
@@ -54,6 +55,10 @@ __device__ static void add_pair(Scene* s, int a, int b) {
     if (f > UG_MAX_FRICTION) f = UG_MAX_FRICTION;
     p->friction = f;
     p->restitution = s->col[a].restitution * s->col[b].restitution;
+    double r = s->col[a].rolling * s->col[b].friction + s->col[a].friction * s->col[b].rolling;
+    if (r < -UG_MAX_FRICTION) r = -UG_MAX_FRICTION;
+    if (r > UG_MAX_FRICTION) r = UG_MAX_FRICTION;
+    p->rolling = r;
 }
 __global__ void k_build_scene(Scene* s, int task) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -62,6 +67,7 @@ __global__ void k_build_scene(Scene* s, int task) {
     s->nobj = 0;
     s->ncol = 0;
     s->npair = 0;
+    for (int o = 0; o < MAXOBJ; o++) s->oncol[o] = 0;
     for (int l = 1; l < UG_NL; l++) {
         Collider* c = &s->col[s->ncol++];
         int si = -1;
@@ -80,6 +86,7 @@ __global__ void k_build_scene(Scene* s, int task) {
         c->disc = UG_LINK_DISC[l];
         c->friction = UG_DEFAULT_FRICTION;
         c->restitution = 0.0;
+        c->rolling = 0.0;
         c->owner = UG_LINK_BODY[l];
         c->ent = 0;
         c->link = l;
@@ -129,6 +136,54 @@ __global__ void k_build_scene(Scene* s, int task) {
         c->owner = -100; c->ent = 11;
         statics[nstat++] = s->ncol++;
     }
+    if (task == UG_TASK_GOLF) {
+        s->nobj = 2;
+        double m = UG_GF_PART_MASS, zc = UG_GF_ZC;
+        double bx = UG_GF_BASE_HX, bz = UG_GF_BASE_HZ, fx = UG_GF_FOOT_HX, fy = UG_GF_FOOT_HY;
+        double r = UG_CYL_R, hh = UG_CYL_HH;
+        v3 Ib = V(m / 12.0 * (4.0 * bx * bx + 4.0 * bz * bz), m / 12.0 * (4.0 * bx * bx + 4.0 * bz * bz),
+                  m / 12.0 * (4.0 * bx * bx + 4.0 * bx * bx));
+        v3 If = V(m / 12.0 * (4.0 * fy * fy + 4.0 * fy * fy), m / 12.0 * (4.0 * fx * fx + 4.0 * fy * fy),
+                  m / 12.0 * (4.0 * fx * fx + 4.0 * fy * fy));
+        double ic = m / 12.0 * (4.0 * hh * hh) + m / 4.0 * (r * r);
+        v3 Ic = V(ic, ic, m / 2.0 * (r * r));
+        double d0 = 0.0 - zc, d1 = UG_GF_FOOT_Z - zc, d2 = UG_GF_DISC_Z - zc;
+        s->omass[0] = 3.0 * m;
+        s->oinertia[0] = V(Ib.x + m * d0 * d0 + If.x + m * d1 * d1 + Ic.x + m * d2 * d2,
+                           Ib.y + m * d0 * d0 + If.y + m * d1 * d1 + Ic.y + m * d2 * d2, Ib.z + If.z + Ic.z);
+        s->ocol[0] = s->ncol;
+        Collider* c = &s->col[s->ncol++];
+        box_collider(c, bx, bx, bz, safe_margin(bx, bx, bz), UG_GF_BASE_FRICTION);
+        c->restitution = UG_GF_BASE_RESTITUTION;
+        c->P = V(0.0, 0.0, d0); c->aP = c->P;
+        c->owner = -2; c->ent = 1;
+        c = &s->col[s->ncol++];
+        box_collider(c, fx, fy, fy, safe_margin(fx, fy, fy), UG_DEFAULT_FRICTION);
+        c->P = V(0.0, 0.0, d1); c->aP = c->P;
+        c->owner = -2; c->ent = 1;
+        c = &s->col[s->ncol++];
+        box_collider(c, r, r, hh, UG_CYL_MARGIN, UG_DEFAULT_FRICTION);
+        c->kind = UG_SHAPE_HULL;
+        c->margin = UG_CYL_MARGIN;
+        c->v0 = UG_CYL_V0; c->nv = UG_CYL_NV; c->f0 = UG_CYL_F0; c->nf = UG_CYL_NF;
+        c->P = V(0.0, 0.0, d2); c->aP = c->P;
+        c->owner = -2; c->ent = 1;
+        s->oncol[0] = 3;
+        double rb = UG_GF_BALL_R, mb = UG_GF_BALL_MASS;
+        s->omass[1] = mb;
+        double ib = 0.4 * mb * rb * rb;
+        s->oinertia[1] = V(ib, ib, ib);
+        c = &s->col[s->ncol];
+        box_collider(c, rb, rb, rb, rb, UG_DEFAULT_FRICTION);
+        c->kind = UG_SHAPE_SPHERE;
+        c->half[1] = c->half[2] = 0.0;
+        c->disc = ug_sqrt(3.0) * rb;
+        c->restitution = UG_GF_BALL_RESTITUTION;
+        c->rolling = UG_GF_BALL_ROLLING;
+        c->owner = -3; c->ent = 2;
+        s->ocol[1] = s->ncol++;
+        s->oncol[1] = 1;
+    }
     if (task == UG_TASK_BALLBALANCE || task == UG_TASK_CUBESPUSH || task == UG_TASK_GOLF) {
         Collider* c = &s->col[s->ncol];
         box_collider(c, 0.5, 1.0, 0.25, safe_margin(0.5, 1.0, 0.25), UG_DEFAULT_FRICTION);
@@ -142,18 +197,32 @@ __global__ void k_build_scene(Scene* s, int task) {
         c->owner = -100; c->ent = 11;
         statics[nstat++] = s->ncol++;
     }
+    if (task == UG_TASK_GOLF) {
+        Collider* c = &s->col[s->ncol];
+        box_collider(c, UG_GF_PITCH_HX + UG_URDF_MARGIN, UG_GF_PITCH_HX + UG_URDF_MARGIN,
+                     UG_GF_PITCH_HZ + UG_URDF_MARGIN, UG_URDF_MARGIN, UG_DEFAULT_FRICTION);
+        c->P = V(UG_GF_PITCH_X, UG_GF_PITCH_Y, UG_GF_PITCH_Z); c->aP = c->P;
+        c->owner = -100; c->ent = 12;
+        statics[nstat++] = s->ncol++;
+    }
     for (int o = 0; o < s->nobj; o++)
-        for (int l = 0; l < nrobot; l++) add_pair(s, l, s->ocol[o]);
+        if (s->oncol[o] == 0) s->oncol[o] = 1;
+    for (int o = 0; o < s->nobj; o++)
+        for (int c = s->ocol[o]; c < s->ocol[o] + s->oncol[o]; c++)
+            for (int l = 0; l < nrobot; l++) add_pair(s, l, c);
     for (int t = 0; t < nstat; t++)
         for (int l = 0; l < nrobot; l++) add_pair(s, l, statics[t]);
     for (int o = 0; o < s->nobj; o++)
-        for (int p = o + 1; p < s->nobj; p++) {
-            int a = s->ocol[o], b = s->ocol[p];
-            if (s->col[b].kind == UG_SHAPE_SPHERE && s->col[a].kind != UG_SHAPE_SPHERE) { int t = a; a = b; b = t; }
-            add_pair(s, a, b);
-        }
+        for (int p = o + 1; p < s->nobj; p++)
+            for (int ca = s->ocol[o]; ca < s->ocol[o] + s->oncol[o]; ca++)
+                for (int cb = s->ocol[p]; cb < s->ocol[p] + s->oncol[p]; cb++) {
+                    int a = ca, b = cb;
+                    if (s->col[b].kind == UG_SHAPE_SPHERE && s->col[a].kind != UG_SHAPE_SPHERE) { int t = a; a = b; b = t; }
+                    add_pair(s, a, b);
+                }
     for (int o = 0; o < s->nobj; o++)
-        for (int t = 0; t < nstat; t++) add_pair(s, s->ocol[o], statics[t]);
+        for (int c = s->ocol[o]; c < s->ocol[o] + s->oncol[o]; c++)
+            for (int t = 0; t < nstat; t++) add_pair(s, c, statics[t]);
 }
 
 // ---------------------------------------------------------------------------
@@ -359,9 +428,8 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
 }
 
 urgym_handle* urgym_create(int task, int n, int dev, int precision, uint32_t seed, int env_offset) {
-    if (task < URGYM_TASK_BALLBALANCE || task > URGYM_TASK_CUBESGRASP) {
-        fail(nullptr, "urgym_create: task " + std::to_string(task) +
-                          " not implemented in this build (BallBalance, CubesPush, CubesGrasp)");
+    if (task < URGYM_TASK_BALLBALANCE || task > URGYM_TASK_GOLF) {
+        fail(nullptr, "urgym_create: unknown task " + std::to_string(task));
         return nullptr;
     }
     if (n <= 0) { fail(nullptr, "urgym_create: n_envs must be > 0"); return nullptr; }

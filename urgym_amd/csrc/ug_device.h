@@ -25,8 +25,8 @@
 #define NV (NB + 6 * MAXOBJ)
 #define MAXMAN UG_MAXMAN
 #define MAXROWS 128
-#define MAXCOL 24
-#define MAXPAIR 96
+#define MAXCOL 28
+#define MAXPAIR 160
 #define MAXCAND 8   /* per-lane narrowphases emit <= 4 points */
 
 #define DF __device__ static
@@ -216,10 +216,10 @@ struct Collider {
     m3 aR; v3 aP;
     v3 ac, ah;
     double disc;
-    double friction, restitution;
+    double friction, restitution, rolling;
     int owner, ent, link;
 };
-struct PairDef { int a, b; double thr, friction, restitution; };
+struct PairDef { int a, b; double thr, friction, restitution, rolling; };
 struct Scene {
     int task;
     double gravity;
@@ -228,7 +228,8 @@ struct Scene {
     v3 oinertia[MAXOBJ];
     int ncol;
     Collider col[MAXCOL];
-    int ocol[MAXOBJ];
+    int ocol[MAXOBJ];  /* first collider of each object */
+    int oncol[MAXOBJ]; /* colliders of each object (consecutive) */
     int npair;
     PairDef pair[MAXPAIR];
 };

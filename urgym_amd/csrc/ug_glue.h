@@ -93,4 +93,49 @@ UG_HD int ugg_cg_reward(int* approached, int* grasped, double dist, double openi
     return success;
 }
 
+/* ---- Golf (env_golf_v0.py) ---- */
+/* create_ball (:335-343): (0 + uniform(-0.2, 0.2), -0.7 + uniform(-0.1, 0.1), 0.1) */
+UG_HD void ugg_gf_ball_xy(double u0, double u1, double* x, double* y) {
+    *x = 0.0 + ugg_uniform(-0.2, 0.2, u0);
+    *y = -0.7 + ugg_uniform(-0.1, 0.1, u1);
+}
+/* step reward, termination precedence (:129-183); hole = pitch base position; returns success */
+UG_HD int ugg_gf_reward(const double* ball, const double* hole, const double* stick, int in_fingers, int floor_contact,
+                        int touched, double* reward, int* terminated) {
+    double r = 0.0;
+    int success = 0, term = 0;
+    if (ug_norm3(hole[0] - ball[0], hole[1] - ball[1], hole[2] - ball[2]) < 0.05) { /* is_ball_in_hole :217-221 */
+        r += 10.0;
+        success = 1;
+        term = 1;
+    } else if (!in_fingers) { /* stick fell :136-140 */
+        r -= 5.0;
+        term = 1;
+    } else if (ball[2] < 0.0) { /* ball off pitch :141-145, :224-228 */
+        r -= 10.0;
+        term = 1;
+    } else {
+        if (floor_contact) r -= 0.01;
+        double d = ug_norm3(stick[0] - ball[0], stick[1] - ball[1], stick[2] - ball[2]);
+        r += ugg_gdr(d, 0.1, 0.5) / 10.0;
+        if (touched) {
+            r += 0.1;
+            double dh = ug_norm3(hole[0] - ball[0], hole[1] - ball[1], hole[2] - ball[2]);
+            r += ugg_gdr(dh, 0.1, 0.5) / 10.0;
+        }
+    }
+    r -= 0.1;
+    *reward = r;
+    *terminated = term;
+    return success;
+}
+/* get_observation (:230-236): stick base (link 0 COM), stick - ball, hole - ball */
+UG_HD void ugg_gf_obs(const double* stick, const double* ball, const double* hole, double* obs) {
+    for (int i = 0; i < 3; i++) {
+        obs[i] = stick[i];
+        obs[3 + i] = stick[i] - ball[i];
+        obs[6 + i] = hole[i] - ball[i];
+    }
+}
+
 #endif

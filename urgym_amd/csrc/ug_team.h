@@ -56,7 +56,7 @@ static_assert(sizeof(EnvState) == UG_STATE_DIM * sizeof(double), "EnvState must 
 
 struct RowS {
     double invD, rinv, rhs, rhsPen, lo, hi, imp, impPen, fric; /* rinv = invD == 0 ? 0 : 1 / invD */
-    int kind; /* 0 limit, 1 motor, 2 gear, 3 normal, 4/5 friction dir 1/2 */
+    int kind; /* 0 limit, 1 motor, 2 gear, 3 normal, 4/5 friction dir 1/2, 6/7 rolling axis 1/2 */
     int a, b; /* limit: dof, side | motor: m | gear: g | contact: manifold, point */
     int nrow; /* friction: position of its normal row */
 };
@@ -209,6 +209,7 @@ __device__ static inline void man_to_st(StMan& S, const Manifold& M) {
 
 /* ---------------- collision ---------------- */
 /* hull (A, robot link) vs box (B): the whole wave.  Produces cand k (<= 4 points) in sh.u.cand. */
+__device__ __noinline__ static void team_reduce4(int n, int k);
 __device__ __noinline__ static void team_hull_box(const Collider& A, const Collider& B, const XF& TA, const XF& TB,
                                      double thr, int k) {
     Shared& sh = g_sh;
@@ -292,7 +293,77 @@ __device__ __noinline__ static void team_hull_box(const Collider& A, const Colli
     if (vvalid) sh.hc[lane_prefix(vb)] = vc;
     if (cvalid) sh.hc[nv + lane_prefix(cb)] = cc;
     __syncthreads();
-    int n = nv + nc;
+    team_reduce4(nv + nc, k);
+}
+
+/* hull (A) vs hull (B) (oracle nc_hull_hull): lane per A vertex against B's planes, lane per B vertex against
+ * A's planes; candidates in canonical order (A vertices, then B vertices; at most 64 kept), then reduce4 */
+__device__ __noinline__ static void team_hull_hull(const Collider& A, const Collider& B, const XF& TA, const XF& TB,
+                                                   double thr, int k) {
+    Shared& sh = g_sh;
+    const int lane = threadIdx.x;
+    double mA = A.margin, mB = B.margin;
+    int avalid = 0, bvalid = 0;
+    Cand ac, bc;
+    if (lane < A.nv) {
+        m3 RAB = mtm(TB.R, TA.R);
+        v3 pAB = mtv(TB.R, vsub(TA.p, TB.p));
+        const double* vv = &UG_HULL_V[3 * (A.v0 + lane)];
+        v3 x = vadd(mv(RAB, V(vv[0], vv[1], vv[2])), pAB);
+        double smax = -1e300;
+        int fm = -1;
+        for (int f = 0; f < B.nf; f++) {
+            const double* F = &UG_HULL_F[4 * (B.f0 + f)];
+            double sd = F[0] * x.x + F[1] * x.y + F[2] * x.z - F[3];
+            if (sd > smax) { smax = sd; fm = f; }
+        }
+        double depth = smax - mA - mB;
+        if (depth < thr) {
+            const double* F = &UG_HULL_F[4 * (B.f0 + fm)];
+            v3 nl = V(F[0], F[1], F[2]);
+            v3 pl = vsub(x, vscale(nl, smax));
+            avalid = 1;
+            ac.n = mv(TB.R, nl);
+            ac.pB = xf_apply(TB, pl);
+            ac.d = depth;
+        }
+    }
+    if (lane < B.nv) {
+        m3 RBA = mtm(TA.R, TB.R);
+        v3 pBA = mtv(TA.R, vsub(TB.p, TA.p));
+        const double* vv = &UG_HULL_V[3 * (B.v0 + lane)];
+        v3 yl = V(vv[0], vv[1], vv[2]);
+        v3 y = vadd(mv(RBA, yl), pBA);
+        double smax = -1e300;
+        int fm = -1;
+        for (int f = 0; f < A.nf; f++) {
+            const double* F = &UG_HULL_F[4 * (A.f0 + f)];
+            double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
+            if (sd > smax) { smax = sd; fm = f; }
+        }
+        double depth = smax - mA - mB;
+        if (depth < thr) {
+            const double* F = &UG_HULL_F[4 * (A.f0 + fm)];
+            v3 nw = mv(TA.R, V(F[0], F[1], F[2]));
+            bvalid = 1;
+            bc.n = vneg(nw);
+            bc.pB = xf_apply(TB, yl);
+            bc.d = depth;
+        }
+    }
+    unsigned long long amask = ballot(avalid), bmask = ballot(bvalid);
+    int na = __popcll(amask), nb = __popcll(bmask);
+    if (avalid) { int pos = lane_prefix(amask); if (pos < 64) sh.hc[pos] = ac; }
+    if (bvalid) { int pos = na + lane_prefix(bmask); if (pos < 64) sh.hc[pos] = bc; }
+    __syncthreads();
+    int n = na + nb;
+    team_reduce4(n < 64 ? n : 64, k);
+}
+
+/* candidates sh.hc[0..n) -> at most 4 in sh.u.cand.c[k] (oracle reduce4: deepest, then farthest-spread) */
+__device__ __noinline__ static void team_reduce4(int n, int k) {
+    Shared& sh = g_sh;
+    const int lane = threadIdx.x;
     if (n <= 4) {
         if (lane < n) sh.u.cand.c[k][lane] = sh.hc[lane];
         if (lane == 0) sh.u.cand.n[k] = n;
@@ -378,6 +449,10 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
                 XF TA = shape_xf(sh.O[P.a], A), TB = shape_xf(sh.O[P.b], B);
                 team_hull_box(A, B, TA, TB, P.thr, k);
                 PROF_CNT(PC_HULL, 1);
+            } else if (A.kind == UG_SHAPE_HULL && B.kind == UG_SHAPE_HULL) {
+                XF TA = shape_xf(sh.O[P.a], A), TB = shape_xf(sh.O[P.b], B);
+                team_hull_hull(A, B, TA, TB, P.thr, k);
+                PROF_CNT(PC_HULL, 1);
             }
         }
         /* lane per pair: remaining narrowphases, manifold update */
@@ -402,8 +477,14 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
             XF TA = shape_xf(sh.O[P.a], A), TB = shape_xf(sh.O[P.b], B);
             CandList L;
             L.n = 0;
-            if (A.kind == UG_SHAPE_HULL && B.kind == UG_SHAPE_BOX) {
+            if (A.kind == UG_SHAPE_HULL && (B.kind == UG_SHAPE_BOX || B.kind == UG_SHAPE_HULL)) {
                 for (int i = 0; i < sh.u.cand.n[lane]; i++) cand_add(L, sh.u.cand.c[lane][i].n, sh.u.cand.c[lane][i].pB, sh.u.cand.c[lane][i].d);
+            } else if (A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_HULL) {
+                CandList L2;
+                L2.n = 0;
+                nc_hull_sphere(TB, B, TA, A, P.thr, L2);
+                for (int i = 0; i < L2.n; i++)
+                    cand_add(L, vneg(L2.c[i].n), vadd(L2.c[i].pB, vscale(L2.c[i].n, L2.c[i].d)), L2.c[i].d);
             } else if (A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_BOX) nc_sphere_box(TA, A, TB, B, P.thr, L);
             else if (A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_SPHERE) nc_sphere_sphere(TA, A, TB, B, P.thr, L);
             else if (A.kind == UG_SHAPE_BOX && B.kind == UG_SHAPE_BOX) nc_box_box(TA, A, TB, B, P.thr, L);
@@ -471,6 +552,24 @@ __device__ static void point_jac(const Scene* sc, const EnvState& e, const Kin& 
         MiJ[0] = d.x * im; MiJ[1] = d.y * im; MiJ[2] = d.z * im; MiJ[3] = ir.x; MiJ[4] = ir.y; MiJ[5] = ir.z;
     }
 }
+__device__ static void ang_jac(const Scene* sc, const EnvState& e, const Kin& k, int ent, int body, v3 u, double* J,
+                               double* MiJ, const double* LDL) {
+    if (ent == 0) {
+        for (int i = 0; i < NB; i++) {
+            J[i] = moves(i, body) ? vdot(u, k.a[i]) : 0.0;
+            MiJ[i] = J[i];
+        }
+        ldlt_solve(LDL, NB, MiJ);
+    } else {
+        int o = ent - 1;
+        J[0] = 0.0; J[1] = 0.0; J[2] = 0.0; J[3] = u.x; J[4] = u.y; J[5] = u.z;
+        m3 R = qmat(e.obj[o].quat);
+        v3 ir = mtv(R, u);
+        ir = V(ir.x / sc->oinertia[o].x, ir.y / sc->oinertia[o].y, ir.z / sc->oinertia[o].z);
+        ir = mv(R, ir);
+        MiJ[0] = 0.0; MiJ[1] = 0.0; MiJ[2] = 0.0; MiJ[3] = ir.x; MiJ[4] = ir.y; MiJ[5] = ir.z;
+    }
+}
 __device__ static inline int ent_of_collider(const Collider& c, int& body) {
     body = -1;
     if (c.owner >= 0) { body = c.owner; return 0; }
@@ -512,39 +611,53 @@ __device__ static void enumerate_rows(Shared& sh, const Scene* s) {
     }
     int nman = (int)e.nman;
     /* contact points kept (capacity: 3 rows each) */
-    int npt = 0;
+    /* accepted points (capacity: 3 rows each, 5 with rolling friction), as the oracle's running count */
+    int npt = 0, nroll = 0, cnt = ncnt;
     for (int m = 0; m < nman; m++) {
         const PairDef& P = s->pair[(int)e.man[m].pair];
         int bA, bB;
         int eA = ent_of_collider(s->col[P.a], bA), eB = ent_of_collider(s->col[P.b], bB);
         if (eA < 0 && eB < 0) continue;
+        int need = P.rolling > 0.0 ? 5 : 3;
         for (int j = 0; j < (int)e.man[m].npts; j++) {
-            if (ncnt + 3 > MAXROWS) { e.overflow += 1.0; continue; }
-            ncnt += 3;
+            if (cnt + need > MAXROWS) { e.overflow += 1.0; continue; }
+            cnt += need;
             npt++;
+            nroll += need == 5;
         }
     }
     nn = npt;
     nf = 2 * npt;
-    int pn = nnc, pf = nnc + nn;
+    /* positions in solve order: normals, frictions, rolling-friction rows */
+    int pn = nnc, pf = nnc + nn, pr = nnc + nn + nf;
+    cnt = ncnt;
     for (int m = 0; m < nman; m++) {
         const PairDef& P = s->pair[(int)e.man[m].pair];
         int bA, bB;
         int eA = ent_of_collider(s->col[P.a], bA), eB = ent_of_collider(s->col[P.b], bB);
         if (eA < 0 && eB < 0) continue;
+        int need = P.rolling > 0.0 ? 5 : 3;
         for (int j = 0; j < (int)e.man[m].npts; j++) {
-            if (pn >= nnc + nn) break;
+            if (cnt + need > MAXROWS) continue;
+            cnt += need;
             RowS& r = sh.rs[pn];
-            r.kind = 3; r.a = m; r.b = j;
+            r.kind = 3; r.a = m; r.b = j; r.nrow = pn;
             for (int f = 0; f < 2; f++) {
                 RowS& q = sh.rs[pf + f];
                 q.kind = 4 + f; q.a = m; q.b = j; q.nrow = pn;
             }
-            pn++;
             pf += 2;
+            if (need == 5) {
+                for (int f = 0; f < 2; f++) {
+                    RowS& q = sh.rs[pr + f];
+                    q.kind = 6 + f; q.a = m; q.b = j; q.nrow = pn;
+                }
+                pr += 2;
+            }
+            pn++;
         }
     }
-    n = nnc + nn + nf;
+    n = nnc + nn + nf + 2 * nroll;
     sh.nrows = n; sh.nnc = nnc; sh.nn = nn; sh.nf = nf;
 }
 /* build row at position pos (one lane): J, M^-1 J^T into stage row sl, scalars into rs[pos] */
@@ -620,6 +733,7 @@ __device__ __noinline__ static void build_row(const Scene* s, int pos, double* w
         v3 pA = xf_apply(OA, cp.lpA), pB = xf_apply(OB, cp.lpB);
         v3 n = cp.n;
         v3 d = n;
+        const bool ang = r.kind >= 6; /* rolling friction: angular rows about the friction axes */
         if (r.kind >= 4) {
             v3 t1, t2;
             if (ug_fabs(n.z) > 0.7071067811865475244) {
@@ -631,19 +745,21 @@ __device__ __noinline__ static void build_row(const Scene* s, int pos, double* w
                 t1 = V(-n.y * kk, n.x * kk, 0);
                 t2 = V(-n.z * t1.y, n.z * t1.x, a * kk);
             }
-            d = r.kind == 4 ? t1 : t2;
+            d = (r.kind == 4 || r.kind == 6) ? t1 : t2;
         }
         double JA[NB], MA[NB], JB[NB], MB[NB];
         double dA = 0.0, dB = 0.0, relv = 0.0;
         if (entA >= 0) {
-            point_jac(s, e, sh.kin, entA, bodyA, pA, d, JA, MA, sh.LDL);
+            if (ang) ang_jac(s, e, sh.kin, entA, bodyA, d, JA, MA, sh.LDL);
+            else point_jac(s, e, sh.kin, entA, bodyA, pA, d, JA, MA, sh.LDL);
             dA = ent_dot_local(entA, JA, MA);
             relv += ent_dot(entA, JA, sh.v0);
             put_seg(entA, JA, J);
             put_seg(entA, MA, MJ);
         }
         if (entB >= 0) {
-            point_jac(s, e, sh.kin, entB, bodyB, pB, vneg(d), JB, MB, sh.LDL);
+            if (ang) ang_jac(s, e, sh.kin, entB, bodyB, vneg(d), JB, MB, sh.LDL);
+            else point_jac(s, e, sh.kin, entB, bodyB, pB, vneg(d), JB, MB, sh.LDL);
             dB = ent_dot_local(entB, JB, MB);
             relv += ent_dot(entB, JB, sh.v0);
             put_seg(entB, JB, J);
@@ -667,7 +783,7 @@ __device__ __noinline__ static void build_row(const Scene* s, int pos, double* w
             imp = cp.imp * UG_WARMSTART;
         } else {
             rhs = 0.0 * invD + (0.0 - relv) * invD;
-            fric = P.friction;
+            fric = ang ? P.rolling : P.friction;
         }
     }
     r.invD = invD; r.rinv = invD == 0.0 ? 0.0 : 1.0 / invD; r.rhs = rhs; r.rhsPen = rhsPen; r.lo = lo; r.hi = hi; r.imp = imp; r.impPen = 0.0; r.fric = fric;
@@ -681,6 +797,7 @@ __device__ __noinline__ static void build_row(const Scene* s, int pos, double* w
 #define NCMAX (2 * NB + 12) /* limits (both sides) + 7 motors + 5 gears */
 struct RowPre {
     double rhs, invD, rinv, lo, hi, fric; /* LDS values, fetched one row ahead */
+    int nrow;                             /* friction / rolling rows: their normal's position */
 };
 /* row impulses, lane-distributed in two VGPR pairs: row r's impulse sits in lane (r & 63) of v[r >> 6]
  * (read with v_readlane, written with a lane-select: no LDS traffic inside the iteration loop) */
@@ -708,6 +825,7 @@ __device__ __forceinline__ RowPre row_fetch(const Shared& sh, int p) {
     x.hi = r.hi;
     x.rhs = PEN ? r.rhsPen : r.rhs;
     x.fric = PEN ? 0.0 : r.fric;
+    x.nrow = PEN ? 0 : r.nrow;
     return x;
 }
 
@@ -766,7 +884,7 @@ __device__ __forceinline__ void pgs_fwd(Shared& sh, const double (&RJ)[NSLOT], c
                 double imp = imp_get<P>(I);
                 bool skip = false;
                 if (!PEN && P >= fb) {
-                    double tot = imp_get_dyn(I, nnc + ((P - fb) >> 1));
+                    double tot = imp_get_dyn(I, __builtin_amdgcn_readfirstlane(cur.nrow));
                     cur.lo = -(cur.fric * tot);
                     cur.hi = cur.fric * tot;
                     skip = __builtin_amdgcn_readfirstlane((int)!(tot > 0.0)) != 0;
@@ -1003,7 +1121,7 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
         StPt& pt = e.man[r.a].pt[r.b];
         if (r.kind == 3) pt.imp = r.imp;
         else if (r.kind == 4) pt.imp1 = r.imp;
-        else pt.imp2 = r.imp;
+        else if (r.kind == 5) pt.imp2 = r.imp;
     }
     __syncthreads();
     serial_post(s, split);
@@ -1056,13 +1174,23 @@ __device__ static v3 gripper_center(const double* q) {
     }
     return V((hi.x + lo.x) / 2.0, (hi.y + lo.y) / 2.0, (hi.z + lo.z) / 2.0);
 }
-__device__ static void remove_object(EnvState& e, const Scene* s, int o) {
-    e.oactive[o] = 0.0;
-    int ci = s->ocol[o];
+__device__ static void drop_manifolds_of(EnvState& e, const Scene* s, int c0, int c1) {
     int k = 0, nm = (int)e.nman;
     for (int m = 0; m < nm; m++) {
         const PairDef& P = s->pair[(int)e.man[m].pair];
-        if (P.a == ci || P.b == ci) continue;
+        if ((P.a >= c0 && P.a < c1) || (P.b >= c0 && P.b < c1)) continue;
+        if (k != m) e.man[k] = e.man[m];
+        k++;
+    }
+    e.nman = (double)k;
+}
+__device__ static void remove_object(EnvState& e, const Scene* s, int o) {
+    e.oactive[o] = 0.0;
+    int c0 = s->ocol[o], c1 = c0 + s->oncol[o];
+    int k = 0, nm = (int)e.nman;
+    for (int m = 0; m < nm; m++) {
+        const PairDef& P = s->pair[(int)e.man[m].pair];
+        if ((P.a >= c0 && P.a < c1) || (P.b >= c0 && P.b < c1)) continue;
         if (k != m) e.man[k] = e.man[m];
         k++;
     }
@@ -1140,9 +1268,32 @@ __device__ static void cg_obs(const EnvState& e, double* obs) {
     obs[10] = e.obj[0].pos.x; obs[11] = e.obj[0].pos.y; obs[12] = e.obj[0].pos.z;
     obs[13] = e.obj[0].quat.x; obs[14] = e.obj[0].quat.y; obs[15] = e.obj[0].quat.z; obs[16] = e.obj[0].quat.w;
 }
+/* Golf: any manifold point between colliders [a0, a1) and [b0, b1) (either side of the pair) */
+__device__ static int pair_contact(const EnvState& e, const Scene* s, int a0, int a1, int b0, int b1) {
+    int nm = (int)e.nman;
+    for (int m = 0; m < nm; m++) {
+        const PairDef& P = s->pair[(int)e.man[m].pair];
+        if (e.man[m].npts <= 0.0) continue;
+        if ((P.a >= a0 && P.a < a1 && P.b >= b0 && P.b < b1) || (P.b >= a0 && P.b < a1 && P.a >= b0 && P.a < b1))
+            return 1;
+    }
+    return 0;
+}
+/* club reference point at base-frame height zoff: composite COM + R (0, 0, zoff - zc) */
+__device__ static v3 club_point(const EnvState& e, double zoff) {
+    m3 R = qmat(e.obj[0].quat);
+    return vadd(e.obj[0].pos, mv(R, V(0.0, 0.0, zoff - UG_GF_ZC)));
+}
+__device__ static void gf_obs(const EnvState& e, double* obs) {
+    v3 st = club_point(e, UG_GF_FOOT_Z);
+    double stick[3] = {st.x, st.y, st.z}, ball[3] = {e.obj[1].pos.x, e.obj[1].pos.y, e.obj[1].pos.z};
+    double hole[3] = {UG_GF_PITCH_X, UG_GF_PITCH_Y, UG_GF_PITCH_Z};
+    ugg_gf_obs(stick, ball, hole, obs);
+}
 __device__ static void task_obs(const Scene* s, const EnvState& e, double* obs) {
     if (s->task == UG_TASK_CUBESPUSH) cp_obs(e, obs);
     else if (s->task == UG_TASK_CUBESGRASP) cg_obs(e, obs);
+    else if (s->task == UG_TASK_GOLF) gf_obs(e, obs);
     else bb_obs(e, obs);
 }
 /* ---------------- the env program: step / reset as one substep loop ----------------
@@ -1186,6 +1337,11 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
                 link_state_of(e.q, UG_EE_LINK, pe, oe);
                 move_ee_end(e, V(pe.x + (double)io.act[0], pe.y + (double)io.act[1], pe.z + (double)io.act[2]),
                             Q(0.0, UG_VQ_S, 0.0, UG_VQ_C));
+            } else if (task == UG_TASK_GOLF) {
+                /* env_golf_v0.py:115-127: EE position + action, the reset orientation (0, 0, -0.7, 0.7) */
+                link_state_of(e.q, UG_EE_LINK, pe, oe);
+                move_ee_end(e, V(pe.x + (double)io.act[0], pe.y + (double)io.act[1], pe.z + (double)io.act[2]),
+                            Q(0.0, 0.0, -0.70, 0.70));
             } else {
                 /* env_ball_balance_v0.py:105-118: move_ee(end pose + action on the euler angles) */
                 link_state_of(e.q, UG_EE_LINK, pe, oe);
@@ -1212,6 +1368,16 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
                 e.goal_approached = (double)app;
                 e.goal_grasped = (double)gr;
                 io.term = io.succ;
+            } else if (task == UG_TASK_GOLF) { /* env_golf_v0.py:129-183 */
+                int c0 = s->ocol[0], c1 = c0 + s->oncol[0], cb = s->ocol[1], cp = static_collider(s, 12);
+                int in_fingers = 0;
+                for (int c = c0; c < c1; c++) in_fingers |= robot_contact(e, s, c, 9, 18);
+                int floor = robot_contact(e, s, cp, 0, UG_NL - 1) || pair_contact(e, s, c0, c1, cp, cp + 1);
+                int touched = pair_contact(e, s, cb, cb + 1, c0, c1);
+                v3 st = club_point(e, UG_GF_FOOT_Z);
+                double stick[3] = {st.x, st.y, st.z}, ball[3] = {e.obj[1].pos.x, e.obj[1].pos.y, e.obj[1].pos.z};
+                double hole[3] = {UG_GF_PITCH_X, UG_GF_PITCH_Y, UG_GF_PITCH_Z};
+                io.succ = ugg_gf_reward(ball, hole, stick, in_fingers, floor, touched, &io.rew, &io.term);
             } else { /* env_ball_balance_v0.py:119-134: reward 1, terminated when the ball falls below the paddle */
                 io.rew = 1.0;
                 io.term = e.obj[1].pos.z < e.obj[0].pos.z;
@@ -1251,6 +1417,12 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
                 link_state_of(e.q, UG_EE_LINK, pe, oe);
                 move_ee_end(e, pe, oe);
                 *next = G_RESET_DONE;
+            } else if (task == UG_TASK_GOLF) { /* env_golf_v0.py:238-252: pitch re-created, start pose, open 20% */
+                int cp = static_collider(s, 12);
+                drop_manifolds_of(e, s, cp, cp + 1);
+                move_ee_end(e, V(0.0, -0.60, 0.40), Q(0.0, 0.0, -0.70, 0.70));
+                open_gripper(e, 20.0);
+                *next = G_RESET_PLACE;
             } else { /* env_ball_balance_v0.py:145-160: move_ee(start pose); open 20% */
                 move_ee_end(e, V(0.0, -0.60, 0.60), Q(0.50, -0.50, -0.50, 0.50));
                 open_gripper(e, 20.0);
@@ -1258,6 +1430,16 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
             }
             return L_WAIT;
         case G_RESET_PLACE: { /* BallBalance: paddle between the fingers, ball above it; close gripper */
+            if (task == UG_TASK_GOLF) { /* env_golf_v0.py:254-265: club under the gripper centre, ball; close */
+                v3 gc = gripper_center(e.q);
+                place_object(e, 0, V(gc.x, gc.y, gc.z - 0.05 + UG_GF_ZC), Q(0, 0, 0, 1));
+                double u0 = io.dr.next(), u1 = io.dr.next(), bx, by;
+                ugg_gf_ball_xy(u0, u1, &bx, &by);
+                place_object(e, 1, V(bx, by, 0.1), Q(0, 0, 0, 1));
+                close_gripper(e, 100.0);
+                *next = G_RESET_DONE;
+                return L_WAIT;
+            }
             v3 pe;
             q4 oe;
             link_state_of(e.q, UG_EE_LINK, pe, oe);

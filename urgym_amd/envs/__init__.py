@@ -74,4 +74,10 @@ def CubesGrasp(camera=None, reward_type="dense", render_mode="human", **kw):
     return URGymEnv(2, max_episode_steps=None, camera=camera, reward_type=reward_type, render_mode=render_mode, **kw)
 
 
-__all__ = ["make", "TASKS", "URGymEnv", "URGymVectorEnv", "BallBalance", "CubesPush", "CubesGrasp", "spaces_for"]
+def Golf(camera=None, reward_type="dense", render_mode="human", **kw):
+    """env_golf_v0.Golf(camera, reward_type, render_mode) signature."""
+    return URGymEnv(3, max_episode_steps=None, camera=camera, reward_type=reward_type, render_mode=render_mode, **kw)
+
+
+__all__ = ["make", "TASKS", "URGymEnv", "URGymVectorEnv", "BallBalance", "CubesPush", "CubesGrasp", "Golf",
+           "spaces_for"]
