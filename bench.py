@@ -47,6 +47,9 @@ def cpu_baseline(task, seconds=10.0):
     arr = (ctypes.c_void_p * n)(*[e.h for e in envs])
     A, O = envs[0].act_dim, envs[0].obs_dim
     rng = np.random.default_rng(20241220)
+    from urgym_amd.envs import spaces_for
+    _, act_space = spaces_for(task)
+    alo, ahi = np.asarray(act_space.low, np.float64), np.asarray(act_space.high, np.float64)
     obs = np.zeros((n, O)); rew = np.zeros(n); term = np.zeros(n, np.uint8); succ = np.zeros(n, np.uint8)
     sub = np.zeros(n, np.int32); el = np.zeros(n, np.int32)
     p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
@@ -54,7 +57,7 @@ def cpu_baseline(task, seconds=10.0):
     substeps = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        act = rng.uniform(-0.1, 0.1, size=(n, A)).astype(np.float32)
+        act = rng.uniform(alo, ahi, size=(n, A)).astype(np.float32)
         substeps += olib().ugo_batch_step(arr, n, p(act), p(obs), p(rew), p(term), p(succ), p(sub), 1,
                                           MAX_STEPS[task], p(el))
         steps += n
@@ -95,7 +98,9 @@ def main():
     A, O = sim.act_dim, sim.obs_dim
     rng = np.random.default_rng(20241220 + rank)
     K, W = args.steps, args.warmup
-    lo, hi = (-0.1, 0.1)
+    from urgym_amd.envs import spaces_for
+    _, act_space = spaces_for(args.task)
+    lo, hi = np.asarray(act_space.low, np.float64), np.asarray(act_space.high, np.float64)
     acts = torch.from_numpy(rng.uniform(lo, hi, size=(W + K, n, A)).astype(np.float32)).to(dev)
     obs = torch.zeros(n, O, dtype=torch.float64, device=dev)
     fin = torch.zeros_like(obs)
@@ -151,7 +156,8 @@ def main():
     bytes_per_env = 2 * S + 4 * A + 8 * O * 2 + 8 + 3 + 4
     achieved_gbs = bytes_per_env * n / (avg_kernel_ms * 1e-3) / 1e9
     line = {
-        "metric": "env-steps/sec at N parallel envs (BallBalance-v0, 4096 envs per MI355X)",
+        "metric": ("env-steps/sec at N parallel envs (BallBalance-v0, 4096 envs per MI355X)" if args.task == 0 and n == 4096
+                   else f"env-steps/sec at N parallel envs ({TASK_NAMES[args.task].split('/')[1]}, {n} envs per MI355X)"),
         "value": value,
         "unit": "env-steps/s",
         "n_gpus": world,
