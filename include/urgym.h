@@ -104,6 +104,11 @@ double urgym_last_kernel_ms(const urgym_handle* h);
  * (collision, dynamics, row build, PGS, split, integration, glue, total, then event counts).
  * Returns -1 unless the library was built with -DUG_PROF. */
 int urgym_debug_prof(urgym_handle* h, unsigned long long* out16, int reset);
+/* Development aid: copy the first count doubles of env's device workspace to out; the workspace size
+ * (doubles per env) is urgym_debug_ws_doubles().  A -DUG_DEBUG_DUMP build stores the last PGS call's
+ * Delassus rows, w and impulses there. */
+int urgym_debug_workspace(urgym_handle* h, int env, double* out, int count);
+int urgym_debug_ws_doubles(void);
 
 #ifdef __cplusplus
 }

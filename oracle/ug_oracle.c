@@ -10,6 +10,7 @@
  */
 #include "ug_oracle.h"
 
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1290,8 +1291,7 @@ static void collide(ugo_env* e, const kin* k) {
 /* constraint rows + projected Gauss-Seidel (btMultiBodyConstraintSolver)    */
 /* ======================================================================== */
 /* A row holds its Jacobian J and M^-1 J^T over the full generalized-velocity vector
- * (robot dofs 0..11, object 0 at 12..17, object 1 at 18..23, zero-padded to UG_NVP = 32 slots), so the
- * PGS dot product is one fixed pairwise tree -- the order the HIP kernel's DPP reduction realises. */
+ * (robot dofs 0..11, object 0 at 12..17, object 1 at 18..23, zero-padded to UG_NVP = 32 slots). */
 #define UG_NVP 32
 typedef struct {
     double J[UG_NVP], MiJ[UG_NVP];
@@ -1319,20 +1319,6 @@ static double ent_dot_local(int ent, const double* a, const double* b) {
     double s = 0.0;
     for (int i = 0; i < n; i++) s += a[i] * b[i];
     return s;
-}
-/* pairwise tree over 16 products: ((x0+x1)+(x2+x3)) + ((x4+x5)+(x6+x7)) ... */
-static double tree16(const double* x) {
-    double a[16];
-    for (int i = 0; i < 16; i++) a[i] = x[i];
-    for (int w = 1; w < 16; w <<= 1)
-        for (int i = 0; i < 16; i += 2 * w) a[i] = a[i] + a[i + w];
-    return a[0];
-}
-/* J . v over the 32-slot layout: two 16-lane rows, each reduced as a tree, then added */
-static double pdot(const double* J, const double* v) {
-    double p[UG_NVP];
-    for (int d = 0; d < UG_NVP; d++) p[d] = J[d] * v[d];
-    return tree16(p) + tree16(p + 16);
 }
 static void scatter(int ent, const double* src, double* dst) {
     int n = ent_dofs(ent), o = ent_off(ent);
@@ -1578,68 +1564,125 @@ static void build_rows(ugo_env* e, const kin* k, const double* LDL, const double
     }
 }
 
-/* resolveSingleConstraintRowGeneric [ext] over the full generalized vector */
-static double solve_row(row* r, double* dv, int pen) {
+/* ---- projected Gauss-Seidel in row space ----
+ * Bullet's btMultiBodyConstraintSolver keeps the solver's velocity delta dv and evaluates each row as
+ * J_r . dv.  The same iteration is written here in row space: w = J dv is kept instead of dv, so a row
+ * update reads w_r and adds column r of the Delassus matrix A = J M^-1 J^T times the impulse change to w.
+ * Mathematically this is the identical sequence of Gauss-Seidel updates (same row order, same clamps,
+ * same residual); only the floating-point summation differs, and it is *defined* here so that the HIP
+ * kernel (one lane per row) reproduces it bit for bit:
+ *   A[i][j] = fma chain over slots d = 0..NV-1 of J_i[d] * MiJ_j[d]   (rows in solve position order)
+ *   w_i     = fma(A[i][r], delta_r, w_i) after each update of row r
+ *   dv[d]   = fma chain over positions k = 0..n-1 of MiJ_k[d] * impulse_k   (after the iterations)
+ * Solve positions: non-contact rows [0, nnc), normals [nnc, fb), frictions, then rolling-friction rows. */
+static __thread double g_A[MAXROWS][MAXROWS];
+static double rdot(const double* J, const double* MiJ) {
+    double s = 0.0;
+    for (int d = 0; d < NV; d++) s = fma(J[d], MiJ[d], s);
+    return s;
+}
+/* resolveSingleConstraintRowGeneric [ext] (cfm = 0) for the row at position p, written in its
+ * FMA-contracted, clamp-the-increment form: delta = clamp(rhs - w_p / D, lo - imp, hi - imp),
+ * imp += delta.  (Bullet clamps imp + delta against [lo, hi] and assigns the bound; the two agree up to
+ * the rounding of imp + (bound - imp), i.e. at most one ulp on a clamped impulse.) */
+static double solve_row_w(row* r, int p, int n, double* w, int pen) {
     double imp = pen ? r->impPen : r->imp;
-    double di = pen ? r->rhsPen : r->rhs; /* - imp * cfm, cfm = 0 */
-    di -= pdot(r->J, dv) * r->invD;
-    double sum = imp + di;
-    if (sum < r->lo) { di = r->lo - imp; imp = r->lo; }
-    else if (sum > r->hi) { di = r->hi - imp; imp = r->hi; }
-    else imp = sum;
+    double di = fma(-w[p], r->invD, pen ? r->rhsPen : r->rhs);
+    double dlo = r->lo - imp, dhi = r->hi - imp;
+    di = di < dlo ? dlo : di; /* v_max_f64 */
+    di = di > dhi ? dhi : di; /* v_min_f64 */
+    imp = imp + di;
     if (pen) r->impPen = imp; else r->imp = imp;
-    for (int d = 0; d < NV; d++) dv[d] = dv[d] + r->MiJ[d] * di;
-    return r->invD == 0.0 ? 0.0 : di * (1.0 / r->invD);
+    for (int q = 0; q < n; q++) w[q] = fma(g_A[q][p], di, w[q]);
+    double rinv = r->invD == 0.0 ? 0.0 : 1.0 / r->invD;
+    return di * rinv;
 }
 
-static void pgs(rowset* rs, double* dv) {
+/* debug record of the last PGS call (tests only): n, nnc, nn, nf, nr, sweeps, split sweeps */
+static __thread int g_dbg[8];
+void ugo_debug_rows(int* out) { memcpy(out, g_dbg, sizeof(g_dbg)); }
+static __thread double g_dbg_w[4 * 128];
+/* last PGS call: A (row-major [MAXROWS][MAXROWS]), w after the warm start, w and impulses after the sweeps */
+void ugo_debug_pgs(double* A, double* w4) {
+    memcpy(A, g_A, sizeof(g_A));
+    memcpy(w4, g_dbg_w, sizeof(g_dbg_w));
+}
+static int pgs(rowset* rs, double* dv, double* dvs) {
+    row* R[MAXROWS];
+    int n = 0, pos_of[MAXROWS];
+    for (int j = 0; j < rs->nnc; j++) R[n++] = &rs->r[rs->idx_nc[j]];
+    for (int j = 0; j < rs->nn; j++) R[n++] = &rs->r[rs->idx_n[j]];
+    for (int j = 0; j < rs->nf; j++) R[n++] = &rs->r[rs->idx_f[j]];
+    for (int j = 0; j < rs->nr; j++) R[n++] = &rs->r[rs->idx_r[j]];
+    for (int p = 0; p < n; p++) pos_of[R[p] - rs->r] = p;
+    const int nnc = rs->nnc, fb = rs->nnc + rs->nn;
+    g_dbg[0] = n; g_dbg[1] = nnc; g_dbg[2] = rs->nn; g_dbg[3] = rs->nf; g_dbg[4] = rs->nr; g_dbg[5] = 0; g_dbg[6] = 0;
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) g_A[i][j] = rdot(R[i]->J, R[j]->MiJ);
+    double w[MAXROWS];
+    for (int q = 0; q < n; q++) w[q] = 0.0;
     /* warm start (normal rows only; Bullet warm-starts friction with 0) */
-    for (int i = 0; i < rs->nn; i++) {
-        row* r = &rs->r[rs->idx_n[i]];
-        if (r->imp != 0.0)
-            for (int d = 0; d < NV; d++) dv[d] = dv[d] + r->MiJ[d] * r->imp;
+    for (int p = nnc; p < fb; p++) {
+        double imp = R[p]->imp;
+        if (imp != 0.0)
+            for (int q = 0; q < n; q++) w[q] = fma(g_A[q][p], imp, w[q]);
     }
+    for (int q = 0; q < 128; q++) g_dbg_w[q] = q < n ? w[q] : 0.0;
     for (int it = 0; it < UG_PGS_ITERS; it++) {
         double res = 0.0;
-        for (int j = 0; j < rs->nnc; j++) {
-            int idx = (it & 1) ? j : rs->nnc - 1 - j;
-            double x = solve_row(&rs->r[rs->idx_nc[idx]], dv, 0);
+        /* non-contact rows: alternate direction (reverse on even sweeps) */
+        for (int j = 0; j < nnc; j++) {
+            int p = (it & 1) ? j : nnc - 1 - j;
+            double x = solve_row_w(R[p], p, n, w, 0);
             x = x * x;
             res = res > x ? res : x;
         }
-        for (int j = 0; j < rs->nn; j++) {
-            double x = solve_row(&rs->r[rs->idx_n[j]], dv, 0);
+        for (int p = nnc; p < fb; p++) {
+            double x = solve_row_w(R[p], p, n, w, 0);
             x = x * x;
             res = res > x ? res : x;
         }
-        for (int j = 0; j < rs->nf + rs->nr; j++) {
-            row* f = &rs->r[j < rs->nf ? rs->idx_f[j] : rs->idx_r[j - rs->nf]];
-            double tot = rs->r[f->nrow].imp;
+        /* friction / rolling rows: bounds +-mu * (their normal's impulse), skipped while it is not positive */
+        for (int p = fb; p < n; p++) {
+            row* f = R[p];
+            double tot = R[pos_of[f->nrow]]->imp;
             if (tot > 0.0) {
                 f->lo = -(f->fric * tot);
                 f->hi = f->fric * tot;
-                double x = solve_row(f, dv, 0);
+                double x = solve_row_w(f, p, n, w, 0);
                 x = x * x;
                 res = res > x ? res : x;
             }
         }
+        g_dbg[5] = it + 1;
         if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
     }
-}
-/* split-impulse pass for deep penetrations (rhsPenetration rows) */
-static int pgs_split(rowset* rs, double* dvs) {
+    for (int q = 0; q < 128; q++) { g_dbg_w[128 + q] = q < n ? w[q] : 0.0; g_dbg_w[256 + q] = q < n ? R[q]->imp : 0.0; }
+    for (int d = 0; d < NV; d++) {
+        double s = 0.0;
+        for (int k = 0; k < n; k++) s = fma(R[k]->MiJ[d], R[k]->imp, s);
+        dv[d] = s;
+    }
+    /* split-impulse pass for deep penetrations (rhsPenetration rows, normals only, from zero) */
     int any = 0;
-    for (int j = 0; j < rs->nn; j++)
-        if (rs->r[rs->idx_n[j]].rhsPen != 0.0) any = 1;
+    for (int p = nnc; p < fb; p++)
+        if (R[p]->rhsPen != 0.0) any = 1;
     if (!any) return 0;
+    for (int q = 0; q < n; q++) w[q] = 0.0;
     for (int it = 0; it < UG_PGS_ITERS; it++) {
         double res = 0.0;
-        for (int j = 0; j < rs->nn; j++) {
-            double x = solve_row(&rs->r[rs->idx_n[j]], dvs, 1);
+        for (int p = nnc; p < fb; p++) {
+            double x = solve_row_w(R[p], p, n, w, 1);
             x = x * x;
             res = res > x ? res : x;
         }
+        g_dbg[6] = it + 1;
         if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
+    }
+    for (int d = 0; d < NV; d++) {
+        double s = 0.0;
+        for (int k = nnc; k < fb; k++) s = fma(R[k]->MiJ[d], R[k]->impPen, s);
+        dvs[d] = s;
     }
     return 1;
 }
@@ -1689,8 +1732,7 @@ static void substep(ugo_env* e) {
     double dv[UG_NVP], dvs[UG_NVP];
     memset(dv, 0, sizeof(dv));
     memset(dvs, 0, sizeof(dvs));
-    pgs(&rs, dv);
-    int split = pgs_split(&rs, dvs);
+    int split = pgs(&rs, dv, dvs);
     for (int i = 0; i < rs.nn; i++) {
         const row* r = &rs.r[rs.idx_n[i]];
         e->man[r->man].pt[r->pt].imp = r->imp;

@@ -42,6 +42,10 @@ void ugo_get_state(const ugo_env* e, double* s);
 void ugo_set_state(ugo_env* e, const double* s);
 /* one physics substep (p.stepSimulation) -- for fine-grained parity tests */
 void ugo_substep(ugo_env* e);
+/* last substep's PGS shape (this thread): n, nnc, nn, nf, nr, sweeps, split sweeps, 0 */
+void ugo_debug_rows(int* out);
+/* last PGS call: A [128][128] row-major, then w4 = w after warm start | w after sweeps | impulses (128 each) */
+void ugo_debug_pgs(double* A, double* w4);
 /* helpers exposed for known-answer tests */
 void ugo_rng_seed(ugo_env* e, uint32_t seed);
 double ugo_rng_random(ugo_env* e);

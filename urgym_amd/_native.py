@@ -16,7 +16,8 @@ SYMBOLS = [
     "urgym_create", "urgym_destroy", "urgym_last_error", "urgym_obs_dim", "urgym_act_dim", "urgym_state_dim",
     "urgym_num_envs", "urgym_set_autoreset", "urgym_reset", "urgym_num_draws", "urgym_step", "urgym_step_device",
     "urgym_reset_device", "urgym_sync", "urgym_stream", "urgym_get_state", "urgym_set_state", "urgym_substep",
-    "urgym_link_state", "urgym_ik", "urgym_last_kernel_ms", "urgym_debug_prof",
+    "urgym_link_state", "urgym_ik", "urgym_last_kernel_ms", "urgym_debug_prof", "urgym_debug_workspace",
+    "urgym_debug_ws_doubles",
 ]
 
 _lib = None
@@ -55,6 +56,8 @@ def lib():
     L.urgym_last_kernel_ms.restype = D
     L.urgym_last_kernel_ms.argtypes = [P]
     L.urgym_debug_prof.argtypes = [P, P, I]
+    L.urgym_debug_workspace.argtypes = [P, I, P, I]
+    L.urgym_debug_ws_doubles.argtypes = []
     _lib = L
     return L
 

@@ -618,4 +618,14 @@ int urgym_debug_prof(urgym_handle* h, unsigned long long* out16, int reset) {
 #endif
 }
 
+// Development aid: copy env's per-env workspace (count doubles from its start) to the host.
+int urgym_debug_workspace(urgym_handle* h, int env, double* out, int count) {
+    if (!h || !out || env < 0 || env >= h->n || count < 0 || count > (int)WS_DOUBLES) return -1;
+    HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(out, h->d_ws + (size_t)env * WS_DOUBLES, sizeof(double) * count, hipMemcpyDeviceToHost));
+    return 0;
+}
+int urgym_debug_ws_doubles(void) { return (int)WS_DOUBLES; }
+
 }  // extern "C"

@@ -32,12 +32,17 @@ namespace ugd {
 
 #define TEAM 64
 #define NVP 32
-#define REGROWS 96          /* rows held in VGPR slots; rows beyond stream from the global workspace */
-#define NSLOT REGROWS       /* one row per register slot: lane d holds J[d], M^-1J[d] */
-/* per-env global workspace (L2-resident): old manifolds (collision), then every row's J | M^-1 J^T
- * (24 + 24 doubles), written lane-per-row by the row build and read back into the register slots */
+#define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
+/* per-env global workspace (L2-resident): old manifolds (collision), every row's J | M^-1 J^T (24 + 24
+ * doubles, written lane-per-row by the row build), then the Delassus columns >= PREG (column-major) */
 #define WS_ROWS (UG_MAXMAN * UG_MAN_DOUBLES)
-#define WS_DOUBLES (WS_ROWS + MAXROWS * 48)
+#define WS_A (WS_ROWS + MAXROWS * 48)
+#ifdef UG_DEBUG_DUMP /* development aid: team_pgs dumps A, w and impulses after the workspace proper */
+#define WS_DBG (WS_A + (MAXROWS - PREG) * MAXROWS)
+#define WS_DOUBLES (WS_DBG + MAXROWS * MAXROWS + 8 * MAXROWS)
+#else
+#define WS_DOUBLES (WS_A + (MAXROWS - PREG) * MAXROWS)
+#endif
 #define STAGE 24
 #define MAXOV 40
 
@@ -75,6 +80,7 @@ struct Shared {
     union {
         double stage[STAGE][48];
         struct { Cand c[MAXOV][4]; int n[MAXOV]; } cand;
+        double impx[MAXROWS]; /* PGS: row impulses gathered through LDS (after the Delassus build) */
     } u;
     Cand hc[64];
     double a12[NB];
@@ -790,44 +796,26 @@ __device__ __noinline__ static void build_row(const Scene* s, int pos, double* w
     for (int i = 0; i < 24; i++) { wrow[i] = J[i]; wrow[24 + i] = MJ[i]; }
 }
 
-/* ---------------- PGS (btMultiBodyConstraintSolver) ----------------
- * Row positions are template parameters, so the register slots RJ[P] / RM[P] are
- * addressed with constants (the arrays stay in VGPRs) and every row-range test is a scalar
- * branch.  Each row's scalars (rhs, 1/D, bounds, impulse) are fetched from LDS one row ahead. */
+/* ---------------- PGS (btMultiBodyConstraintSolver), row space ----------------
+ * The solver keeps w = J dv (one entry per row) instead of dv: lane l owns the rows at positions l and
+ * l + 64 (slot 0 / slot 1) -- their scalars, their impulse and their w -- and holds its rows of the
+ * Delassus matrix A = J M^-1 J^T in VGPRs (A0[P] / A1[P] = A[l][P], A[l+64][P]).  Updating row P is
+ * lane-parallel arithmetic on every lane's own row (only lane P's result is used), one broadcast of the
+ * impulse change (two v_readlane) and one fma per slot: w += A[:, P] * delta.  No cross-lane reduction
+ * and no LDS traffic inside a sweep.  The owner lane only records the w it saw; its new impulse and
+ * residual are recomputed from that w after the section (same operations, so the same bits).  Row
+ * positions are template parameters, so A0[P] / A1[P] are compile-time register names and every
+ * row-range test is a scalar branch.  Columns P >= PREG come from the global workspace.  Arithmetic
+ * order is the oracle's pgs() (oracle/ug_oracle.c). */
 #define NCMAX (2 * NB + 12) /* limits (both sides) + 7 motors + 5 gears */
-struct RowPre {
-    double rhs, invD, rinv, lo, hi, fric; /* LDS values, fetched one row ahead */
-    int nrow;                             /* friction / rolling rows: their normal's position */
+#define MJCHUNK 48          /* M^-1J rows staged in LDS per chunk of the Delassus build */
+typedef __attribute__((address_space(1))) const double gcdouble;
+typedef __attribute__((address_space(1))) double gdouble;
+struct Lrow { /* the two rows this lane owns (slot s: position lane + 64 s) */
+    double rhs[2], invD[2], rinv[2], lo[2], hi[2], imp[2];
+    double dlo[2], dhi[2]; /* lo - imp, hi - imp */
+    double dsv[2];         /* the increment applied when the row was solved in this section */
 };
-/* row impulses, lane-distributed in two VGPR pairs: row r's impulse sits in lane (r & 63) of v[r >> 6]
- * (read with v_readlane, written with a lane-select: no LDS traffic inside the iteration loop) */
-struct Imps {
-    double v[2];
-};
-template <int P>
-__device__ __forceinline__ double imp_get(const Imps& I) { return readlane_d(I.v[P >> 6], P & 63); }
-__device__ __forceinline__ double imp_get_dyn(const Imps& I, int r) {
-    double src = r >= 64 ? I.v[1] : I.v[0];
-    return readlane_d(src, r & 63);
-}
-template <int P>
-__device__ __forceinline__ void imp_set(Imps& I, double x) {
-    I.v[P >> 6] = (int)threadIdx.x == (P & 63) ? x : I.v[P >> 6];
-}
-
-template <int PEN>
-__device__ __forceinline__ RowPre row_fetch(const Shared& sh, int p) {
-    const RowS& r = sh.rs[p];
-    RowPre x;
-    x.invD = r.invD;
-    x.rinv = r.rinv;
-    x.lo = r.lo;
-    x.hi = r.hi;
-    x.rhs = PEN ? r.rhsPen : r.rhs;
-    x.fric = PEN ? 0.0 : r.fric;
-    x.nrow = PEN ? 0 : r.nrow;
-    return x;
-}
 
 /* branch-free select on the bit patterns (keeps the clamp out of control flow) */
 __device__ __forceinline__ double bsel(bool c, double a, double b) {
@@ -835,116 +823,145 @@ __device__ __forceinline__ double bsel(bool c, double a, double b) {
     unsigned long long r = (__double_as_longlong(a) & m) | (__double_as_longlong(b) & ~m);
     return __longlong_as_double(r);
 }
-/* resolveSingleConstraintRowGeneric [ext] (oracle solve_row).  Lane d owns generalized-velocity slot d
- * (both halves hold the same slots): the dot is a 16-lane DPP tree per row of lanes plus two readlanes,
- * after which the row's scalar math is wave-uniform and the velocity update is lane-local. */
-__device__ __forceinline__ double pgs_update(double Js, double Ms, const RowPre& c, double imp, double& dv,
-                                             double& res) {
-    double red = reduce16(Js * dv);
-    double dot = readlane_d(red, 0) + readlane_d(red, 16);
-    double di = c.rhs - dot * c.invD;
-    double sum = imp + di;
-    bool below = sum < c.lo, above = sum > c.hi;
-    double dlo = c.lo - imp, dhi = c.hi - imp;
-    double dn = bsel(below, dlo, bsel(above, dhi, di));
-    double in = bsel(below, c.lo, bsel(above, c.hi, sum));
-    dv = dv + Ms * dn;
-    double x = dn * c.rinv;
-    x = x * x;
-    res = res > x ? res : x;
-    return in;
-}
-
 template <int P>
-__device__ __forceinline__ void row_jm(const double (&RJ)[NSLOT], const double (&RM)[NSLOT], const double* ws, int d,
-                                       double& Js, double& Ms) {
-    if constexpr (P < REGROWS) {
-        Js = RJ[P];
-        Ms = RM[P];
+__device__ __forceinline__ void colA(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA, int lane,
+                                     double& a0, double& a1) {
+    if constexpr (P < PREG) {
+        a0 = A0[P];
+        a1 = A1[P];
     } else {
-        const double* x = ws + WS_ROWS + P * 48;
-        int dd = d < 24 ? d : 0;
-        double a = x[dd], b = x[24 + dd];
-        Js = d < 24 ? a : 0.0;
-        Ms = d < 24 ? b : 0.0;
+        a0 = wsA[(P - PREG) * MAXROWS + lane];
+        a1 = wsA[(P - PREG) * MAXROWS + 64 + lane];
     }
 }
-/* rows [start, end) in increasing position; cur = fetched data of row max(P, start).  Friction rows
- * (P >= fb) take bounds +-mu * (their normal's current impulse) and are skipped while it is not positive */
-template <int P, int PEN>
-__device__ __forceinline__ void pgs_fwd(Shared& sh, const double (&RJ)[NSLOT], const double (&RM)[NSLOT], const double* ws,
-                                        int d, int start, int end, int nnc, int fb, Imps& I, double& dv, double& res,
-                                        RowPre cur) {
+/* lane L of the result := x (uniform), other lanes keep old: two v_writelane_b32 */
+template <int L>
+__device__ __forceinline__ double writelane_d(double old, double x) {
+    int lo = __double2loint(old), hi = __double2hiint(old);
+    const int xl = __builtin_amdgcn_readfirstlane(__double2loint(x)), xh = __builtin_amdgcn_readfirstlane(__double2hiint(x));
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(lo) : "s"(xl), "i"(L));
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(hi) : "s"(xh), "i"(L));
+    return __hiloint2double(hi, lo);
+}
+/* resolveSingleConstraintRowGeneric [ext] (oracle solve_row_w) for the row at position P: every lane
+ * forms the clamped increment of its own row, lane (P & 63)'s is broadcast, applied to w and recorded in
+ * that lane (the impulse itself is advanced after the section).  Chain: fma, max, min, readlane, fma. */
+template <int P>
+__device__ __forceinline__ void row_upd(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA, int lane,
+                                        Lrow& L, double (&W)[2]) {
+    constexpr int s = P >> 6, O = P & 63;
+    double a0, a1;
+    colA<P>(A0, A1, wsA, lane, a0, a1);
+    double di = __builtin_fma(-W[s], L.invD[s], L.rhs[s]);
+    double dn = __builtin_fmin(__builtin_fmax(di, L.dlo[s]), L.dhi[s]);
+    double d = readlane_d(dn, O);
+    L.dsv[s] = writelane_d<O>(L.dsv[s], d);
+    W[0] = __builtin_fma(a0, d, W[0]);
+    W[1] = __builtin_fma(a1, d, W[1]);
+}
+/* after a section: the lanes whose row was solved advance their impulse by the recorded increment and
+ * fold (delta / D)^2 into their residual */
+__device__ __forceinline__ void row_finish(Lrow& L, unsigned long long m0, unsigned long long m1, int lane,
+                                           double& res) {
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        const bool did = (((s ? m1 : m0) >> lane) & 1ull) != 0ull;
+        const double dn = L.dsv[s];
+        double x = dn * L.rinv[s];
+        x = x * x;
+        double r2 = res > x ? res : x;
+        res = did ? r2 : res;
+        L.imp[s] = did ? L.imp[s] + dn : L.imp[s];
+        L.dlo[s] = L.lo[s] - L.imp[s];
+        L.dhi[s] = L.hi[s] - L.imp[s];
+    }
+}
+/* lanes whose slot-s row position lies in [a, b), minus skip */
+__device__ __forceinline__ unsigned long long pos_mask(int s, int a, int b, unsigned long long skip) {
+    const int lo = a - 64 * s, hi = b - 64 * s; /* lane range */
+    const int l0 = lo < 0 ? 0 : (lo > 64 ? 64 : lo), l1 = hi < 0 ? 0 : (hi > 64 ? 64 : hi);
+    if (l1 <= l0) return 0ull;
+    unsigned long long m = (l1 - l0 == 64) ? ~0ull : (((1ull << (l1 - l0)) - 1ull) << l0);
+    return m & ~skip;
+}
+/* rows [start, end) in increasing position.  LOWSTART: start is 0 or nnc <= NCMAX, so rows from NCMAX on
+ * need no start test (the contact section); otherwise every row is tested (the friction section) */
+template <int P, bool LOWSTART>
+__device__ __forceinline__ void sweep_fwd(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA,
+                                          int lane, int start, int end, Lrow& L, double (&W)[2]) {
     if constexpr (P < MAXROWS) {
         if (P < end) {
-            RowPre next = cur;
-            /* start is 0 or nnc <= NCMAX: rows from NCMAX on are always inside the range */
-            if (P >= NCMAX || P >= start) {
-                RowPre nxt = row_fetch<PEN>(sh, P + 1 < MAXROWS ? P + 1 : P);
-                double imp = imp_get<P>(I);
-                bool skip = false;
-                if (!PEN && P >= fb) {
-                    double tot = imp_get_dyn(I, __builtin_amdgcn_readfirstlane(cur.nrow));
-                    cur.lo = -(cur.fric * tot);
-                    cur.hi = cur.fric * tot;
-                    skip = __builtin_amdgcn_readfirstlane((int)!(tot > 0.0)) != 0;
-                }
-                if (!skip) {
-                    double Js, Ms;
-                    row_jm<P>(RJ, RM, ws, d, Js, Ms);
-                    imp_set<P>(I, pgs_update(Js, Ms, cur, imp, dv, res));
-                }
-                next = nxt;
-            }
-            pgs_fwd<P + 1, PEN>(sh, RJ, RM, ws, d, start, end, nnc, fb, I, dv, res, next);
+            if ((LOWSTART && P >= NCMAX) || P >= start) row_upd<P>(A0, A1, wsA, lane, L, W);
+            sweep_fwd<P + 1, LOWSTART>(A0, A1, wsA, lane, start, end, L, W);
         }
     }
 }
-/* non-contact rows in decreasing position (even iterations); cur = fetched data of row min(P, nnc-1) */
+/* non-contact rows [0, nnc) in decreasing position (even sweeps); nnc <= NCMAX < 64 */
 template <int P>
-__device__ __forceinline__ void pgs_rev(Shared& sh, const double (&RJ)[NSLOT], const double (&RM)[NSLOT], int nnc,
-                                        Imps& I, double& dv, double& res, RowPre cur) {
+__device__ __forceinline__ void sweep_rev(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA,
+                                          int lane, int nnc, Lrow& L, double (&W)[2]) {
     if constexpr (P >= 0) {
-        RowPre next = cur;
-        if (P < nnc) {
-            next = row_fetch<0>(sh, P > 0 ? P - 1 : 0);
-            imp_set<P>(I, pgs_update(RJ[P], RM[P], cur, imp_get<P>(I), dv, res));
-        }
-        pgs_rev<P - 1>(sh, RJ, RM, nnc, I, dv, res, next);
+        if (P < nnc) row_upd<P>(A0, A1, wsA, lane, L, W);
+        sweep_rev<P - 1>(A0, A1, wsA, lane, nnc, L, W);
     }
 }
-/* warm start: normal rows with a carried impulse */
+/* warm start: normal rows [nnc, fb) with a carried impulse, w += A[:, P] * impulse */
 template <int P>
-__device__ __forceinline__ void pgs_warm(const double (&RJ)[NSLOT], const double (&RM)[NSLOT], const double* ws,
-                                         int d, int nnc, int fb, const Imps& I, double& dv) {
+__device__ __forceinline__ void sweep_warm(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA,
+                                           int lane, int nnc, int fb, const Lrow& L, double (&W)[2]) {
     if constexpr (P < MAXROWS) {
         if (P < fb) {
             if (P >= nnc) {
-                double imp = imp_get<P>(I);
-                double Js, Ms;
-                row_jm<P>(RJ, RM, ws, d, Js, Ms);
-                double dvn = dv + Ms * imp;
-                dv = imp != 0.0 ? dvn : dv;
+                double imp = readlane_d(L.imp[P >> 6], P & 63);
+                if (imp != 0.0) {
+                    double a0, a1;
+                    colA<P>(A0, A1, wsA, lane, a0, a1);
+                    W[0] = __builtin_fma(a0, imp, W[0]);
+                    W[1] = __builtin_fma(a1, imp, W[1]);
+                }
             }
-            pgs_warm<P + 1>(RJ, RM, ws, d, nnc, fb, I, dv);
+            sweep_warm<P + 1>(A0, A1, wsA, lane, nnc, fb, L, W);
         }
     }
 }
-/* rows (global workspace) -> register slots of their half: lane d of half h holds J[d], M^-1J[d] of row 2*SL+h */
-template <int SL>
-__device__ __forceinline__ void load_slots(const double* ws, double (&RJ)[NSLOT], double (&RM)[NSLOT], int n, int d) {
-    if constexpr (SL < NSLOT) {
-        if (SL < n) {
-            bool in = d < 24;
-            const double* x = ws + WS_ROWS + SL * 48 + (in ? d : 0);
-            double vj = x[0], vm = x[24];
-            RJ[SL] = in ? vj : 0.0;
-            RM[SL] = in ? vm : 0.0;
-            load_slots<SL + 1>(ws, RJ, RM, n, d);
+/* M^-1J of rows [c0, c0 + MJCHUNK) -> LDS (sh.u.stage viewed as [MJCHUNK][24]) */
+__device__ __forceinline__ void stage_mj(gcdouble* rows, int c0, int n, int lane) {
+    double* st = &g_sh.u.stage[0][0];
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < MJCHUNK * 24; i += TEAM) {
+        const int j = c0 + i / 24, d = i % 24;
+        st[i] = j < n ? rows[j * 48 + 24 + d] : 0.0;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+/* Delassus row of this lane's slot: A[r][j] = fma chain over d of J_r[d] * M^-1J_j[d], j = 0..n-1 */
+template <int J, int S>
+__device__ __forceinline__ void build_A(gcdouble* rows, const double (&Jr)[NV], double (&A)[PREG], gdouble* wsA,
+                                        int n, int lane) {
+    if constexpr (J < MAXROWS) {
+        if (J < n) {
+            if constexpr (J % MJCHUNK == 0) stage_mj(rows, J, n, lane);
+            const double* mj = &g_sh.u.stage[0][0] + (J % MJCHUNK) * 24; /* same address on every lane */
+            /* a compiler barrier per column: otherwise the scheduler hoists every column's LDS reads and
+             * spills them (the A rows already fill the register file) */
+            asm volatile("" ::: "memory");
+            double a = 0.0;
+#pragma unroll
+            for (int d = 0; d < NV; d++) a = __builtin_fma(Jr[d], mj[d], a);
+            asm volatile("" : "+v"(a)); /* materialise the entry here (no sinking into its uses) */
+            if constexpr (J < PREG) A[J] = a;
+            else wsA[(J - PREG) * MAXROWS + 64 * S + lane] = a;
+            build_A<J + 1, S>(rows, Jr, A, wsA, n, lane);
         }
     }
 }
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+    unsigned long long u = (unsigned long long)p;
+    unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u), hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+    return (T*)(((unsigned long long)hi << 32) | lo);
+}
 
 /* lane 0: external forces (robot gravity/gyroscopic/damping via CRBA + RNEA, free objects), the LDL^T of
  * the mass matrix, and the row enumeration */
@@ -1024,54 +1041,181 @@ __device__ __noinline__ static void serial_fk() {
     if (threadIdx.x == 0) fk(g_sh.e.q, g_sh.kin);
 }
 
-/* PGS over the rows in the register slots: warm start (normals), iterations (residual early-out), and
- * the split-impulse pass; returns whether the split pass ran (dvs valid) */
-__device__ __forceinline__ static int team_pgs(const double* ws, int n, int nnc, int nn, int d,
-                                               const double (&RJ)[NSLOT], const double (&RM)[NSLOT], double& dv,
-                                               double& dvs) {
+#ifdef UG_DEBUG_DUMP
+template <int J>
+__device__ __forceinline__ void dump_A(const double (&A0)[PREG], const double (&A1)[PREG], double* dbg, int n, int lane) {
+    if constexpr (J < PREG) {
+        if (J < n) {
+            dbg[J * MAXROWS + lane] = A0[J];
+            dbg[J * MAXROWS + 64 + lane] = A1[J];
+            dump_A<J + 1>(A0, A1, dbg, n, lane);
+        }
+    }
+}
+#endif
+/* PGS: Delassus rows, warm start (normals), sweeps (residual early-out), the split-impulse pass; returns
+ * whether the split pass ran (dvs valid).  Impulses are written back to sh.rs[].imp.  Its own function:
+ * the 2 x PREG register rows of A get a register allocation of their own. */
+__device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int nn_, double& dv, double& dvs) {
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
+    /* arguments of a non-kernel function arrive in VGPRs: make the uniform ones scalar again */
+    const int n = uniform(n_), nnc = uniform(nnc_), nn = uniform(nn_);
+    double* ws = uniform_ptr(ws_);
     const int fb = nnc + nn;
-    dv = 0.0;
-    dvs = 0.0;
-    Imps I;
-    I.v[0] = lane < n ? sh.rs[lane].imp : 0.0;
-    I.v[1] = lane + 64 < n ? sh.rs[lane + 64].imp : 0.0;
-    pgs_warm<0>(RJ, RM, ws, d, nnc, fb, I, dv);
-    for (int it = 0; it < UG_PGS_ITERS; it++) {
-        double res = 0.0;
-        /* opaque per-iteration copies: keeps the per-row scalar tests inside the loop instead of
-         * hoisting ~128 of them into (spilled) SGPRs */
-        int o_n = n, o_nnc = nnc, o_fb = fb;
-        const double* o_ws = ws;
-        asm volatile("" : "+s"(o_n), "+s"(o_nnc), "+s"(o_fb), "+s"(o_ws));
-        int start = 0;
-        if (!(it & 1)) {
-            if (o_nnc > 0) pgs_rev<NCMAX - 1>(sh, RJ, RM, o_nnc, I, dv, res, row_fetch<0>(sh, o_nnc - 1));
-            start = o_nnc;
-        }
-        if (start < o_n) pgs_fwd<0, 0>(sh, RJ, RM, o_ws, d, start, o_n, o_nnc, o_fb, I, dv, res, row_fetch<0>(sh, start));
-        PROF_CNT(PC_ITERS, 1);
-        if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
+    gcdouble* rows = (gcdouble*)(ws + WS_ROWS);
+    gdouble* wsA = (gdouble*)(ws + WS_A);
+    double A0[PREG], A1[PREG];
+    /* slot 1 first, then slot 0 */
+    if (n > 64) {
+        double Jr[NV];
+        const int r = lane + 64 < n ? lane + 64 : 0;
+#pragma unroll
+        for (int d = 0; d < NV; d++) Jr[d] = lane + 64 < n ? rows[r * 48 + d] : 0.0;
+        build_A<0, 1>(rows, Jr, A1, wsA, n, lane);
+    } else {
+#pragma unroll
+        for (int j = 0; j < PREG; j++) A1[j] = 0.0;
     }
-    if (lane < n) sh.rs[lane].imp = I.v[0];
-    if (lane + 64 < n) sh.rs[lane + 64].imp = I.v[1];
-    int anypen = 0;
-    for (int p = nnc + lane; p < fb; p += TEAM) anypen |= sh.rs[p].rhsPen != 0.0;
-    int split = ballot(anypen) != 0ull;
-    if (split) {
-        Imps IP;
-        IP.v[0] = 0.0;
-        IP.v[1] = 0.0;
+    {
+        double Jr[NV];
+        const int r = lane < n ? lane : 0;
+#pragma unroll
+        for (int d = 0; d < NV; d++) Jr[d] = lane < n ? rows[r * 48 + d] : 0.0;
+        build_A<0, 0>(rows, Jr, A0, wsA, n, lane);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    gcdouble* wsAr = (gcdouble*)wsA;
+    Lrow L;
+    double fric[2], rhsPen[2];
+    int nrow[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        const int p = lane + 64 * s;
+        const bool in = p < n;
+        const RowS& r = sh.rs[in ? p : 0];
+        L.rhs[s] = in ? r.rhs : 0.0;
+        L.invD[s] = in ? r.invD : 0.0;
+        L.rinv[s] = in ? r.rinv : 0.0;
+        L.lo[s] = in ? r.lo : 0.0;
+        L.hi[s] = in ? r.hi : 0.0;
+        L.imp[s] = in ? r.imp : 0.0;
+        L.dsv[s] = 0.0;
+        fric[s] = in ? r.fric : 0.0;
+        nrow[s] = in ? r.nrow : 0;
+        rhsPen[s] = in ? r.rhsPen : 0.0;
+    }
+    double W[2] = {0.0, 0.0};
+    sweep_warm<0>(A0, A1, wsAr, lane, nnc, fb, L, W);
+#ifdef UG_DEBUG_DUMP
+    double* dbg = ws + WS_DBG;
+    dump_A<0>(A0, A1, dbg, n, lane);
+    dbg[MAXROWS * MAXROWS + lane] = W[0];
+    dbg[MAXROWS * MAXROWS + 64 + lane] = W[1];
+#endif
+    int split = 0;
+    /* pass 0: the velocity solve; pass 1: the split-impulse pass (normals only, from zero) */
+#pragma nounroll
+    for (int pass = 0; pass < 2; pass++) {
+        const int pen = pass;
+        if (pen) {
+            int anypen = 0;
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                const int p = lane + 64 * s;
+                anypen |= p >= nnc && p < fb && rhsPen[s] != 0.0;
+            }
+            split = ballot(anypen) != 0ull;
+            if (!split) break;
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                L.rhs[s] = rhsPen[s];
+                L.imp[s] = 0.0;
+            }
+            W[0] = 0.0;
+            W[1] = 0.0;
+        }
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            L.dlo[s] = L.lo[s] - L.imp[s];
+            L.dhi[s] = L.hi[s] - L.imp[s];
+        }
         for (int it = 0; it < UG_PGS_ITERS; it++) {
             double res = 0.0;
-            int o_nnc = nnc, o_fb = fb;
-            const double* o_ws = ws;
-            asm volatile("" : "+s"(o_nnc), "+s"(o_fb), "+s"(o_ws));
-            pgs_fwd<0, 1>(sh, RJ, RM, o_ws, d, o_nnc, o_fb, o_nnc, o_fb, IP, dvs, res, row_fetch<1>(sh, o_nnc));
-            if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
+            /* opaque per-sweep copies: keeps the per-row scalar tests inside the loop instead of
+             * hoisting ~128 of them into (spilled) SGPRs */
+            int o_n = n, o_nnc = nnc, o_fb = fb;
+            gcdouble* o_wsA = wsAr;
+            asm volatile("" : "+s"(o_n), "+s"(o_nnc), "+s"(o_fb), "+s"(o_wsA));
+            /* (even sweeps) non-contact rows reversed, then [s0, fb) */
+            if (!pen && !(it & 1) && o_nnc > 0) sweep_rev<NCMAX - 1>(A0, A1, o_wsA, lane, o_nnc, L, W);
+            const int s0 = (pen || !(it & 1)) ? o_nnc : 0;
+            if (s0 < o_fb) sweep_fwd<0, true>(A0, A1, o_wsA, lane, s0, o_fb, L, W);
+            const int f0 = pen ? o_nnc : 0;
+            row_finish(L, pos_mask(0, f0, o_fb, 0ull), pos_mask(1, f0, o_fb, 0ull), lane, res);
+            /* friction and rolling rows: bounds +-mu * (their normal's impulse, final for this sweep),
+             * skipped while it is not positive.  A skipped row is made neutral instead of branched over:
+             * rhs = 1/D = 0 and infinite increment bounds give a delta of exactly +-0, and w + a * (+-0)
+             * == w (w is never -0: it starts at +0 and an fma only yields -0 from -0). */
+            if (!pen && o_fb < o_n) {
+                sh.u.impx[lane] = L.imp[0];
+                sh.u.impx[64 + lane] = L.imp[1];
+                __builtin_amdgcn_wave_barrier();
+                unsigned long long sk[2];
+                Lrow F = L;
+#pragma unroll
+                for (int s = 0; s < 2; s++) {
+                    const int p = lane + 64 * s;
+                    const bool isf = p >= o_fb && p < o_n;
+                    double tot = sh.u.impx[isf ? nrow[s] : 0];
+                    const bool skip = isf && !(tot > 0.0);
+                    L.lo[s] = isf ? -(fric[s] * tot) : L.lo[s];
+                    L.hi[s] = isf ? fric[s] * tot : L.hi[s];
+                    L.dlo[s] = L.lo[s] - L.imp[s];
+                    L.dhi[s] = L.hi[s] - L.imp[s];
+                    sk[s] = ballot(skip);
+                    F.dlo[s] = skip ? -__builtin_inf() : L.dlo[s];
+                    F.dhi[s] = skip ? __builtin_inf() : L.dhi[s];
+                    F.rhs[s] = skip ? 0.0 : L.rhs[s];
+                    F.invD[s] = skip ? 0.0 : L.invD[s];
+                }
+                __builtin_amdgcn_wave_barrier();
+                sweep_fwd<0, false>(A0, A1, o_wsA, lane, o_fb, o_n, F, W);
+#pragma unroll
+                for (int s = 0; s < 2; s++) L.dsv[s] = F.dsv[s];
+                row_finish(L, pos_mask(0, o_fb, o_n, sk[0]), pos_mask(1, o_fb, o_n, sk[1]), lane, res);
+            }
+            PROF_CNT(PC_ITERS, 1);
+            if (ballot(!(res <= UG_RESIDUAL_THR)) == 0ull || it >= UG_PGS_ITERS - 1) break;
+        }
+        if (!pen) {
+#pragma unroll
+            for (int s = 0; s < 2; s++)
+                if (lane + 64 * s < n) sh.rs[lane + 64 * s].imp = L.imp[s];
+#ifdef UG_DEBUG_DUMP
+            dbg[MAXROWS * MAXROWS + 128 + lane] = W[0];
+            dbg[MAXROWS * MAXROWS + 192 + lane] = W[1];
+            dbg[MAXROWS * MAXROWS + 256 + lane] = L.imp[0];
+            dbg[MAXROWS * MAXROWS + 320 + lane] = L.imp[1];
+#endif
         }
     }
+    /* dv[d] (dvs[d]) = fma chain over positions k of M^-1J_k[d] * impulse_k (lane d < NV) */
+    __builtin_amdgcn_wave_barrier();
+    if (split) {
+        sh.u.impx[lane] = L.imp[0];
+        sh.u.impx[64 + lane] = L.imp[1];
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int d = lane < NV ? lane : 0;
+    double acc = 0.0, accs = 0.0;
+    for (int k = 0; k < n; k++) acc = __builtin_fma(rows[k * 48 + 24 + d], sh.rs[k].imp, acc);
+    if (split)
+        for (int k = nnc; k < fb; k++) accs = __builtin_fma(rows[k * 48 + 24 + d], sh.u.impx[k], accs);
+    dv = lane < NV ? acc : 0.0;
+    dvs = lane < NV ? accs : 0.0;
+    __builtin_amdgcn_wave_barrier();
     return split;
 }
 
@@ -1079,9 +1223,7 @@ __device__ __forceinline__ static int team_pgs(const double* ws, int n, int nnc,
 __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) {
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
-    const int h = lane >> 5, d = lane & 31;
     EnvState& e = sh.e;
-    const double dt = UG_DT;
     PROF_T0(t_col);
     serial_fk();
     __syncthreads();
@@ -1093,23 +1235,18 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     PROF_ADD(PF_DYN, t_dyn);
     PROF_T0(t_rows);
     const int n = uniform(sh.nrows), nnc = uniform(sh.nnc), nn = uniform(sh.nn);
-    const int fb = nnc + nn;
     PROF_CNT(PC_SUBSTEPS, 1);
     PROF_CNT(PC_ROWS, n);
     PROF_CNT(PC_OVL, sh.nov);
     PROF_CNT(PC_NMAN, (int)e.nman);
-    /* rows: built lane-per-row in batches, then moved into the register slots of their half */
+    /* rows: built lane-per-row into the workspace (J | M^-1 J^T) and LDS (scalars) */
     for (int p = lane; p < n; p += TEAM) build_row(s, p, ws + WS_ROWS + p * 48);
     __threadfence_block();
     __syncthreads();
-    double RJ[NSLOT], RM[NSLOT];
-#pragma unroll
-    for (int sl = 0; sl < NSLOT; sl++) { RJ[sl] = 0.0; RM[sl] = 0.0; }
-    load_slots<0>(ws, RJ, RM, n, d);
     PROF_ADD(PF_ROWS, t_rows);
     PROF_T0(t_pgs);
     double dv, dvs;
-    int split = team_pgs(ws, n, nnc, nn, d, RJ, RM, dv, dvs);
+    int split = team_pgs(ws, n, nnc, nn, dv, dvs);
     PROF_ADD(PF_PGS, t_pgs);
     PROF_T0(t_split);
     PROF_ADD(PF_SPLIT, t_split);
