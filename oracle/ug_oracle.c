@@ -1566,34 +1566,35 @@ static void build_rows(ugo_env* e, const kin* k, const double* LDL, const double
 
 /* ---- projected Gauss-Seidel in row space ----
  * Bullet's btMultiBodyConstraintSolver keeps the solver's velocity delta dv and evaluates each row as
- * J_r . dv.  The same iteration is written here in row space: w = J dv is kept instead of dv, so a row
- * update reads w_r and adds column r of the Delassus matrix A = J M^-1 J^T times the impulse change to w.
- * Mathematically this is the identical sequence of Gauss-Seidel updates (same row order, same clamps,
- * same residual); only the floating-point summation differs, and it is *defined* here so that the HIP
- * kernel (one lane per row) reproduces it bit for bit:
- *   A[i][j] = fma chain over slots d = 0..NV-1 of J_i[d] * MiJ_j[d]   (rows in solve position order)
- *   w_i     = fma(A[i][r], delta_r, w_i) after each update of row r
- *   dv[d]   = fma chain over positions k = 0..n-1 of MiJ_k[d] * impulse_k   (after the iterations)
+ * delta_r = rhs_r - (J_r . dv) / D_r.  The same iteration is written here in row space: the unclamped
+ * increment u_r = rhs_r - (J_r . dv) / D_r of every row is kept instead of dv, so a row update reads u_r
+ * and adds column r of the scaled Delassus matrix NB[i][j] = -(J_i M^-1 J_j^T) / D_i times the impulse
+ * change to u.  Mathematically this is the identical sequence of Gauss-Seidel updates (same row order,
+ * same clamps, same residual); only the floating-point rounding differs, and it is *defined* here so that
+ * the HIP kernel (one lane per row) reproduces it bit for bit:
+ *   NB[i][j] = -((fma chain over slots d = 0..NV-1 of J_i[d] * MiJ_j[d]) * invD_i)  (solve positions)
+ *   u_i      = rhs_i, then u_i = fma(NB[i][r], delta_r, u_i) after each update of row r
+ *   dv[d]    = fma chain over positions k = 0..n-1 of MiJ_k[d] * impulse_k   (after the iterations)
  * Solve positions: non-contact rows [0, nnc), normals [nnc, fb), frictions, then rolling-friction rows. */
-static __thread double g_A[MAXROWS][MAXROWS];
+static __thread double g_A[MAXROWS][MAXROWS]; /* NB */
 static double rdot(const double* J, const double* MiJ) {
     double s = 0.0;
     for (int d = 0; d < NV; d++) s = fma(J[d], MiJ[d], s);
     return s;
 }
-/* resolveSingleConstraintRowGeneric [ext] (cfm = 0) for the row at position p, written in its
- * FMA-contracted, clamp-the-increment form: delta = clamp(rhs - w_p / D, lo - imp, hi - imp),
- * imp += delta.  (Bullet clamps imp + delta against [lo, hi] and assigns the bound; the two agree up to
- * the rounding of imp + (bound - imp), i.e. at most one ulp on a clamped impulse.) */
-static double solve_row_w(row* r, int p, int n, double* w, int pen) {
+/* resolveSingleConstraintRowGeneric [ext] (cfm = 0) for the row at position p, in its clamp-the-increment
+ * form: delta = clamp(u_p, lo - imp, hi - imp), imp += delta.  (Bullet clamps imp + delta against
+ * [lo, hi] and assigns the bound; the two agree up to the rounding of imp + (bound - imp), i.e. at most
+ * one ulp on a clamped impulse.) */
+static double solve_row_u(row* r, int p, int n, double* u, int pen) {
     double imp = pen ? r->impPen : r->imp;
-    double di = fma(-w[p], r->invD, pen ? r->rhsPen : r->rhs);
     double dlo = r->lo - imp, dhi = r->hi - imp;
+    double di = u[p];
     di = di < dlo ? dlo : di; /* v_max_f64 */
     di = di > dhi ? dhi : di; /* v_min_f64 */
     imp = imp + di;
     if (pen) r->impPen = imp; else r->imp = imp;
-    for (int q = 0; q < n; q++) w[q] = fma(g_A[q][p], di, w[q]);
+    for (int q = 0; q < n; q++) u[q] = fma(g_A[q][p], di, u[q]);
     double rinv = r->invD == 0.0 ? 0.0 : 1.0 / r->invD;
     return di * rinv;
 }
@@ -1618,9 +1619,9 @@ static int pgs(rowset* rs, double* dv, double* dvs) {
     const int nnc = rs->nnc, fb = rs->nnc + rs->nn;
     g_dbg[0] = n; g_dbg[1] = nnc; g_dbg[2] = rs->nn; g_dbg[3] = rs->nf; g_dbg[4] = rs->nr; g_dbg[5] = 0; g_dbg[6] = 0;
     for (int i = 0; i < n; i++)
-        for (int j = 0; j < n; j++) g_A[i][j] = rdot(R[i]->J, R[j]->MiJ);
-    double w[MAXROWS];
-    for (int q = 0; q < n; q++) w[q] = 0.0;
+        for (int j = 0; j < n; j++) g_A[i][j] = -(rdot(R[i]->J, R[j]->MiJ) * R[i]->invD);
+    double w[MAXROWS]; /* u */
+    for (int q = 0; q < n; q++) w[q] = R[q]->rhs;
     /* warm start (normal rows only; Bullet warm-starts friction with 0) */
     for (int p = nnc; p < fb; p++) {
         double imp = R[p]->imp;
@@ -1633,12 +1634,12 @@ static int pgs(rowset* rs, double* dv, double* dvs) {
         /* non-contact rows: alternate direction (reverse on even sweeps) */
         for (int j = 0; j < nnc; j++) {
             int p = (it & 1) ? j : nnc - 1 - j;
-            double x = solve_row_w(R[p], p, n, w, 0);
+            double x = solve_row_u(R[p], p, n, w, 0);
             x = x * x;
             res = res > x ? res : x;
         }
         for (int p = nnc; p < fb; p++) {
-            double x = solve_row_w(R[p], p, n, w, 0);
+            double x = solve_row_u(R[p], p, n, w, 0);
             x = x * x;
             res = res > x ? res : x;
         }
@@ -1649,7 +1650,7 @@ static int pgs(rowset* rs, double* dv, double* dvs) {
             if (tot > 0.0) {
                 f->lo = -(f->fric * tot);
                 f->hi = f->fric * tot;
-                double x = solve_row_w(f, p, n, w, 0);
+                double x = solve_row_u(f, p, n, w, 0);
                 x = x * x;
                 res = res > x ? res : x;
             }
@@ -1668,11 +1669,11 @@ static int pgs(rowset* rs, double* dv, double* dvs) {
     for (int p = nnc; p < fb; p++)
         if (R[p]->rhsPen != 0.0) any = 1;
     if (!any) return 0;
-    for (int q = 0; q < n; q++) w[q] = 0.0;
+    for (int q = 0; q < n; q++) w[q] = R[q]->rhsPen;
     for (int it = 0; it < UG_PGS_ITERS; it++) {
         double res = 0.0;
         for (int p = nnc; p < fb; p++) {
-            double x = solve_row_w(R[p], p, n, w, 1);
+            double x = solve_row_u(R[p], p, n, w, 1);
             x = x * x;
             res = res > x ? res : x;
         }

@@ -112,7 +112,7 @@ __device__ unsigned long long g_prof[16];
 #define PROF_CNT(k, x)
 #endif
 enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_TOTAL,
-       PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN };
+       PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN, PF_SWEEPS };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -797,13 +797,13 @@ __device__ __noinline__ static void build_row(const Scene* s, int pos, double* w
 }
 
 /* ---------------- PGS (btMultiBodyConstraintSolver), row space ----------------
- * The solver keeps w = J dv (one entry per row) instead of dv: lane l owns the rows at positions l and
- * l + 64 (slot 0 / slot 1) -- their scalars, their impulse and their w -- and holds its rows of the
- * Delassus matrix A = J M^-1 J^T in VGPRs (A0[P] / A1[P] = A[l][P], A[l+64][P]).  Updating row P is
- * lane-parallel arithmetic on every lane's own row (only lane P's result is used), one broadcast of the
- * impulse change (two v_readlane) and one fma per slot: w += A[:, P] * delta.  No cross-lane reduction
- * and no LDS traffic inside a sweep.  The owner lane only records the w it saw; its new impulse and
- * residual are recomputed from that w after the section (same operations, so the same bits).  Row
+ * The solver keeps u = rhs - (J dv) / D (each row's unclamped increment, one entry per row) instead of
+ * dv: lane l owns the rows at positions l and l + 64 (slot 0 / slot 1) -- their scalars, their impulse and
+ * their u -- and holds its rows of the scaled Delassus matrix NB = -diag(1/D) J M^-1 J^T in VGPRs
+ * (A0[P] / A1[P] = NB[l][P], NB[l+64][P]).  Updating row P is lane-parallel arithmetic on every lane's
+ * own row (only lane P's result is used), one broadcast of the impulse change (two v_readlane) and one
+ * fma per slot: u += NB[:, P] * delta.  No cross-lane reduction and no LDS traffic inside a sweep.  The
+ * owner lane records the increment; its impulse and residual are advanced after the section.  Row
  * positions are template parameters, so A0[P] / A1[P] are compile-time register names and every
  * row-range test is a scalar branch.  Columns P >= PREG come from the global workspace.  Arithmetic
  * order is the oracle's pgs() (oracle/ug_oracle.c). */
@@ -845,19 +845,19 @@ __device__ __forceinline__ double writelane_d(double old, double x) {
 }
 /* resolveSingleConstraintRowGeneric [ext] (oracle solve_row_w) for the row at position P: every lane
  * forms the clamped increment of its own row, lane (P & 63)'s is broadcast, applied to w and recorded in
- * that lane (the impulse itself is advanced after the section).  Chain: fma, max, min, readlane, fma. */
+ * that lane (the impulse itself is advanced after the section).  W holds each row's unclamped increment
+ * u = rhs - (J dv) / D and A0 / A1 the negated, 1/D-scaled Delassus rows.  Chain: max, min, readlane, fma. */
 template <int P>
 __device__ __forceinline__ void row_upd(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA, int lane,
                                         Lrow& L, double (&W)[2]) {
     constexpr int s = P >> 6, O = P & 63;
     double a0, a1;
     colA<P>(A0, A1, wsA, lane, a0, a1);
-    double di = __builtin_fma(-W[s], L.invD[s], L.rhs[s]);
-    double dn = __builtin_fmin(__builtin_fmax(di, L.dlo[s]), L.dhi[s]);
+    double dn = __builtin_fmin(__builtin_fmax(W[s], L.dlo[s]), L.dhi[s]);
     double d = readlane_d(dn, O);
-    L.dsv[s] = writelane_d<O>(L.dsv[s], d);
     W[0] = __builtin_fma(a0, d, W[0]);
     W[1] = __builtin_fma(a1, d, W[1]);
+    L.dsv[s] = writelane_d<O>(L.dsv[s], d);
 }
 /* after a section: the lanes whose row was solved advance their impulse by the recorded increment and
  * fold (delta / D)^2 into their residual */
@@ -884,26 +884,47 @@ __device__ __forceinline__ unsigned long long pos_mask(int s, int a, int b, unsi
     unsigned long long m = (l1 - l0 == 64) ? ~0ull : (((1ull << (l1 - l0)) - 1ull) << l0);
     return m & ~skip;
 }
-/* rows [start, end) in increasing position.  LOWSTART: start is 0 or nnc <= NCMAX, so rows from NCMAX on
- * need no start test (the contact section); otherwise every row is tested (the friction section) */
-template <int P, bool LOWSTART>
-__device__ __forceinline__ void sweep_fwd(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA,
-                                          int lane, int start, int end, Lrow& L, double (&W)[2]) {
-    if constexpr (P < MAXROWS) {
-        if (P < end) {
-            if ((LOWSTART && P >= NCMAX) || P >= start) row_upd<P>(A0, A1, wsA, lane, L, W);
-            sweep_fwd<P + 1, LOWSTART>(A0, A1, wsA, lane, start, end, L, W);
-        }
+/* one 8-row chunk, rows in increasing (REV: decreasing) position, no per-row tests */
+template <int C, bool REV, int K>
+__device__ __forceinline__ void chunk_rows(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA, int lane,
+                                           Lrow& L, double (&W)[2]) {
+    if constexpr (K < 8) {
+        row_upd<REV ? 8 * C + 7 - K : 8 * C + K>(A0, A1, wsA, lane, L, W);
+        chunk_rows<C, REV, K + 1>(A0, A1, wsA, lane, L, W);
     }
 }
-/* non-contact rows [0, nnc) in decreasing position (even sweeps); nnc <= NCMAX < 64 */
-template <int P>
-__device__ __forceinline__ void sweep_rev(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA,
-                                          int lane, int nnc, Lrow& L, double (&W)[2]) {
-    if constexpr (P >= 0) {
-        if (P < nnc) row_upd<P>(A0, A1, wsA, lane, L, W);
-        sweep_rev<P - 1>(A0, A1, wsA, lane, nnc, L, W);
+/* the chunks [c_lo, c_hi] of a section, in increasing (REV: decreasing) order.  Rows of those chunks
+ * outside the section are neutral: the caller zeroes their increment bounds, so they broadcast +-0 and
+ * leave u unchanged.  One scalar test per chunk instead of per row. */
+template <int I, bool REV, int NCH>
+__device__ __forceinline__ void sweep_chunks(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA,
+                                             int lane, int c_lo, int c_hi, Lrow& L, double (&W)[2]) {
+    if constexpr (I < NCH) {
+        constexpr int C = REV ? NCH - 1 - I : I;
+        if (C >= c_lo && C <= c_hi) chunk_rows<C, REV, 0>(A0, A1, wsA, lane, L, W);
+        sweep_chunks<I + 1, REV, NCH>(A0, A1, wsA, lane, c_lo, c_hi, L, W);
     }
+}
+/* the section [a, b) (a < b): a copy of the lane rows with zero increment bounds outside it (and on the
+ * rows set in skip), swept chunk-wise; the recorded increments come back in L.dsv */
+template <bool REV, int NCH>
+__device__ __forceinline__ void sweep_section(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA,
+                                              int lane, int a, int b, unsigned long long sk0, unsigned long long sk1,
+                                              Lrow& L, double (&W)[2]) {
+    Lrow F = L;
+    bool in[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        const int p = lane + 64 * s;
+        const bool skip = (((s ? sk1 : sk0) >> lane) & 1ull) != 0ull;
+        in[s] = p >= a && p < b && !skip;
+        F.dlo[s] = in[s] ? L.dlo[s] : 0.0;
+        F.dhi[s] = in[s] ? L.dhi[s] : 0.0;
+    }
+    sweep_chunks<0, REV, NCH>(A0, A1, wsA, lane, a >> 3, (b - 1) >> 3, F, W);
+    /* only the section's own records: a neutral row's record would clobber one still to be finished */
+#pragma unroll
+    for (int s = 0; s < 2; s++) L.dsv[s] = in[s] ? F.dsv[s] : L.dsv[s];
 }
 /* warm start: normal rows [nnc, fb) with a carried impulse, w += A[:, P] * impulse */
 template <int P>
@@ -934,12 +955,12 @@ __device__ __forceinline__ void stage_mj(gcdouble* rows, int c0, int n, int lane
     }
     __builtin_amdgcn_wave_barrier();
 }
-/* Delassus row of this lane's slot: A[r][j] = fma chain over d of J_r[d] * M^-1J_j[d], j = 0..n-1 */
+/* scaled Delassus row of this lane's slot: NB[r][j] = -((fma chain over d of J_r[d] * M^-1J_j[d]) / D_r) */
 template <int J, int S>
-__device__ __forceinline__ void build_A(gcdouble* rows, const double (&Jr)[NV], double (&A)[PREG], gdouble* wsA,
-                                        int n, int lane) {
+__device__ __forceinline__ void build_A(gcdouble* rows, const double (&Jr)[NV], double invDr, double (&A)[PREG],
+                                        gdouble* wsA, int n, int lane) {
     if constexpr (J < MAXROWS) {
-        if (J < n) {
+        if (J < ((n + 7) & ~7)) { /* through the end of the last 8-row chunk: zero columns beyond n */
             if constexpr (J % MJCHUNK == 0) stage_mj(rows, J, n, lane);
             const double* mj = &g_sh.u.stage[0][0] + (J % MJCHUNK) * 24; /* same address on every lane */
             /* a compiler barrier per column: otherwise the scheduler hoists every column's LDS reads and
@@ -948,10 +969,11 @@ __device__ __forceinline__ void build_A(gcdouble* rows, const double (&Jr)[NV], 
             double a = 0.0;
 #pragma unroll
             for (int d = 0; d < NV; d++) a = __builtin_fma(Jr[d], mj[d], a);
+            a = -(a * invDr);
             asm volatile("" : "+v"(a)); /* materialise the entry here (no sinking into its uses) */
             if constexpr (J < PREG) A[J] = a;
             else wsA[(J - PREG) * MAXROWS + 64 * S + lane] = a;
-            build_A<J + 1, S>(rows, Jr, A, wsA, n, lane);
+            build_A<J + 1, S>(rows, Jr, invDr, A, wsA, n, lane);
         }
     }
 }
@@ -1063,6 +1085,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     const int n = uniform(n_), nnc = uniform(nnc_), nn = uniform(nn_);
     double* ws = uniform_ptr(ws_);
     const int fb = nnc + nn;
+    PROF_T0(t_setup);
     gcdouble* rows = (gcdouble*)(ws + WS_ROWS);
     gdouble* wsA = (gdouble*)(ws + WS_A);
     double A0[PREG], A1[PREG];
@@ -1072,7 +1095,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         const int r = lane + 64 < n ? lane + 64 : 0;
 #pragma unroll
         for (int d = 0; d < NV; d++) Jr[d] = lane + 64 < n ? rows[r * 48 + d] : 0.0;
-        build_A<0, 1>(rows, Jr, A1, wsA, n, lane);
+        build_A<0, 1>(rows, Jr, lane + 64 < n ? sh.rs[r].invD : 0.0, A1, wsA, n, lane);
     } else {
 #pragma unroll
         for (int j = 0; j < PREG; j++) A1[j] = 0.0;
@@ -1082,7 +1105,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         const int r = lane < n ? lane : 0;
 #pragma unroll
         for (int d = 0; d < NV; d++) Jr[d] = lane < n ? rows[r * 48 + d] : 0.0;
-        build_A<0, 0>(rows, Jr, A0, wsA, n, lane);
+        build_A<0, 0>(rows, Jr, lane < n ? sh.rs[r].invD : 0.0, A0, wsA, n, lane);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -1106,8 +1129,10 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         nrow[s] = in ? r.nrow : 0;
         rhsPen[s] = in ? r.rhsPen : 0.0;
     }
-    double W[2] = {0.0, 0.0};
+    double W[2] = {L.rhs[0], L.rhs[1]}; /* u */
     sweep_warm<0>(A0, A1, wsAr, lane, nnc, fb, L, W);
+    PROF_ADD(PF_SPLIT, t_setup);
+    PROF_T0(t_sweeps);
 #ifdef UG_DEBUG_DUMP
     double* dbg = ws + WS_DBG;
     dump_A<0>(A0, A1, dbg, n, lane);
@@ -1133,8 +1158,8 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                 L.rhs[s] = rhsPen[s];
                 L.imp[s] = 0.0;
             }
-            W[0] = 0.0;
-            W[1] = 0.0;
+            W[0] = L.rhs[0];
+            W[1] = L.rhs[1];
         }
 #pragma unroll
         for (int s = 0; s < 2; s++) {
@@ -1143,27 +1168,26 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         }
         for (int it = 0; it < UG_PGS_ITERS; it++) {
             double res = 0.0;
-            /* opaque per-sweep copies: keeps the per-row scalar tests inside the loop instead of
-             * hoisting ~128 of them into (spilled) SGPRs */
+            /* opaque per-sweep copies: keeps the per-chunk scalar tests inside the loop */
             int o_n = n, o_nnc = nnc, o_fb = fb;
             gcdouble* o_wsA = wsAr;
             asm volatile("" : "+s"(o_n), "+s"(o_nnc), "+s"(o_fb), "+s"(o_wsA));
             /* (even sweeps) non-contact rows reversed, then [s0, fb) */
-            if (!pen && !(it & 1) && o_nnc > 0) sweep_rev<NCMAX - 1>(A0, A1, o_wsA, lane, o_nnc, L, W);
+            if (!pen && !(it & 1) && o_nnc > 0)
+                sweep_section<true, (NCMAX + 7) / 8>(A0, A1, o_wsA, lane, 0, o_nnc, 0ull, 0ull, L, W);
             const int s0 = (pen || !(it & 1)) ? o_nnc : 0;
-            if (s0 < o_fb) sweep_fwd<0, true>(A0, A1, o_wsA, lane, s0, o_fb, L, W);
+            if (s0 < o_fb) sweep_section<false, MAXROWS / 8>(A0, A1, o_wsA, lane, s0, o_fb, 0ull, 0ull, L, W);
             const int f0 = pen ? o_nnc : 0;
             row_finish(L, pos_mask(0, f0, o_fb, 0ull), pos_mask(1, f0, o_fb, 0ull), lane, res);
             /* friction and rolling rows: bounds +-mu * (their normal's impulse, final for this sweep),
-             * skipped while it is not positive.  A skipped row is made neutral instead of branched over:
-             * rhs = 1/D = 0 and infinite increment bounds give a delta of exactly +-0, and w + a * (+-0)
-             * == w (w is never -0: it starts at +0 and an fma only yields -0 from -0). */
+             * skipped while it is not positive.  A skipped row is made neutral (sweep_section):
+             * increment bounds [0, 0] give a delta of +-0, and u + a * (+-0) == u up to the sign of a
+             * zero u (which never reaches a non-zero result). */
             if (!pen && o_fb < o_n) {
                 sh.u.impx[lane] = L.imp[0];
                 sh.u.impx[64 + lane] = L.imp[1];
                 __builtin_amdgcn_wave_barrier();
                 unsigned long long sk[2];
-                Lrow F = L;
 #pragma unroll
                 for (int s = 0; s < 2; s++) {
                     const int p = lane + 64 * s;
@@ -1175,21 +1199,16 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                     L.dlo[s] = L.lo[s] - L.imp[s];
                     L.dhi[s] = L.hi[s] - L.imp[s];
                     sk[s] = ballot(skip);
-                    F.dlo[s] = skip ? -__builtin_inf() : L.dlo[s];
-                    F.dhi[s] = skip ? __builtin_inf() : L.dhi[s];
-                    F.rhs[s] = skip ? 0.0 : L.rhs[s];
-                    F.invD[s] = skip ? 0.0 : L.invD[s];
                 }
                 __builtin_amdgcn_wave_barrier();
-                sweep_fwd<0, false>(A0, A1, o_wsA, lane, o_fb, o_n, F, W);
-#pragma unroll
-                for (int s = 0; s < 2; s++) L.dsv[s] = F.dsv[s];
+                sweep_section<false, MAXROWS / 8>(A0, A1, o_wsA, lane, o_fb, o_n, sk[0], sk[1], L, W);
                 row_finish(L, pos_mask(0, o_fb, o_n, sk[0]), pos_mask(1, o_fb, o_n, sk[1]), lane, res);
             }
             PROF_CNT(PC_ITERS, 1);
             if (ballot(!(res <= UG_RESIDUAL_THR)) == 0ull || it >= UG_PGS_ITERS - 1) break;
         }
         if (!pen) {
+            PROF_ADD(PF_SWEEPS, t_sweeps);
 #pragma unroll
             for (int s = 0; s < 2; s++)
                 if (lane + 64 * s < n) sh.rs[lane + 64 * s].imp = L.imp[s];
@@ -1248,8 +1267,6 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     double dv, dvs;
     int split = team_pgs(ws, n, nnc, nn, dv, dvs);
     PROF_ADD(PF_PGS, t_pgs);
-    PROF_T0(t_split);
-    PROF_ADD(PF_SPLIT, t_split);
     PROF_T0(t_int);
     if (lane < NVP) { sh.dvout[lane] = dv; sh.dvsout[lane] = dvs; }
     /* impulses back into the manifold points (lane per row) */
