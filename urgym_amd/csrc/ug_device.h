@@ -288,13 +288,21 @@ DFI SV spatial_inertia_mul(double m, v3 h, const m3& J, SV x) {
     r.v = vsub(vscale(x.v, m), vcross(h, x.w));
     return r;
 }
-DF void robot_dynamics(const double* qd, const Kin& k, double g, double* M, double* C) {
-    double m[NB];
-    v3 h[NB];
-    m3 J[NB];
-    double cm[NB];
-    v3 ch[NB];
-    m3 cJ[NB];
+/* work arrays of robot_dynamics: the team kernels place them in LDS (a private array would live in
+ * scratch, whose latency the serial recursions pay at every access) */
+struct DynWork {
+    double m[NB], cm[NB];
+    v3 h[NB], ch[NB];
+    m3 J[NB], cJ[NB];
+    SV S[NB], Vb[NB], Ab[NB], f[NB];
+};
+DF void robot_dynamics(const double* qd, const Kin& k, double g, double* M, double* C, DynWork& w) {
+    double* m = w.m;
+    v3* h = w.h;
+    m3* J = w.J;
+    double* cm = w.cm;
+    v3* ch = w.ch;
+    m3* cJ = w.cJ;
     for (int b = 0; b < NB; b++) {
         m[b] = UG_BODY_MASS[b];
         v3 c = k.c[b];
@@ -315,7 +323,7 @@ DF void robot_dynamics(const double* qd, const Kin& k, double g, double* M, doub
         ch[p] = vadd(ch[p], ch[b]);
         for (int i = 0; i < 9; i++) cJ[p].m[i] += cJ[b].m[i];
     }
-    SV S[NB];
+    SV* S = w.S;
     for (int b = 0; b < NB; b++) { S[b].w = k.a[b]; S[b].v = vcross(k.p[b], k.a[b]); }
     for (int i = 0; i < NB * NB; i++) M[i] = 0.0;
     for (int b = 0; b < NB; b++) {
@@ -329,7 +337,7 @@ DF void robot_dynamics(const double* qd, const Kin& k, double g, double* M, doub
             j = UG_BODY_PARENT[j];
         }
     }
-    SV Vb[NB], Ab[NB], f[NB];
+    SV *Vb = w.Vb, *Ab = w.Ab, *f = w.f;
     for (int b = 0; b < NB; b++) {
         int p = UG_BODY_PARENT[b];
         SV Vp, Ap;

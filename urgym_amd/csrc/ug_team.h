@@ -81,6 +81,7 @@ struct Shared {
         double stage[STAGE][48];
         struct { Cand c[MAXOV][4]; int n[MAXOV]; } cand;
         double impx[MAXROWS]; /* PGS: row impulses gathered through LDS (after the Delassus build) */
+        DynWork dyn;          /* serial_pre: robot_dynamics work arrays */
     } u;
     Cand hc[64];
     double a12[NB];
@@ -112,7 +113,7 @@ __device__ unsigned long long g_prof[16];
 #define PROF_CNT(k, x)
 #endif
 enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_TOTAL,
-       PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN, PF_SWEEPS };
+       PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN, PF_SWEEPS, PF_HULL };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -266,6 +267,7 @@ __device__ __noinline__ static void team_hull_box(const Collider& A, const Colli
     v3 y = vadd(mv(RBA, cl), pBA);
     double smax = -1e300;
     int fm = 0x7fffffff;
+#pragma unroll 4 /* plane loads in flight together (the loop is load-latency bound otherwise) */
     for (int f = j; f < A.nf; f += 8) {
         const double* F = &UG_HULL_F[4 * (A.f0 + f)];
         double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
@@ -318,6 +320,7 @@ __device__ __noinline__ static void team_hull_hull(const Collider& A, const Coll
         v3 x = vadd(mv(RAB, V(vv[0], vv[1], vv[2])), pAB);
         double smax = -1e300;
         int fm = -1;
+#pragma unroll 8
         for (int f = 0; f < B.nf; f++) {
             const double* F = &UG_HULL_F[4 * (B.f0 + f)];
             double sd = F[0] * x.x + F[1] * x.y + F[2] * x.z - F[3];
@@ -342,6 +345,7 @@ __device__ __noinline__ static void team_hull_hull(const Collider& A, const Coll
         v3 y = vadd(mv(RBA, yl), pBA);
         double smax = -1e300;
         int fm = -1;
+#pragma unroll 8
         for (int f = 0; f < A.nf; f++) {
             const double* F = &UG_HULL_F[4 * (A.f0 + f)];
             double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
@@ -447,6 +451,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
     for (int c0 = 0; c0 < nov; c0 += MAXOV) {
         int cn = nov - c0 < MAXOV ? nov - c0 : MAXOV;
         /* hull-box pairs of this chunk: cooperative narrowphase */
+        PROF_T0(t_hull);
         for (int k = 0; k < cn; k++) {
             const PairDef& P = s->pair[sh.ov[c0 + k]];
             const Collider& A = s->col[P.a];
@@ -461,6 +466,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
                 PROF_CNT(PC_HULL, 1);
             }
         }
+        PROF_ADD(PF_HULL, t_hull);
         /* lane per pair: remaining narrowphases, manifold update */
         Manifold M;
         M.npts = 0;
@@ -666,28 +672,125 @@ __device__ static void enumerate_rows(Shared& sh, const Scene* s) {
     n = nnc + nn + nf + 2 * nroll;
     sh.nrows = n; sh.nnc = nnc; sh.nn = nn; sh.nf = nf;
 }
-/* build row at position pos (one lane): J, M^-1 J^T into stage row sl, scalars into rs[pos] */
+/* ---- register-resident row build: every array index below is a compile-time constant (fully unrolled
+ * loops, selects instead of dynamic stores), so the per-lane arrays stay in VGPRs instead of scratch.
+ * Same operations in the same order as the oracle's build_rows (contact_row / dof_row / point_jac). */
+/* ldlt() with compile-time indices */
+__device__ __forceinline__ void ldlt_r(double (&A)[NB * NB]) {
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+        double d = A[j * NB + j];
+#pragma unroll
+        for (int k2 = 0; k2 < j; k2++) d -= A[j * NB + k2] * A[j * NB + k2] * A[k2 * NB + k2];
+        A[j * NB + j] = d;
+#pragma unroll
+        for (int i = j + 1; i < NB; i++) {
+            double s = A[i * NB + j];
+#pragma unroll
+            for (int k2 = 0; k2 < j; k2++) s -= A[i * NB + k2] * A[j * NB + k2] * A[k2 * NB + k2];
+            A[i * NB + j] = s / d;
+        }
+    }
+}
+template <typename M>
+__device__ __forceinline__ void ldlt_solve_r(const M& A, double (&x)[NB]) {
+#pragma unroll
+    for (int i = 0; i < NB; i++)
+#pragma unroll
+        for (int k2 = 0; k2 < i; k2++) x[i] -= A[i * NB + k2] * x[k2];
+#pragma unroll
+    for (int i = 0; i < NB; i++) x[i] = x[i] / A[i * NB + i];
+#pragma unroll
+    for (int i = NB - 1; i >= 0; i--)
+#pragma unroll
+        for (int k2 = i + 1; k2 < NB; k2++) x[i] -= A[k2 * NB + i] * x[k2];
+}
+/* sum over the entity's dofs (12 robot / 6 object) of a[i] * b(i), in index order */
+__device__ __forceinline__ double ent_dot_r(int ent, const double (&a)[NB], const double (&b)[NB]) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < NB; i++)
+        if (i < 6 || ent == 0) s += a[i] * b[i];
+    return s;
+}
+__device__ __forceinline__ double ent_dot_v0(int ent, const double (&a)[NB], const double* v0) {
+    const int o = ent_off(ent);
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < NB; i++)
+        if (i < 6 || ent == 0) s += a[i] * v0[o + i];
+    return s;
+}
+/* dst[entity segment] = src[0 .. dofs) */
+__device__ __forceinline__ void put_seg_r(int ent, const double (&src)[NB], double (&dst)[NV]) {
+#pragma unroll
+    for (int i = 0; i < NB; i++) dst[i] = ent == 0 ? src[i] : dst[i];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        dst[NB + i] = ent == 1 ? src[i] : dst[NB + i];
+        dst[NB + 6 + i] = ent == 2 ? src[i] : dst[NB + 6 + i];
+    }
+}
+/* Jacobian of a point p on entity ent along d (ANG: angular component along d, rolling rows) and
+ * M^-1 J^T of it; for an object only [0, 6) is set */
+template <bool ANG>
+__device__ __forceinline__ void ent_jac_r(const Scene* sc, const EnvState& e, const Kin& k, int ent, int body, v3 p, v3 d,
+                                          double (&J)[NB], double (&MiJ)[NB], const double* LDL) {
+    if (ent == 0) {
+#pragma unroll
+        for (int i = 0; i < NB; i++) {
+            double x;
+            if (ANG) x = vdot(d, k.a[i]);
+            else x = vdot(d, vcross(k.a[i], vsub(p, k.p[i])));
+            J[i] = moves(i, body) ? x : 0.0;
+            MiJ[i] = J[i];
+        }
+        ldlt_solve_r(LDL, MiJ);
+    } else {
+        const int o = ent - 1;
+        m3 R = qmat(e.obj[o].quat);
+        if (ANG) {
+            J[0] = 0.0; J[1] = 0.0; J[2] = 0.0; J[3] = d.x; J[4] = d.y; J[5] = d.z;
+            v3 ir = mtv(R, d);
+            ir = V(ir.x / sc->oinertia[o].x, ir.y / sc->oinertia[o].y, ir.z / sc->oinertia[o].z);
+            ir = mv(R, ir);
+            MiJ[0] = 0.0; MiJ[1] = 0.0; MiJ[2] = 0.0; MiJ[3] = ir.x; MiJ[4] = ir.y; MiJ[5] = ir.z;
+        } else {
+            v3 r = vsub(p, e.obj[o].pos);
+            v3 rn = vcross(r, d);
+            J[0] = d.x; J[1] = d.y; J[2] = d.z; J[3] = rn.x; J[4] = rn.y; J[5] = rn.z;
+            double im = 1.0 / sc->omass[o];
+            v3 ir = mtv(R, rn);
+            ir = V(ir.x / sc->oinertia[o].x, ir.y / sc->oinertia[o].y, ir.z / sc->oinertia[o].z);
+            ir = mv(R, ir);
+            MiJ[0] = d.x * im; MiJ[1] = d.y * im; MiJ[2] = d.z * im; MiJ[3] = ir.x; MiJ[4] = ir.y; MiJ[5] = ir.z;
+        }
+#pragma unroll
+        for (int i = 6; i < NB; i++) { J[i] = 0.0; MiJ[i] = 0.0; }
+    }
+}
+/* build row at position pos (one lane): J | M^-1 J^T into the workspace row, scalars into rs[pos] */
 __device__ __noinline__ static void build_row(const Scene* s, int pos, double* wrow) {
     Shared& sh = g_sh;
     const EnvState& e = sh.e;
     const double dt = UG_DT;
     RowS& r = sh.rs[pos];
-    double J[NVP], MJ[NVP];
-    for (int i = 0; i < NVP; i++) { J[i] = 0.0; MJ[i] = 0.0; }
+    double J[NV], MJ[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) { J[i] = 0.0; MJ[i] = 0.0; }
     double invD = 0.0, rhs = 0.0, rhsPen = 0.0, lo = 0.0, hi = 0.0, imp = 0.0, fric = 0.0;
     if (r.kind <= 1) {
         int d = r.kind == 0 ? r.a : (r.a < 6 ? r.a : UG_FINGER_DOF);
         double sgn = (r.kind == 0 && r.b == 1) ? -1.0 : 1.0;
         double Jl[NB], Ml[NB];
-        for (int i = 0; i < NB; i++) Jl[i] = 0.0;
-        Jl[d] = sgn;
-        for (int i = 0; i < NB; i++) Ml[i] = Jl[i];
-        ldlt_solve(sh.LDL, NB, Ml);
-        double den = ent_dot_local(0, Jl, Ml);
+#pragma unroll
+        for (int i = 0; i < NB; i++) { Jl[i] = i == d ? sgn : 0.0; Ml[i] = Jl[i]; }
+        ldlt_solve_r(sh.LDL, Ml);
+        double den = ent_dot_r(0, Jl, Ml);
         invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
-        put_seg(0, Jl, J);
-        put_seg(0, Ml, MJ);
-        double relv = ent_dot(0, Jl, sh.v0);
+        put_seg_r(0, Jl, J);
+        put_seg_r(0, Ml, MJ);
+        double relv = ent_dot_v0(0, Jl, sh.v0);
         if (r.kind == 0) {
             double pen = r.b == 0 ? e.q[d] - UG_DOF_LOWER[d] : UG_DOF_UPPER[d] - e.q[d];
             double erp = (pen > UG_SPLIT_PEN_THR) ? UG_ERP : UG_ERP2;
@@ -709,19 +812,23 @@ __device__ __noinline__ static void build_row(const Scene* s, int pos, double* w
             lo = -maxImp; hi = maxImp;
         }
     } else if (r.kind == 2) {
-        int pa = UG_FINGER_DOF, cb = UG_GEAR_CHILD[r.a];
+        const int pa = UG_FINGER_DOF, cb = UG_GEAR_CHILD[r.a];
         double ratio = UG_GEAR_RATIO[r.a];
         double JA[NB], JB[NB], MA[NB], MB[NB];
-        for (int i = 0; i < NB; i++) { JA[i] = 0.0; JB[i] = 0.0; }
-        JA[pa] = 1.0;
-        JB[cb] = ratio;
-        for (int i = 0; i < NB; i++) { MA[i] = JA[i]; MB[i] = JB[i]; }
-        ldlt_solve(sh.LDL, NB, MA);
-        ldlt_solve(sh.LDL, NB, MB);
-        double den = ent_dot_local(0, JA, MA) + ent_dot_local(0, JB, MB);
+#pragma unroll
+        for (int i = 0; i < NB; i++) {
+            JA[i] = i == pa ? 1.0 : 0.0;
+            JB[i] = i == cb ? ratio : 0.0;
+            MA[i] = JA[i];
+            MB[i] = JB[i];
+        }
+        ldlt_solve_r(sh.LDL, MA);
+        ldlt_solve_r(sh.LDL, MB);
+        double den = ent_dot_r(0, JA, MA) + ent_dot_r(0, JB, MB);
         invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
+#pragma unroll
         for (int i = 0; i < NB; i++) { J[i] = JA[i] + JB[i]; MJ[i] = MA[i] + MB[i]; }
-        double relv = ent_dot(0, JA, sh.v0) + ent_dot(0, JB, sh.v0);
+        double relv = ent_dot_v0(0, JA, sh.v0) + ent_dot_v0(0, JB, sh.v0);
         double diff = e.q[cb] * ratio + e.q[pa];
         double pen = -UG_GEAR_ERP * (0.0 - diff);
         double perr = -pen * UG_ERP / dt, verr = 0.0 - relv;
@@ -756,20 +863,20 @@ __device__ __noinline__ static void build_row(const Scene* s, int pos, double* w
         double JA[NB], MA[NB], JB[NB], MB[NB];
         double dA = 0.0, dB = 0.0, relv = 0.0;
         if (entA >= 0) {
-            if (ang) ang_jac(s, e, sh.kin, entA, bodyA, d, JA, MA, sh.LDL);
-            else point_jac(s, e, sh.kin, entA, bodyA, pA, d, JA, MA, sh.LDL);
-            dA = ent_dot_local(entA, JA, MA);
-            relv += ent_dot(entA, JA, sh.v0);
-            put_seg(entA, JA, J);
-            put_seg(entA, MA, MJ);
+            if (ang) ent_jac_r<true>(s, e, sh.kin, entA, bodyA, pA, d, JA, MA, sh.LDL);
+            else ent_jac_r<false>(s, e, sh.kin, entA, bodyA, pA, d, JA, MA, sh.LDL);
+            dA = ent_dot_r(entA, JA, MA);
+            relv += ent_dot_v0(entA, JA, sh.v0);
+            put_seg_r(entA, JA, J);
+            put_seg_r(entA, MA, MJ);
         }
         if (entB >= 0) {
-            if (ang) ang_jac(s, e, sh.kin, entB, bodyB, vneg(d), JB, MB, sh.LDL);
-            else point_jac(s, e, sh.kin, entB, bodyB, pB, vneg(d), JB, MB, sh.LDL);
-            dB = ent_dot_local(entB, JB, MB);
-            relv += ent_dot(entB, JB, sh.v0);
-            put_seg(entB, JB, J);
-            put_seg(entB, MB, MJ);
+            if (ang) ent_jac_r<true>(s, e, sh.kin, entB, bodyB, pB, vneg(d), JB, MB, sh.LDL);
+            else ent_jac_r<false>(s, e, sh.kin, entB, bodyB, pB, vneg(d), JB, MB, sh.LDL);
+            dB = ent_dot_r(entB, JB, MB);
+            relv += ent_dot_v0(entB, JB, sh.v0);
+            put_seg_r(entB, JB, J);
+            put_seg_r(entB, MB, MJ);
         }
         double den = dA + dB;
         invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
@@ -793,7 +900,8 @@ __device__ __noinline__ static void build_row(const Scene* s, int pos, double* w
         }
     }
     r.invD = invD; r.rinv = invD == 0.0 ? 0.0 : 1.0 / invD; r.rhs = rhs; r.rhsPen = rhsPen; r.lo = lo; r.hi = hi; r.imp = imp; r.impPen = 0.0; r.fric = fric;
-    for (int i = 0; i < 24; i++) { wrow[i] = J[i]; wrow[24 + i] = MJ[i]; }
+#pragma unroll
+    for (int i = 0; i < NV; i++) { wrow[i] = J[i]; wrow[24 + i] = MJ[i]; }
 }
 
 /* ---------------- PGS (btMultiBodyConstraintSolver), row space ----------------
@@ -994,11 +1102,18 @@ __device__ __noinline__ static void serial_pre(const Scene* s) {
     const int lane = threadIdx.x;
     if (lane == 0) {
         double C[NB];
-        robot_dynamics(e.qd, sh.kin, s->gravity, sh.LDL, C);
-        ldlt(sh.LDL, NB);
+        robot_dynamics(e.qd, sh.kin, s->gravity, sh.LDL, C, sh.u.dyn);
+        /* LDL^T and the qdd solve with the matrix in registers (compile-time indices, same order) */
+        double A[NB * NB];
+#pragma unroll
+        for (int i = 0; i < NB * NB; i++) A[i] = sh.LDL[i];
+        ldlt_r(A);
+#pragma unroll
+        for (int i = 0; i < NB * NB; i++) sh.LDL[i] = A[i];
         double qdd[NB];
+#pragma unroll
         for (int i = 0; i < NB; i++) qdd[i] = -C[i];
-        ldlt_solve(sh.LDL, NB, qdd);
+        ldlt_solve_r(A, qdd);
         for (int i = 0; i < NVP; i++) sh.v0[i] = 0.0;
         for (int i = 0; i < NB; i++) { e.qd[i] = e.qd[i] + qdd[i] * dt; sh.v0[i] = e.qd[i]; }
         for (int o = 0; o < s->nobj; o++) {
