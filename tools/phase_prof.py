@@ -18,7 +18,8 @@ sys.path.insert(0, ROOT)
 os.environ.setdefault("URGYM_LIB", os.path.join(ROOT, "urgym_amd", "_lib", "liburgym_prof.so"))
 
 NAMES = ["collide", "dyn+enum", "rows", "pgs", "pgs_setup", "integrate", "glue", "total",
-         "substeps", "nrows", "pgs_iters", "overlap_pairs", "hull_pairs", "manifolds", "pgs_sweeps", "hull_narrowphase"]
+         "substeps", "nrows", "pgs_iters", "overlap_pairs", "hull_pairs", "manifolds", "pgs_sweeps", "hull_narrowphase",
+         "robot_dynamics", "enumerate", "broadphase", "pair_narrowphase"]
 
 
 def main():
@@ -29,7 +30,7 @@ def main():
     from urgym_amd._native import Sim
     sim = Sim(0, a.envs, seed=20241220)
     sim.set_autoreset(True, 500)
-    buf = np.zeros(16, np.uint64)
+    buf = np.zeros(24, np.uint64)
     sim.reset()
     sim.sync()
     rc = sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
@@ -41,7 +42,7 @@ def main():
     sim.sync()
     sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     es = a.envs * a.steps
-    d = {k: float(v) for k, v in zip(NAMES, buf[:16])}
+    d = {k: float(v) for k, v in zip(NAMES, buf[:20])}
     out = {"per_env_step_cycles": {k: d[k] / es for k in NAMES[:8]},
            "substeps_per_env_step": d["substeps"] / es,
            "rows_per_substep": d["nrows"] / max(d["substeps"], 1),
@@ -52,7 +53,8 @@ def main():
            "hull_pairs_per_substep": d["hull_pairs"] / max(d["substeps"], 1),
            "manifolds_per_substep": d["manifolds"] / max(d["substeps"], 1)}
     out["pgs_sweep_cycles_per_row_update"] = d["pgs_sweeps"] / max(d["nrows"] * d["pgs_iters"] / max(d["substeps"], 1), 1)
-    for k in ("dyn+enum", "rows", "pgs", "pgs_setup", "pgs_sweeps", "hull_narrowphase", "integrate"):
+    for k in ("dyn+enum", "rows", "pgs", "pgs_setup", "pgs_sweeps", "hull_narrowphase", "robot_dynamics",
+              "enumerate", "broadphase", "pair_narrowphase", "integrate"):
         out[k + "_cycles_per_substep"] = d[k] / max(d["substeps"], 1)
     print(json.dumps(out, indent=1))
     sim.close()

@@ -600,15 +600,15 @@ int urgym_ik(urgym_handle* h, const double* target, double* q_out) {
 }
 
 // Phase cycle counters of the team kernels (only a -DUG_PROF build records them):
-// out16 receives the 16 accumulators (ug_team.h PF_* / PC_*); reset != 0 zeroes them.
+// out16 receives the UG_NPROF (24) accumulators (ug_team.h PF_* / PC_*); reset != 0 zeroes them.
 int urgym_debug_prof(urgym_handle* h, unsigned long long* out16, int reset) {
 #ifdef UG_PROF
     if (!h || !out16) return -1;
     HIPCHK(h, hipSetDevice(h->dev));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    HIPCHK(h, hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16));
+    HIPCHK(h, hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * UG_NPROF));
     if (reset) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[UG_NPROF] = {0};
         HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
     }
     return 0;

@@ -303,6 +303,7 @@ DF void robot_dynamics(const double* qd, const Kin& k, double g, double* M, doub
     double* cm = w.cm;
     v3* ch = w.ch;
     m3* cJ = w.cJ;
+#pragma unroll
     for (int b = 0; b < NB; b++) {
         m[b] = UG_BODY_MASS[b];
         v3 c = k.c[b];
@@ -316,21 +317,28 @@ DF void robot_dynamics(const double* qd, const Kin& k, double g, double* M, doub
         J[b] = Jb;
         cm[b] = m[b]; ch[b] = h[b]; cJ[b] = Jb;
     }
+#pragma unroll
     for (int b = NB - 1; b >= 0; b--) {
         int p = UG_BODY_PARENT[b];
         if (p < 0) continue;
         cm[p] += cm[b];
         ch[p] = vadd(ch[p], ch[b]);
+#pragma unroll
         for (int i = 0; i < 9; i++) cJ[p].m[i] += cJ[b].m[i];
     }
     SV* S = w.S;
+#pragma unroll
     for (int b = 0; b < NB; b++) { S[b].w = k.a[b]; S[b].v = vcross(k.p[b], k.a[b]); }
+#pragma unroll
     for (int i = 0; i < NB * NB; i++) M[i] = 0.0;
+#pragma unroll
     for (int b = 0; b < NB; b++) {
         SV F = spatial_inertia_mul(cm[b], ch[b], cJ[b], S[b]);
         M[b * NB + b] = vdot(S[b].w, F.w) + vdot(S[b].v, F.v);
         int j = UG_BODY_PARENT[b];
-        while (j >= 0) {
+#pragma unroll
+        for (int depth = 0; depth < NB; depth++) { /* the ancestors of b (compile-time after unrolling) */
+            if (j < 0) break;
             double x = vdot(S[j].w, F.w) + vdot(S[j].v, F.v);
             M[j * NB + b] = x;
             M[b * NB + j] = x;
@@ -338,6 +346,7 @@ DF void robot_dynamics(const double* qd, const Kin& k, double g, double* M, doub
         }
     }
     SV *Vb = w.Vb, *Ab = w.Ab, *f = w.f;
+#pragma unroll
     for (int b = 0; b < NB; b++) {
         int p = UG_BODY_PARENT[b];
         SV Vp, Ap;
@@ -356,6 +365,7 @@ DF void robot_dynamics(const double* qd, const Kin& k, double g, double* M, doub
         v3 tau = vscale(mv(D, Vb[b].w), UG_ANG_DAMP + UG_ANG_DAMP * wn);
         f[b].w = vadd(f[b].w, tau);
     }
+#pragma unroll
     for (int l = 1; l < UG_NL; l++) {
         int b = UG_LINK_BODY[l];
         if (b < 0) continue;
@@ -366,6 +376,7 @@ DF void robot_dynamics(const double* qd, const Kin& k, double g, double* M, doub
         f[b].v = vadd(f[b].v, fd);
         f[b].w = vadd(f[b].w, vcross(cl, fd));
     }
+#pragma unroll
     for (int b = NB - 1; b >= 0; b--) {
         C[b] = vdot(S[b].w, f[b].w) + vdot(S[b].v, f[b].v);
         int p = UG_BODY_PARENT[b];

@@ -31,6 +31,7 @@
 namespace ugd {
 
 #define TEAM 64
+#define UG_NPROF 24 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* per-env global workspace (L2-resident): old manifolds (collision), every row's J | M^-1 J^T (24 + 24
@@ -88,7 +89,7 @@ struct Shared {
     double fs[8];
     int is[8];
 #ifdef UG_PROF
-    unsigned long long prof[16];
+    unsigned long long prof[UG_NPROF];
 #endif
 };
 
@@ -97,7 +98,7 @@ static __shared__ Shared g_sh;
 
 /* phase timers (build with -DUG_PROF; read back with urgym_debug_prof) */
 #ifdef UG_PROF
-__device__ unsigned long long g_prof[16];
+__device__ unsigned long long g_prof[UG_NPROF];
 #define PROF_T0(v) unsigned long long v = __builtin_readcyclecounter()
 #define PROF_ADD(k, v)                                                   \
     do {                                                                 \
@@ -113,7 +114,8 @@ __device__ unsigned long long g_prof[16];
 #define PROF_CNT(k, x)
 #endif
 enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_TOTAL,
-       PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN, PF_SWEEPS, PF_HULL };
+       PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN, PF_SWEEPS, PF_HULL,
+       PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -429,6 +431,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
     __threadfence_block();
     __syncthreads();
     /* broadphase: ordered list of overlapping pairs */
+    PROF_T0(t_broad);
     int base = 0;
     for (int p0 = 0; p0 < s->npair; p0 += TEAM) {
         int p = p0 + lane;
@@ -446,6 +449,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
     }
     if (lane == 0) sh.nov = base;
     __syncthreads();
+    PROF_ADD(PF_BROAD, t_broad);
     int nov = base;
     int nnew = 0;
     for (int c0 = 0; c0 < nov; c0 += MAXOV) {
@@ -467,6 +471,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
             }
         }
         PROF_ADD(PF_HULL, t_hull);
+        PROF_T0(t_pairs);
         /* lane per pair: remaining narrowphases, manifold update */
         Manifold M;
         M.npts = 0;
@@ -520,6 +525,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         }
         nnew += __popcll(hm);
         __syncthreads();
+        PROF_ADD(PF_PAIRS, t_pairs);
     }
     if (lane == 0) {
         if (nnew > MAXMAN) e.overflow += (double)(nnew - MAXMAN);
@@ -1102,7 +1108,9 @@ __device__ __noinline__ static void serial_pre(const Scene* s) {
     const int lane = threadIdx.x;
     if (lane == 0) {
         double C[NB];
+        PROF_T0(t_rd);
         robot_dynamics(e.qd, sh.kin, s->gravity, sh.LDL, C, sh.u.dyn);
+        PROF_ADD(PF_RDYN, t_rd);
         /* LDL^T and the qdd solve with the matrix in registers (compile-time indices, same order) */
         double A[NB * NB];
 #pragma unroll
@@ -1135,7 +1143,9 @@ __device__ __noinline__ static void serial_pre(const Scene* s) {
             sh.v0[off] = ob.v.x; sh.v0[off + 1] = ob.v.y; sh.v0[off + 2] = ob.v.z;
             sh.v0[off + 3] = ob.w.x; sh.v0[off + 4] = ob.w.y; sh.v0[off + 5] = ob.w.z;
         }
+        PROF_T0(t_en);
         enumerate_rows(sh, s);
+        PROF_ADD(PF_ENUM, t_en);
     }
 }
 /* lane 0: velocities += solver delta, positions integrate (v + split velocity) */
@@ -1781,7 +1791,7 @@ __device__ static void team_load(const double* S) {
     double* dst = (double*)&sh.e;
     for (int i = threadIdx.x; i < UG_STATE_DIM; i += TEAM) dst[i] = S[i];
 #ifdef UG_PROF
-    if (threadIdx.x < 16) sh.prof[threadIdx.x] = 0;
+    if (threadIdx.x < UG_NPROF) sh.prof[threadIdx.x] = 0;
 #endif
     __syncthreads();
 }
@@ -1789,7 +1799,7 @@ __device__ static void team_prof_flush() {
     Shared& sh = g_sh;
 #ifdef UG_PROF
     __syncthreads();
-    if (threadIdx.x < 16) atomicAdd(&g_prof[threadIdx.x], sh.prof[threadIdx.x]);
+    if (threadIdx.x < UG_NPROF) atomicAdd(&g_prof[threadIdx.x], sh.prof[threadIdx.x]);
 #endif
 }
 /* manifold slots beyond nman are written as (pair -1, zeros), as ugo_get_state does */
