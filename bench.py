@@ -22,8 +22,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-TASK_NAMES = {0: "URGym/BallBalance-v0", 1: "URGym/CubesPush-v0", 2: "URGym/CubesGrasp-v0", 3: "URGym/Golf-v0"}
-MAX_STEPS = {0: 500, 1: 50, 2: 20, 3: 100}
+TASK_NAMES = {0: "URGym/BallBalance-v0", 1: "URGym/CubesPush-v0", 2: "URGym/CubesGrasp-v0", 3: "URGym/Golf-v0",
+              4: "URGym/CubesPushDiff-v0", 5: "URGym/GolfJoints-v0"}
+MAX_STEPS = {0: 500, 1: 50, 2: 20, 3: 100, 4: 50, 5: 100}
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector spec
 

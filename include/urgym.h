@@ -28,6 +28,8 @@ typedef struct urgym_handle urgym_handle;
 #define URGYM_TASK_CUBESPUSH 1   /* urgym/envs/__init__.py:10-14  URGym/CubesPush-v0   */
 #define URGYM_TASK_CUBESGRASP 2  /* urgym/envs/__init__.py:22-26  URGym/CubesGrasp-v0  */
 #define URGYM_TASK_GOLF 3        /* urgym/envs/__init__.py:40-44  URGym/Golf-v0        */
+#define URGYM_TASK_CUBESPUSHDIFF 4 /* urgym/envs/__init__.py:16-20  URGym/CubesPushDiff-v0 (env_cubes_push_diff_v0.py) */
+#define URGYM_TASK_GOLFJOINTS 5    /* urgym/envs/__init__.py:46-50  URGym/GolfJoints-v0 (env_golf_joints_v0.py)      */
 
 /* Replaces: gym.make(id) -> Env.__init__ (p.connect(DIRECT), loadURDF plane/table/robot,
  *   UR5Robotiq85.load(), env_ball_balance_v0.py:34-80; robot.py:178-211).

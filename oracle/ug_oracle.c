@@ -238,7 +238,8 @@ typedef struct {
 typedef struct { int a, b; double thr, friction, restitution, rolling; } pairdef;
 
 typedef struct {
-    int task;
+    int task;    /* base task: scene and physics */
+    int variant; /* the env id's task (a variant shares its base task's scene) */
     double gravity;
     int nobj;
     double omass[MAXOBJ];
@@ -1940,8 +1941,8 @@ static int robot_reset(ugo_env* e) {
 /* ======================================================================== */
 /* tasks                                                                     */
 /* ======================================================================== */
-int ugo_obs_dim(int task) { return task == UG_TASK_BALLBALANCE ? 6 : (task == UG_TASK_CUBESGRASP ? 17 : 9); }
-int ugo_act_dim(int task) { return task == UG_TASK_CUBESGRASP ? 9 : 3; }
+int ugo_obs_dim(int task) { return UG_OBS_DIM(task); }
+int ugo_act_dim(int task) { return UG_ACT_DIM(task); }
 int ugo_state_dim(void) { return STATE_DIM; }
 
 static void bb_obs(const ugo_env* e, double* obs) {
@@ -2021,6 +2022,13 @@ static void cp_obs(const ugo_env* e, double* obs) {
     q4 oe;
     link_state(e, UG_EE_LINK, &pe, &oe);
     obs[0] = pe.x; obs[1] = pe.y; obs[2] = pe.z;
+    if (e->sc.variant == UG_TASK_CUBESPUSHDIFF) {
+        /* env_cubes_push_diff_v0.py:202-212: cube positions relative to the ee (np.array(cube) - np.array(ee)) */
+        for (int o = 0; o < 2; o++) {
+            obs[3 + 3 * o] = e->opos[o].x - pe.x; obs[4 + 3 * o] = e->opos[o].y - pe.y; obs[5 + 3 * o] = e->opos[o].z - pe.z;
+        }
+        return;
+    }
     for (int o = 0; o < 2; o++) { obs[3 + 3 * o] = e->opos[o].x; obs[4 + 3 * o] = e->opos[o].y; obs[5 + 3 * o] = e->opos[o].z; }
 }
 static int cp_reset(ugo_env* e, const double* draws, double* obs) {
@@ -2160,6 +2168,11 @@ static v3 club_point(const ugo_env* e, double zoff) {
     return vadd(e->opos[0], mv(&R, V(0.0, 0.0, zoff - UG_GF_ZC)));
 }
 static void gf_obs(const ugo_env* e, double* obs) {
+    if (e->sc.variant == UG_TASK_GOLFJOINTS) {
+        /* env_golf_joints_v0.py:228-235: np.append(joints[0:6], [stick, ball - stick, hole - ball]) */
+        for (int i = 0; i < 6; i++) obs[i] = e->q[i];
+        obs += 6;
+    }
     v3 st = club_point(e, UG_GF_FOOT_Z); /* getLinkState(stick, 0)[0] (:240-244) */
     double stick[3] = {st.x, st.y, st.z}, ball[3] = {e->opos[1].x, e->opos[1].y, e->opos[1].z};
     double hole[3] = {UG_GF_PITCH_X, UG_GF_PITCH_Y, UG_GF_PITCH_Z};
@@ -2189,10 +2202,17 @@ static int gf_reset(ugo_env* e, const double* draws, double* obs) {
 }
 static int gf_step(ugo_env* e, const float* a, double* obs, double* rew, uint8_t* term, uint8_t* succ) {
     /* :115-183 */
-    v3 pe;
-    q4 oe;
-    link_state(e, UG_EE_LINK, &pe, &oe);
-    move_ee_end(e, V(pe.x + (double)a[0], pe.y + (double)a[1], pe.z + (double)a[2]), Q(0.0, 0.0, -0.70, 0.70));
+    if (e->sc.variant == UG_TASK_GOLFJOINTS) {
+        /* env_golf_joints_v0.py:122-124: get_joint_states() + action (float64 + float32 -> float64), 'joint' */
+        double q6[6];
+        for (int i = 0; i < 6; i++) q6[i] = e->q[i] + (double)a[i];
+        move_ee_joint(e, q6);
+    } else {
+        v3 pe;
+        q4 oe;
+        link_state(e, UG_EE_LINK, &pe, &oe);
+        move_ee_end(e, V(pe.x + (double)a[0], pe.y + (double)a[1], pe.z + (double)a[2]), Q(0.0, 0.0, -0.70, 0.70));
+    }
     int n = wait_until_stable(e);
     const scene* s = &e->sc;
     int c0 = s->ocol[0], c1 = c0 + s->oncol[0], cb = s->ocol[1], cp = static_collider(s, 12);
@@ -2218,7 +2238,8 @@ static int gf_step(ugo_env* e, const float* a, double* obs, double* rew, uint8_t
 /* ======================================================================== */
 ugo_env* ugo_create(int task, uint32_t seed) {
     ugo_env* e = (ugo_env*)calloc(1, sizeof(ugo_env));
-    build_scene(&e->sc, task);
+    build_scene(&e->sc, UG_BASE_TASK(task));
+    e->sc.variant = task;
     mt_seed(&e->rng, seed);
     return e;
 }
@@ -2330,7 +2351,7 @@ long ugo_batch_step(ugo_env** envs, int n, const float* actions, double* obs, do
                     uint8_t* success, int32_t* substeps, int autoreset, int max_episode_steps, int32_t* elapsed) {
     long total = 0;
     if (n <= 0) return 0;
-    int task = envs[0]->sc.task;
+    int task = envs[0]->sc.variant;
     int A = ugo_act_dim(task), O = ugo_obs_dim(task);
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : total)
     for (int i = 0; i < n; i++) {

@@ -29,8 +29,9 @@ def test_library_exports_every_declared_symbol(built):
 def test_static_shapes(built):
     from urgym_amd._native import lib
     L = lib()
-    assert [L.urgym_obs_dim(t) for t in range(4)] == [6, 9, 17, 9]
-    assert [L.urgym_act_dim(t) for t in range(4)] == [3, 3, 9, 3]
+    assert [L.urgym_obs_dim(t) for t in range(6)] == [6, 9, 17, 9, 9, 15]
+    assert [L.urgym_act_dim(t) for t in range(6)] == [3, 3, 9, 3, 3, 6]
+    assert [L.urgym_num_draws(t) for t in range(6)] == [2, 1, 2, 2, 1, 2]
     from oracle.pyoracle import lib as olib
     assert L.urgym_state_dim() == olib().ugo_state_dim()
 
@@ -41,6 +42,10 @@ def test_spaces_match_reference(built):
     obs, act = spaces_for(0)
     assert obs.shape == (6,) and act.shape == (3,) and act.dtype == np.float32 and obs.dtype == np.float64
     assert np.allclose(act.low, -0.1) and np.allclose(obs.high[:3], np.pi)
+    obs, act = spaces_for(5)  # GolfJoints: 6 joint deltas, joints + Golf obs
+    assert obs.shape == (15,) and act.shape == (6,) and np.allclose(obs.high[:6], 2 * np.pi)
+    from urgym_amd.envs import TASKS
+    assert TASKS["URGym/CubesPushDiff-v0"] == (4, 50) and TASKS["URGym/GolfJoints-v0"] == (5, 100)
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="GPU present")

@@ -118,3 +118,33 @@ def test_paddle_stays_grasped_and_ball_dynamics_finite(ora):
     p1 = e.get_state()[40:43]
     # the paddle is carried by the gripper: it moved with the end effector, it did not fall to the table
     assert p1[2] > 0.3 and np.linalg.norm(p1 - p0) < 0.3
+
+
+def test_variants_share_their_base_physics(ora):
+    """CubesPushDiff / GolfJoints differ from CubesPush / Golf only in step and obs
+    glue: the same seed resets to the same state, and the obs is the reference's function of it
+    (env_cubes_push_diff_v0.py:202-212: cube - ee; env_golf_joints_v0.py:228-235: joints[0:6] + Golf obs)."""
+    for base, var in ((1, 4), (3, 5)):
+        b, v = ora.OracleEnv(base, SEED), ora.OracleEnv(var, SEED)
+        ob, nb = b.reset()
+        ov, nv = v.reset()
+        assert nb == nv and np.array_equal(b.get_state(), v.get_state())
+        if var == 4:
+            assert ov.shape == (9,) and np.array_equal(ov[:3], ob[:3])
+            assert np.array_equal(ov[3:6], ob[3:6] - ob[:3]) and np.array_equal(ov[6:9], ob[6:9] - ob[:3])
+        else:
+            assert ov.shape == (15,) and np.array_equal(ov[6:], ob)
+            assert np.array_equal(ov[:6], v.get_state()[:6])
+
+
+def test_golf_joints_step_is_joint_control(ora):
+    """GolfJoints.step: targets = get_joint_states() + action (float64 + float32), 'joint' control
+    (env_golf_joints_v0.py:122-124, robot.py:122-128): the arm motors hold q + a after the step."""
+    v = ora.OracleEnv(5, SEED)
+    v.reset()
+    q0 = v.get_state()[:6].copy()
+    a = np.array([0.05, -0.05, 0.02, 0.0, 0.01, -0.02], np.float32)
+    v.step(a)
+    st = v.get_state()
+    mtarget = st[24:30]  # state layout: q[12], qd[12], mtarget[7] ...
+    assert np.array_equal(mtarget, q0 + a.astype(np.float64))

@@ -52,6 +52,14 @@ UG_CONST double UG_GEAR_RATIO[5] = {1.0, -1.0, -1.0, 1.0, -1.0};
 #define UG_TASK_CUBESPUSH 1
 #define UG_TASK_CUBESGRASP 2
 #define UG_TASK_GOLF 3
+/* variants: same scene and physics as their base task, different step/obs glue */
+#define UG_TASK_CUBESPUSHDIFF 4 /* env_cubes_push_diff_v0.py: obs = ee, cube - ee (x2) */
+#define UG_TASK_GOLFJOINTS 5    /* env_golf_joints_v0.py: joint-space action[6], obs = joints + Golf obs */
+#define UG_NTASK 6
+#define UG_BASE_TASK(t) ((t) == UG_TASK_CUBESPUSHDIFF ? UG_TASK_CUBESPUSH : ((t) == UG_TASK_GOLFJOINTS ? UG_TASK_GOLF : (t)))
+#define UG_OBS_DIM(t) ((t) == 0 ? 6 : ((t) == 2 ? 17 : ((t) == 5 ? 15 : 9)))
+#define UG_ACT_DIM(t) ((t) == 2 ? 9 : ((t) == 5 ? 6 : 3))
+#define UG_NDRAW(t) ((t) == 1 || (t) == 4 ? 1 : 2)
 
 /* ---- shapes ---- */
 #define UG_SHAPE_BOX 0

@@ -60,9 +60,11 @@ __device__ static void add_pair(Scene* s, int a, int b) {
     if (r > UG_MAX_FRICTION) r = UG_MAX_FRICTION;
     p->rolling = r;
 }
-__global__ void k_build_scene(Scene* s, int task) {
+__global__ void k_build_scene(Scene* s, int variant) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int task = UG_BASE_TASK(variant);
     s->task = task;
+    s->variant = variant;
     s->gravity = task == UG_TASK_CUBESGRASP ? -10.0 : -9.8;
     s->nobj = 0;
     s->ncol = 0;
@@ -229,9 +231,9 @@ __global__ void k_build_scene(Scene* s, int task) {
 // kernels: one wavefront (block of 64) per environment, state resident in LDS
 // ---------------------------------------------------------------------------
 
-static __device__ int task_obs_dim(int task) { return task == UG_TASK_BALLBALANCE ? 6 : (task == UG_TASK_CUBESGRASP ? 17 : 9); }
-static __device__ int task_act_dim(int task) { return task == UG_TASK_CUBESGRASP ? 9 : 3; }
-static __device__ int task_ndraw(int task) { return task == UG_TASK_CUBESPUSH ? 1 : 2; }
+static __device__ int task_obs_dim(int variant) { return UG_OBS_DIM(variant); }
+static __device__ int task_act_dim(int variant) { return UG_ACT_DIM(variant); }
+static __device__ int task_ndraw(int variant) { return UG_NDRAW(variant); }
 
 __global__ void __launch_bounds__(TEAM, 1) k_reset(const Scene* sc, double* S, uint32_t* mt, int* elapsed, double* ws,
                                                    int n, const uint8_t* mask, const double* draws, double* obs,
@@ -243,9 +245,9 @@ __global__ void __launch_bounds__(TEAM, 1) k_reset(const Scene* sc, double* S, u
     team_load(Si);
     RunIO io;
     io.act = nullptr;
-    io.obs = obs + (size_t)i * task_obs_dim(sc->task);
+    io.obs = obs + (size_t)i * task_obs_dim(sc->variant);
     io.final_obs = nullptr;
-    io.dr = Draws{Rng{mt + (size_t)i * UG_MT_WORDS, 1, 0}, draws ? draws + (size_t)i * task_ndraw(sc->task) : nullptr, 0};
+    io.dr = Draws{Rng{mt + (size_t)i * UG_MT_WORDS, 1, 0}, draws ? draws + (size_t)i * task_ndraw(sc->variant) : nullptr, 0};
     io.autoreset = 0;
     io.trunc = 0;
     PROF_T0(t_tot);
@@ -267,7 +269,7 @@ __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, ui
     if (i >= n) return;
     double* Si = S + (size_t)i * UG_STATE_DIM;
     team_load(Si);
-    const int O = task_obs_dim(sc->task), A = task_act_dim(sc->task);
+    const int O = task_obs_dim(sc->variant), A = task_act_dim(sc->variant);
     const int el = elapsed[i] + 1;
     RunIO io;
     io.act = act + (size_t)i * A;
@@ -384,10 +386,10 @@ static void mt_seed_host(uint32_t* mt, uint32_t seed) {
 
 extern "C" {
 
-int urgym_obs_dim(int task) { return task == 0 ? 6 : (task == 2 ? 17 : 9); }
-int urgym_act_dim(int task) { return task == 2 ? 9 : 3; }
+int urgym_obs_dim(int task) { return UG_OBS_DIM(task); }
+int urgym_act_dim(int task) { return UG_ACT_DIM(task); }
 int urgym_state_dim(void) { return UG_STATE_DIM; }
-int urgym_num_draws(int task) { return task == 1 ? 1 : 2; }
+int urgym_num_draws(int task) { return UG_NDRAW(task); }
 int urgym_num_envs(const urgym_handle* h) { return h ? h->n : 0; }
 const char* urgym_last_error(const urgym_handle* h) { return h ? h->err.c_str() : g_create_error.c_str(); }
 
@@ -428,7 +430,7 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
 }
 
 urgym_handle* urgym_create(int task, int n, int dev, int precision, uint32_t seed, int env_offset) {
-    if (task < URGYM_TASK_BALLBALANCE || task > URGYM_TASK_GOLF) {
+    if (task < URGYM_TASK_BALLBALANCE || task > URGYM_TASK_GOLFJOINTS) {
         fail(nullptr, "urgym_create: unknown task " + std::to_string(task));
         return nullptr;
     }

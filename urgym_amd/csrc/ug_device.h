@@ -221,7 +221,8 @@ struct Collider {
 };
 struct PairDef { int a, b; double thr, friction, restitution, rolling; };
 struct Scene {
-    int task;
+    int task;    /* base task: scene and physics */
+    int variant; /* the env id's task (== task, or a variant's UG_TASK_*): step / obs glue */
     double gravity;
     int nobj;
     double omass[MAXOBJ];

@@ -1569,10 +1569,24 @@ __device__ static void gf_obs(const EnvState& e, double* obs) {
     double hole[3] = {UG_GF_PITCH_X, UG_GF_PITCH_Y, UG_GF_PITCH_Z};
     ugg_gf_obs(stick, ball, hole, obs);
 }
+/* CubesPushDiff obs (env_cubes_push_diff_v0.py:202-212): ee position, each cube minus the ee position */
+__device__ static void cpd_obs(const EnvState& e, double* obs) {
+    v3 pe;
+    q4 oe;
+    link_state_of(e.q, UG_EE_LINK, pe, oe);
+    obs[0] = pe.x; obs[1] = pe.y; obs[2] = pe.z;
+    for (int o = 0; o < 2; o++) {
+        obs[3 + 3 * o] = e.obj[o].pos.x - pe.x; obs[4 + 3 * o] = e.obj[o].pos.y - pe.y; obs[5 + 3 * o] = e.obj[o].pos.z - pe.z;
+    }
+}
 __device__ static void task_obs(const Scene* s, const EnvState& e, double* obs) {
-    if (s->task == UG_TASK_CUBESPUSH) cp_obs(e, obs);
+    if (s->variant == UG_TASK_CUBESPUSHDIFF) cpd_obs(e, obs);
+    else if (s->task == UG_TASK_CUBESPUSH) cp_obs(e, obs);
     else if (s->task == UG_TASK_CUBESGRASP) cg_obs(e, obs);
-    else if (s->task == UG_TASK_GOLF) gf_obs(e, obs);
+    else if (s->variant == UG_TASK_GOLFJOINTS) { /* env_golf_joints_v0.py:228-235: arm joints, then the Golf obs */
+        for (int i = 0; i < 6; i++) obs[i] = e.q[i];
+        gf_obs(e, obs + 6);
+    } else if (s->task == UG_TASK_GOLF) gf_obs(e, obs);
     else bb_obs(e, obs);
 }
 /* ---------------- the env program: step / reset as one substep loop ----------------
@@ -1594,7 +1608,7 @@ struct RunIO {
 __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* next) {
     EnvState& e = g_sh.e;
     const int task = s->task;
-    const int O = task == UG_TASK_BALLBALANCE ? 6 : (task == UG_TASK_CUBESGRASP ? 17 : 9);
+    const int O = UG_OBS_DIM(s->variant);
     switch (pc) {
         case G_STEP: {
             v3 pe;
@@ -1616,6 +1630,12 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
                 link_state_of(e.q, UG_EE_LINK, pe, oe);
                 move_ee_end(e, V(pe.x + (double)io.act[0], pe.y + (double)io.act[1], pe.z + (double)io.act[2]),
                             Q(0.0, UG_VQ_S, 0.0, UG_VQ_C));
+            } else if (s->variant == UG_TASK_GOLFJOINTS) {
+                /* env_golf_joints_v0.py:122-124: arm joint positions + action (float64 + float32 -> float64),
+                 * move_ee(..., 'joint') */
+                double q6[6];
+                for (int i = 0; i < 6; i++) q6[i] = e.q[i] + (double)io.act[i];
+                move_ee_joint(e, q6);
             } else if (task == UG_TASK_GOLF) {
                 /* env_golf_v0.py:115-127: EE position + action, the reset orientation (0, 0, -0.7, 0.7) */
                 link_state_of(e.q, UG_EE_LINK, pe, oe);

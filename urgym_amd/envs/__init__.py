@@ -23,9 +23,11 @@ TASKS = {
     "URGym/CubesPush-v0": (1, 50),      # :10-14
     "URGym/CubesGrasp-v0": (2, 20),     # :22-26
     "URGym/Golf-v0": (3, 100),          # :40-44
+    "URGym/CubesPushDiff-v0": (4, 50),  # :16-20  (variant of CubesPush: relative obs)
+    "URGym/GolfJoints-v0": (5, 100),    # :46-50  (variant of Golf: joint-space action, joints in obs)
 }
-UNSUPPORTED = {  # registered by the reference, out of this tier's scope
-    "URGym/Box-v0": 200, "URGym/CubesPushDiff-v0": 50, "URGym/TwoBallsBalance-v0": 500, "URGym/GolfJoints-v0": 100,
+UNSUPPORTED = {  # registered by the reference, not built yet
+    "URGym/Box-v0": 200, "URGym/TwoBallsBalance-v0": 500,
 }
 
 
@@ -34,9 +36,13 @@ def spaces_for(task):
     if task == 0:  # env_ball_balance_v0.py:52-54
         obs = Box(low=np.array([-math.pi] * 3 + [-1.0] * 3), high=np.array([math.pi] * 3 + [1.0] * 3), dtype=np.float64)
         act = Box(low=np.array([-0.1] * 3), high=np.array([+0.1] * 3), dtype=np.float32)
-    elif task in (1, 3):  # env_cubes_push_v0.py:58-60, env_golf_v0.py:58-60
+    elif task in (1, 3, 4):  # env_cubes_push_v0.py:58-60, env_golf_v0.py:58-60, env_cubes_push_diff_v0.py:58-62
         obs = Box(low=np.array([-1.0] * 9), high=np.array([1.0] * 9), dtype=np.float64)
         act = Box(low=np.array([-0.1] * 3), high=np.array([+0.1] * 3), dtype=np.float32)
+    elif task == 5:  # env_golf_joints_v0.py:59-63
+        obs = Box(low=np.array([-2 * math.pi] * 6 + [-1.0] * 3 + [-1.0] * 3 + [-1.0] * 3),
+                  high=np.array([2 * math.pi] * 6 + [1.0] * 3 + [1.0] * 3 + [1.0] * 3), dtype=np.float64)
+        act = Box(low=np.array([-0.1] * 6), high=np.array([+0.1] * 6), dtype=np.float32)
     else:  # env_cubes_grasp_v0.py:72-74
         obs = Box(low=np.array([0] * 2 + [-1.0] * 3 + [-1] * 4 + [0] + [-1.0] * 3 + [-1.0] * 4),
                   high=np.array([1] * 2 + [1.0] * 3 + [1.0] * 4 + [1] + [1.0] * 3 + [1.0] * 4), dtype=np.float64)
@@ -79,5 +85,15 @@ def Golf(camera=None, reward_type="dense", render_mode="human", **kw):
     return URGymEnv(3, max_episode_steps=None, camera=camera, reward_type=reward_type, render_mode=render_mode, **kw)
 
 
+def CubesPushDiff(camera=None, reward_type="dense", render_mode="human", **kw):
+    """env_cubes_push_diff_v0.CubesPushDiff(camera, reward_type, render_mode) signature."""
+    return URGymEnv(4, max_episode_steps=None, camera=camera, reward_type=reward_type, render_mode=render_mode, **kw)
+
+
+def GolfJoints(camera=None, reward_type="dense", render_mode="human", **kw):
+    """env_golf_joints_v0.GolfJoints(camera, reward_type, render_mode) signature."""
+    return URGymEnv(5, max_episode_steps=None, camera=camera, reward_type=reward_type, render_mode=render_mode, **kw)
+
+
 __all__ = ["make", "TASKS", "URGymEnv", "URGymVectorEnv", "BallBalance", "CubesPush", "CubesGrasp", "Golf",
-           "spaces_for"]
+           "CubesPushDiff", "GolfJoints", "spaces_for"]
