@@ -158,6 +158,7 @@ def main():
               open(os.path.join(OUT, "wait_until_stable.json"), "w"), indent=1)
     gen_cubes(p, rng)
     gen_golf(p)
+    gen_variants(p)
     print("wrote", sorted(os.listdir(OUT)))
 
 
@@ -429,5 +430,55 @@ def gen_golf(p):
     json.dump(out, open(os.path.join(OUT, "golf_glue.json"), "w"), indent=1)
 
 
+def gen_variants(p):
+    """CubesPushDiff (env_cubes_push_diff_v0.py) and GolfJoints (env_golf_joints_v0.py) glue: the variant
+    observations and GolfJoints' joint-space control, with scripted physics queries."""
+    from urgym.envs.env_cubes_push_diff_v0 import CubesPush as CubesPushDiff  # noqa: E402 (class keeps the base name)
+    from urgym.envs.env_golf_joints_v0 import Golf as GolfJoints  # noqa: E402
+    out = {"push_diff_obs": [], "golf_joints_step": []}
+    rng = np.random.default_rng(4)
+    for _ in range(4):
+        env = CubesPushDiff.__new__(CubesPushDiff)
+        env.cubes = [31, 32]
+        ee = tuple(float(x) for x in rng.uniform(-0.8, 0.8, 3))
+        cubes = {31: tuple(float(x) for x in rng.uniform(-0.8, 0.8, 3)), 32: tuple(float(x) for x in rng.uniform(-0.8, 0.8, 3))}
+        env.robot = types.SimpleNamespace(get_joint_obs=lambda: {"ee_pos": ee + (0.0, 0.0, 0.0, 1.0)})
+        p.reset_mock()
+        p.getBasePositionAndOrientation.side_effect = lambda i: (cubes[i], (0.0, 0.0, 0.0, 1.0))
+        obs = env.get_observation()
+        out["push_diff_obs"].append({"ee": list(ee), "cube0": list(cubes[31]), "cube1": list(cubes[32]),
+                                     "obs": [float(x) for x in obs]})
+    hole = (0.0, -0.6, 0.02)
+    for k in range(4):
+        env = GolfJoints.__new__(GolfJoints)
+        env.visualize = False
+        env.reward_type = "dense"
+        env.positive_reward_radius = 0.1
+        env.control_method = "joint"
+        env.stick_id, env.ball_id, env.pitch_id = 20, 21, 3
+        q6 = [float(x) for x in rng.uniform(-2.0, 2.0, 6)]
+        moves = []
+        env.robot = types.SimpleNamespace(id=1, get_joint_states=lambda: list(q6),
+                                          move_ee=lambda act, m: moves.append(([float(x) for x in act], m)))
+        env.wait_until_stable = lambda: True
+        ball = tuple(float(x) for x in rng.uniform(-0.3, 0.3, 2)) + (0.06,)
+        stick = (0.05, -0.6, 0.07)
+        p.reset_mock()
+        p.getBasePositionAndOrientation.side_effect = lambda i: ((ball if i == 21 else hole), (0.0, 0.0, 0.0, 1.0))
+        p.getLinkState.side_effect = lambda bid, l: (stick, (0, 0, 0, 1))
+        p.getContactPoints.side_effect = lambda *a, **kw: [contact(0, 12)] if (a[:2] == (20, 1)) else []
+        a = rng.uniform(-0.1, 0.1, 6).astype(np.float32)
+        obs, rew, term, trunc, info = env.step(a)
+        out["golf_joints_step"].append({"q6": q6, "action": a.tolist(), "ball": list(ball), "stick": list(stick),
+                                        "hole": list(hole), "move_target": moves[0][0], "control": moves[0][1],
+                                        "obs": [float(x) for x in obs], "reward": float(rew),
+                                        "terminated": bool(term)})
+    json.dump(out, open(os.path.join(OUT, "variants_glue.json"), "w"), indent=1)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "variants":  # only the variant fixtures
+        os.makedirs(OUT, exist_ok=True)
+        gen_variants(install_stubs())
+    else:
+        main()
