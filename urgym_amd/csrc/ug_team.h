@@ -922,7 +922,6 @@ __device__ __noinline__ static void build_row(const Scene* s, int pos, double* w
  * row-range test is a scalar branch.  Columns P >= PREG come from the global workspace.  Arithmetic
  * order is the oracle's pgs() (oracle/ug_oracle.c). */
 #define NCMAX (2 * NB + 12) /* limits (both sides) + 7 motors + 5 gears */
-#define MJCHUNK 48          /* M^-1J rows staged in LDS per chunk of the Delassus build */
 typedef __attribute__((address_space(1))) const double gcdouble;
 typedef __attribute__((address_space(1))) double gdouble;
 struct Lrow { /* the two rows this lane owns (slot s: position lane + 64 s) */
@@ -1059,35 +1058,65 @@ __device__ __forceinline__ void sweep_warm(const double (&A0)[PREG], const doubl
         }
     }
 }
-/* M^-1J of rows [c0, c0 + MJCHUNK) -> LDS (sh.u.stage viewed as [MJCHUNK][24]) */
-__device__ __forceinline__ void stage_mj(gcdouble* rows, int c0, int n, int lane) {
-    double* st = &g_sh.u.stage[0][0];
-    __builtin_amdgcn_wave_barrier();
-    for (int i = lane; i < MJCHUNK * 24; i += TEAM) {
-        const int j = c0 + i / 24, d = i % 24;
-        st[i] = j < n ? rows[j * 48 + 24 + d] : 0.0;
-    }
-    __builtin_amdgcn_wave_barrier();
+/* ---- Delassus rows on the matrix cores ----
+ * A[i][p] = fma chain over the 24 dof slots of J_i[d] * M^-1J_p[d] is a 24-deep dot product, so a 16x16
+ * tile of A is 6 chained v_mfma_f64_16x16x4_f64: their numerics are a k-ordered fma chain, bit-identical
+ * to the oracle's rdot() (checked on MI355X: tools/micro/mfma64.hip, mfma_build.hip).  For the column
+ * block PB (columns p = 16 PB + 0..15) the four row tiles of slot S are computed with the columns on the
+ * A operand, so tile g leaves A[64 S + 16 g + m][16 PB + h + 4 r] in lane 16 h + m, register r; a 4x4
+ * transpose of (tile, lane row) with permlane32_swap / permlane16_swap then hands lane l its own row:
+ * A[64 S + l][16 PB + h + 4 r] in W[h][r].  Rows and columns beyond n are zero. */
+typedef double d4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void swap32_d(double& x, double& y) {
+    auto l = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(x), (unsigned)__double2loint(y), false, false);
+    auto h = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(x), (unsigned)__double2hiint(y), false, false);
+    x = __hiloint2double(h[0], l[0]);
+    y = __hiloint2double(h[1], l[1]);
 }
-/* scaled Delassus row of this lane's slot: NB[r][j] = -((fma chain over d of J_r[d] * M^-1J_j[d]) / D_r) */
-template <int J, int S>
-__device__ __forceinline__ void build_A(gcdouble* rows, const double (&Jr)[NV], double invDr, double (&A)[PREG],
-                                        gdouble* wsA, int n, int lane) {
-    if constexpr (J < MAXROWS) {
-        if (J < ((n + 7) & ~7)) { /* through the end of the last 8-row chunk: zero columns beyond n */
-            if constexpr (J % MJCHUNK == 0) stage_mj(rows, J, n, lane);
-            const double* mj = &g_sh.u.stage[0][0] + (J % MJCHUNK) * 24; /* same address on every lane */
-            /* a compiler barrier per column: otherwise the scheduler hoists every column's LDS reads and
-             * spills them (the A rows already fill the register file) */
-            asm volatile("" ::: "memory");
-            double a = 0.0;
+__device__ __forceinline__ void swap16_d(double& x, double& y) {
+    auto l = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(x), (unsigned)__double2loint(y), false, false);
+    auto h = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(x), (unsigned)__double2hiint(y), false, false);
+    x = __hiloint2double(h[0], l[0]);
+    y = __hiloint2double(h[1], l[1]);
+}
+template <int PB, int S>
+__device__ __forceinline__ void mfma_block(gcdouble* rows, double invDr, double (&A)[PREG], gdouble* wsA, int n,
+                                           int lane) {
+    if constexpr (16 * PB < MAXROWS) {
+        if (16 * PB < n) {
+            d4v acc[4];
 #pragma unroll
-            for (int d = 0; d < NV; d++) a = __builtin_fma(Jr[d], mj[d], a);
-            a = -(a * invDr);
-            asm volatile("" : "+v"(a)); /* materialise the entry here (no sinking into its uses) */
-            if constexpr (J < PREG) A[J] = a;
-            else wsA[(J - PREG) * MAXROWS + 64 * S + lane] = a;
-            build_A<J + 1, S>(rows, Jr, invDr, A, wsA, n, lane);
+            for (int g = 0; g < 4; g++) acc[g] = d4v{0.0, 0.0, 0.0, 0.0};
+            const int p = 16 * PB + (lane & 15);
+#pragma unroll
+            for (int ks = 0; ks < 6; ks++) {
+                const int d = 4 * ks + (lane >> 4);
+                const double a = p < n ? rows[p * 48 + 24 + d] : 0.0;
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const int i = 64 * S + 16 * g + (lane & 15);
+                    const double b = i < n ? rows[i * 48 + d] : 0.0;
+                    acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[g], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                double v[4] = {acc[0][r], acc[1][r], acc[2][r], acc[3][r]};
+                swap32_d(v[0], v[2]);
+                swap32_d(v[1], v[3]);
+                swap16_d(v[0], v[1]);
+                swap16_d(v[2], v[3]);
+#pragma unroll
+                for (int h = 0; h < 4; h++) {
+                    constexpr int base = 16 * PB;
+                    double x = -(v[h] * invDr);      /* NB = -(A / D) of this lane's row */
+                    asm volatile("" : "+v"(x));      /* materialise here (no sinking into the sweeps) */
+                    const int P = base + h + 4 * r;  /* compile-time after unrolling */
+                    if (P < PREG) A[P < PREG ? P : 0] = x;
+                    else wsA[(P - PREG) * MAXROWS + 64 * S + lane] = x;
+                }
+            }
+            mfma_block<PB + 1, S>(rows, invDr, A, wsA, n, lane);
         }
     }
 }
@@ -1214,23 +1243,13 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     gcdouble* rows = (gcdouble*)(ws + WS_ROWS);
     gdouble* wsA = (gdouble*)(ws + WS_A);
     double A0[PREG], A1[PREG];
-    /* slot 1 first, then slot 0 */
+    /* scaled Delassus rows on the matrix cores (mfma_block); slot 1 only when rows >= 64 exist */
+    mfma_block<0, 0>(rows, lane < n ? sh.rs[lane].invD : 0.0, A0, wsA, n, lane);
     if (n > 64) {
-        double Jr[NV];
-        const int r = lane + 64 < n ? lane + 64 : 0;
-#pragma unroll
-        for (int d = 0; d < NV; d++) Jr[d] = lane + 64 < n ? rows[r * 48 + d] : 0.0;
-        build_A<0, 1>(rows, Jr, lane + 64 < n ? sh.rs[r].invD : 0.0, A1, wsA, n, lane);
+        mfma_block<0, 1>(rows, lane + 64 < n ? sh.rs[lane + 64].invD : 0.0, A1, wsA, n, lane);
     } else {
 #pragma unroll
         for (int j = 0; j < PREG; j++) A1[j] = 0.0;
-    }
-    {
-        double Jr[NV];
-        const int r = lane < n ? lane : 0;
-#pragma unroll
-        for (int d = 0; d < NV; d++) Jr[d] = lane < n ? rows[r * 48 + d] : 0.0;
-        build_A<0, 0>(rows, Jr, lane < n ? sh.rs[r].invD : 0.0, A0, wsA, n, lane);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
