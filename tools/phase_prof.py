@@ -19,7 +19,8 @@ os.environ.setdefault("URGYM_LIB", os.path.join(ROOT, "urgym_amd", "_lib", "libu
 
 NAMES = ["collide", "dyn+enum", "rows", "pgs", "pgs_setup", "integrate", "glue", "total",
          "substeps", "nrows", "pgs_iters", "overlap_pairs", "hull_pairs", "manifolds", "pgs_sweeps", "hull_narrowphase",
-         "robot_dynamics", "enumerate", "broadphase", "pair_narrowphase"]
+         "robot_dynamics", "enumerate", "broadphase", "pair_narrowphase",
+         "hullbox_vertices", "hullbox_corners", "hullbox_reduce"]
 
 
 def main():
@@ -42,7 +43,7 @@ def main():
     sim.sync()
     sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     es = a.envs * a.steps
-    d = {k: float(v) for k, v in zip(NAMES, buf[:20])}
+    d = {k: float(v) for k, v in zip(NAMES, buf[:23])}
     out = {"per_env_step_cycles": {k: d[k] / es for k in NAMES[:8]},
            "substeps_per_env_step": d["substeps"] / es,
            "rows_per_substep": d["nrows"] / max(d["substeps"], 1),
@@ -54,7 +55,8 @@ def main():
            "manifolds_per_substep": d["manifolds"] / max(d["substeps"], 1)}
     out["pgs_sweep_cycles_per_row_update"] = d["pgs_sweeps"] / max(d["nrows"] * d["pgs_iters"] / max(d["substeps"], 1), 1)
     for k in ("dyn+enum", "rows", "pgs", "pgs_setup", "pgs_sweeps", "hull_narrowphase", "robot_dynamics",
-              "enumerate", "broadphase", "pair_narrowphase", "integrate"):
+              "enumerate", "broadphase", "pair_narrowphase", "hullbox_vertices", "hullbox_corners",
+              "hullbox_reduce", "integrate"):
         out[k + "_cycles_per_substep"] = d[k] / max(d["substeps"], 1)
     print(json.dumps(out, indent=1))
     sim.close()

@@ -296,6 +296,8 @@ struct DynWork {
     v3 h[NB], ch[NB];
     m3 J[NB], cJ[NB];
     SV S[NB], Vb[NB], Ab[NB], f[NB];
+    v3 fdl[UG_NL], tl[UG_NL]; /* link damping force / torque (team version) */
+    double C[NB];             /* bias forces (team version) */
 };
 DF void robot_dynamics(const double* qd, const Kin& k, double g, double* M, double* C, DynWork& w) {
     double* m = w.m;

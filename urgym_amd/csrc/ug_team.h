@@ -115,7 +115,7 @@ __device__ unsigned long long g_prof[UG_NPROF];
 #endif
 enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_TOTAL,
        PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN, PF_SWEEPS, PF_HULL,
-       PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS };
+       PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -223,6 +223,7 @@ __device__ __noinline__ static void team_hull_box(const Collider& A, const Colli
                                      double thr, int k) {
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
+    PROF_T0(t_hv);
     m3 RAB = mtm(TB.R, TA.R);
     v3 pAB = mtv(TB.R, vsub(TA.p, TB.p));
     v3 h = V(B.half[0], B.half[1], B.half[2]);
@@ -261,6 +262,8 @@ __device__ __noinline__ static void team_hull_box(const Collider& A, const Colli
             vc.d = depth;
         }
     }
+    PROF_ADD(PF_HB_VERT, t_hv);
+    PROF_T0(t_hc);
     /* box corners: 8 lanes per corner, faces strided over the group, then a group arg-max */
     int c = lane >> 3, j = lane & 7;
     m3 RBA = mtm(TA.R, TB.R);
@@ -297,6 +300,8 @@ __device__ __noinline__ static void team_hull_box(const Collider& A, const Colli
             cc.d = depth;
         }
     }
+    PROF_ADD(PF_HB_CORNER, t_hc);
+    PROF_T0(t_hr);
     /* collect in canonical order: vertices by index, then corners by index */
     unsigned long long vb = ballot(vvalid), cb = ballot(cvalid);
     int nv = __popcll(vb), nc = __popcll(cb);
@@ -304,6 +309,7 @@ __device__ __noinline__ static void team_hull_box(const Collider& A, const Colli
     if (cvalid) sh.hc[nv + lane_prefix(cb)] = cc;
     __syncthreads();
     team_reduce4(nv + nc, k);
+    PROF_ADD(PF_HB_REDUCE, t_hr);
 }
 
 /* hull (A) vs hull (B) (oracle nc_hull_hull): lane per A vertex against B's planes, lane per B vertex against
@@ -1128,6 +1134,153 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
     return (T*)(((unsigned long long)hi << 32) | lo);
 }
 
+/* ---- robot dynamics, wave-parallel (same operations and order as robot_dynamics / the oracle) ----
+ * lane b < NB owns body b (inertias, spatial axis, mass-matrix column, RNEA forward step, forces); the
+ * tree accumulations (composite inertia, force back-propagation) run component-parallel: lane c owns
+ * one scalar component and walks the bodies in the serial code's descending order.  The RNEA forward
+ * pass goes level by level down the (compile-time) tree.  Results: M -> LDL (LDS), C -> w.C. */
+__device__ __forceinline__ int body_depth(int b) {
+    int d = 0;
+    for (int j = UG_BODY_PARENT[b]; j >= 0; j = UG_BODY_PARENT[j]) d++;
+    return d;
+}
+__device__ __noinline__ static void team_robot_dynamics(double g_) {
+    /* the LDS image is addressed directly (pointer arguments would turn every access into a flat one) */
+    const double* qd = g_sh.e.qd;
+    const Kin& k = g_sh.kin;
+    double* M = g_sh.LDL;
+    DynWork& w = g_sh.u.dyn;
+    const double g = g_;
+    const int lane = threadIdx.x;
+    const bool own = lane < NB;
+    const int b = own ? lane : 0;
+    /* 1. per body: mass, first moment, world inertia about the origin, spatial axis */
+    double m = 0.0;
+    v3 h = V(0, 0, 0);
+    m3 Jb;
+    if (own) {
+        m = UG_BODY_MASS[b];
+        v3 c = k.c[b];
+        h = vscale(c, m);
+        m3 Iw = inertia_world(k.R[b], &UG_BODY_I[6 * b]);
+        double cc = vdot(c, c);
+        Jb.m[0] = Iw.m[0] + m * (cc - c.x * c.x); Jb.m[1] = Iw.m[1] - m * (c.x * c.y); Jb.m[2] = Iw.m[2] - m * (c.x * c.z);
+        Jb.m[3] = Iw.m[3] - m * (c.y * c.x); Jb.m[4] = Iw.m[4] + m * (cc - c.y * c.y); Jb.m[5] = Iw.m[5] - m * (c.y * c.z);
+        Jb.m[6] = Iw.m[6] - m * (c.z * c.x); Jb.m[7] = Iw.m[7] - m * (c.z * c.y); Jb.m[8] = Iw.m[8] + m * (cc - c.z * c.z);
+        w.m[b] = m; w.h[b] = h; w.J[b] = Jb;
+        w.cm[b] = m; w.ch[b] = h; w.cJ[b] = Jb;
+        w.S[b].w = k.a[b];
+        w.S[b].v = vcross(k.p[b], k.a[b]);
+    }
+    for (int i = lane; i < NB * NB; i += TEAM) M[i] = 0.0;
+    __syncthreads();
+    /* 2. composite inertias: cm[p] += cm[b], ch[p] += ch[b], cJ[p] += cJ[b] for b = NB-1 .. 0 (13 components) */
+    if (lane < 13) {
+        double* base = lane == 0 ? w.cm : (lane < 4 ? &w.ch[0].x + (lane - 1) : &w.cJ[0].m[0] + (lane - 4));
+        const int stride = lane == 0 ? 1 : (lane < 4 ? 3 : 9);
+        double v[NB];
+#pragma unroll
+        for (int i = 0; i < NB; i++) v[i] = base[i * stride];
+#pragma unroll
+        for (int i = NB - 1; i >= 0; i--) {
+            const int p = UG_BODY_PARENT[i];
+            if (p >= 0) v[p] = v[p] + v[i];
+        }
+#pragma unroll
+        for (int i = 0; i < NB; i++) base[i * stride] = v[i];
+    }
+    __syncthreads();
+    /* 3. mass matrix column of body b: M[b][b] and M[j][b] = M[b][j] for its ancestors j */
+    if (own) {
+        SV F = spatial_inertia_mul(w.cm[b], w.ch[b], w.cJ[b], w.S[b]);
+        const SV Sb = w.S[b];
+        M[b * NB + b] = vdot(Sb.w, F.w) + vdot(Sb.v, F.v);
+        for (int j = UG_BODY_PARENT[b]; j >= 0; j = UG_BODY_PARENT[j]) {
+            double x = vdot(w.S[j].w, F.w) + vdot(w.S[j].v, F.v);
+            M[j * NB + b] = x;
+            M[b * NB + j] = x;
+        }
+    }
+    /* 4. RNEA forward, one tree level at a time; then the body's force (independent of the others) */
+    const int depth = own ? body_depth(b) : -1;
+    SV f;
+    f.w = V(0, 0, 0);
+    f.v = V(0, 0, 0);
+    SV Vbb;
+    Vbb.w = V(0, 0, 0);
+    Vbb.v = V(0, 0, 0);
+    for (int L = 0; L < NB; L++) {
+        if (own && depth == L) {
+            const int p = UG_BODY_PARENT[b];
+            SV Vp, Ap;
+            if (p < 0) { Vp.w = V(0, 0, 0); Vp.v = V(0, 0, 0); Ap.w = V(0, 0, 0); Ap.v = V(0, 0, -g); }
+            else { Vp = w.Vb[p]; Ap = w.Ab[p]; }
+            const SV Sb = w.S[b];
+            SV vj; vj.w = vscale(Sb.w, qd[b]); vj.v = vscale(Sb.v, qd[b]);
+            SV Vb, Ab;
+            Vb.w = vadd(Vp.w, vj.w); Vb.v = vadd(Vp.v, vj.v);
+            Ab.w = vadd(Ap.w, vcross(Vb.w, vj.w));
+            Ab.v = vadd(Ap.v, vadd(vcross(Vb.w, vj.v), vcross(Vb.v, vj.w)));
+            w.Vb[b] = Vb;
+            w.Ab[b] = Ab;
+            SV IA = spatial_inertia_mul(m, h, Jb, Ab);
+            SV IV = spatial_inertia_mul(m, h, Jb, Vb);
+            f.w = vadd(IA.w, vadd(vcross(Vb.w, IV.w), vcross(Vb.v, IV.v)));
+            f.v = vadd(IA.v, vcross(Vb.w, IV.v));
+            double wn = vlen(Vb.w);
+            m3 D = inertia_world(k.R[b], &UG_BODY_DAMPI[6 * b]);
+            v3 tau = vscale(mv(D, Vb.w), UG_ANG_DAMP + UG_ANG_DAMP * wn);
+            f.w = vadd(f.w, tau);
+            Vbb = Vb;
+        }
+        __syncthreads();
+    }
+    /* 5. link damping: lane l computes link l's force and torque; body b adds its links in link order */
+    if (lane >= 1 && lane < UG_NL) {
+        const int l = lane, bl = UG_LINK_BODY[l];
+        if (bl >= 0) {
+            v3 cl = vadd(k.p[bl], mv(k.R[bl], V(UG_LINK_COMP[3 * l], UG_LINK_COMP[3 * l + 1], UG_LINK_COMP[3 * l + 2])));
+            const SV Vl = w.Vb[bl];
+            v3 vl = vadd(Vl.v, vcross(Vl.w, cl));
+            double vn = vlen(vl);
+            v3 fd = vscale(vl, UG_LINK_MASS[l] * (UG_LIN_DAMP + UG_LIN_DAMP * vn));
+            w.fdl[l] = fd;
+            w.tl[l] = vcross(cl, fd);
+        }
+    }
+    __syncthreads();
+    if (own) {
+        for (int l = 1; l < UG_NL; l++) {
+            if (UG_LINK_BODY[l] != b) continue;
+            f.v = vadd(f.v, w.fdl[l]);
+            f.w = vadd(f.w, w.tl[l]);
+        }
+        w.f[b] = f;
+    }
+    __syncthreads();
+    /* 6. forces back up the tree (6 components, descending bodies), then C[b] = S_b . f_b */
+    if (lane < 6) {
+        double* base = (lane < 3 ? &w.f[0].w.x : &w.f[0].v.x) + (lane % 3);
+        const int stride = sizeof(SV) / sizeof(double);
+        double v[NB];
+#pragma unroll
+        for (int i = 0; i < NB; i++) v[i] = base[i * stride];
+#pragma unroll
+        for (int i = NB - 1; i >= 0; i--) {
+            const int p = UG_BODY_PARENT[i];
+            if (p >= 0) v[p] = v[p] + v[i];
+        }
+#pragma unroll
+        for (int i = 0; i < NB; i++) base[i * stride] = v[i];
+    }
+    __syncthreads();
+    if (own) {
+        const SV Sb = w.S[b], fb = w.f[b];
+        w.C[b] = vdot(Sb.w, fb.w) + vdot(Sb.v, fb.v);
+    }
+    __syncthreads();
+    (void)Vbb;
+}
 /* lane 0: external forces (robot gravity/gyroscopic/damping via CRBA + RNEA, free objects), the LDL^T of
  * the mass matrix, and the row enumeration */
 __device__ __noinline__ static void serial_pre(const Scene* s) {
@@ -1135,11 +1288,13 @@ __device__ __noinline__ static void serial_pre(const Scene* s) {
     EnvState& e = sh.e;
     const double dt = UG_DT;
     const int lane = threadIdx.x;
+    PROF_T0(t_rd);
+    team_robot_dynamics(s->gravity);
+    PROF_ADD(PF_RDYN, t_rd);
     if (lane == 0) {
         double C[NB];
-        PROF_T0(t_rd);
-        robot_dynamics(e.qd, sh.kin, s->gravity, sh.LDL, C, sh.u.dyn);
-        PROF_ADD(PF_RDYN, t_rd);
+#pragma unroll
+        for (int i = 0; i < NB; i++) C[i] = sh.u.dyn.C[i];
         /* LDL^T and the qdd solve with the matrix in registers (compile-time indices, same order) */
         double A[NB * NB];
 #pragma unroll
