@@ -23,6 +23,7 @@
 #ifndef UG_TEAM_H
 #define UG_TEAM_H
 
+#include <type_traits>
 #include <utility>
 
 #include "ug_device.h"
@@ -966,7 +967,7 @@ __device__ __forceinline__ double writelane_d(double old, double x) {
  * forms the clamped increment of its own row, lane (P & 63)'s is broadcast, applied to w and recorded in
  * that lane (the impulse itself is advanced after the section).  W holds each row's unclamped increment
  * u = rhs - (J dv) / D and A0 / A1 the negated, 1/D-scaled Delassus rows.  Chain: max, min, readlane, fma. */
-template <int P>
+template <int P, bool TWO>
 __device__ __forceinline__ void row_upd(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA, int lane,
                                         Lrow& L, double (&W)[2]) {
     constexpr int s = P >> 6, O = P & 63;
@@ -975,15 +976,16 @@ __device__ __forceinline__ void row_upd(const double (&A0)[PREG], const double (
     double dn = __builtin_fmin(__builtin_fmax(W[s], L.dlo[s]), L.dhi[s]);
     double d = readlane_d(dn, O);
     W[0] = __builtin_fma(a0, d, W[0]);
-    W[1] = __builtin_fma(a1, d, W[1]);
+    if (TWO) W[1] = __builtin_fma(a1, d, W[1]); /* slot 1 exists only with more than 64 rows */
     L.dsv[s] = writelane_d<O>(L.dsv[s], d);
 }
 /* after a section: the lanes whose row was solved advance their impulse by the recorded increment and
  * fold (delta / D)^2 into their residual */
+template <bool TWO>
 __device__ __forceinline__ void row_finish(Lrow& L, unsigned long long m0, unsigned long long m1, int lane,
                                            double& res) {
 #pragma unroll
-    for (int s = 0; s < 2; s++) {
+    for (int s = 0; s < (TWO ? 2 : 1); s++) {
         const bool did = (((s ? m1 : m0) >> lane) & 1ull) != 0ull;
         const double dn = L.dsv[s];
         double x = dn * L.rinv[s];
@@ -1004,46 +1006,46 @@ __device__ __forceinline__ unsigned long long pos_mask(int s, int a, int b, unsi
     return m & ~skip;
 }
 /* one 8-row chunk, rows in increasing (REV: decreasing) position, no per-row tests */
-template <int C, bool REV, int K>
+template <int C, bool REV, int K, bool TWO>
 __device__ __forceinline__ void chunk_rows(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA, int lane,
                                            Lrow& L, double (&W)[2]) {
     if constexpr (K < 8) {
-        row_upd<REV ? 8 * C + 7 - K : 8 * C + K>(A0, A1, wsA, lane, L, W);
-        chunk_rows<C, REV, K + 1>(A0, A1, wsA, lane, L, W);
+        row_upd<REV ? 8 * C + 7 - K : 8 * C + K, TWO>(A0, A1, wsA, lane, L, W);
+        chunk_rows<C, REV, K + 1, TWO>(A0, A1, wsA, lane, L, W);
     }
 }
 /* the chunks [c_lo, c_hi] of a section, in increasing (REV: decreasing) order.  Rows of those chunks
  * outside the section are neutral: the caller zeroes their increment bounds, so they broadcast +-0 and
  * leave u unchanged.  One scalar test per chunk instead of per row. */
-template <int I, bool REV, int NCH>
+template <int I, bool REV, int NCH, bool TWO>
 __device__ __forceinline__ void sweep_chunks(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA,
                                              int lane, int c_lo, int c_hi, Lrow& L, double (&W)[2]) {
     if constexpr (I < NCH) {
         constexpr int C = REV ? NCH - 1 - I : I;
-        if (C >= c_lo && C <= c_hi) chunk_rows<C, REV, 0>(A0, A1, wsA, lane, L, W);
-        sweep_chunks<I + 1, REV, NCH>(A0, A1, wsA, lane, c_lo, c_hi, L, W);
+        if (C >= c_lo && C <= c_hi) chunk_rows<C, REV, 0, TWO>(A0, A1, wsA, lane, L, W);
+        sweep_chunks<I + 1, REV, NCH, TWO>(A0, A1, wsA, lane, c_lo, c_hi, L, W);
     }
 }
 /* the section [a, b) (a < b): a copy of the lane rows with zero increment bounds outside it (and on the
  * rows set in skip), swept chunk-wise; the recorded increments come back in L.dsv */
-template <bool REV, int NCH>
+template <bool REV, int NCH, bool TWO>
 __device__ __forceinline__ void sweep_section(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA,
                                               int lane, int a, int b, unsigned long long sk0, unsigned long long sk1,
                                               Lrow& L, double (&W)[2]) {
     Lrow F = L;
-    bool in[2];
+    bool in[2] = {false, false};
 #pragma unroll
-    for (int s = 0; s < 2; s++) {
+    for (int s = 0; s < (TWO ? 2 : 1); s++) {
         const int p = lane + 64 * s;
         const bool skip = (((s ? sk1 : sk0) >> lane) & 1ull) != 0ull;
         in[s] = p >= a && p < b && !skip;
         F.dlo[s] = in[s] ? L.dlo[s] : 0.0;
         F.dhi[s] = in[s] ? L.dhi[s] : 0.0;
     }
-    sweep_chunks<0, REV, NCH>(A0, A1, wsA, lane, a >> 3, (b - 1) >> 3, F, W);
+    sweep_chunks<0, REV, NCH, TWO>(A0, A1, wsA, lane, a >> 3, (b - 1) >> 3, F, W);
     /* only the section's own records: a neutral row's record would clobber one still to be finished */
 #pragma unroll
-    for (int s = 0; s < 2; s++) L.dsv[s] = in[s] ? F.dsv[s] : L.dsv[s];
+    for (int s = 0; s < (TWO ? 2 : 1); s++) L.dsv[s] = in[s] ? F.dsv[s] : L.dsv[s];
 }
 /* warm start: normal rows [nnc, fb) with a carried impulse, w += A[:, P] * impulse */
 template <int P>
@@ -1431,94 +1433,101 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     double W[2] = {L.rhs[0], L.rhs[1]}; /* u */
     sweep_warm<0>(A0, A1, wsAr, lane, nnc, fb, L, W);
     PROF_ADD(PF_SPLIT, t_setup);
-    PROF_T0(t_sweeps);
 #ifdef UG_DEBUG_DUMP
     double* dbg = ws + WS_DBG;
     dump_A<0>(A0, A1, dbg, n, lane);
     dbg[MAXROWS * MAXROWS + lane] = W[0];
     dbg[MAXROWS * MAXROWS + 64 + lane] = W[1];
 #endif
-    int split = 0;
-    /* pass 0: the velocity solve; pass 1: the split-impulse pass (normals only, from zero) */
-#pragma nounroll
-    for (int pass = 0; pass < 2; pass++) {
-        const int pen = pass;
-        if (pen) {
-            int anypen = 0;
-#pragma unroll
-            for (int s = 0; s < 2; s++) {
-                const int p = lane + 64 * s;
-                anypen |= p >= nnc && p < fb && rhsPen[s] != 0.0;
-            }
-            split = ballot(anypen) != 0ull;
-            if (!split) break;
-#pragma unroll
-            for (int s = 0; s < 2; s++) {
-                L.rhs[s] = rhsPen[s];
-                L.imp[s] = 0.0;
-            }
-            W[0] = L.rhs[0];
-            W[1] = L.rhs[1];
-        }
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            L.dlo[s] = L.lo[s] - L.imp[s];
-            L.dhi[s] = L.hi[s] - L.imp[s];
-        }
-        for (int it = 0; it < UG_PGS_ITERS; it++) {
-            double res = 0.0;
-            /* opaque per-sweep copies: keeps the per-chunk scalar tests inside the loop */
-            int o_n = n, o_nnc = nnc, o_fb = fb;
-            gcdouble* o_wsA = wsAr;
-            asm volatile("" : "+s"(o_n), "+s"(o_nnc), "+s"(o_fb), "+s"(o_wsA));
-            /* (even sweeps) non-contact rows reversed, then [s0, fb) */
-            if (!pen && !(it & 1) && o_nnc > 0)
-                sweep_section<true, (NCMAX + 7) / 8>(A0, A1, o_wsA, lane, 0, o_nnc, 0ull, 0ull, L, W);
-            const int s0 = (pen || !(it & 1)) ? o_nnc : 0;
-            if (s0 < o_fb) sweep_section<false, MAXROWS / 8>(A0, A1, o_wsA, lane, s0, o_fb, 0ull, 0ull, L, W);
-            const int f0 = pen ? o_nnc : 0;
-            row_finish(L, pos_mask(0, f0, o_fb, 0ull), pos_mask(1, f0, o_fb, 0ull), lane, res);
-            /* friction and rolling rows: bounds +-mu * (their normal's impulse, final for this sweep),
-             * skipped while it is not positive.  A skipped row is made neutral (sweep_section):
-             * increment bounds [0, 0] give a delta of +-0, and u + a * (+-0) == u up to the sign of a
-             * zero u (which never reaches a non-zero result). */
-            if (!pen && o_fb < o_n) {
-                sh.u.impx[lane] = L.imp[0];
-                sh.u.impx[64 + lane] = L.imp[1];
-                __builtin_amdgcn_wave_barrier();
-                unsigned long long sk[2];
-#pragma unroll
+    /* the sweeps, specialised on whether slot 1 (rows 64..127) exists: with <= 64 rows the second u
+     * register, its fma and its bookkeeping drop out of every row */
+    auto passes = [&](auto two_tag) -> int {
+        constexpr bool TWO = decltype(two_tag)::value;
+        int split = 0;
+        PROF_T0(t_sw);
+        /* pass 0: the velocity solve; pass 1: the split-impulse pass (normals only, from zero) */
+    #pragma nounroll
+        for (int pass = 0; pass < 2; pass++) {
+            const int pen = pass;
+            if (pen) {
+                int anypen = 0;
+    #pragma unroll
                 for (int s = 0; s < 2; s++) {
                     const int p = lane + 64 * s;
-                    const bool isf = p >= o_fb && p < o_n;
-                    double tot = sh.u.impx[isf ? nrow[s] : 0];
-                    const bool skip = isf && !(tot > 0.0);
-                    L.lo[s] = isf ? -(fric[s] * tot) : L.lo[s];
-                    L.hi[s] = isf ? fric[s] * tot : L.hi[s];
-                    L.dlo[s] = L.lo[s] - L.imp[s];
-                    L.dhi[s] = L.hi[s] - L.imp[s];
-                    sk[s] = ballot(skip);
+                    anypen |= p >= nnc && p < fb && rhsPen[s] != 0.0;
                 }
-                __builtin_amdgcn_wave_barrier();
-                sweep_section<false, MAXROWS / 8>(A0, A1, o_wsA, lane, o_fb, o_n, sk[0], sk[1], L, W);
-                row_finish(L, pos_mask(0, o_fb, o_n, sk[0]), pos_mask(1, o_fb, o_n, sk[1]), lane, res);
+                split = ballot(anypen) != 0ull;
+                if (!split) break;
+    #pragma unroll
+                for (int s = 0; s < 2; s++) {
+                    L.rhs[s] = rhsPen[s];
+                    L.imp[s] = 0.0;
+                }
+                W[0] = L.rhs[0];
+                W[1] = L.rhs[1];
             }
-            PROF_CNT(PC_ITERS, 1);
-            if (ballot(!(res <= UG_RESIDUAL_THR)) == 0ull || it >= UG_PGS_ITERS - 1) break;
+    #pragma unroll
+            for (int s = 0; s < 2; s++) {
+                L.dlo[s] = L.lo[s] - L.imp[s];
+                L.dhi[s] = L.hi[s] - L.imp[s];
+            }
+            for (int it = 0; it < UG_PGS_ITERS; it++) {
+                double res = 0.0;
+                /* opaque per-sweep copies: keeps the per-chunk scalar tests inside the loop */
+                int o_n = n, o_nnc = nnc, o_fb = fb;
+                gcdouble* o_wsA = wsAr;
+                asm volatile("" : "+s"(o_n), "+s"(o_nnc), "+s"(o_fb), "+s"(o_wsA));
+                /* (even sweeps) non-contact rows reversed, then [s0, fb) */
+                if (!pen && !(it & 1) && o_nnc > 0)
+                    sweep_section<true, (NCMAX + 7) / 8, TWO>(A0, A1, o_wsA, lane, 0, o_nnc, 0ull, 0ull, L, W);
+                const int s0 = (pen || !(it & 1)) ? o_nnc : 0;
+                if (s0 < o_fb) sweep_section<false, TWO ? MAXROWS / 8 : 8, TWO>(A0, A1, o_wsA, lane, s0, o_fb, 0ull, 0ull, L, W);
+                const int f0 = pen ? o_nnc : 0;
+                row_finish<TWO>(L, pos_mask(0, f0, o_fb, 0ull), pos_mask(1, f0, o_fb, 0ull), lane, res);
+                /* friction and rolling rows: bounds +-mu * (their normal's impulse, final for this sweep),
+                 * skipped while it is not positive.  A skipped row is made neutral (sweep_section):
+                 * increment bounds [0, 0] give a delta of +-0, and u + a * (+-0) == u up to the sign of a
+                 * zero u (which never reaches a non-zero result). */
+                if (!pen && o_fb < o_n) {
+                    g_sh.u.impx[lane] = L.imp[0];
+                    g_sh.u.impx[64 + lane] = L.imp[1];
+                    __builtin_amdgcn_wave_barrier();
+                    unsigned long long sk[2] = {0ull, 0ull};
+    #pragma unroll
+                    for (int s = 0; s < (TWO ? 2 : 1); s++) {
+                        const int p = lane + 64 * s;
+                        const bool isf = p >= o_fb && p < o_n;
+                        double tot = g_sh.u.impx[isf ? nrow[s] : 0];
+                        const bool skip = isf && !(tot > 0.0);
+                        L.lo[s] = isf ? -(fric[s] * tot) : L.lo[s];
+                        L.hi[s] = isf ? fric[s] * tot : L.hi[s];
+                        L.dlo[s] = L.lo[s] - L.imp[s];
+                        L.dhi[s] = L.hi[s] - L.imp[s];
+                        sk[s] = ballot(skip);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    sweep_section<false, TWO ? MAXROWS / 8 : 8, TWO>(A0, A1, o_wsA, lane, o_fb, o_n, sk[0], sk[1], L, W);
+                    row_finish<TWO>(L, pos_mask(0, o_fb, o_n, sk[0]), pos_mask(1, o_fb, o_n, sk[1]), lane, res);
+                }
+                PROF_CNT(PC_ITERS, 1);
+                if (ballot(!(res <= UG_RESIDUAL_THR)) == 0ull || it >= UG_PGS_ITERS - 1) break;
+            }
+            if (!pen) {
+                PROF_ADD(PF_SWEEPS, t_sw);
+    #pragma unroll
+                for (int s = 0; s < 2; s++)
+                    if (lane + 64 * s < n) g_sh.rs[lane + 64 * s].imp = L.imp[s];
+    #ifdef UG_DEBUG_DUMP
+                dbg[MAXROWS * MAXROWS + 128 + lane] = W[0];
+                dbg[MAXROWS * MAXROWS + 192 + lane] = W[1];
+                dbg[MAXROWS * MAXROWS + 256 + lane] = L.imp[0];
+                dbg[MAXROWS * MAXROWS + 320 + lane] = L.imp[1];
+    #endif
+            }
         }
-        if (!pen) {
-            PROF_ADD(PF_SWEEPS, t_sweeps);
-#pragma unroll
-            for (int s = 0; s < 2; s++)
-                if (lane + 64 * s < n) sh.rs[lane + 64 * s].imp = L.imp[s];
-#ifdef UG_DEBUG_DUMP
-            dbg[MAXROWS * MAXROWS + 128 + lane] = W[0];
-            dbg[MAXROWS * MAXROWS + 192 + lane] = W[1];
-            dbg[MAXROWS * MAXROWS + 256 + lane] = L.imp[0];
-            dbg[MAXROWS * MAXROWS + 320 + lane] = L.imp[1];
-#endif
-        }
-    }
+        return split;
+    };
+    const int split = n > 64 ? passes(std::true_type{}) : passes(std::false_type{});
     /* dv[d] (dvs[d]) = fma chain over positions k of M^-1J_k[d] * impulse_k (lane d < NV) */
     __builtin_amdgcn_wave_barrier();
     if (split) {
