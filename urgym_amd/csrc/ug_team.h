@@ -926,9 +926,10 @@ __device__ __noinline__ static void build_row(const Scene* s, int pos, double* w
  * fma per slot: u += NB[:, P] * delta.  No cross-lane reduction and no LDS traffic inside a sweep.  The
  * owner lane records the increment; its impulse and residual are advanced after the section.  Row
  * positions are template parameters, so A0[P] / A1[P] are compile-time register names and every
- * row-range test is a scalar branch.  Columns P >= PREG come from the global workspace.  Arithmetic
+ * row-range test is a scalar branch (one per CHUNK rows).  Columns P >= PREG come from the global workspace.  Arithmetic
  * order is the oracle's pgs() (oracle/ug_oracle.c). */
 #define NCMAX (2 * NB + 12) /* limits (both sides) + 7 motors + 5 gears */
+#define CHUNK 8             /* rows per branch-free sweep chunk (one scalar test per chunk; 4 measured slower) */
 typedef __attribute__((address_space(1))) const double gcdouble;
 typedef __attribute__((address_space(1))) double gdouble;
 struct Lrow { /* the two rows this lane owns (slot s: position lane + 64 s) */
@@ -1005,12 +1006,12 @@ __device__ __forceinline__ unsigned long long pos_mask(int s, int a, int b, unsi
     unsigned long long m = (l1 - l0 == 64) ? ~0ull : (((1ull << (l1 - l0)) - 1ull) << l0);
     return m & ~skip;
 }
-/* one 8-row chunk, rows in increasing (REV: decreasing) position, no per-row tests */
+/* one CHUNK-row chunk, rows in increasing (REV: decreasing) position, no per-row tests */
 template <int C, bool REV, int K, bool TWO>
 __device__ __forceinline__ void chunk_rows(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA, int lane,
                                            Lrow& L, double (&W)[2]) {
-    if constexpr (K < 8) {
-        row_upd<REV ? 8 * C + 7 - K : 8 * C + K, TWO>(A0, A1, wsA, lane, L, W);
+    if constexpr (K < CHUNK) {
+        row_upd<REV ? CHUNK * C + CHUNK - 1 - K : CHUNK * C + K, TWO>(A0, A1, wsA, lane, L, W);
         chunk_rows<C, REV, K + 1, TWO>(A0, A1, wsA, lane, L, W);
     }
 }
@@ -1042,7 +1043,7 @@ __device__ __forceinline__ void sweep_section(const double (&A0)[PREG], const do
         F.dlo[s] = in[s] ? L.dlo[s] : 0.0;
         F.dhi[s] = in[s] ? L.dhi[s] : 0.0;
     }
-    sweep_chunks<0, REV, NCH, TWO>(A0, A1, wsA, lane, a >> 3, (b - 1) >> 3, F, W);
+    sweep_chunks<0, REV, NCH, TWO>(A0, A1, wsA, lane, a / CHUNK, (b - 1) / CHUNK, F, W);
     /* only the section's own records: a neutral row's record would clobber one still to be finished */
 #pragma unroll
     for (int s = 0; s < (TWO ? 2 : 1); s++) L.dsv[s] = in[s] ? F.dsv[s] : L.dsv[s];
@@ -1479,9 +1480,9 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                 asm volatile("" : "+s"(o_n), "+s"(o_nnc), "+s"(o_fb), "+s"(o_wsA));
                 /* (even sweeps) non-contact rows reversed, then [s0, fb) */
                 if (!pen && !(it & 1) && o_nnc > 0)
-                    sweep_section<true, (NCMAX + 7) / 8, TWO>(A0, A1, o_wsA, lane, 0, o_nnc, 0ull, 0ull, L, W);
+                    sweep_section<true, (NCMAX + CHUNK - 1) / CHUNK, TWO>(A0, A1, o_wsA, lane, 0, o_nnc, 0ull, 0ull, L, W);
                 const int s0 = (pen || !(it & 1)) ? o_nnc : 0;
-                if (s0 < o_fb) sweep_section<false, TWO ? MAXROWS / 8 : 8, TWO>(A0, A1, o_wsA, lane, s0, o_fb, 0ull, 0ull, L, W);
+                if (s0 < o_fb) sweep_section<false, TWO ? MAXROWS / CHUNK : 64 / CHUNK, TWO>(A0, A1, o_wsA, lane, s0, o_fb, 0ull, 0ull, L, W);
                 const int f0 = pen ? o_nnc : 0;
                 row_finish<TWO>(L, pos_mask(0, f0, o_fb, 0ull), pos_mask(1, f0, o_fb, 0ull), lane, res);
                 /* friction and rolling rows: bounds +-mu * (their normal's impulse, final for this sweep),
@@ -1506,7 +1507,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                         sk[s] = ballot(skip);
                     }
                     __builtin_amdgcn_wave_barrier();
-                    sweep_section<false, TWO ? MAXROWS / 8 : 8, TWO>(A0, A1, o_wsA, lane, o_fb, o_n, sk[0], sk[1], L, W);
+                    sweep_section<false, TWO ? MAXROWS / CHUNK : 64 / CHUNK, TWO>(A0, A1, o_wsA, lane, o_fb, o_n, sk[0], sk[1], L, W);
                     row_finish<TWO>(L, pos_mask(0, o_fb, o_n, sk[0]), pos_mask(1, o_fb, o_n, sk[1]), lane, res);
                 }
                 PROF_CNT(PC_ITERS, 1);
