@@ -89,6 +89,7 @@ struct Shared {
     double a12[NB];
     double fs[8];
     int is[8];
+    int ecnt[2 * MAXMAN]; /* team_enumerate: accepted points / rolling points per manifold */
 #ifdef UG_PROF
     unsigned long long prof[UG_NPROF];
 #endif
@@ -684,6 +685,92 @@ __device__ static void enumerate_rows(Shared& sh, const Scene* s) {
     }
     n = nnc + nn + nf + 2 * nroll;
     sh.nrows = n; sh.nnc = nnc; sh.nn = nn; sh.nf = nf;
+}
+/* enumerate_rows, wave-parallel: lane per limit side / motor / gear / manifold, positions by prefix
+ * counts.  Identical output when every contact point fits (the usual case); when the capacity check
+ * of the serial code would reject points, the serial enumeration runs instead. */
+__device__ __noinline__ static void team_enumerate(const Scene* s) {
+    Shared& sh = g_sh;
+    EnvState& e = sh.e;
+    const int lane = threadIdx.x;
+    /* non-contact rows: limits (dof, side) in index order, enabled motors, the 5 gears (<= NCMAX rows) */
+    const bool lim = lane < 2 * NB && ([&] {
+        const int d = lane >> 1, side = lane & 1;
+        double pen = side == 0 ? e.q[d] - UG_DOF_LOWER[d] : UG_DOF_UPPER[d] - e.q[d];
+        return !(pen > 0);
+    })();
+    const unsigned long long mlim = ballot(lim);
+    const int nlim = __popcll(mlim);
+    if (lim) {
+        RowS& r = sh.rs[lane_prefix(mlim)];
+        r.kind = 0; r.a = lane >> 1; r.b = lane & 1;
+    }
+    const bool mot = lane < 7 && e.mon[lane < 7 ? lane : 0] != 0.0;
+    const unsigned long long mmot = ballot(mot);
+    const int nmot = __popcll(mmot);
+    if (mot) {
+        RowS& r = sh.rs[nlim + lane_prefix(mmot)];
+        r.kind = 1; r.a = lane;
+    }
+    if (lane < 5) {
+        RowS& r = sh.rs[nlim + nmot + lane];
+        r.kind = 2; r.a = lane;
+    }
+    const int nnc = nlim + nmot + 5;
+    /* contact points per manifold (lane m) */
+    const int nman = (int)e.nman;
+    int npt = 0, nroll = 0;
+    if (lane < nman) {
+        const PairDef& P = s->pair[(int)e.man[lane].pair];
+        int bA, bB;
+        int eA = ent_of_collider(s->col[P.a], bA), eB = ent_of_collider(s->col[P.b], bB);
+        if (!(eA < 0 && eB < 0)) {
+            npt = (int)e.man[lane].npts;
+            nroll = P.rolling > 0.0 ? npt : 0;
+        }
+        sh.ecnt[lane] = npt;
+        sh.ecnt[MAXMAN + lane] = nroll;
+    }
+    __builtin_amdgcn_wave_barrier();
+    int pbase = 0, rbase = 0, tp = 0, tr = 0;
+    for (int m = 0; m < nman; m++) {
+        const int a = sh.ecnt[m], r = sh.ecnt[MAXMAN + m];
+        if (m < lane) { pbase += a; rbase += r; }
+        tp += a;
+        tr += r;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int total = nnc + 3 * tp + 2 * tr;
+    if (total > MAXROWS) { /* the serial code's capacity checks decide which points are kept */
+        if (lane == 0) enumerate_rows(sh, s);
+        return;
+    }
+    const int nn = tp, nf = 2 * tp;
+    if (lane < nman) {
+        for (int j = 0; j < npt; j++) {
+            const int pn = nnc + pbase + j;
+            RowS& r = sh.rs[pn];
+            r.kind = 3; r.a = lane; r.b = j; r.nrow = pn;
+#pragma unroll
+            for (int f = 0; f < 2; f++) {
+                RowS& q = sh.rs[nnc + nn + 2 * (pbase + j) + f];
+                q.kind = 4 + f; q.a = lane; q.b = j; q.nrow = pn;
+            }
+            if (nroll) {
+#pragma unroll
+                for (int f = 0; f < 2; f++) {
+                    RowS& q = sh.rs[nnc + nn + nf + 2 * (rbase + j) + f];
+                    q.kind = 6 + f; q.a = lane; q.b = j; q.nrow = pn;
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        sh.nrows = nnc + nn + nf + 2 * tr;
+        sh.nnc = nnc;
+        sh.nn = nn;
+        sh.nf = nf;
+    }
 }
 /* ---- register-resident row build: every array index below is a compile-time constant (fully unrolled
  * loops, selects instead of dynamic stores), so the per-lane arrays stay in VGPRs instead of scratch.
@@ -1330,10 +1417,11 @@ __device__ __noinline__ static void serial_pre(const Scene* s) {
             sh.v0[off] = ob.v.x; sh.v0[off + 1] = ob.v.y; sh.v0[off + 2] = ob.v.z;
             sh.v0[off + 3] = ob.w.x; sh.v0[off + 4] = ob.w.y; sh.v0[off + 5] = ob.w.z;
         }
-        PROF_T0(t_en);
-        enumerate_rows(sh, s);
-        PROF_ADD(PF_ENUM, t_en);
     }
+    __syncthreads();
+    PROF_T0(t_en);
+    team_enumerate(s);
+    PROF_ADD(PF_ENUM, t_en);
 }
 /* lane 0: velocities += solver delta, positions integrate (v + split velocity) */
 __device__ __noinline__ static void serial_post(const Scene* s, int split) {
