@@ -264,9 +264,9 @@ __global__ void __launch_bounds__(TEAM, 1) k_reset(const Scene* sc, double* S, u
 __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, uint32_t* mt, int* elapsed, double* ws,
                                                   int n, const float* act, double* obs, double* final_obs, double* rew,
                                                   uint8_t* term, uint8_t* trunc, uint8_t* succ, int32_t* substeps,
-                                                  int autoreset, int max_steps) {
-    const int i = blockIdx.x;
-    if (i >= n) return;
+                                                  int autoreset, int max_steps, const int* order, uint8_t* prio) {
+    if ((int)blockIdx.x >= n) return;
+    const int i = order[blockIdx.x];
     double* Si = S + (size_t)i * UG_STATE_DIM;
     team_load(Si);
     const int O = task_obs_dim(sc->variant), A = task_act_dim(sc->variant);
@@ -291,7 +291,38 @@ __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, ui
         if (trunc) trunc[i] = (uint8_t)io.trunc;
         if (succ) succ[i] = (uint8_t)io.succ;
         if (substeps) substeps[i] = ns;
+        prio[i] = (uint8_t)team_priority(sc, ns, elapsed[i] + 1, max_steps, autoreset);
     }
+}
+
+/* next launch order: envs by descending priority (stable counting sort, one block; deterministic) */
+#define ORDER_THREADS 1024
+__global__ void __launch_bounds__(ORDER_THREADS) k_order(const uint8_t* prio, int* order, int n) {
+    __shared__ int wsum[ORDER_THREADS / WAVE];
+    __shared__ int base;
+    const int t = threadIdx.x, w = t / WAVE, l = t % WAVE;
+    if (t == 0) base = 0;
+    __syncthreads();
+    for (int b = 15; b >= 0; b--) {
+        for (int c = 0; c < n; c += ORDER_THREADS) {
+            const int i = c + t;
+            const bool f = i < n && prio[i] == b;
+            const unsigned long long m = __ballot(f);
+            if (l == 0) wsum[w] = __popcll(m);
+            __syncthreads();
+            int off = base;
+            for (int k = 0; k < w; k++) off += wsum[k];
+            if (f) order[off + __popcll(m & ((1ull << l) - 1ull))] = i;
+            __syncthreads();
+            if (t == 0)
+                for (int k = 0; k < ORDER_THREADS / WAVE; k++) base += wsum[k];
+            __syncthreads();
+        }
+    }
+}
+__global__ void k_iota(int* order, uint8_t* prio, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) { order[i] = i; prio[i] = 0; }
 }
 
 __global__ void __launch_bounds__(TEAM, 1) k_substep(const Scene* sc, double* S, double* ws, int n) {
@@ -344,6 +375,8 @@ struct urgym_handle {
     double *d_obs = nullptr, *d_final = nullptr, *d_rew = nullptr, *d_draws = nullptr, *d_aux = nullptr;
     uint8_t *d_term = nullptr, *d_trunc = nullptr, *d_succ = nullptr, *d_mask = nullptr;
     int32_t* d_sub = nullptr;
+    int* d_order = nullptr;   // k_step launch order (blockIdx -> env), from the previous step's priorities
+    uint8_t* d_prio = nullptr;
     int autoreset = 0, max_steps = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
@@ -417,6 +450,10 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     HIPCHK(h, hipMalloc(&h->d_succ, N));
     HIPCHK(h, hipMalloc(&h->d_mask, N));
     HIPCHK(h, hipMalloc(&h->d_sub, sizeof(int32_t) * N));
+    HIPCHK(h, hipMalloc(&h->d_order, sizeof(int) * N));
+    HIPCHK(h, hipMalloc(&h->d_prio, N));
+    k_iota<<<grid_of(n), WAVE, 0, h->stream>>>(h->d_order, h->d_prio, n);
+    HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipMemsetAsync(h->d_state, 0, sizeof(double) * UG_STATE_DIM * N, h->stream));
     HIPCHK(h, hipMemsetAsync(h->d_elapsed, 0, sizeof(int) * N, h->stream));
     // per-env MT19937 streams seeded with seed + env_offset + i, UG_MT_WORDS words per env
@@ -451,7 +488,7 @@ void urgym_destroy(urgym_handle* h) {
     hipSetDevice(h->dev);
     if (h->stream) hipStreamSynchronize(h->stream);
     void* ptrs[] = {h->d_scene, h->d_state, h->d_ws, h->d_mt, h->d_elapsed, h->d_act, h->d_obs, h->d_final, h->d_rew,
-                    h->d_draws, h->d_aux, h->d_term, h->d_trunc, h->d_succ, h->d_mask, h->d_sub};
+                    h->d_draws, h->d_aux, h->d_term, h->d_trunc, h->d_succ, h->d_mask, h->d_sub, h->d_order, h->d_prio};
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -518,9 +555,12 @@ int urgym_step_device(urgym_handle* h, const float* d_act, double* d_obs, double
     HIPCHK(h, hipSetDevice(h->dev));
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
     k_step<<<h->n, TEAM, 0, h->stream>>>(h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->d_ws, h->n, d_act, d_obs,
-                                          d_final, d_rew, d_term, d_trunc, d_succ, d_sub, h->autoreset, h->max_steps);
+                                          d_final, d_rew, d_term, d_trunc, d_succ, d_sub, h->autoreset, h->max_steps, h->d_order,
+                                          h->d_prio);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+    k_order<<<1, ORDER_THREADS, 0, h->stream>>>(h->d_prio, h->d_order, h->n);
+    HIPCHK(h, hipGetLastError());
     h->timed = true;
     return 0;
 }

@@ -2094,6 +2094,34 @@ __device__ static void team_prof_flush() {
     if (threadIdx.x < UG_NPROF) atomicAdd(&g_prof[threadIdx.x], sh.prof[threadIdx.x]);
 #endif
 }
+/* Launch-order priority of an env for the next k_step (0..15, higher runs first).  The launch time is the
+ * longest env chain, and an env-step that ends its episode carries a ~170-substep autoreset: envs likely
+ * to end next step are dispatched first so their reset overlaps the other envs' steps.  Scheduling only --
+ * every env computes the same thing whatever its position in the launch.  Predicted truncation: 15;
+ * BallBalance: how far the ball is (now, and extrapolated ~2 env-steps) towards / past the paddle's edge;
+ * otherwise the env's last substep count (longest first). */
+__device__ static int team_priority(const Scene* s, int nsub, int el_next, int max_steps, int autoreset) {
+    const EnvState& e = g_sh.e;
+    if (autoreset && max_steps > 0 && el_next >= max_steps) return 15;
+    if (s->task == UG_TASK_BALLBALANCE && e.oactive[0] != 0.0 && e.oactive[1] != 0.0) {
+        const m3 R = qmat(e.obj[0].quat);
+        const v3 r = vsub(e.obj[1].pos, e.obj[0].pos);
+        const v3 rv = vsub(e.obj[1].v, e.obj[0].v);
+        const double T = 24.0 * UG_DT;
+        double f = 0.0;
+        for (int k = 0; k < 2; k++) {
+            const v3 l = mtv(R, k ? vadd(r, vscale(rv, T)) : r);
+            double g = fmax(fabs(l.x) / UG_BB_PADDLE_HX, fabs(l.y) / UG_BB_PADDLE_HY);
+            if (l.z < UG_BB_PADDLE_HZ) g = fmax(g, 1.0);
+            f = fmax(f, g);
+        }
+        const int b = (int)(f * 10.0);
+        return b > 14 ? 14 : (b < 0 ? 0 : b);
+    }
+    int b = 0;
+    while (b < 14 && (2 << b) <= nsub) b++;
+    return b;
+}
 /* manifold slots beyond nman are written as (pair -1, zeros), as ugo_get_state does */
 __device__ static void team_store(double* S) {
     const Shared& sh = g_sh;
