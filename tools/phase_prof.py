@@ -20,7 +20,7 @@ os.environ.setdefault("URGYM_LIB", os.path.join(ROOT, "urgym_amd", "_lib", "libu
 NAMES = ["collide", "dyn+enum", "rows", "pgs", "pgs_setup", "integrate", "glue", "total",
          "substeps", "nrows", "pgs_iters", "overlap_pairs", "hull_pairs", "manifolds", "pgs_sweeps", "hull_narrowphase",
          "robot_dynamics", "enumerate", "broadphase", "pair_narrowphase",
-         "hullbox_vertices", "hullbox_corners", "hullbox_reduce"]
+         "hullbox_vertices", "hullbox_corners", "hullbox_reduce", "fk"]
 
 
 def main():
@@ -36,14 +36,15 @@ def main():
     sim.sync()
     rc = sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     assert rc == 0, "library not built with -DUG_PROF"
-    print("reset:", json.dumps(dict(zip(NAMES, (int(x) for x in buf[:14])))))
+    r = {k: float(v) for k, v in zip(NAMES, buf[:24])}
+    print("reset (cycles per substep):", json.dumps({k: round(r[k] / max(r["substeps"], 1), 1) for k in NAMES}))
     rng = np.random.default_rng(1)
     for _ in range(a.steps):
         sim.step(rng.uniform(-0.1, 0.1, size=(a.envs, 3)).astype(np.float32))
     sim.sync()
     sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     es = a.envs * a.steps
-    d = {k: float(v) for k, v in zip(NAMES, buf[:23])}
+    d = {k: float(v) for k, v in zip(NAMES, buf[:24])}
     out = {"per_env_step_cycles": {k: d[k] / es for k in NAMES[:8]},
            "substeps_per_env_step": d["substeps"] / es,
            "rows_per_substep": d["nrows"] / max(d["substeps"], 1),
@@ -56,7 +57,7 @@ def main():
     out["pgs_sweep_cycles_per_row_update"] = d["pgs_sweeps"] / max(d["nrows"] * d["pgs_iters"] / max(d["substeps"], 1), 1)
     for k in ("dyn+enum", "rows", "pgs", "pgs_setup", "pgs_sweeps", "hull_narrowphase", "robot_dynamics",
               "enumerate", "broadphase", "pair_narrowphase", "hullbox_vertices", "hullbox_corners",
-              "hullbox_reduce", "integrate"):
+              "hullbox_reduce", "fk", "integrate"):
         out[k + "_cycles_per_substep"] = d[k] / max(d["substeps"], 1)
     print(json.dumps(out, indent=1))
     sim.close()

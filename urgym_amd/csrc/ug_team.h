@@ -117,7 +117,7 @@ __device__ unsigned long long g_prof[UG_NPROF];
 #endif
 enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_TOTAL,
        PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN, PF_SWEEPS, PF_HULL,
-       PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE };
+       PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE, PF_FK };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -1459,8 +1459,37 @@ __device__ __noinline__ static void serial_post(const Scene* s, int split) {
         }
     }
 }
+/* fk() wave-parallel: lane b < NB forms its joint rotation, then the tree is composed one level at a
+ * time (same operations as fk(), parent frames read from LDS) */
 __device__ __noinline__ static void serial_fk() {
-    if (threadIdx.x == 0) fk(g_sh.e.q, g_sh.kin);
+    Kin& k = g_sh.kin;
+    const int lane = threadIdx.x;
+    const bool own = lane < NB;
+    const int b = own ? lane : 0;
+    const int pb = UG_BODY_PARENT[b];
+    const m3 Rpb = mload(&UG_BODY_R[9 * b]);
+    const v3 Ppb = V(UG_BODY_P[3 * b], UG_BODY_P[3 * b + 1], UG_BODY_P[3 * b + 2]);
+    const v3 ax = V(UG_BODY_AXIS[3 * b], UG_BODY_AXIS[3 * b + 1], UG_BODY_AXIS[3 * b + 2]);
+    const v3 com = V(UG_BODY_COM[3 * b], UG_BODY_COM[3 * b + 1], UG_BODY_COM[3 * b + 2]);
+    const m3 Rj = axis_angle(ax, g_sh.e.q[b]);
+    const int depth = own ? body_depth(b) : -1;
+    for (int L = 0; L < NB; L++) {
+        if (depth == L) {
+            m3 Rp;
+            v3 pp;
+            if (pb < 0) { Rp = mident(); pp = V(0, 0, 0); }
+            else { Rp = k.R[pb]; pp = k.p[pb]; }
+            const m3 Rtmp = mm(Rp, Rpb);
+            const m3 R = mm(Rtmp, Rj);
+            const v3 p = vadd(pp, mv(Rp, Ppb));
+            k.R[b] = R;
+            k.p[b] = p;
+            k.a[b] = mv(Rtmp, ax);
+            k.c[b] = vadd(p, mv(R, com));
+        }
+        __syncthreads();
+        if (ballot(depth > L) == 0ull) break;
+    }
 }
 
 #ifdef UG_DEBUG_DUMP
@@ -1643,6 +1672,7 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     PROF_T0(t_col);
     serial_fk();
     __syncthreads();
+    PROF_ADD(PF_FK, t_col);
     team_collide(s, ws);
     PROF_ADD(PF_COLLIDE, t_col);
     PROF_T0(t_dyn);
