@@ -20,7 +20,8 @@ os.environ.setdefault("URGYM_LIB", os.path.join(ROOT, "urgym_amd", "_lib", "libu
 NAMES = ["collide", "dyn+enum", "rows", "pgs", "pgs_setup", "integrate", "glue", "total",
          "substeps", "nrows", "pgs_iters", "overlap_pairs", "hull_pairs", "manifolds", "pgs_sweeps", "hull_narrowphase",
          "robot_dynamics", "enumerate", "broadphase", "pair_narrowphase",
-         "hullbox_vertices", "hullbox_corners", "hullbox_reduce", "fk"]
+         "hullbox_vertices", "hullbox_corners", "hullbox_reduce", "fk", "lane0_ldl_objects", "unit_solves",
+         "row_build", "rb_jacobians", "rb_solves", "rb_scalars"]
 
 
 def main():
@@ -31,12 +32,12 @@ def main():
     from urgym_amd._native import Sim
     sim = Sim(0, a.envs, seed=20241220)
     sim.set_autoreset(True, 500)
-    buf = np.zeros(24, np.uint64)
+    buf = np.zeros(32, np.uint64)
     sim.reset()
     sim.sync()
     rc = sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     assert rc == 0, "library not built with -DUG_PROF"
-    r = {k: float(v) for k, v in zip(NAMES, buf[:24])}
+    r = {k: float(v) for k, v in zip(NAMES, buf[:30])}
     print("reset (cycles per substep):", json.dumps({k: round(r[k] / max(r["substeps"], 1), 1) for k in NAMES}))
     rng = np.random.default_rng(1)
     for _ in range(a.steps):
@@ -44,7 +45,7 @@ def main():
     sim.sync()
     sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     es = a.envs * a.steps
-    d = {k: float(v) for k, v in zip(NAMES, buf[:24])}
+    d = {k: float(v) for k, v in zip(NAMES, buf[:30])}
     out = {"per_env_step_cycles": {k: d[k] / es for k in NAMES[:8]},
            "substeps_per_env_step": d["substeps"] / es,
            "rows_per_substep": d["nrows"] / max(d["substeps"], 1),
@@ -57,7 +58,8 @@ def main():
     out["pgs_sweep_cycles_per_row_update"] = d["pgs_sweeps"] / max(d["nrows"] * d["pgs_iters"] / max(d["substeps"], 1), 1)
     for k in ("dyn+enum", "rows", "pgs", "pgs_setup", "pgs_sweeps", "hull_narrowphase", "robot_dynamics",
               "enumerate", "broadphase", "pair_narrowphase", "hullbox_vertices", "hullbox_corners",
-              "hullbox_reduce", "fk", "integrate"):
+              "hullbox_reduce", "fk", "lane0_ldl_objects", "unit_solves", "row_build", "rb_jacobians", "rb_solves",
+              "rb_scalars", "integrate"):
         out[k + "_cycles_per_substep"] = d[k] / max(d["substeps"], 1)
     print(json.dumps(out, indent=1))
     sim.close()

@@ -32,7 +32,7 @@
 namespace ugd {
 
 #define TEAM 64
-#define UG_NPROF 24 /* phase accumulators of the -DUG_PROF build */
+#define UG_NPROF 32 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* per-env global workspace (L2-resident): old manifolds (collision), every row's J | M^-1 J^T (24 + 24
@@ -45,7 +45,7 @@ namespace ugd {
 #else
 #define WS_DOUBLES (WS_A + (MAXROWS - PREG) * MAXROWS)
 #endif
-#define STAGE 24
+
 #define MAXOV 40
 
 /* ---------------- env state (canonical layout) ---------------- */
@@ -80,7 +80,7 @@ struct Shared {
     int nrows, nnc, nn, nf, split;
     RowS rs[MAXROWS];
     union {
-        double stage[STAGE][48];
+        double mcol[NB + 5][NB]; /* row build: M^-1 e_d (d < NB) and M^-1 (ratio_g e_child_g) of gear g */
         struct { Cand c[MAXOV][4]; int n[MAXOV]; } cand;
         double impx[MAXROWS]; /* PGS: row impulses gathered through LDS (after the Delassus build) */
         DynWork dyn;          /* serial_pre: robot_dynamics work arrays */
@@ -90,6 +90,7 @@ struct Shared {
     double fs[8];
     int is[8];
     int ecnt[2 * MAXMAN]; /* team_enumerate: accepted points / rolling points per manifold */
+    int anc[NB];          /* bit d set: dof d moves body b (moves(d, b)); filled by team_load */
 #ifdef UG_PROF
     unsigned long long prof[UG_NPROF];
 #endif
@@ -117,7 +118,7 @@ __device__ unsigned long long g_prof[UG_NPROF];
 #endif
 enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_TOTAL,
        PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN, PF_SWEEPS, PF_HULL,
-       PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE, PF_FK };
+       PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE, PF_FK, PF_LDL, PF_UNIT, PF_ROWB, PF_RB1, PF_RB2, PF_RB3 };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -219,6 +220,7 @@ __device__ static inline void man_to_st(StMan& S, const Manifold& M) {
 }
 
 /* ---------------- collision ---------------- */
+#define HB_FACE_UNROLL 12 /* covers hulls of up to 96 faces (the model's largest has 89) */
 /* hull (A, robot link) vs box (B): the whole wave.  Produces cand k (<= 4 points) in sh.u.cand. */
 __device__ __noinline__ static void team_reduce4(int n, int k);
 __device__ __noinline__ static void team_hull_box(const Collider& A, const Collider& B, const XF& TA, const XF& TB,
@@ -274,8 +276,17 @@ __device__ __noinline__ static void team_hull_box(const Collider& A, const Colli
     v3 y = vadd(mv(RBA, cl), pBA);
     double smax = -1e300;
     int fm = 0x7fffffff;
-#pragma unroll 4 /* plane loads in flight together (the loop is load-latency bound otherwise) */
-    for (int f = j; f < A.nf; f += 8) {
+    /* the first HB_FACE_UNROLL x 8 faces with every plane load issued up front (clamped index, predicated
+     * update: one load latency instead of one per face); faces beyond that (none in this model) in a loop */
+    const int nf = A.nf;
+#pragma unroll
+    for (int i = 0; i < HB_FACE_UNROLL; i++) {
+        const int f = j + 8 * i;
+        const double* F = &UG_HULL_F[4 * (A.f0 + (f < nf ? f : 0))];
+        double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
+        if (f < nf && sd > smax) { smax = sd; fm = f; }
+    }
+    for (int f = j + 8 * HB_FACE_UNROLL; f < nf; f += 8) {
         const double* F = &UG_HULL_F[4 * (A.f0 + f)];
         double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
         if (sd > smax) { smax = sd; fm = f; }
@@ -870,28 +881,164 @@ __device__ __forceinline__ void ent_jac_r(const Scene* sc, const EnvState& e, co
     }
 }
 /* build row at position pos (one lane): J | M^-1 J^T into the workspace row, scalars into rs[pos] */
+/* the LDL solves every limit / motor / gear row would repeat, once per substep: lane d < NB solves for the
+ * unit vector e_d, lane NB + g for gear g's ratio * e_child (the same computation as the row's own) */
+__device__ __noinline__ static void team_unit_solves() {
+    const int lane = threadIdx.x;
+    if (lane < NB + 5) {
+        const int g = lane - NB;
+        const int c = g < 0 ? lane : UG_GEAR_CHILD[g < 0 ? 0 : g];
+        const double v = g < 0 ? 1.0 : UG_GEAR_RATIO[g < 0 ? 0 : g];
+        double x[NB];
+#pragma unroll
+        for (int i = 0; i < NB; i++) x[i] = i == c ? v : 0.0;
+        ldlt_solve_r(g_sh.LDL, x);
+#pragma unroll
+        for (int i = 0; i < NB; i++) g_sh.u.mcol[lane][i] = x[i];
+    }
+    __syncthreads();
+}
+/* robot part of a point Jacobian along d (ANG: angular rows) -- ent_jac_r's robot branch without the
+ * solve, with the row kind's ANG as a runtime select so that every contact lane runs the same code */
+__device__ __forceinline__ void robot_jac_sel(const Kin& k, bool ang, int body, v3 p, v3 d, double (&J)[NB]) {
+    const int am = g_sh.anc[body]; /* the dofs that move the body (moves(), one LDS read) */
+#pragma unroll
+    for (int i = 0; i < NB; i++) {
+        const double xa = vdot(d, k.a[i]);
+        const double xl = vdot(d, vcross(k.a[i], vsub(p, k.p[i])));
+        const double x = ang ? xa : xl;
+        J[i] = ((am >> i) & 1) ? x : 0.0;
+    }
+}
+/* object part of a point Jacobian and its M^-1 J^T (ent_jac_r's object branch, ANG as a select) */
+__device__ __forceinline__ void object_jac_sel(const Scene* sc, const EnvState& e, bool ang, int ent, v3 p, v3 d,
+                                               double (&J)[NB], double (&MiJ)[NB]) {
+    const int o = ent - 1;
+    const m3 R = qmat(e.obj[o].quat);
+    const v3 r = vsub(p, e.obj[o].pos);
+    const v3 rn = vcross(r, d);
+    const v3 w = ang ? d : rn; /* the angular part of J */
+    v3 ir = mtv(R, w);
+    ir = V(ir.x / sc->oinertia[o].x, ir.y / sc->oinertia[o].y, ir.z / sc->oinertia[o].z);
+    ir = mv(R, ir);
+    const double im = 1.0 / sc->omass[o];
+    J[0] = ang ? 0.0 : d.x; J[1] = ang ? 0.0 : d.y; J[2] = ang ? 0.0 : d.z;
+    J[3] = w.x; J[4] = w.y; J[5] = w.z;
+    MiJ[0] = ang ? 0.0 : d.x * im; MiJ[1] = ang ? 0.0 : d.y * im; MiJ[2] = ang ? 0.0 : d.z * im;
+    MiJ[3] = ir.x; MiJ[4] = ir.y; MiJ[5] = ir.z;
+#pragma unroll
+    for (int i = 6; i < NB; i++) { J[i] = 0.0; MiJ[i] = 0.0; }
+}
+/* Build the row at position pos (one lane): J | M^-1 J^T into the workspace row, scalars into rs[pos].
+ * Three phases so that the expensive part is convergent across the wave: (1) per kind, the entity
+ * Jacobians (robot parts unsolved; limit / motor / gear rows take the shared unit solves), (2) the LDL
+ * solves of the robot parts, once for all lanes that need one, (3) per kind, dots, rhs and bounds.  Every
+ * row's arithmetic is the oracle's (build_rows in oracle/ug_oracle.c). */
 __device__ __noinline__ static void build_row(const Scene* s, int pos, double* wrow) {
     Shared& sh = g_sh;
     const EnvState& e = sh.e;
     const double dt = UG_DT;
     RowS& r = sh.rs[pos];
-    double J[NV], MJ[NV];
-#pragma unroll
-    for (int i = 0; i < NV; i++) { J[i] = 0.0; MJ[i] = 0.0; }
+    const int kind = r.kind;
     double invD = 0.0, rhs = 0.0, rhsPen = 0.0, lo = 0.0, hi = 0.0, imp = 0.0, fric = 0.0;
-    if (r.kind <= 1) {
-        int d = r.kind == 0 ? r.a : (r.a < 6 ? r.a : UG_FINGER_DOF);
-        double sgn = (r.kind == 0 && r.b == 1) ? -1.0 : 1.0;
-        double Jl[NB], Ml[NB];
+    /* ---- phase 1: Jacobians ---- */
+    PROF_T0(t_rb1);
+    double JA[NB], MA[NB], JB[NB], MB[NB];
 #pragma unroll
-        for (int i = 0; i < NB; i++) { Jl[i] = i == d ? sgn : 0.0; Ml[i] = Jl[i]; }
-        ldlt_solve_r(sh.LDL, Ml);
-        double den = ent_dot_r(0, Jl, Ml);
+    for (int i = 0; i < NB; i++) { JA[i] = 0.0; MA[i] = 0.0; JB[i] = 0.0; MB[i] = 0.0; }
+    bool solA = false, solB = false;
+    int dof = 0;
+    double sgn = 1.0;
+    int entA = -1, entB = -1;
+    const StPt* cp = nullptr;
+    const PairDef* PP = nullptr;
+    bool ang = false;
+    if (kind <= 1) {
+        dof = kind == 0 ? r.a : (r.a < 6 ? r.a : UG_FINGER_DOF);
+        sgn = (kind == 0 && r.b == 1) ? -1.0 : 1.0;
+#pragma unroll
+        for (int i = 0; i < NB; i++) {
+            JA[i] = i == dof ? sgn : 0.0;
+            MA[i] = sgn > 0.0 ? sh.u.mcol[dof][i] : JA[i]; /* the shared solve of e_dof (team_unit_solves) */
+        }
+        solA = !(sgn > 0.0);
+    } else if (kind == 2) {
+        const int pa = UG_FINGER_DOF, cb = UG_GEAR_CHILD[r.a];
+        const double ratio = UG_GEAR_RATIO[r.a];
+#pragma unroll
+        for (int i = 0; i < NB; i++) {
+            JA[i] = i == pa ? 1.0 : 0.0;
+            JB[i] = i == cb ? ratio : 0.0;
+            MA[i] = sh.u.mcol[pa][i];      /* = ldlt_solve(JA) */
+            MB[i] = sh.u.mcol[NB + r.a][i]; /* = ldlt_solve(JB) */
+        }
+    } else {
+        const StMan& M = e.man[r.a];
+        PP = &s->pair[(int)M.pair];
+        int bodyA, bodyB;
+        entA = ent_of_collider(s->col[PP->a], bodyA);
+        entB = ent_of_collider(s->col[PP->b], bodyB);
+        XF OA = owner_xf(e, sh.kin, s->col[PP->a].owner), OB = owner_xf(e, sh.kin, s->col[PP->b].owner);
+        cp = &M.pt[r.b];
+        v3 pA = xf_apply(OA, cp->lpA), pB = xf_apply(OB, cp->lpB);
+        v3 n = cp->n;
+        v3 d = n;
+        ang = kind >= 6; /* rolling friction: angular rows about the friction axes */
+        if (kind >= 4) {
+            v3 t1, t2;
+            if (ug_fabs(n.z) > 0.7071067811865475244) {
+                double a = n.y * n.y + n.z * n.z, kk = 1.0 / ug_sqrt(a);
+                t1 = V(0, -n.z * kk, n.y * kk);
+                t2 = V(a * kk, -n.x * t1.z, n.x * t1.y);
+            } else {
+                double a = n.x * n.x + n.y * n.y, kk = 1.0 / ug_sqrt(a);
+                t1 = V(-n.y * kk, n.x * kk, 0);
+                t2 = V(-n.z * t1.y, n.z * t1.x, a * kk);
+            }
+            d = (kind == 4 || kind == 6) ? t1 : t2;
+        }
+        if (entA == 0) {
+            robot_jac_sel(sh.kin, ang, bodyA, pA, d, JA);
+            solA = true;
+        } else if (entA > 0) {
+            object_jac_sel(s, e, ang, entA, pA, d, JA, MA);
+        }
+        const v3 dB = vneg(d);
+        if (entB == 0) {
+            robot_jac_sel(sh.kin, ang, bodyB, pB, dB, JB);
+            solB = true;
+        } else if (entB > 0) {
+            object_jac_sel(s, e, ang, entB, pB, dB, JB, MB);
+        }
+    }
+    PROF_ADD(PF_RB1, t_rb1);
+    PROF_T0(t_rb2);
+    /* ---- phase 2: M^-1 J^T of the robot parts, one solve for every lane that needs it ---- */
+    if (ballot(solA) != 0ull) {
+        double x[NB];
+#pragma unroll
+        for (int i = 0; i < NB; i++) x[i] = JA[i];
+        ldlt_solve_r(sh.LDL, x);
+#pragma unroll
+        for (int i = 0; i < NB; i++) MA[i] = solA ? x[i] : MA[i];
+    }
+    if (ballot(solB) != 0ull) {
+        double x[NB];
+#pragma unroll
+        for (int i = 0; i < NB; i++) x[i] = JB[i];
+        ldlt_solve_r(sh.LDL, x);
+#pragma unroll
+        for (int i = 0; i < NB; i++) MB[i] = solB ? x[i] : MB[i];
+    }
+    PROF_ADD(PF_RB2, t_rb2);
+    PROF_T0(t_rb3);
+    /* ---- phase 3: dots, rhs, bounds ---- */
+    if (kind <= 1) {
+        const int d = dof;
+        double den = ent_dot_r(0, JA, MA);
         invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
-        put_seg_r(0, Jl, J);
-        put_seg_r(0, Ml, MJ);
-        double relv = ent_dot_v0(0, Jl, sh.v0);
-        if (r.kind == 0) {
+        double relv = ent_dot_v0(0, JA, sh.v0);
+        if (kind == 0) {
             double pen = r.b == 0 ? e.q[d] - UG_DOF_LOWER[d] : UG_DOF_UPPER[d] - e.q[d];
             double erp = (pen > UG_SPLIT_PEN_THR) ? UG_ERP : UG_ERP2;
             double perr = -pen * erp / dt, verr = -relv;
@@ -911,23 +1058,11 @@ __device__ __noinline__ static void build_row(const Scene* s, int pos, double* w
             rhs = 0.0 * invD + (des - relv) * invD;
             lo = -maxImp; hi = maxImp;
         }
-    } else if (r.kind == 2) {
+    } else if (kind == 2) {
         const int pa = UG_FINGER_DOF, cb = UG_GEAR_CHILD[r.a];
         double ratio = UG_GEAR_RATIO[r.a];
-        double JA[NB], JB[NB], MA[NB], MB[NB];
-#pragma unroll
-        for (int i = 0; i < NB; i++) {
-            JA[i] = i == pa ? 1.0 : 0.0;
-            JB[i] = i == cb ? ratio : 0.0;
-            MA[i] = JA[i];
-            MB[i] = JB[i];
-        }
-        ldlt_solve_r(sh.LDL, MA);
-        ldlt_solve_r(sh.LDL, MB);
         double den = ent_dot_r(0, JA, MA) + ent_dot_r(0, JB, MB);
         invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
-#pragma unroll
-        for (int i = 0; i < NB; i++) { J[i] = JA[i] + JB[i]; MJ[i] = MA[i] + MB[i]; }
         double relv = ent_dot_v0(0, JA, sh.v0) + ent_dot_v0(0, JB, sh.v0);
         double diff = e.q[cb] * ratio + e.q[pa];
         double pen = -UG_GEAR_ERP * (0.0 - diff);
@@ -936,52 +1071,20 @@ __device__ __noinline__ static void build_row(const Scene* s, int pos, double* w
         double maxImp = UG_GEAR_MAXF * dt;
         lo = -maxImp; hi = maxImp;
     } else {
-        const StMan& M = e.man[r.a];
-        const PairDef& P = s->pair[(int)M.pair];
-        int bodyA, bodyB;
-        int entA = ent_of_collider(s->col[P.a], bodyA);
-        int entB = ent_of_collider(s->col[P.b], bodyB);
-        XF OA = owner_xf(e, sh.kin, s->col[P.a].owner), OB = owner_xf(e, sh.kin, s->col[P.b].owner);
-        const StPt& cp = M.pt[r.b];
-        v3 pA = xf_apply(OA, cp.lpA), pB = xf_apply(OB, cp.lpB);
-        v3 n = cp.n;
-        v3 d = n;
-        const bool ang = r.kind >= 6; /* rolling friction: angular rows about the friction axes */
-        if (r.kind >= 4) {
-            v3 t1, t2;
-            if (ug_fabs(n.z) > 0.7071067811865475244) {
-                double a = n.y * n.y + n.z * n.z, kk = 1.0 / ug_sqrt(a);
-                t1 = V(0, -n.z * kk, n.y * kk);
-                t2 = V(a * kk, -n.x * t1.z, n.x * t1.y);
-            } else {
-                double a = n.x * n.x + n.y * n.y, kk = 1.0 / ug_sqrt(a);
-                t1 = V(-n.y * kk, n.x * kk, 0);
-                t2 = V(-n.z * t1.y, n.z * t1.x, a * kk);
-            }
-            d = (r.kind == 4 || r.kind == 6) ? t1 : t2;
-        }
-        double JA[NB], MA[NB], JB[NB], MB[NB];
+        const PairDef& P = *PP;
         double dA = 0.0, dB = 0.0, relv = 0.0;
         if (entA >= 0) {
-            if (ang) ent_jac_r<true>(s, e, sh.kin, entA, bodyA, pA, d, JA, MA, sh.LDL);
-            else ent_jac_r<false>(s, e, sh.kin, entA, bodyA, pA, d, JA, MA, sh.LDL);
             dA = ent_dot_r(entA, JA, MA);
             relv += ent_dot_v0(entA, JA, sh.v0);
-            put_seg_r(entA, JA, J);
-            put_seg_r(entA, MA, MJ);
         }
         if (entB >= 0) {
-            if (ang) ent_jac_r<true>(s, e, sh.kin, entB, bodyB, pB, vneg(d), JB, MB, sh.LDL);
-            else ent_jac_r<false>(s, e, sh.kin, entB, bodyB, pB, vneg(d), JB, MB, sh.LDL);
             dB = ent_dot_r(entB, JB, MB);
             relv += ent_dot_v0(entB, JB, sh.v0);
-            put_seg_r(entB, JB, J);
-            put_seg_r(entB, MB, MJ);
         }
         double den = dA + dB;
         invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
-        if (r.kind == 3) {
-            double pen = cp.dist + UG_LINEAR_SLOP;
+        if (kind == 3) {
+            double pen = cp->dist + UG_LINEAR_SLOP;
             double rest = 0.0;
             if (!(ug_fabs(relv) < UG_REST_VEL_THR)) rest = P.restitution * -relv;
             if (rest <= 0.0) rest = 0.0;
@@ -993,15 +1096,31 @@ __device__ __noinline__ static void build_row(const Scene* s, int pos, double* w
             if (pen > UG_SPLIT_PEN_THR) { rhs = pimp + vimp; rhsPen = 0.0; }
             else { rhs = vimp; rhsPen = pimp; }
             lo = 0.0; hi = 1e10;
-            imp = cp.imp * UG_WARMSTART;
+            imp = cp->imp * UG_WARMSTART;
         } else {
             rhs = 0.0 * invD + (0.0 - relv) * invD;
             fric = ang ? P.rolling : P.friction;
         }
     }
     r.invD = invD; r.rinv = invD == 0.0 ? 0.0 : 1.0 / invD; r.rhs = rhs; r.rhsPen = rhsPen; r.lo = lo; r.hi = hi; r.imp = imp; r.impPen = 0.0; r.fric = fric;
+    /* J | M^-1 J^T over the NV dof slots: limit / motor rows their robot part, gear rows the sum of both
+     * robot parts, contact rows each side's entity segment (put_seg_r semantics; zero elsewhere) */
+    const int eA = kind <= 2 ? 0 : entA, eB = kind == 2 ? 0 : (kind <= 1 ? -1 : entB);
 #pragma unroll
-    for (int i = 0; i < NV; i++) { wrow[i] = J[i]; wrow[24 + i] = MJ[i]; }
+    for (int i = 0; i < NV; i++) {
+        const int ent = i < NB ? 0 : (i < NB + 6 ? 1 : 2);
+        const int k = i < NB ? i : (i - NB) % 6;
+        double j = 0.0, m = 0.0;
+        if (kind == 2) {
+            if (i < NB) { j = JA[i] + JB[i]; m = MA[i] + MB[i]; }
+        } else {
+            if (eA == ent) { j = JA[k]; m = MA[k]; }
+            if (eB == ent) { j = JB[k]; m = MB[k]; }
+        }
+        wrow[i] = j;
+        wrow[24 + i] = m;
+    }
+    PROF_ADD(PF_RB3, t_rb3);
 }
 
 /* ---------------- PGS (btMultiBodyConstraintSolver), row space ----------------
@@ -1381,6 +1500,7 @@ __device__ __noinline__ static void serial_pre(const Scene* s) {
     PROF_T0(t_rd);
     team_robot_dynamics(s->gravity);
     PROF_ADD(PF_RDYN, t_rd);
+    PROF_T0(t_ldl);
     if (lane == 0) {
         double C[NB];
 #pragma unroll
@@ -1419,6 +1539,7 @@ __device__ __noinline__ static void serial_pre(const Scene* s) {
         }
     }
     __syncthreads();
+    PROF_ADD(PF_LDL, t_ldl);
     PROF_T0(t_en);
     team_enumerate(s);
     PROF_ADD(PF_ENUM, t_en);
@@ -1686,7 +1807,12 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     PROF_CNT(PC_OVL, sh.nov);
     PROF_CNT(PC_NMAN, (int)e.nman);
     /* rows: built lane-per-row into the workspace (J | M^-1 J^T) and LDS (scalars) */
+    PROF_T0(t_unit);
+    team_unit_solves();
+    PROF_ADD(PF_UNIT, t_unit);
+    PROF_T0(t_rowb);
     for (int p = lane; p < n; p += TEAM) build_row(s, p, ws + WS_ROWS + p * 48);
+    PROF_ADD(PF_ROWB, t_rowb);
     __threadfence_block();
     __syncthreads();
     PROF_ADD(PF_ROWS, t_rows);
@@ -2112,6 +2238,11 @@ __device__ static void team_load(const double* S) {
     Shared& sh = g_sh;
     double* dst = (double*)&sh.e;
     for (int i = threadIdx.x; i < UG_STATE_DIM; i += TEAM) dst[i] = S[i];
+    if (threadIdx.x < NB) {
+        int m = 0;
+        for (int b = threadIdx.x; b >= 0; b = UG_BODY_PARENT[b]) m |= 1 << b;
+        sh.anc[threadIdx.x] = m;
+    }
 #ifdef UG_PROF
     if (threadIdx.x < UG_NPROF) sh.prof[threadIdx.x] = 0;
 #endif
