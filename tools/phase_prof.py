@@ -21,7 +21,8 @@ NAMES = ["collide", "dyn+enum", "rows", "pgs", "pgs_setup", "integrate", "glue",
          "substeps", "nrows", "pgs_iters", "overlap_pairs", "hull_pairs", "manifolds", "pgs_sweeps", "hull_narrowphase",
          "robot_dynamics", "enumerate", "broadphase", "pair_narrowphase",
          "hullbox_vertices", "hullbox_corners", "hullbox_reduce", "fk", "lane0_ldl_objects", "unit_solves",
-         "row_build", "rb_jacobians", "rb_solves", "rb_scalars"]
+         "row_build", "rb_jacobians", "rb_solves", "rb_scalars", "pgs_mfma",
+         "pgs_warm"]
 
 
 def main():
@@ -37,7 +38,7 @@ def main():
     sim.sync()
     rc = sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     assert rc == 0, "library not built with -DUG_PROF"
-    r = {k: float(v) for k, v in zip(NAMES, buf[:30])}
+    r = {k: float(v) for k, v in zip(NAMES, buf[:32])}
     print("reset (cycles per substep):", json.dumps({k: round(r[k] / max(r["substeps"], 1), 1) for k in NAMES}))
     rng = np.random.default_rng(1)
     for _ in range(a.steps):
@@ -45,7 +46,7 @@ def main():
     sim.sync()
     sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     es = a.envs * a.steps
-    d = {k: float(v) for k, v in zip(NAMES, buf[:30])}
+    d = {k: float(v) for k, v in zip(NAMES, buf[:32])}
     out = {"per_env_step_cycles": {k: d[k] / es for k in NAMES[:8]},
            "substeps_per_env_step": d["substeps"] / es,
            "rows_per_substep": d["nrows"] / max(d["substeps"], 1),
@@ -59,7 +60,7 @@ def main():
     for k in ("dyn+enum", "rows", "pgs", "pgs_setup", "pgs_sweeps", "hull_narrowphase", "robot_dynamics",
               "enumerate", "broadphase", "pair_narrowphase", "hullbox_vertices", "hullbox_corners",
               "hullbox_reduce", "fk", "lane0_ldl_objects", "unit_solves", "row_build", "rb_jacobians", "rb_solves",
-              "rb_scalars", "integrate"):
+              "rb_scalars", "pgs_mfma", "pgs_warm", "integrate"):
         out[k + "_cycles_per_substep"] = d[k] / max(d["substeps"], 1)
     print(json.dumps(out, indent=1))
     sim.close()

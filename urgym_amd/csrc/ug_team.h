@@ -118,7 +118,7 @@ __device__ unsigned long long g_prof[UG_NPROF];
 #endif
 enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_TOTAL,
        PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN, PF_SWEEPS, PF_HULL,
-       PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE, PF_FK, PF_LDL, PF_UNIT, PF_ROWB, PF_RB1, PF_RB2, PF_RB3 };
+       PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE, PF_FK, PF_LDL, PF_UNIT, PF_ROWB, PF_RB1, PF_RB2, PF_RB3, PF_MFMA, PF_WARM };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -1294,26 +1294,28 @@ __device__ __forceinline__ void swap16_d(double& x, double& y) {
     x = __hiloint2double(h[0], l[0]);
     y = __hiloint2double(h[1], l[1]);
 }
+/* the slot's row operands (J of rows 64 S + 16 g + (lane & 15), dof slots 4 ks + (lane >> 4)) are the same
+ * for every column block: loaded once per slot into B; each block then loads only its 6 column operands */
+template <int PB>
+__device__ __forceinline__ void mfma_cols(gcdouble* rows, int n, int lane, double (&a)[6]) {
+    const int p = 16 * PB + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < 6; ks++) a[ks] = p < n ? rows[p * 48 + 24 + 4 * ks + (lane >> 4)] : 0.0;
+}
 template <int PB, int S>
-__device__ __forceinline__ void mfma_block(gcdouble* rows, double invDr, double (&A)[PREG], gdouble* wsA, int n,
-                                           int lane) {
+__device__ __forceinline__ void mfma_block(gcdouble* rows, const double (&B)[6][4], const double (&a)[6], double invDr,
+                                           double (&A)[PREG], gdouble* wsA, int n, int lane) {
     if constexpr (16 * PB < MAXROWS) {
         if (16 * PB < n) {
+            double an[6]; /* the next block's column operands, in flight during this block */
+            if (16 * PB + 16 < n) mfma_cols<PB + 1>(rows, n, lane, an);
             d4v acc[4];
 #pragma unroll
             for (int g = 0; g < 4; g++) acc[g] = d4v{0.0, 0.0, 0.0, 0.0};
-            const int p = 16 * PB + (lane & 15);
 #pragma unroll
-            for (int ks = 0; ks < 6; ks++) {
-                const int d = 4 * ks + (lane >> 4);
-                const double a = p < n ? rows[p * 48 + 24 + d] : 0.0;
+            for (int ks = 0; ks < 6; ks++)
 #pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const int i = 64 * S + 16 * g + (lane & 15);
-                    const double b = i < n ? rows[i * 48 + d] : 0.0;
-                    acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[g], 0, 0, 0);
-                }
-            }
+                for (int g = 0; g < 4; g++) acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], B[ks][g], acc[g], 0, 0, 0);
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 double v[4] = {acc[0][r], acc[1][r], acc[2][r], acc[3][r]};
@@ -1331,9 +1333,24 @@ __device__ __forceinline__ void mfma_block(gcdouble* rows, double invDr, double 
                     else wsA[(P - PREG) * MAXROWS + 64 * S + lane] = x;
                 }
             }
-            mfma_block<PB + 1, S>(rows, invDr, A, wsA, n, lane);
+            mfma_block<PB + 1, S>(rows, B, an, invDr, A, wsA, n, lane);
         }
     }
+}
+template <int S>
+__device__ __forceinline__ void mfma_slot(gcdouble* rows, double invDr, double (&A)[PREG], gdouble* wsA, int n,
+                                          int lane) {
+    double B[6][4];
+#pragma unroll
+    for (int ks = 0; ks < 6; ks++)
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const int i = 64 * S + 16 * g + (lane & 15);
+            B[ks][g] = i < n ? rows[i * 48 + 4 * ks + (lane >> 4)] : 0.0;
+        }
+    double a[6];
+    mfma_cols<0>(rows, n, lane, a);
+    mfma_block<0, S>(rows, B, a, invDr, A, wsA, n, lane);
 }
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
 template <typename T>
@@ -1640,15 +1657,17 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     gdouble* wsA = (gdouble*)(ws + WS_A);
     double A0[PREG], A1[PREG];
     /* scaled Delassus rows on the matrix cores (mfma_block); slot 1 only when rows >= 64 exist */
-    mfma_block<0, 0>(rows, lane < n ? sh.rs[lane].invD : 0.0, A0, wsA, n, lane);
+    PROF_T0(t_mf);
+    mfma_slot<0>(rows, lane < n ? sh.rs[lane].invD : 0.0, A0, wsA, n, lane);
     if (n > 64) {
-        mfma_block<0, 1>(rows, lane + 64 < n ? sh.rs[lane + 64].invD : 0.0, A1, wsA, n, lane);
+        mfma_slot<1>(rows, lane + 64 < n ? sh.rs[lane + 64].invD : 0.0, A1, wsA, n, lane);
     } else {
 #pragma unroll
         for (int j = 0; j < PREG; j++) A1[j] = 0.0;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
+    PROF_ADD(PF_MFMA, t_mf);
     gcdouble* wsAr = (gcdouble*)wsA;
     Lrow L;
     double fric[2], rhsPen[2];
@@ -1670,7 +1689,9 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         rhsPen[s] = in ? r.rhsPen : 0.0;
     }
     double W[2] = {L.rhs[0], L.rhs[1]}; /* u */
+    PROF_T0(t_wm);
     sweep_warm<0>(A0, A1, wsAr, lane, nnc, fb, L, W);
+    PROF_ADD(PF_WARM, t_wm);
     PROF_ADD(PF_SPLIT, t_setup);
 #ifdef UG_DEBUG_DUMP
     double* dbg = ws + WS_DBG;
