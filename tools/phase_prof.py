@@ -22,7 +22,7 @@ NAMES = ["collide", "dyn+enum", "rows", "pgs", "pgs_setup", "integrate", "glue",
          "robot_dynamics", "enumerate", "broadphase", "pair_narrowphase",
          "hullbox_vertices", "hullbox_corners", "hullbox_reduce", "fk", "lane0_ldl_objects", "unit_solves",
          "row_build", "rb_jacobians", "rb_solves", "rb_scalars", "pgs_mfma",
-         "pgs_warm"]
+         "pgs_warm", "sw_nc", "sw_contact", "sw_finish", "sw_fric_prep", "sw_fric", "sw_res"]
 
 
 def main():
@@ -33,12 +33,12 @@ def main():
     from urgym_amd._native import Sim
     sim = Sim(0, a.envs, seed=20241220)
     sim.set_autoreset(True, 500)
-    buf = np.zeros(32, np.uint64)
+    buf = np.zeros(40, np.uint64)
     sim.reset()
     sim.sync()
     rc = sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     assert rc == 0, "library not built with -DUG_PROF"
-    r = {k: float(v) for k, v in zip(NAMES, buf[:32])}
+    r = {k: float(v) for k, v in zip(NAMES, buf[:38])}
     print("reset (cycles per substep):", json.dumps({k: round(r[k] / max(r["substeps"], 1), 1) for k in NAMES}))
     rng = np.random.default_rng(1)
     for _ in range(a.steps):
@@ -46,7 +46,7 @@ def main():
     sim.sync()
     sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     es = a.envs * a.steps
-    d = {k: float(v) for k, v in zip(NAMES, buf[:32])}
+    d = {k: float(v) for k, v in zip(NAMES, buf[:38])}
     out = {"per_env_step_cycles": {k: d[k] / es for k in NAMES[:8]},
            "substeps_per_env_step": d["substeps"] / es,
            "rows_per_substep": d["nrows"] / max(d["substeps"], 1),
@@ -60,7 +60,8 @@ def main():
     for k in ("dyn+enum", "rows", "pgs", "pgs_setup", "pgs_sweeps", "hull_narrowphase", "robot_dynamics",
               "enumerate", "broadphase", "pair_narrowphase", "hullbox_vertices", "hullbox_corners",
               "hullbox_reduce", "fk", "lane0_ldl_objects", "unit_solves", "row_build", "rb_jacobians", "rb_solves",
-              "rb_scalars", "pgs_mfma", "pgs_warm", "integrate"):
+              "rb_scalars", "pgs_mfma", "pgs_warm", "sw_nc", "sw_contact", "sw_finish",
+              "sw_fric_prep", "sw_fric", "sw_res", "integrate"):
         out[k + "_cycles_per_substep"] = d[k] / max(d["substeps"], 1)
     print(json.dumps(out, indent=1))
     sim.close()

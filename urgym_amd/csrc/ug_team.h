@@ -32,7 +32,7 @@
 namespace ugd {
 
 #define TEAM 64
-#define UG_NPROF 32 /* phase accumulators of the -DUG_PROF build */
+#define UG_NPROF 40 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* per-env global workspace (L2-resident): old manifolds (collision), every row's J | M^-1 J^T (24 + 24
@@ -118,7 +118,8 @@ __device__ unsigned long long g_prof[UG_NPROF];
 #endif
 enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_TOTAL,
        PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN, PF_SWEEPS, PF_HULL,
-       PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE, PF_FK, PF_LDL, PF_UNIT, PF_ROWB, PF_RB1, PF_RB2, PF_RB3, PF_MFMA, PF_WARM };
+       PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE, PF_FK, PF_LDL, PF_UNIT, PF_ROWB, PF_RB1, PF_RB2, PF_RB3, PF_MFMA, PF_WARM, PF_SW_NC, PF_SW_CT, PF_SW_FIN, PF_SW_FPREP, PF_SW_FR,
+       PF_SW_RES };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -934,7 +935,7 @@ __device__ __forceinline__ void object_jac_sel(const Scene* sc, const EnvState& 
  * Jacobians (robot parts unsolved; limit / motor / gear rows take the shared unit solves), (2) the LDL
  * solves of the robot parts, once for all lanes that need one, (3) per kind, dots, rhs and bounds.  Every
  * row's arithmetic is the oracle's (build_rows in oracle/ug_oracle.c). */
-__device__ __noinline__ static void build_row(const Scene* s, int pos, double* wrow) {
+__device__ __forceinline__ static void build_row(const Scene* s, int pos, double* wrow) {
     Shared& sh = g_sh;
     const EnvState& e = sh.e;
     const double dt = UG_DT;
@@ -1738,16 +1739,23 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                 gcdouble* o_wsA = wsAr;
                 asm volatile("" : "+s"(o_n), "+s"(o_nnc), "+s"(o_fb), "+s"(o_wsA));
                 /* (even sweeps) non-contact rows reversed, then [s0, fb) */
+                PROF_T0(t_s1);
                 if (!pen && !(it & 1) && o_nnc > 0)
                     sweep_section<true, (NCMAX + CHUNK - 1) / CHUNK, TWO>(A0, A1, o_wsA, lane, 0, o_nnc, 0ull, 0ull, L, W);
+                PROF_ADD(PF_SW_NC, t_s1);
+                PROF_T0(t_s2);
                 const int s0 = (pen || !(it & 1)) ? o_nnc : 0;
                 if (s0 < o_fb) sweep_section<false, TWO ? MAXROWS / CHUNK : 64 / CHUNK, TWO>(A0, A1, o_wsA, lane, s0, o_fb, 0ull, 0ull, L, W);
+                PROF_ADD(PF_SW_CT, t_s2);
+                PROF_T0(t_s3);
                 const int f0 = pen ? o_nnc : 0;
                 row_finish<TWO>(L, pos_mask(0, f0, o_fb, 0ull), pos_mask(1, f0, o_fb, 0ull), lane, res);
+                PROF_ADD(PF_SW_FIN, t_s3);
                 /* friction and rolling rows: bounds +-mu * (their normal's impulse, final for this sweep),
                  * skipped while it is not positive.  A skipped row is made neutral (sweep_section):
                  * increment bounds [0, 0] give a delta of +-0, and u + a * (+-0) == u up to the sign of a
                  * zero u (which never reaches a non-zero result). */
+                PROF_T0(t_s4);
                 if (!pen && o_fb < o_n) {
                     g_sh.u.impx[lane] = L.imp[0];
                     g_sh.u.impx[64 + lane] = L.imp[1];
@@ -1766,11 +1774,16 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                         sk[s] = ballot(skip);
                     }
                     __builtin_amdgcn_wave_barrier();
+                    PROF_ADD(PF_SW_FPREP, t_s4);
+                    PROF_T0(t_s5);
                     sweep_section<false, TWO ? MAXROWS / CHUNK : 64 / CHUNK, TWO>(A0, A1, o_wsA, lane, o_fb, o_n, sk[0], sk[1], L, W);
                     row_finish<TWO>(L, pos_mask(0, o_fb, o_n, sk[0]), pos_mask(1, o_fb, o_n, sk[1]), lane, res);
+                    PROF_ADD(PF_SW_FR, t_s5);
                 }
                 PROF_CNT(PC_ITERS, 1);
+                PROF_T0(t_s6);
                 if (ballot(!(res <= UG_RESIDUAL_THR)) == 0ull || it >= UG_PGS_ITERS - 1) break;
+                PROF_ADD(PF_SW_RES, t_s6);
             }
             if (!pen) {
                 PROF_ADD(PF_SWEEPS, t_sw);
