@@ -729,17 +729,38 @@ DF void nc_box_box(const XF& TA, const Collider& A, const XF& TB, const Collider
     }
 }
 
+/* max over the hull's face planes of the signed distance of y, first face attaining it (sequential scan
+ * semantics).  Planes are fetched HP_BATCH at a time with every load issued before the first use: the
+ * per-face loop would otherwise wait one memory latency per face. */
+#define HP_BATCH 8
+DFI void hull_plane_max(const Collider& A, v3 y, double& smax, int& fm) {
+    const int nf = A.nf, f0 = A.f0;
+    for (int b = 0; b < nf; b += HP_BATCH) {
+        double F[HP_BATCH][4];
+#pragma unroll
+        for (int u = 0; u < HP_BATCH; u++) {
+            const int f = b + u < nf ? b + u : nf - 1;
+#pragma unroll
+            for (int c = 0; c < 4; c++) F[u][c] = UG_HULL_F[4 * (f0 + f) + c];
+        }
+#pragma unroll
+        for (int u = 0; u < HP_BATCH; u++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) asm volatile("" : "+v"(F[u][c])); /* all loads complete here, together */
+#pragma unroll
+        for (int u = 0; u < HP_BATCH; u++) {
+            double sd = F[u][0] * y.x + F[u][1] * y.y + F[u][2] * y.z - F[u][3];
+            if (b + u < nf && sd > smax) { smax = sd; fm = b + u; }
+        }
+    }
+}
 /* hull (robot link) vs box: cooperative, one wavefront per pair -- ug_team.h team_hull_box */
 DF void nc_hull_sphere(const XF& TA, const Collider& A, const XF& TB, const Collider& B, double thr, CandList& out) {
     v3 y = mtv(TA.R, vsub(TB.p, TA.p));
     double r = B.half[0];
     double smax = -1e300;
     int fm = -1;
-    for (int f = 0; f < A.nf; f++) {
-        const double* F = &UG_HULL_F[4 * (A.f0 + f)];
-        double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
-        if (sd > smax) { smax = sd; fm = f; }
-    }
+    hull_plane_max(A, y, smax, fm);
     double depth = smax - r - A.margin;
     if (depth >= thr) return;
     const double* F = &UG_HULL_F[4 * (A.f0 + fm)];

@@ -280,12 +280,24 @@ __device__ __noinline__ static void team_hull_box(const Collider& A, const Colli
     /* the first HB_FACE_UNROLL x 8 faces with every plane load issued up front (clamped index, predicated
      * update: one load latency instead of one per face); faces beyond that (none in this model) in a loop */
     const int nf = A.nf;
+    {
+        double F[HB_FACE_UNROLL][4];
 #pragma unroll
-    for (int i = 0; i < HB_FACE_UNROLL; i++) {
-        const int f = j + 8 * i;
-        const double* F = &UG_HULL_F[4 * (A.f0 + (f < nf ? f : 0))];
-        double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
-        if (f < nf && sd > smax) { smax = sd; fm = f; }
+        for (int i = 0; i < HB_FACE_UNROLL; i++) {
+            const int f = j + 8 * i;
+#pragma unroll
+            for (int c = 0; c < 4; c++) F[i][c] = UG_HULL_F[4 * (A.f0 + (f < nf ? f : 0)) + c];
+        }
+#pragma unroll
+        for (int i = 0; i < HB_FACE_UNROLL; i++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) asm volatile("" : "+v"(F[i][c])); /* one memory latency for all planes */
+#pragma unroll
+        for (int i = 0; i < HB_FACE_UNROLL; i++) {
+            const int f = j + 8 * i;
+            double sd = F[i][0] * y.x + F[i][1] * y.y + F[i][2] * y.z - F[i][3];
+            if (f < nf && sd > smax) { smax = sd; fm = f; }
+        }
     }
     for (int f = j + 8 * HB_FACE_UNROLL; f < nf; f += 8) {
         const double* F = &UG_HULL_F[4 * (A.f0 + f)];
@@ -342,12 +354,7 @@ __device__ __noinline__ static void team_hull_hull(const Collider& A, const Coll
         v3 x = vadd(mv(RAB, V(vv[0], vv[1], vv[2])), pAB);
         double smax = -1e300;
         int fm = -1;
-#pragma unroll 8
-        for (int f = 0; f < B.nf; f++) {
-            const double* F = &UG_HULL_F[4 * (B.f0 + f)];
-            double sd = F[0] * x.x + F[1] * x.y + F[2] * x.z - F[3];
-            if (sd > smax) { smax = sd; fm = f; }
-        }
+        hull_plane_max(B, x, smax, fm);
         double depth = smax - mA - mB;
         if (depth < thr) {
             const double* F = &UG_HULL_F[4 * (B.f0 + fm)];
@@ -367,12 +374,7 @@ __device__ __noinline__ static void team_hull_hull(const Collider& A, const Coll
         v3 y = vadd(mv(RBA, yl), pBA);
         double smax = -1e300;
         int fm = -1;
-#pragma unroll 8
-        for (int f = 0; f < A.nf; f++) {
-            const double* F = &UG_HULL_F[4 * (A.f0 + f)];
-            double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
-            if (sd > smax) { smax = sd; fm = f; }
-        }
+        hull_plane_max(A, y, smax, fm);
         double depth = smax - mA - mB;
         if (depth < thr) {
             const double* F = &UG_HULL_F[4 * (A.f0 + fm)];
