@@ -104,7 +104,7 @@ int urgym_ik(urgym_handle* h, const double* target, double* q_out);
 double urgym_last_kernel_ms(const urgym_handle* h);
 /* Development aid, no reference counterpart: phase cycle counters of the step/reset kernels
  * (collision, dynamics, row build, PGS, split, integration, glue, total, then event counts and sub-phase
- * timers; out16 must hold 40 values).  Returns -1 unless the library was built with -DUG_PROF. */
+ * timers; out16 must hold 48 values).  Returns -1 unless the library was built with -DUG_PROF. */
 int urgym_debug_prof(urgym_handle* h, unsigned long long* out16, int reset);
 /* Development aid: copy the first count doubles of env's device workspace to out; the workspace size
  * (doubles per env) is urgym_debug_ws_doubles().  A -DUG_DEBUG_DUMP build stores the last PGS call's

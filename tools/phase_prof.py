@@ -22,7 +22,8 @@ NAMES = ["collide", "dyn+enum", "rows", "pgs", "pgs_setup", "integrate", "glue",
          "robot_dynamics", "enumerate", "broadphase", "pair_narrowphase",
          "hullbox_vertices", "hullbox_corners", "hullbox_reduce", "fk", "lane0_ldl_objects", "unit_solves",
          "row_build", "rb_jacobians", "rb_solves", "rb_scalars", "pgs_mfma",
-         "pgs_warm", "sw_nc", "sw_contact", "sw_finish", "sw_fric_prep", "sw_fric", "sw_res"]
+         "pgs_warm", "sw_nc", "sw_contact", "sw_finish", "sw_fric_prep", "sw_fric", "sw_res",
+         "pr_lookup", "pr_narrow", "pr_manifold", "pr_store"]
 
 
 def main():
@@ -33,12 +34,12 @@ def main():
     from urgym_amd._native import Sim
     sim = Sim(0, a.envs, seed=20241220)
     sim.set_autoreset(True, 500)
-    buf = np.zeros(40, np.uint64)
+    buf = np.zeros(48, np.uint64)
     sim.reset()
     sim.sync()
     rc = sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     assert rc == 0, "library not built with -DUG_PROF"
-    r = {k: float(v) for k, v in zip(NAMES, buf[:38])}
+    r = {k: float(v) for k, v in zip(NAMES, buf[:42])}
     print("reset (cycles per substep):", json.dumps({k: round(r[k] / max(r["substeps"], 1), 1) for k in NAMES}))
     rng = np.random.default_rng(1)
     for _ in range(a.steps):
@@ -46,7 +47,7 @@ def main():
     sim.sync()
     sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     es = a.envs * a.steps
-    d = {k: float(v) for k, v in zip(NAMES, buf[:38])}
+    d = {k: float(v) for k, v in zip(NAMES, buf[:42])}
     out = {"per_env_step_cycles": {k: d[k] / es for k in NAMES[:8]},
            "substeps_per_env_step": d["substeps"] / es,
            "rows_per_substep": d["nrows"] / max(d["substeps"], 1),
@@ -61,7 +62,7 @@ def main():
               "enumerate", "broadphase", "pair_narrowphase", "hullbox_vertices", "hullbox_corners",
               "hullbox_reduce", "fk", "lane0_ldl_objects", "unit_solves", "row_build", "rb_jacobians", "rb_solves",
               "rb_scalars", "pgs_mfma", "pgs_warm", "sw_nc", "sw_contact", "sw_finish",
-              "sw_fric_prep", "sw_fric", "sw_res", "integrate"):
+              "sw_fric_prep", "sw_fric", "sw_res", "pr_lookup", "pr_narrow", "pr_manifold", "pr_store", "integrate"):
         out[k + "_cycles_per_substep"] = d[k] / max(d["substeps"], 1)
     print(json.dumps(out, indent=1))
     sim.close()

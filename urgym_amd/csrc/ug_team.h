@@ -32,7 +32,7 @@
 namespace ugd {
 
 #define TEAM 64
-#define UG_NPROF 40 /* phase accumulators of the -DUG_PROF build */
+#define UG_NPROF 48 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* per-env global workspace (L2-resident): old manifolds (collision), every row's J | M^-1 J^T (24 + 24
@@ -119,7 +119,7 @@ __device__ unsigned long long g_prof[UG_NPROF];
 enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_TOTAL,
        PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN, PF_SWEEPS, PF_HULL,
        PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE, PF_FK, PF_LDL, PF_UNIT, PF_ROWB, PF_RB1, PF_RB2, PF_RB3, PF_MFMA, PF_WARM, PF_SW_NC, PF_SW_CT, PF_SW_FIN, PF_SW_FPREP, PF_SW_FR,
-       PF_SW_RES };
+       PF_SW_RES, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -504,6 +504,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
             const Collider& A = s->col[P.a];
             const Collider& B = s->col[P.b];
             M.pair = p;
+            PROF_T0(t_pl);
             for (int m = 0; m < nold; m++) {
                 if ((int)ws[m * UG_MAN_DOUBLES] == p) {
                     StMan tmp;
@@ -513,6 +514,8 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
                     break;
                 }
             }
+            PROF_ADD(PF_PR_LOOK, t_pl);
+            PROF_T0(t_pn);
             XF TA = shape_xf(sh.O[P.a], A), TB = shape_xf(sh.O[P.b], B);
             CandList L;
             L.n = 0;
@@ -535,10 +538,14 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
                 for (int i = 0; i < L2.n; i++)
                     cand_add(L, vneg(L2.c[i].n), vadd(L2.c[i].pB, vscale(L2.c[i].n, L2.c[i].d)), L2.c[i].d);
             }
+            PROF_ADD(PF_PR_NP, t_pn);
+            PROF_T0(t_pm);
             for (int i = 0; i < L.n; i++) manifold_add(M, sh.O[P.a], sh.O[P.b], L.c[i], P.thr);
             if (M.npts) manifold_refresh(M, sh.O[P.a], sh.O[P.b], P.thr);
             has = M.npts > 0;
+            PROF_ADD(PF_PR_MAN, t_pm);
         }
+        PROF_T0(t_ps);
         __syncthreads();
         unsigned long long hm = ballot(has);
         if (has) {
@@ -547,6 +554,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         }
         nnew += __popcll(hm);
         __syncthreads();
+        PROF_ADD(PF_PR_ST, t_ps);
         PROF_ADD(PF_PAIRS, t_pairs);
     }
     if (lane == 0) {
