@@ -298,7 +298,9 @@ def main():
     w("#define UG_NL 19          /* PyBullet link count (link index = DFS order) */")
     w("#define UG_EE_LINK 7")
     w("/* body b: joint frame in parent body frame at q=0 (rotation matrix row-major, translation) */")
-    arr("UG_BODY_PARENT", [b["parent"] for b in bodies], "int")
+    w("#define UG_BODY_PARENT_INIT {%s} /* also a compile-time table in the HIP code */"
+      % ", ".join(str(int(b["parent"])) for b in bodies))
+    w("UG_CONST int UG_BODY_PARENT[%d] = UG_BODY_PARENT_INIT;" % len(bodies))
     arr("UG_BODY_LINK", [b["link"] for b in bodies], "int")
     arr("UG_BODY_R", [b["T_pb"][:3, :3] for b in bodies])
     arr("UG_BODY_P", [b["T_pb"][:3, 3] for b in bodies])

@@ -91,6 +91,7 @@ struct Shared {
     int is[8];
     int ecnt[2 * MAXMAN]; /* team_enumerate: accepted points / rolling points per manifold */
     int anc[NB];          /* bit d set: dof d moves body b (moves(d, b)); filled by team_load */
+    int bdepth[NB];       /* tree depth of body b (body_depth); filled by team_load */
 #ifdef UG_PROF
     unsigned long long prof[UG_NPROF];
 #endif
@@ -1376,6 +1377,9 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
  * tree accumulations (composite inertia, force back-propagation) run component-parallel: lane c owns
  * one scalar component and walks the bodies in the serial code's descending order.  The RNEA forward
  * pass goes level by level down the (compile-time) tree.  Results: M -> LDL (LDS), C -> w.C. */
+/* the kinematic tree as compile-time data (same initializer as UG_BODY_PARENT): tree loops with constant
+ * parents keep their per-body arrays in registers */
+constexpr int kParent[NB] = UG_BODY_PARENT_INIT;
 __device__ __forceinline__ int body_depth(int b) {
     int d = 0;
     for (int j = UG_BODY_PARENT[b]; j >= 0; j = UG_BODY_PARENT[j]) d++;
@@ -1420,7 +1424,7 @@ __device__ __noinline__ static void team_robot_dynamics(double g_) {
         for (int i = 0; i < NB; i++) v[i] = base[i * stride];
 #pragma unroll
         for (int i = NB - 1; i >= 0; i--) {
-            const int p = UG_BODY_PARENT[i];
+            const int p = kParent[i]; /* a constant after unrolling */
             if (p >= 0) v[p] = v[p] + v[i];
         }
 #pragma unroll
@@ -1432,14 +1436,18 @@ __device__ __noinline__ static void team_robot_dynamics(double g_) {
         SV F = spatial_inertia_mul(w.cm[b], w.ch[b], w.cJ[b], w.S[b]);
         const SV Sb = w.S[b];
         M[b * NB + b] = vdot(Sb.w, F.w) + vdot(Sb.v, F.v);
-        for (int j = UG_BODY_PARENT[b]; j >= 0; j = UG_BODY_PARENT[j]) {
-            double x = vdot(w.S[j].w, F.w) + vdot(w.S[j].v, F.v);
-            M[j * NB + b] = x;
-            M[b * NB + j] = x;
+        const int am = g_sh.anc[b]; /* ancestors j of b (the parent walk, from the LDS mask) */
+#pragma unroll
+        for (int j = NB - 1; j >= 0; j--) {
+            if (j != b && ((am >> j) & 1)) {
+                double x = vdot(w.S[j].w, F.w) + vdot(w.S[j].v, F.v);
+                M[j * NB + b] = x;
+                M[b * NB + j] = x;
+            }
         }
     }
     /* 4. RNEA forward, one tree level at a time; then the body's force (independent of the others) */
-    const int depth = own ? body_depth(b) : -1;
+    const int depth = own ? g_sh.bdepth[b] : -1; /* body_depth(b), cached in LDS */
     SV f;
     f.w = V(0, 0, 0);
     f.v = V(0, 0, 0);
@@ -1504,7 +1512,7 @@ __device__ __noinline__ static void team_robot_dynamics(double g_) {
         for (int i = 0; i < NB; i++) v[i] = base[i * stride];
 #pragma unroll
         for (int i = NB - 1; i >= 0; i--) {
-            const int p = UG_BODY_PARENT[i];
+            const int p = kParent[i]; /* a constant after unrolling */
             if (p >= 0) v[p] = v[p] + v[i];
         }
 #pragma unroll
@@ -1621,7 +1629,7 @@ __device__ __noinline__ static void serial_fk() {
     const v3 ax = V(UG_BODY_AXIS[3 * b], UG_BODY_AXIS[3 * b + 1], UG_BODY_AXIS[3 * b + 2]);
     const v3 com = V(UG_BODY_COM[3 * b], UG_BODY_COM[3 * b + 1], UG_BODY_COM[3 * b + 2]);
     const m3 Rj = axis_angle(ax, g_sh.e.q[b]);
-    const int depth = own ? body_depth(b) : -1;
+    const int depth = own ? g_sh.bdepth[b] : -1; /* body_depth(b), cached in LDS */
     for (int L = 0; L < NB; L++) {
         if (depth == L) {
             m3 Rp;
@@ -2286,6 +2294,7 @@ __device__ static void team_load(const double* S) {
         int m = 0;
         for (int b = threadIdx.x; b >= 0; b = UG_BODY_PARENT[b]) m |= 1 << b;
         sh.anc[threadIdx.x] = m;
+        sh.bdepth[threadIdx.x] = body_depth(threadIdx.x);
     }
 #ifdef UG_PROF
     if (threadIdx.x < UG_NPROF) sh.prof[threadIdx.x] = 0;
