@@ -107,6 +107,19 @@ UG_HD double ug_cos(double x) {
     }
 }
 
+/* sin and cos together, branch-free: the same kernels on the same reduced argument as ug_sin / ug_cos (the
+ * small-argument path as a select), so the results are identical to theirs */
+UG_HD void ug_sincos(double x, double* sn, double* cs) {
+    double r0, r1;
+    int nr = ug__rem_pio2(x, &r0, &r1);
+    const int small = ug_fabs(x) <= 7.85398163397448278999e-01;
+    const double y0 = small ? x : r0, y1 = small ? 0.0 : r1;
+    const int q = (small ? 0 : nr) & 3;
+    const double ks = ug__ksin(y0, y1), kc = ug__kcos(y0, y1);
+    *sn = q == 0 ? ks : (q == 1 ? kc : (q == 2 ? -ks : -kc));
+    *cs = q == 0 ? kc : (q == 1 ? -ks : (q == 2 ? -kc : ks));
+}
+
 /* ---- atan / atan2 ---- */
 UG_HD double ug_atan(double x) {
     const double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01,

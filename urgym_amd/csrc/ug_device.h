@@ -102,7 +102,9 @@ DFI m3 inertia_world(const m3& R, const double* I6) {
     return C;
 }
 DFI m3 axis_angle(v3 a, double q) {
-    double c = ug_cos(q), s = ug_sin(q), t = 1.0 - c;
+    double s, c;
+    ug_sincos(q, &s, &c);
+    double t = 1.0 - c;
     m3 R;
     R.m[0] = t * a.x * a.x + c;       R.m[1] = t * a.x * a.y - s * a.z; R.m[2] = t * a.x * a.z + s * a.y;
     R.m[3] = t * a.x * a.y + s * a.z; R.m[4] = t * a.y * a.y + c;       R.m[5] = t * a.y * a.z - s * a.x;
