@@ -68,6 +68,20 @@ def cpu_baseline(task, seconds=10.0):
                       f"({substeps} substeps) in {dt:.1f}s; C restatement (oracle/), OpenMP {threads} threads"}
 
 
+def pmc_traffic(task, n, K, W):
+    """HBM bytes per k_step launch from the committed PMC summary of this same workload
+    (profiles/traffic_k_step.json, made by tools/pmc_traffic.py from separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of `bench.py --steps K --warmup W`); None if it does not match."""
+    path = os.path.join(ROOT, "profiles", "traffic_k_step.json")
+    try:
+        t = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    if (t.get("task"), t.get("envs"), t.get("steps"), t.get("warmup")) != (task, n, K, W):
+        return None, None
+    return float(t["hbm_bytes_per_launch"]), "profiles/traffic_k_step.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -170,6 +184,7 @@ def main():
     S = state_bytes()
     bytes_per_env = 2 * S + 4 * A + 8 * O * 2 + 8 + 3 + 4
     achieved_gbs = bytes_per_env * n / (avg_kernel_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(args.task, n, K, W)
     line = {
         "metric": ("env-steps/sec at N parallel envs (BallBalance-v0, 4096 envs per MI355X)" if args.task == 0 and n == 4096
                    else f"env-steps/sec at N parallel envs ({TASK_NAMES[args.task].split('/')[1]}, {n} envs per MI355X)"),
@@ -190,7 +205,8 @@ def main():
         "substeps_per_env_step": float(tot[0].item()) / env_steps,
         "resets": int(tot[1].item()),
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
                      "kernel": "k_step", "avg_kernel_ms": avg_kernel_ms,
                      "algorithmic_bytes_per_env_step": bytes_per_env,
                      "note": "path is FP64-VALU/latency bound, not HBM bound (DESIGN.md); PMC traffic in profiles/"},

@@ -9,10 +9,12 @@ export TMPDIR=/tmp
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 timeout -k 10 240 python -c "import __graft_entry__ as g; g.build()" > $OUT/build.log 2>&1 || { echo BUILD_FAIL; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --no-cpu-baseline "$@" > $OUT/trace.log 2>&1 || { echo TRACE_FAIL; exit 1; }
+echo TRACE_OK
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --no-cpu-baseline "$@" > $OUT/pmc_fetch.log 2>&1 || { echo PMC1_FAIL; exit 1; }
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py --no-cpu-baseline "$@" > $OUT/pmc_write.log 2>&1 || { echo PMC2_FAIL; exit 1; }
+echo PMC_OK
+python3 tools/pmc_traffic.py $OUT/pmc_fetch/run_counter_collection.csv $OUT/pmc_write/run_counter_collection.csv $OUT/traffic_k_step.json --steps 20 --warmup 3 "$@" > /dev/null && cp $OUT/traffic_k_step.json profiles/traffic_k_step.json && echo TRAFFIC_OK
 timeout -k 10 600 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err || { echo BENCH_FAIL; exit 1; }
 echo BENCH_OK
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/trace.log 2>&1 || { echo TRACE_FAIL; exit 1; }
-echo TRACE_OK
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > $OUT/pmc_fetch.log 2>&1 || { echo PMC1_FAIL; exit 1; }
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > $OUT/pmc_write.log 2>&1 || { echo PMC2_FAIL; exit 1; }
-echo PMC_OK
+
