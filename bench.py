@@ -1,15 +1,17 @@
 #!/usr/bin/env python3
 """Headline benchmark: env-steps/sec of URGym/BallBalance-v0 x 4096 envs per MI355X.
 
-Contract (see DESIGN.md "Measurement"):
-  python bench.py --gpus N --steps K --warmup W
-One process per GPU (torch.distributed.run for N>1, RCCL all-gather of the
-per-step returns).  A step = one batched env.step() on every env of the shard:
-IK + joint motors + wait_until_stable (<=480 physics substeps) + reward, and the
-same-step autoreset of finished episodes (reset cost counted).  Actions are
-synthetic (PCG64 seed 20241220 + rank, uniform in the action space) and are
-resident in HBM before the timed region; outputs stay in HBM.  Rank 0 prints
-one JSON line.
+Contract:
+  python bench.py --gpus N --steps K --warmup W [--reps R] [--task T --envs E]
+One process per GPU.  With --gpus N > 1 and no torch.distributed environment, bench.py starts its N
+ranks itself (torch.distributed.run, 127.0.0.1) as child processes before any GPU call; under a launcher
+WORLD_SIZE must equal N.  A step = one batched env.step() on every env of the rank's shard: IK + joint
+motors + wait_until_stable (<= 480 physics substeps) + reward, and the same-step autoreset of finished
+episodes (reset cost counted); with N > 1 the per-step returns are all-gathered over RCCL (xGMI).
+Actions are synthetic (PCG64 seed 20241220 + rank, uniform in the action space) and resident in HBM
+before the timed region; outputs stay in HBM.  Protocol: W untimed warm-up steps, then R
+repetitions of K timed steps, each bracketed by barrier + synchronize, time = max over ranks; `value` is
+the median repetition.  Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -25,8 +27,8 @@ sys.path.insert(0, ROOT)
 TASK_NAMES = {0: "URGym/BallBalance-v0", 1: "URGym/CubesPush-v0", 2: "URGym/CubesGrasp-v0", 3: "URGym/Golf-v0",
               4: "URGym/CubesPushDiff-v0", 5: "URGym/GolfJoints-v0"}
 MAX_STEPS = {0: 500, 1: 50, 2: 20, 3: 100, 4: 50, 5: 100}
-HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector spec
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
+FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (AMD spec; the path's bounding roofline)
 
 
 def state_bytes():
@@ -34,64 +36,112 @@ def state_bytes():
     return lib().urgym_state_dim() * 8
 
 
-def cpu_baseline(task, seconds=10.0):
-    """CPU restatement (oracle/, test infrastructure) timed on this host's cores: a bounded sample
-    of the same workload (same task, random actions, autoreset), OpenMP one env per thread."""
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _oracle_sample(task, n, threads, seconds):
     import ctypes
     from oracle.pyoracle import OracleEnv, lib as olib
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    os.environ["OMP_NUM_THREADS"] = str(threads)
-    n = 4 * threads
+    from urgym_amd.envs import spaces_for
     envs = [OracleEnv(task, 20241220 + i) for i in range(n)]
     for e in envs:
         e.reset()
     arr = (ctypes.c_void_p * n)(*[e.h for e in envs])
     A, O = envs[0].act_dim, envs[0].obs_dim
     rng = np.random.default_rng(20241220)
-    from urgym_amd.envs import spaces_for
     _, act_space = spaces_for(task)
     alo, ahi = np.asarray(act_space.low, np.float64), np.asarray(act_space.high, np.float64)
     obs = np.zeros((n, O)); rew = np.zeros(n); term = np.zeros(n, np.uint8); succ = np.zeros(n, np.uint8)
     sub = np.zeros(n, np.int32); el = np.zeros(n, np.int32)
     p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
-    steps = 0
-    substeps = 0
+    steps = substeps = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         act = rng.uniform(alo, ahi, size=(n, A)).astype(np.float32)
         substeps += olib().ugo_batch_step(arr, n, p(act), p(obs), p(rew), p(term), p(succ), p(sub), 1,
                                           MAX_STEPS[task], p(el))
         steps += n
-    dt = time.perf_counter() - t0
+    return steps, substeps, time.perf_counter() - t0
+
+
+def cpu_baseline(task, seconds=10.0, seconds_1core=5.0):
+    """CPU restatement (oracle/, test infrastructure) timed on this host's cores: bounded samples of the same
+    workload (same task, random actions, autoreset) -- all cores with OpenMP (one env per thread at a time,
+    4 envs per thread) and the 1-env / 1-core analogue of config A."""
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    n = 4 * threads
+    steps, substeps, dt = _oracle_sample(task, n, threads, seconds)
+    s1, sub1, dt1 = _oracle_sample(task, 1, 1, seconds_1core)
     return {"value": steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{TASK_NAMES[task]} x {n} envs, {steps} env-steps incl. autoresets "
-                      f"({substeps} substeps) in {dt:.1f}s; C restatement (oracle/), OpenMP {threads} threads"}
+            "cpu_model": cpu_model(),
+            "sample": f"{TASK_NAMES[task]} x {n} envs, {steps} env-steps incl. autoresets ({substeps} substeps) in "
+                      f"{dt:.1f}s; C restatement (oracle/), OpenMP {threads} threads",
+            "one_core": {"value": s1 / dt1, "unit": "env-steps/s", "cores": 1,
+                         "sample": f"1 env, {s1} env-steps ({sub1} substeps) in {dt1:.1f}s, 1 thread"}}
 
 
-def pmc_traffic(task, n, K, W):
-    """HBM bytes per k_step launch from the committed PMC summary of this same workload
-    (profiles/traffic_k_step.json, made by tools/pmc_traffic.py from separate rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes of `bench.py --steps K --warmup W`); None if it does not match."""
+def pmc_traffic(task, n):
+    """HBM bytes per k_step launch from the committed PMC summary of this workload (profiles/traffic_k_step.json,
+    tools/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), keyed on (task, envs)."""
     path = os.path.join(ROOT, "profiles", "traffic_k_step.json")
     try:
         t = json.load(open(path))
     except (OSError, ValueError):
         return None, None
-    if (t.get("task"), t.get("envs"), t.get("steps"), t.get("warmup")) != (task, n, K, W):
+    for rec in (t if isinstance(t, list) else [t]):
+        if (rec.get("task"), rec.get("envs")) == (task, n):
+            return float(rec["hbm_bytes_per_launch"]), \
+                f"profiles/traffic_k_step.json ({rec.get('source', 'rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE')})"
+    return None, None
+
+
+def work_model(task):
+    """FP64 FLOPs per substep / per env-step outside substeps (profiles/work_model.json, tools/opcount.py)"""
+    try:
+        m = json.load(open(os.path.join(ROOT, "profiles", "work_model.json")))["tasks"][str(task)]
+        return float(m["F_sub"]), float(m["F_nonsub_per_env_step"])
+    except (OSError, ValueError, KeyError):
         return None, None
-    return float(t["hbm_bytes_per_launch"]), "profiles/traffic_k_step.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
 
 
-def main():
+def maybe_spawn(args, argv):
+    """--gpus N > 1 outside a launcher: start the N ranks as children (before any GPU call) and return their
+    exit code; under a launcher, refuse a WORLD_SIZE that disagrees with --gpus.  None: run in-process."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is None:
+        if args.gpus > 1:
+            from urgym_amd.parallel import spawn_ranks
+            return spawn_ranks(args.gpus, os.path.abspath(__file__), argv)
+        return None
+    if int(world) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
+    return None
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--task", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+    rc = maybe_spawn(args, argv)
+    if rc is not None:
+        return rc
 
     import torch
     import torch.distributed as dist
@@ -103,6 +153,7 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", rank=rank, world_size=world)
+        world = dist.get_world_size()
     dev = torch.device("cuda", local)
 
     from urgym_amd._native import Sim
@@ -112,11 +163,11 @@ def main():
     sim.reset()
     A, O = sim.act_dim, sim.obs_dim
     rng = np.random.default_rng(20241220 + rank)
-    K, W = args.steps, args.warmup
+    K, W, R = args.steps, args.warmup, args.reps
     from urgym_amd.envs import spaces_for
     _, act_space = spaces_for(args.task)
     lo, hi = np.asarray(act_space.low, np.float64), np.asarray(act_space.high, np.float64)
-    acts = torch.from_numpy(rng.uniform(lo, hi, size=(W + K, n, A)).astype(np.float32)).to(dev)
+    acts = torch.from_numpy(rng.uniform(lo, hi, size=(W + K * R, n, A)).astype(np.float32)).to(dev)
     obs = torch.zeros(n, O, dtype=torch.float64, device=dev)
     fin = torch.zeros_like(obs)
     rew = torch.zeros(n, dtype=torch.float64, device=dev)
@@ -125,6 +176,8 @@ def main():
     succ = torch.zeros_like(term)
     sub = torch.zeros(n, dtype=torch.int32, device=dev)
     stream = torch.cuda.ExternalStream(sim.L.urgym_stream(sim.h), device=dev)
+    if world > 1:
+        from urgym_amd.parallel import gather_returns
 
     def one_step(t, e=None):
         sim.step_device(acts[t].data_ptr(), obs.data_ptr(), fin.data_ptr(), rew.data_ptr(), term.data_ptr(),
@@ -132,8 +185,7 @@ def main():
         if e is not None:
             e.record(stream)
         if world > 1:
-            # returns gathered over RCCL (xGMI): obs | reward | terminated | truncated
-            from urgym_amd.parallel import gather_returns
+            # returns gathered over RCCL (xGMI): obs | reward | terminated | truncated, global env-id order
             with torch.cuda.stream(stream):
                 gather_returns(obs, rew, term, trunc)
 
@@ -146,45 +198,72 @@ def main():
             res_tot += (term | trunc).sum()
     sim.sync()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    # per-launch HIP events on the handle's stream (the stream k_step runs on); substep / reset counts
-    # accumulate on the device, so the timed loop has no host round trip per step
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-    sub_tot.zero_()
-    res_tot.zero_()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k, t in enumerate(range(W, W + K)):
-        ev[k][0].record(stream)
-        one_step(t, ev[k][1])
-        with torch.cuda.stream(stream):
-            sub_tot += sub.sum()
-            res_tot += (term | trunc).sum()
-    sim.sync()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    substeps = int(sub_tot.item())
-    resets = int(res_tot.item())
-    dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    tot = torch.tensor([float(substeps), float(resets)], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    dt = float(dt_t.item())
+
+    reps = []
+    for r in range(R):
+        # per-launch HIP events on the handle's stream (the stream k_step runs on); substep / reset counts
+        # accumulate on the device, so the timed loop has no host round trip per step
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+        sub_tot.zero_()
+        res_tot.zero_()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(K):
+            t = W + r * K + k
+            ev[k][0].record(stream)
+            one_step(t, ev[k][1])
+            with torch.cuda.stream(stream):
+                sub_tot += sub.sum()
+                res_tot += (term | trunc).sum()
+        sim.sync()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        kern_ms = [a.elapsed_time(b) for a, b in ev]
+        vals = torch.tensor([dt, float(sub_tot.item()), float(res_tot.item()), float(np.mean(kern_ms))],
+                            dtype=torch.float64, device=dev)
+        if world > 1:
+            mx = vals.clone()
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            dist.all_reduce(vals, op=dist.ReduceOp.SUM)
+            vals[0] = mx[0]
+            vals[3] = mx[3]
+        reps.append([float(x) for x in vals.tolist()])
+    order = sorted(range(R), key=lambda i: reps[i][0])
+    med = reps[order[R // 2]]
+    dt, substeps, resets, avg_kernel_ms = med
     env_steps = n * K * world
     value = env_steps / dt
-    avg_kernel_ms = float(np.mean(kern_ms))
+    # roofline of the dominant kernel (k_step): FP64 VALU, algorithmic FLOPs per launch from the op-counted
+    # restatement (profiles/work_model.json) with this run's substep count, over the HIP-event launch time
+    F_sub, F_non = work_model(args.task)
+    flops_per_launch = None
+    if F_sub is not None:
+        flops_per_launch = (F_sub * substeps + F_non * env_steps) / (K * world)
     # algorithmic HBM bytes per env-step: state in + out, actions, obs (+final obs), reward, flags, substeps
     S = state_bytes()
     bytes_per_env = 2 * S + 4 * A + 8 * O * 2 + 8 + 3 + 4
     achieved_gbs = bytes_per_env * n / (avg_kernel_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args.task, n, K, W)
+    traffic, traffic_src = pmc_traffic(args.task, n)
+    if flops_per_launch is not None:
+        tf = flops_per_launch / (avg_kernel_ms * 1e-3) / 1e12
+        roof = {"bound": "fp64-valu", "achieved": tf, "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": tf / FP64_VALU_PEAK_TFLOPS, "traffic": traffic, "traffic_unit": "HBM bytes per launch",
+                "traffic_source": traffic_src, "kernel": "k_step", "avg_kernel_ms": avg_kernel_ms,
+                "flops_per_launch": flops_per_launch, "flops_per_substep": F_sub,
+                "flops_nonsub_per_env_step": F_non, "work_model": "profiles/work_model.json (tools/opcount.py)",
+                "hbm": {"achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_env_step": bytes_per_env}}
+    else:
+        roof = {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_step",
+                "avg_kernel_ms": avg_kernel_ms, "algorithmic_bytes_per_env_step": bytes_per_env,
+                "note": "work model missing (profiles/work_model.json): HBM fraction only"}
     line = {
         "metric": ("env-steps/sec at N parallel envs (BallBalance-v0, 4096 envs per MI355X)" if args.task == 0 and n == 4096
                    else f"env-steps/sec at N parallel envs ({TASK_NAMES[args.task].split('/')[1]}, {n} envs per MI355X)"),
@@ -193,6 +272,7 @@ def main():
         "n_gpus": world,
         "steps": K,
         "warmup": W,
+        "reps": R,
         "ms_per_step": dt / K * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
@@ -201,15 +281,11 @@ def main():
         "data": "synthetic: uniform random actions (PCG64 seed 20241220+rank), per-env MT19937 reset draws",
         "config": {"workload": f"{TASK_NAMES[args.task]} x {n} envs per GPU, autoreset, max_episode_steps "
                                f"{MAX_STEPS[args.task]}", "envs_per_gpu": n, "total_envs": n * world,
-                   "parallelism": f"env-dp{world}"},
-        "substeps_per_env_step": float(tot[0].item()) / env_steps,
-        "resets": int(tot[1].item()),
-        "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
-                     "kernel": "k_step", "avg_kernel_ms": avg_kernel_ms,
-                     "algorithmic_bytes_per_env_step": bytes_per_env,
-                     "note": "path is FP64-VALU/latency bound, not HBM bound (DESIGN.md); PMC traffic in profiles/"},
+                   "parallelism": f"env-dp{world}", "world_size": world},
+        "rep_values": [env_steps / x[0] for x in reps],
+        "substeps_per_env_step": substeps / env_steps,
+        "resets": int(resets),
+        "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.task, args.cpu_seconds)
@@ -218,7 +294,8 @@ def main():
     sim.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

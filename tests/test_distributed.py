@@ -59,3 +59,44 @@ def test_gather_returns_world2_gloo():
     assert np.array_equal(o, ids[:, None] * 10.0 + np.arange(od)[None, :])
     assert np.array_equal(r, ids * 0.5)
     assert np.array_equal(t, ids % 3 == 0) and np.array_equal(tr, ids % 5 == 0)
+
+
+def test_spawn_ranks_world2(tmp_path):
+    """parallel.spawn_ranks (what `bench.py --gpus 2` uses) starts 2 ranks through torch.distributed.run;
+    their gathered returns come back in global env-id order."""
+    import json
+
+    import numpy as np
+    from urgym_amd.parallel import spawn_ranks
+    out = tmp_path / "gathered.json"
+    total, od = 12, 4
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_rank_worker.py")
+    rc = spawn_ranks(2, worker, [str(out), str(total), str(od)])
+    assert rc == 0
+    g = json.load(open(out))
+    ids = np.arange(total)
+    assert g["world"] == 2
+    assert np.array_equal(np.array(g["obs"]), ids[:, None] * 10.0 + np.arange(od)[None, :])
+    assert np.array_equal(np.array(g["rew"]), ids * 0.5)
+    assert np.array_equal(np.array(g["term"]), ids % 3 == 0) and np.array_equal(np.array(g["trunc"]), ids % 5 == 0)
+
+
+def test_bench_gpus_flag_spawns_or_refuses(monkeypatch):
+    """bench.py --gpus N: outside a launcher it starts N ranks itself (before any GPU call); under a launcher a
+    WORLD_SIZE that disagrees with --gpus is refused; --gpus 1 runs in-process."""
+    import importlib
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    bench = importlib.import_module("bench")
+    import urgym_amd.parallel as par
+    calls = []
+    monkeypatch.setattr(par, "spawn_ranks", lambda n, script, argv: calls.append((n, script, list(argv))) or 0)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    argv = ["--gpus", "2", "--steps", "3"]
+    assert bench.main(argv) == 0
+    assert calls == [(2, os.path.abspath(bench.__file__), argv)]
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    assert bench.main(["--gpus", "2"]) == 2
+    monkeypatch.delenv("WORLD_SIZE")
+    args = type("A", (), {"gpus": 1})()
+    assert bench.maybe_spawn(args, []) is None

@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""Op-counting build of the CPU restatement (oracle/ug_oracle.c) -> profiles/work_model.json.
+
+The algorithmic work of the hot path (F_env-step = F_IK + k * F_sub) is counted on the
+restatement, not on the GPU kernel (whose redundant / idle lanes are not algorithmic work):
+
+  1. clang compiles oracle/ug_oracle.c to LLVM IR exactly as the oracle is built (FP64, no FMA
+     contraction), with inlining and vectorisation off so every FP operation stays a scalar IR
+     instruction inside the function that performs it;
+  2. this script adds, at the top of every basic block, counter increments for the block's FP64
+     operations by kind (add, sub, mul, div, fma, sqrt, compare) into a per-phase table; the phase is the
+     innermost active "phase function" (substep, collide, robot_dynamics, build_rows, pgs, ik_solve) --
+     entering one saves and sets the current phase, every return restores it;
+  3. the instrumented library runs a canonical seeded trajectory through the oracle's own ugo_step /
+     ugo_reset (the bench workload: random actions in the action space, autoreset at max_episode_steps)
+     and the per-phase counts become the work model.
+
+FLOPs = add + sub + mul + div + sqrt + 2 * fma (compares, min/max, fabs and selects are not counted).
+Usage: python tools/opcount.py [--tasks 0,1,...]   (CPU only, this container; minutes)
+"""
+import argparse
+import ctypes
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLANG = "/opt/rocm/lib/llvm/bin/clang"
+PHASES = ["other", "substep", "collide", "robot_dynamics", "build_rows", "pgs", "ik_solve"]
+KINDS = ["fadd", "fsub", "fmul", "fdiv", "fma", "sqrt", "fcmp"]
+NPH, NK = 8, 8
+
+OP_RES = [
+    ("fadd", re.compile(r"= fadd (?:[a-z ]+ )?double ")),
+    ("fsub", re.compile(r"= fsub (?:[a-z ]+ )?double ")),
+    ("fmul", re.compile(r"= fmul (?:[a-z ]+ )?double ")),
+    ("fdiv", re.compile(r"= fdiv (?:[a-z ]+ )?double ")),
+    ("fma", re.compile(r"call (?:[a-z ]+ )?double @llvm\.(?:fma|fmuladd)\.f64\(")),
+    ("sqrt", re.compile(r"call (?:[a-z ]+ )?double @(?:llvm\.sqrt\.f64|sqrt)\(")),
+    ("fcmp", re.compile(r"= fcmp [a-z]+ double ")),
+]
+VEC_RE = re.compile(r"= f(?:add|sub|mul|div) [^=]*<\d+ x double>")
+LABEL_RE = re.compile(r"^([A-Za-z0-9_.$-]+):")
+DEFINE_RE = re.compile(r"^define .*@([A-Za-z0-9_.$]+)\(")
+
+RT_C = r"""
+long long __opc[8][8];
+int __opc_cur;
+void ugo_opcount_read(long long* out) { for (int i = 0; i < 64; i++) out[i] = ((long long*)__opc)[i]; }
+void ugo_opcount_reset(void) { for (int i = 0; i < 64; i++) ((long long*)__opc)[i] = 0; __opc_cur = 0; }
+"""
+
+
+def instrument(ir):
+    out = []
+    in_fn = None
+    blk = 0
+    pending = []   # lines of the current block (before insertion point is decided)
+    saved = None
+
+    def flush_block(lines, fn, idx, phase_entry):
+        """emit the block with its counter increments after the leading label / phi lines"""
+        counts = [0] * NK
+        for ln in lines:
+            if VEC_RE.search(ln):
+                raise SystemExit(f"vector FP op in {fn}: {ln.strip()} (build with -fno-vectorize)")
+            for k, (name, rx) in enumerate(OP_RES):
+                if rx.search(ln):
+                    counts[k] += 1
+        i = 0
+        if lines and LABEL_RE.match(lines[0]):
+            i = 1
+        while i < len(lines) and re.search(r"= phi ", lines[i]):
+            i += 1
+        ins = []
+        tag = f"%oc.{fn}.{idx}"
+        if phase_entry is not None:
+            ins.append(f"  {tag}.saved = load i32, ptr @__opc_cur\n")
+            ins.append(f"  store i32 {phase_entry}, ptr @__opc_cur\n")
+        if any(counts):
+            ins.append(f"  {tag}.cur = load i32, ptr @__opc_cur\n")
+            ins.append(f"  {tag}.row = sext i32 {tag}.cur to i64\n")
+            for k, c in enumerate(counts):
+                if c:
+                    ins.append(f"  {tag}.p{k} = getelementptr [8 x [8 x i64]], ptr @__opc, i64 0, i64 {tag}.row, i64 {k}\n")
+                    ins.append(f"  {tag}.v{k} = load i64, ptr {tag}.p{k}\n")
+                    ins.append(f"  {tag}.a{k} = add i64 {tag}.v{k}, {c}\n")
+                    ins.append(f"  store i64 {tag}.a{k}, ptr {tag}.p{k}\n")
+        return lines[:i] + ins + lines[i:]
+
+    for line in ir.splitlines(keepends=True):
+        if in_fn is None:
+            m = DEFINE_RE.match(line)
+            if m and line.rstrip().endswith("{"):
+                in_fn = m.group(1)
+                blk = 0
+                pending = []
+                saved = None
+                out.append(line)
+                continue
+            out.append(line)
+            continue
+        if line.startswith("}"):
+            out.extend(finish(pending, in_fn, blk, saved, flush_block))
+            out.append(line)
+            in_fn = None
+            continue
+        if LABEL_RE.match(line) and pending:
+            out.extend(finish(pending, in_fn, blk, saved, flush_block))
+            blk += 1
+            pending = []
+        pending.append(line)
+        if blk == 0 and saved is None:
+            saved = in_fn in PHASES
+    out.append("\n@__opc = external global [8 x [8 x i64]]\n@__opc_cur = external global i32\n")
+    return "".join(out)
+
+
+def finish(lines, fn, idx, is_phase, flush_block):
+    phase_entry = PHASES.index(fn) if (idx == 0 and is_phase) else None
+    body = flush_block(lines, fn, idx, phase_entry)
+    if is_phase:
+        res = []
+        for ln in body:
+            if re.match(r"\s+ret ", ln):
+                res.append(f"  store i32 %oc.{fn}.0.saved, ptr @__opc_cur\n")
+            res.append(ln)
+        body = res
+    return body
+
+
+def build(tmp):
+    ll = os.path.join(tmp, "ug.ll")
+    subprocess.run([CLANG, "-O1", "-fno-inline", "-fno-vectorize", "-fno-slp-vectorize", "-ffp-contract=off",
+                    "-fno-fast-math", "-mfma", "-std=gnu99", "-fPIC", "-S", "-emit-llvm", "-o", ll,
+                    os.path.join(ROOT, "oracle", "ug_oracle.c")], check=True)
+    inst = os.path.join(tmp, "ug_inst.ll")
+    open(inst, "w").write(instrument(open(ll).read()))
+    rt = os.path.join(tmp, "rt.c")
+    open(rt, "w").write(RT_C)
+    so = os.path.join(tmp, "libugoracle_opcount.so")
+    subprocess.run([CLANG, "-O1", "-shared", "-fPIC", "-o", so, inst, rt, "-lm"], check=True)
+    return so
+
+
+def count_task(L, pyoracle, spaces_for, task, n_envs, steps):
+    """per-phase FP64 op counts of a canonical trajectory of one task"""
+    tab = np.zeros(64, np.int64)
+    L.ugo_opcount_reset()
+    max_steps = {0: 500, 1: 50, 2: 20, 3: 100, 4: 50, 5: 100}[task]
+    envs = [pyoracle.OracleEnv(task, 20241220 + i) for i in range(n_envs)]
+    for e in envs:
+        e.reset()
+    L.ugo_opcount_read(tab.ctypes.data_as(ctypes.c_void_p))
+    reset0 = tab.reshape(8, 8).copy()
+    L.ugo_opcount_reset()
+    _, act_space = spaces_for(task)
+    rng = np.random.default_rng(20241220)
+    lo, hi = np.asarray(act_space.low, np.float64), np.asarray(act_space.high, np.float64)
+    substeps = resets = env_steps = 0
+    elapsed = [0] * n_envs
+    for t in range(steps):
+        act = rng.uniform(lo, hi, size=(n_envs, len(lo))).astype(np.float32)
+        for i, e in enumerate(envs):
+            _, _, term, _, ns = e.step(act[i])
+            substeps += ns
+            env_steps += 1
+            elapsed[i] += 1
+            if term or elapsed[i] >= max_steps:
+                _, ns2 = e.reset()
+                substeps += ns2
+                resets += 1
+                elapsed[i] = 0
+    L.ugo_opcount_read(tab.ctypes.data_as(ctypes.c_void_p))
+    c = tab.reshape(8, 8)
+
+    def flops(row):
+        return int(row[0] + row[1] + row[2] + row[3] + row[5] + 2 * row[4])
+
+    per_phase = {PHASES[p]: {"flops": flops(c[p]), **{KINDS[k]: int(c[p][k]) for k in range(len(KINDS))}}
+                 for p in range(len(PHASES))}
+    sub_phases = ["substep", "collide", "robot_dynamics", "build_rows", "pgs"]
+    f_sub_total = sum(per_phase[p]["flops"] for p in sub_phases)
+    f_total = sum(per_phase[p]["flops"] for p in PHASES)
+    return {
+        "envs": n_envs, "steps_per_env": steps, "env_steps": env_steps, "substeps": substeps, "resets": resets,
+        "mean_substeps_per_env_step": substeps / env_steps,
+        "F_sub": f_sub_total / substeps,
+        "F_env_step_total": f_total / env_steps,
+        "F_nonsub_per_env_step": (f_total - f_sub_total) / env_steps,
+        "F_IK_per_env_step": per_phase["ik_solve"]["flops"] / env_steps,
+        "substep_breakdown_per_substep": {p: per_phase[p]["flops"] / substeps for p in sub_phases},
+        "initial_reset_flops_per_env": flops(reset0.sum(0)) / n_envs,
+        "per_phase": per_phase,
+    }
+
+
+# canonical trajectories (envs, steps per env): long enough to include autoresets
+CANON = {0: (32, 80), 1: (16, 60), 2: (16, 30), 3: (8, 40), 4: (16, 60), 5: (8, 40)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tasks", default="0,1,2,3,4,5")
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "work_model.json"))
+    args = ap.parse_args()
+    sys.path.insert(0, ROOT)
+    from oracle import pyoracle
+    from urgym_amd.envs import spaces_for
+    model = {"what": "FP64 FLOPs of the CPU restatement (oracle/ug_oracle.c) on canonical seeded trajectories "
+                     "(random actions in the action space, seeds 20241220 + env, autoreset at max_episode_steps); "
+                     "FLOPs = add + sub + mul + div + sqrt + 2*fma, counted by tools/opcount.py (LLVM-IR op counters). "
+                     "bench.py: achieved = F_sub * substeps + F_nonsub_per_env_step * env_steps per launch.",
+             "tasks": {}}
+    if os.path.exists(args.out):
+        model["tasks"] = json.load(open(args.out)).get("tasks", {})
+    with tempfile.TemporaryDirectory() as tmp:
+        so = build(tmp)
+        pyoracle.LIB_PATH = so
+        pyoracle._lib = None
+        L = pyoracle.lib()
+        L.ugo_opcount_read.argtypes = [ctypes.c_void_p]
+        for t in [int(x) for x in args.tasks.split(",")]:
+            n, k = CANON[t]
+            m = count_task(L, pyoracle, spaces_for, t, n, k)
+            model["tasks"][str(t)] = m
+            print(t, json.dumps({k2: m[k2] for k2 in ("env_steps", "substeps", "resets", "mean_substeps_per_env_step",
+                                                      "F_sub", "F_nonsub_per_env_step", "F_IK_per_env_step")}), flush=True)
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    json.dump(model, open(args.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

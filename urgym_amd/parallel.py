@@ -8,8 +8,37 @@ of the returns (obs | reward | terminated | truncated) for a consumer that
 needs the whole batch (a central policy): torch.distributed backend "nccl" is
 RCCL over xGMI on MI355X; tests use "gloo" on CPU.
 """
+import os
+import socket
+import subprocess
+import sys
+
 import torch
 import torch.distributed as dist
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_command(nproc, script, argv, port):
+    """torch.distributed.run command line: one process per GPU of this node, rendezvous on 127.0.0.1"""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), script] + list(argv)
+
+
+def spawn_ranks(nproc, script, argv, port=None):
+    """Run `script argv` as nproc ranks (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set by torch.distributed.run)
+    in child processes and return their exit code.  The caller must not have touched the GPU: the ranks are
+    children, never an exec of the caller."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver (RCCL)
+    cmd = launch_command(nproc, script, argv, port or free_port())
+    return subprocess.call(cmd, env=env)
 
 
 def shard(total_envs, world_size, rank):
