@@ -30,6 +30,7 @@ typedef struct urgym_handle urgym_handle;
 #define URGYM_TASK_GOLF 3        /* urgym/envs/__init__.py:40-44  URGym/Golf-v0        */
 #define URGYM_TASK_CUBESPUSHDIFF 4 /* urgym/envs/__init__.py:16-20  URGym/CubesPushDiff-v0 (env_cubes_push_diff_v0.py) */
 #define URGYM_TASK_GOLFJOINTS 5    /* urgym/envs/__init__.py:46-50  URGym/GolfJoints-v0 (env_golf_joints_v0.py)      */
+#define URGYM_TASK_TWOBALLSBALANCE 6 /* urgym/envs/__init__.py:34-38 URGym/TwoBallsBalance-v0 (env_two_balls_balance_v0.py) */
 
 /* Replaces: gym.make(id) -> Env.__init__ (p.connect(DIRECT), loadURDF plane/table/robot,
  *   UR5Robotiq85.load(), env_ball_balance_v0.py:34-80; robot.py:178-211).
@@ -90,6 +91,35 @@ void* urgym_stream(urgym_handle* h);
  * saves env state). */
 int urgym_get_state(urgym_handle* h, double* state);
 int urgym_set_state(urgym_handle* h, const double* state);
+
+/* Replaces: the ctor kwarg reward_type ('dense' / 'sparse', env_cubes_push_v0.py:42,159; env_golf_v0.py:151,163).
+ * sparse != 0 drops the distance-shaping terms of CubesPush(Diff) / Golf(Joints); BallBalance, TwoBallsBalance and
+ * CubesGrasp store but never read it in the reference, so it changes nothing there. */
+int urgym_set_reward_type(urgym_handle* h, int sparse);
+
+/* Failure surfacing (no reference counterpart beyond the "did not stabilize" print, env_ball_balance_v0.py:102-103,
+ * SURVEY.md 5).  flags: n_envs bytes, UG_FLAG_* bits (urgym_amd/csrc/ug_layout.h) of the last step / reset call:
+ * 1 a wait_until_stable loop hit 480 substeps unsettled, 2 the state went non-finite (the env was terminated with
+ * reward 0 and, with autoreset, reset from a clean state), 4 contacts were dropped at a capacity limit.
+ * stats: n_envs x 8 int32 cumulative counters (UG_STAT_*: unstable waits, split-impulse substeps, row-capacity
+ * substeps, manifold-capacity substeps, non-finite terminations, substeps). */
+int urgym_get_flags(urgym_handle* h, uint8_t* flags);
+const uint8_t* urgym_flags_device(urgym_handle* h);
+int urgym_get_stats(urgym_handle* h, int32_t* stats);
+
+/* Checkpoint companion of urgym_get_state/urgym_set_state: each env's Python-random MT19937 stream
+ * (n_envs x 625 uint32: 624 words + index) and its elapsed episode steps (n_envs int32, may be NULL). */
+int urgym_get_rng(urgym_handle* h, uint32_t* mt, int32_t* elapsed);
+int urgym_set_rng(urgym_handle* h, const uint32_t* mt, const int32_t* elapsed);
+
+/* Replaces: p.getContactPoints(bodyA, bodyB, linkIndexA, linkIndexB) (env_cubes_grasp_v0.py:209-226) for every
+ * env.  Bodies are entity codes (0 robot, 1 + i task object i, 10 table, 11 plane, 12 golf pitch, -1 any), links
+ * the robot link index / -1 object base (Golf club parts 0, 1) / -2 any.  out: n_envs x max_pts x 24 doubles,
+ * pybullet's tuple (flag, bodyA, bodyB, linkA, linkB, positionOnA[3], positionOnB[3], contactNormalOnB[3],
+ * distance, normalForce, lateralFriction1, lateralFrictionDir1[3], lateralFriction2, lateralFrictionDir2[3]);
+ * count: n_envs matching points (may exceed max_pts; only max_pts are written). */
+int urgym_contact_points(urgym_handle* h, int body_a, int body_b, int link_a, int link_b, int max_pts, double* out,
+                         int32_t* count);
 
 /* Replaces: one p.stepSimulation() for every env (fine-grained parity tests). */
 int urgym_substep(urgym_handle* h);

@@ -39,7 +39,7 @@ def lib():
         L.ugo_norm3.restype = D
         L.ugo_g_cp_cube1_x.argtypes = [D]
         L.ugo_g_cp_cube1_x.restype = D
-        L.ugo_g_cp_reward.argtypes = [I, I, P, P, P]
+        L.ugo_g_cp_reward.argtypes = [I, I, P, P, I, P]
         L.ugo_g_cg_cube_xy.argtypes = [D, D, P]
         L.ugo_g_cg_choose.argtypes = [ctypes.c_float, ctypes.c_float, D]
         L.ugo_g_cg_opening.argtypes = [D]
@@ -47,7 +47,15 @@ def lib():
         L.ugo_g_cg_reward.argtypes = [P, D, D, I, D, P]
         L.ugo_g_union_center.argtypes = [P, P]
         L.ugo_g_gf_ball_xy.argtypes = [D, D, P]
-        L.ugo_g_gf_reward.argtypes = [P, P, P, I, I, I, P, P]
+        L.ugo_g_gf_reward.argtypes = [P, P, P, I, I, I, I, P, P]
+        L.ugo_g_tb_balls.argtypes = [P, P, P, P]
+        L.ugo_g_tb_reward.argtypes = [P, P, P, D, P]
+        L.ugo_flags.argtypes = [P]
+        L.ugo_get_stats.argtypes = [P, P]
+        L.ugo_set_reward_type.argtypes = [P, I]
+        L.ugo_get_rng.argtypes = [P, P]
+        L.ugo_set_rng.argtypes = [P, P]
+        L.ugo_contact_points.argtypes = [P, I, I, I, I, P, I]
         L.ugo_step.argtypes = [P, P, P, P, P, P]
         L.ugo_get_state.argtypes = [P, P]
         L.ugo_set_state.argtypes = [P, P]
@@ -129,6 +137,31 @@ class OracleEnv:
 
     def substep(self):
         self.L.ugo_substep(self.h)
+
+    def flags(self):
+        """UG_FLAG_* bits of the last step / reset call"""
+        return self.L.ugo_flags(self.h)
+
+    def stats(self):
+        out = np.zeros(8, np.int32)
+        self.L.ugo_get_stats(self.h, _p(out))
+        return out
+
+    def set_reward_type(self, reward_type):
+        self.L.ugo_set_reward_type(self.h, int(reward_type == "sparse"))
+
+    def get_rng(self):
+        out = np.zeros(625, np.uint32)
+        self.L.ugo_get_rng(self.h, _p(out))
+        return out
+
+    def set_rng(self, mt):
+        self.L.ugo_set_rng(self.h, _p(np.ascontiguousarray(mt, np.uint32)))
+
+    def contact_points(self, body_a=-1, body_b=-1, link_a=-2, link_b=-2, max_pts=64):
+        out = np.zeros((max_pts, 24))
+        n = self.L.ugo_contact_points(self.h, body_a, body_b, link_a, link_b, _p(out), max_pts)
+        return out[:min(n, max_pts)]
 
     def get_state(self):
         s = np.zeros(self.state_dim)

@@ -25,7 +25,7 @@ extern "C" {
 
 typedef struct ugo_env ugo_env;
 
-/* task: 0 BallBalance, 1 CubesPush, 2 CubesGrasp, 3 Golf */
+/* task: 0 BallBalance, 1 CubesPush, 2 CubesGrasp, 3 Golf, 4 CubesPushDiff, 5 GolfJoints, 6 TwoBallsBalance */
 ugo_env* ugo_create(int task, uint32_t seed);
 void ugo_destroy(ugo_env* e);
 int ugo_obs_dim(int task);
@@ -39,6 +39,16 @@ int ugo_reset_draws(ugo_env* e, const double* draws, double* obs);
 int ugo_step(ugo_env* e, const float* action, double* obs, double* reward, uint8_t* terminated,
              uint8_t* success);
 void ugo_get_state(const ugo_env* e, double* s);
+/* UG_FLAG_* of the last ugo_step / ugo_reset call; UG_STAT_* counters (UG_NSTAT int32) */
+int ugo_flags(const ugo_env* e);
+void ugo_get_stats(const ugo_env* e, int32_t* out);
+/* reward_type: 0 'dense', 1 'sparse' (ctor kwarg of every reference env) */
+void ugo_set_reward_type(ugo_env* e, int sparse);
+/* Python-random stream checkpoint: 624 MT words + index */
+void ugo_get_rng(const ugo_env* e, uint32_t* mt625);
+void ugo_set_rng(ugo_env* e, const uint32_t* mt625);
+/* p.getContactPoints over the manifold cache: 24 doubles per point (see ug_oracle.c); returns the count */
+int ugo_contact_points(const ugo_env* e, int bodyA, int bodyB, int linkA, int linkB, double* out, int max_pts);
 void ugo_set_state(ugo_env* e, const double* s);
 /* one physics substep (p.stepSimulation) -- for fine-grained parity tests */
 void ugo_substep(ugo_env* e);
@@ -68,7 +78,7 @@ int ugo_choose(ugo_env* e, float w0, float w1);
 double ugo_norm3(const double* v);
 /* shared task glue (urgym_amd/csrc/ug_glue.h) for the golden tests */
 double ugo_g_cp_cube1_x(double u);
-int ugo_g_cp_reward(int table, int touched, const double* c0, const double* c1, double* r);
+int ugo_g_cp_reward(int table, int touched, const double* c0, const double* c1, int sparse, double* r);
 void ugo_g_cg_cube_xy(double u0, double u1, double* xy);
 int ugo_g_cg_choose(float w0, float w1, double u);
 double ugo_g_cg_opening(double d);
@@ -76,7 +86,9 @@ int ugo_g_cg_reward(int* flags, double dist, double opening, int grasp, double c
 void ugo_g_union_center(const double* aabbs, double* c);
 void ugo_g_gf_ball_xy(double u0, double u1, double* xy);
 int ugo_g_gf_reward(const double* ball, const double* hole, const double* stick, int in_fingers, int floor_contact,
-                    int touched, double* r, int* term);
+                    int touched, int sparse, double* r, int* term);
+void ugo_g_tb_balls(const double* paddle, const double* u4, double* b1, double* b2);
+int ugo_g_tb_reward(const float* a, const double* b1, const double* b2, double paddle_z, double* r);
 /* batched CPU baseline: n envs, OpenMP over envs; returns total substeps */
 long ugo_batch_step(ugo_env** envs, int n, const float* actions, double* obs, double* reward,
                     uint8_t* terminated, uint8_t* success, int32_t* substeps, int autoreset,

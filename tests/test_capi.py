@@ -29,9 +29,9 @@ def test_library_exports_every_declared_symbol(built):
 def test_static_shapes(built):
     from urgym_amd._native import lib
     L = lib()
-    assert [L.urgym_obs_dim(t) for t in range(6)] == [6, 9, 17, 9, 9, 15]
-    assert [L.urgym_act_dim(t) for t in range(6)] == [3, 3, 9, 3, 3, 6]
-    assert [L.urgym_num_draws(t) for t in range(6)] == [2, 1, 2, 2, 1, 2]
+    assert [L.urgym_obs_dim(t) for t in range(7)] == [6, 9, 17, 9, 9, 15, 9]
+    assert [L.urgym_act_dim(t) for t in range(7)] == [3, 3, 9, 3, 3, 6, 3]
+    assert [L.urgym_num_draws(t) for t in range(7)] == [2, 1, 2, 2, 1, 2, 4]
     from oracle.pyoracle import lib as olib
     assert L.urgym_state_dim() == olib().ugo_state_dim()
 
@@ -46,6 +46,23 @@ def test_spaces_match_reference(built):
     assert obs.shape == (15,) and act.shape == (6,) and np.allclose(obs.high[:6], 2 * np.pi)
     from urgym_amd.envs import TASKS
     assert TASKS["URGym/CubesPushDiff-v0"] == (4, 50) and TASKS["URGym/GolfJoints-v0"] == (5, 100)
+    assert TASKS["URGym/TwoBallsBalance-v0"] == (6, 500)
+    obs, act = spaces_for(6)  # TwoBallsBalance: euler + two relative ball positions
+    assert obs.shape == (9,) and act.shape == (3,) and np.allclose(obs.low[3:], -1.0)
+
+
+def test_wrappers_refuse_what_they_do_not_implement(built):
+    from urgym_amd.envs import make
+    with pytest.raises(NotImplementedError):
+        make("URGym/Box-v0")
+    with pytest.raises(KeyError):
+        make("URGym/NoSuchEnv-v0")
+    from urgym_amd.envs.core import _check_kwargs
+    with pytest.raises(ValueError):
+        _check_kwargs(None, "shaped")
+    with pytest.raises(NotImplementedError):
+        _check_kwargs(object(), "dense")
+    _check_kwargs(None, "sparse")
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="GPU present")

@@ -66,9 +66,10 @@ def test_ballbalance_step_glue(ora):
         # obs via the oracle's observe() on a state holding the scripted paddle/ball poses
         e = ora.OracleEnv(0, 0)
         s = e.get_state()
-        s[38:40] = 1  # objects active
-        s[40:47] = c["paddle"]
-        s[53:56] = c["ball"]
+        from urgym_amd import layout as LY
+        s[LY.F_OACTIVE:LY.F_OACTIVE + 2] = 1  # objects active
+        s[LY.obj(0):LY.obj(0) + 7] = c["paddle"]
+        s[LY.obj(1):LY.obj(1) + 3] = c["ball"]
         e.set_state(s)
         obs = e.observe()
         assert obs[3:].tolist() == c["obs"][3:]

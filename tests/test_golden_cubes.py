@@ -52,7 +52,9 @@ def test_cubespush_step_reward_and_target(L):
         table = any(l != 0 for l in c["table_links"])                    # :176-183
         touched = any(9 <= l <= 18 for l in c["cube1_links"])            # :185-194
         r = np.zeros(1)
-        succ = L.ugo_g_cp_reward(int(table), int(touched), P(np.array(c["cube0"])), P(np.array(c["cube1"])), P(r))
+        sparse = int(c["reward_type"] == "sparse")                      # :159 reward_type
+        succ = L.ugo_g_cp_reward(int(table), int(touched), P(np.array(c["cube0"])), P(np.array(c["cube1"])), sparse,
+                                 P(r))
         assert r[0] == pytest.approx(c["reward"], rel=0, abs=4e-16), c
         assert bool(succ) == c["is_success"] == c["terminated"]
         assert c["obs"] == c["ee_pose"][:3] + c["cube0"] + c["cube1"]   # :196-205

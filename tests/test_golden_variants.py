@@ -46,5 +46,5 @@ def test_golf_joints_step(L):
         assert c["obs"] == list(q6) + list(stick) + list(stick - ball) + list(hole - ball)
         r = np.zeros(1)
         t = np.zeros(1, np.int32)
-        L.ugo_g_gf_reward(P(ball), P(hole), P(stick), 1, 0, 0, P(r), P(t))  # stick in fingers, no floor/touch
+        L.ugo_g_gf_reward(P(ball), P(hole), P(stick), 1, 0, 0, 0, P(r), P(t))  # stick in fingers, no floor/touch
         assert r[0] == pytest.approx(c["reward"], rel=0, abs=4e-16) and bool(t[0]) == c["terminated"]

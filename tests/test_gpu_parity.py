@@ -145,12 +145,12 @@ def _task_actions(task, rng, n):
         lo = np.array([0, 0] + [-np.pi] * 6 + [0], np.float64)
         hi = np.array([1, 1] + [np.pi] * 6 + [1], np.float64)
         return rng.uniform(lo, hi, size=(n, 9)).astype(np.float32)
-    if task == 5:  # GolfJoints: 6 joint deltas
+    if task == 5:  # GolfJoints: 6 joint deltas (TwoBallsBalance (6) has BallBalance's 3 euler deltas)
         return rng.uniform(-0.1, 0.1, size=(n, 6)).astype(np.float32)
     return rng.uniform(-0.1, 0.1, size=(n, 3)).astype(np.float32)
 
 
-@pytest.mark.parametrize("task,max_steps", [(1, 50), (2, 20), (3, 100), (4, 50), (5, 100)])
+@pytest.mark.parametrize("task,max_steps", [(1, 50), (2, 20), (3, 100), (4, 50), (5, 100), (6, 500)])
 def test_cube_tasks_bit_exact_with_autoreset(mods, task, max_steps):
     """CubesPush / CubesGrasp / Golf and the variants CubesPushDiff / GolfJoints
     (8(f) rank 1): reset, steps with contact-predicate rewards, subgoal flags, random.choices draws, the

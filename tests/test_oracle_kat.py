@@ -1,6 +1,8 @@
 """Known-answer tests and physics invariants of the CPU restatement (no PyBullet exists here,
 so these pin conventions and mechanics independently -- SURVEY.md 4)."""
 import numpy as np
+
+from urgym_amd import layout as LY
 import pytest
 from scipy.spatial.transform import Rotation
 
@@ -43,10 +45,11 @@ def _blank_with_ball(ora, pos, vel=(0, 0, 0)):
     s = e.get_state()
     s[:] = 0
     s[0:6] = [0, -1.57, 0, 0, 0, 0]
-    s[38:40] = [0, 1]           # paddle inactive, ball active
-    s[53:56] = pos
-    s[56:60] = [0, 0, 0, 1]
-    s[60:63] = vel
+    s[LY.F_OACTIVE:LY.F_OACTIVE + 2] = [0, 1]   # paddle inactive, ball active
+    b = LY.obj(1)
+    s[b:b + 3] = pos
+    s[b + 3:b + 7] = [0, 0, 0, 1]
+    s[b + 7:b + 10] = vel
     e.set_state(s)
     return e
 
@@ -61,8 +64,9 @@ def test_free_fall_matches_semi_implicit_euler_with_bullet_damping(ora):
         v = v + (g - v * (k + k * np.linalg.norm(v))) * dt
         x = x + v * dt
     s = e.get_state()
-    assert np.allclose(s[53:56], x, rtol=0, atol=1e-12)
-    assert np.allclose(s[60:63], v, rtol=0, atol=1e-12)
+    b = LY.obj(1)
+    assert np.allclose(s[b:b + 3], x, rtol=0, atol=1e-12)
+    assert np.allclose(s[b + 7:b + 10], v, rtol=0, atol=1e-12)
 
 
 def test_ball_comes_to_rest_on_table(ora):
@@ -70,8 +74,9 @@ def test_ball_comes_to_rest_on_table(ora):
     for _ in range(480):
         e.substep()
     s = e.get_state()
-    assert abs(s[55] - 0.02) < 2e-3          # centre one radius above the table top (z = 0)
-    assert np.linalg.norm(s[60:63]) < 1e-3   # at rest
+    b = LY.obj(1)
+    assert abs(s[b + 2] - 0.02) < 2e-3               # centre one radius above the table top (z = 0)
+    assert np.linalg.norm(s[b + 7:b + 10]) < 1e-3    # at rest
 
 
 def test_ik_converges_to_reachable_target(ora):
@@ -109,13 +114,13 @@ def test_paddle_stays_grasped_and_ball_dynamics_finite(ora):
     e = ora.OracleEnv(0, SEED)
     e.reset()
     rng = np.random.default_rng(3)
-    p0 = e.get_state()[40:43].copy()
+    p0 = e.get_state()[LY.obj(0):LY.obj(0) + 3].copy()
     for _ in range(15):
         obs, r, term, succ, n = e.step(rng.uniform(-0.1, 0.1, 3).astype(np.float32))
         assert np.all(np.isfinite(obs)) and 1 <= n <= 480
         if term:
             break
-    p1 = e.get_state()[40:43]
+    p1 = e.get_state()[LY.obj(0):LY.obj(0) + 3]
     # the paddle is carried by the gripper: it moved with the end effector, it did not fall to the table
     assert p1[2] > 0.3 and np.linalg.norm(p1 - p0) < 0.3
 

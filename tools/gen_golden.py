@@ -159,6 +159,7 @@ def main():
     gen_cubes(p, rng)
     gen_golf(p)
     gen_variants(p)
+    gen_twoballs(p)
     print("wrote", sorted(os.listdir(OUT)))
 
 
@@ -221,10 +222,10 @@ def gen_cubes(p, rng):
         ((0.07, 0.03, -0.05), [0, 0], [18], (0.0, -0.5, 0.02), (0.06, -0.58, 0.021)),
         ((0.02, 0.02, 0.02), [], [10], (0.1, -0.45, 0.02), (0.1, -0.7, 0.02)),
     ]
-    for act, table_links, cube_links, c0, c1 in cases:
+    for (act, table_links, cube_links, c0, c1), rtype in [(c, rt) for rt in ("dense", "sparse") for c in cases]:
         env = CubesPush.__new__(CubesPush)
         env.visualize = False
-        env.reward_type = "dense"
+        env.reward_type = rtype
         env.positive_reward_radius = 0.1
         env.vertical_quaternion = tuple(vq)
         env.control_method = "end"
@@ -253,6 +254,7 @@ def gen_cubes(p, rng):
         obs, rew, term, trunc, info = env.step(a)
         steps.append({"action": a.tolist(), "ee_pose": list(ee_pose), "table_links": table_links,
                       "cube1_links": cube_links, "cube0": list(c0), "cube1": list(c1), "ik_target": moves[0][0],
+                      "reward_type": rtype,
                       "obs": [float(x) for x in obs], "reward": float(rew), "terminated": bool(term),
                       "is_success": bool(info["is_success"])})
     out["cubespush_step"] = steps
@@ -389,10 +391,11 @@ def gen_golf(p):
         ((0.1, -0.65, 0.06), (0.08, -0.66, 0.07), [11, 18], [], False, True),  # touched
         ((0.3, -0.9, 0.06), (0.05, -0.6, 0.07), [13], [], False, False),       # dense only
     ]
-    for ball, stick, fingers, robot_pitch, stick_pitch, touched in cases:
+    for (ball, stick, fingers, robot_pitch, stick_pitch, touched), rtype in [(c, rt) for rt in ("dense", "sparse")
+                                                                              for c in cases]:
         env = Golf.__new__(Golf)
         env.visualize = False
-        env.reward_type = "dense"
+        env.reward_type = rtype
         env.positive_reward_radius = 0.1
         env.control_method = "end"
         env.vertical_quaternion = [0.0, 0.0, -0.7, 0.7]
@@ -420,14 +423,79 @@ def gen_golf(p):
             return []
         p.getContactPoints.side_effect = cps
         a = np.array([0.03, -0.02, 0.01], np.float32)
-        obs, rew, term, trunc, info = env.step(a)
+        try:
+            obs, rew, term, trunc, info = env.step(a)
+        except UnboundLocalError as exc:
+            # reference defect: with reward_type='sparse' and neither floor contact nor ball touch, `success` is
+            # never assigned (env_golf_v0.py:146-172) and step() raises; recorded as such
+            steps.append({"ball": list(ball), "hole": list(hole), "stick": list(stick), "finger_links": fingers,
+                          "robot_pitch_links": robot_pitch, "stick_pitch": stick_pitch, "touched": touched,
+                          "action": a.tolist(), "reward_type": rtype, "raises": type(exc).__name__})
+            continue
         steps.append({"ball": list(ball), "hole": list(hole), "stick": list(stick), "finger_links": fingers,
                       "robot_pitch_links": robot_pitch, "stick_pitch": stick_pitch, "touched": touched,
-                      "action": a.tolist(), "ee_pose": list(ee), "ik_target": moves[0][0],
+                      "action": a.tolist(), "ee_pose": list(ee), "ik_target": moves[0][0], "reward_type": rtype,
                       "obs": [float(x) for x in obs], "reward": float(rew), "terminated": bool(term),
                       "is_success": bool(info["is_success"])})
     out["golf_step"] = steps
     json.dump(out, open(os.path.join(OUT, "golf_glue.json"), "w"), indent=1)
+
+
+def gen_twoballs(p):
+    """TwoBallsBalance (env_two_balls_balance_v0.py) glue: create_balls draw order and placement, step reward
+    (action penalty, per-axis 1 - x^2 shaping), termination and observation with scripted physics.
+
+    numpy: the reference pins numpy 1.26.4 (setup.py:8), under which `0 + np.float32` promotes to float64, so
+    the action penalty is summed in float64.  This container has numpy 2 (NEP 50 keeps float32), so the step is
+    driven with the float32 action values held in a float64 array -- the same values, summed as numpy 1.26 does."""
+    from urgym.envs.env_two_balls_balance_v0 import TwoBallsBalance  # noqa: E402
+    out = {"create_balls": [], "step": []}
+    for seed, paddle in [(0, (0.01, -0.8, 0.61)), (20241220, (-0.02, -0.79, 0.612)), (99, (0.0, -0.8, 0.6))]:
+        env = TwoBallsBalance.__new__(TwoBallsBalance)
+        env.paddle_id = 5
+        p.reset_mock()
+        p.getBasePositionAndOrientation.side_effect = None
+        p.getBasePositionAndOrientation.return_value = (paddle, (0.0, 0.0, 0.0, 1.0))
+        bodies = []
+        p.createMultiBody.side_effect = lambda *a, **k: bodies.append([float(a[0]), [float(x) for x in a[3]]]) or 40 + len(bodies)
+        p.createCollisionShape.side_effect = lambda **k: ("sphere", float(k.get("radius", -1)))
+        random.seed(seed)
+        env.create_balls(0.003)
+        random.seed(seed)
+        u = [random.random() for _ in range(4)]
+        radius = p.createCollisionShape.call_args.kwargs["radius"]
+        out["create_balls"].append({"seed": seed, "paddle": list(paddle), "draws": u, "radius": radius,
+                                    "bodies": bodies})
+        p.createMultiBody.side_effect = None
+        p.createCollisionShape.side_effect = None
+    rng = np.random.default_rng(11)
+    ee_pose = (0.1, -0.6, 0.6, 0.5, -0.5, -0.5, 0.5)
+    for k in range(8):
+        env = TwoBallsBalance.__new__(TwoBallsBalance)
+        env.visualize = False
+        env.control_method = "end"
+        env.paddle_id, env.ball1_id, env.ball2_id = 5, 6, 7
+        moves = []
+        env.robot = types.SimpleNamespace(get_ee_pose=lambda: ee_pose,
+                                          move_ee=lambda pose, m: moves.append(([float(x) for x in pose], m)))
+        env.wait_until_stable = lambda: True
+        paddle = tuple(float(x) for x in (rng.uniform(-0.05, 0.05), -0.8 + rng.uniform(-0.05, 0.05), 0.6))
+        b1 = (float(rng.uniform(-1.2, 1.2)), float(rng.uniform(-1.2, 1.2)), 0.6 + float(rng.uniform(-0.01, 0.03)))
+        b2 = (float(rng.uniform(-0.3, 0.3)), float(rng.uniform(-0.9, -0.5)), 0.6 + float(rng.uniform(-0.01, 0.03)))
+        pq = (0.01, -0.02, 0.003, 0.9997)
+        bodies = {5: (paddle, pq), 6: (b1, (0, 0, 0, 1)), 7: (b2, (0, 0, 0, 1))}
+        p.reset_mock()
+        p.getBasePositionAndOrientation.side_effect = lambda i: bodies[i]
+        p.getEulerFromQuaternion.side_effect = lambda q: (0.25, -0.125, 0.5) if tuple(q) == ee_pose[3:] else (0.01, 0.02, 0.03)
+        p.getQuaternionFromEuler.side_effect = lambda e: (0.1, 0.2, 0.3, 0.9)
+        a32 = rng.uniform(-0.1, 0.1, 3).astype(np.float32)
+        obs, rew, term, trunc, info = env.step(a32.astype(np.float64))
+        euler_in = [float(x) for x in p.getQuaternionFromEuler.call_args.args[0]]
+        out["step"].append({"action": a32.tolist(), "paddle": list(paddle), "paddle_quat": list(pq), "ball1": list(b1),
+                            "ball2": list(b2), "ee_euler": [0.25, -0.125, 0.5], "euler_plus_action": euler_in,
+                            "ik_target": moves[0][0], "obs": [float(x) for x in obs], "reward": float(rew),
+                            "terminated": bool(term), "info": info})
+    json.dump(out, open(os.path.join(OUT, "twoballs_glue.json"), "w"), indent=1)
 
 
 def gen_variants(p):
@@ -480,5 +548,8 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "variants":  # only the variant fixtures
         os.makedirs(OUT, exist_ok=True)
         gen_variants(install_stubs())
+    elif len(sys.argv) > 1 and sys.argv[1] == "twoballs":
+        os.makedirs(OUT, exist_ok=True)
+        gen_twoballs(install_stubs())
     else:
         main()

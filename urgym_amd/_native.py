@@ -17,8 +17,15 @@ SYMBOLS = [
     "urgym_num_envs", "urgym_set_autoreset", "urgym_reset", "urgym_num_draws", "urgym_step", "urgym_step_device",
     "urgym_reset_device", "urgym_sync", "urgym_stream", "urgym_get_state", "urgym_set_state", "urgym_substep",
     "urgym_link_state", "urgym_ik", "urgym_last_kernel_ms", "urgym_debug_prof", "urgym_debug_workspace",
-    "urgym_debug_ws_doubles",
+    "urgym_debug_ws_doubles", "urgym_set_reward_type", "urgym_get_flags", "urgym_flags_device", "urgym_get_stats",
+    "urgym_get_rng", "urgym_set_rng", "urgym_contact_points",
 ]
+
+# UG_FLAG_* / UG_STAT_* (urgym_amd/csrc/ug_layout.h)
+FLAG_UNSTABLE, FLAG_NONFINITE, FLAG_DROPPED = 1, 2, 4
+STAT_NAMES = ["unstable_waits", "split_substeps", "row_capacity_substeps", "manifold_capacity_substeps",
+              "nonfinite_terminations", "substeps", "reserved6", "reserved7"]
+CONTACT_FIELDS = 24  # pybullet getContactPoints tuple, flattened
 
 _lib = None
 
@@ -58,6 +65,14 @@ def lib():
     L.urgym_debug_prof.argtypes = [P, P, I]
     L.urgym_debug_workspace.argtypes = [P, I, P, I]
     L.urgym_debug_ws_doubles.argtypes = []
+    L.urgym_set_reward_type.argtypes = [P, I]
+    L.urgym_get_flags.argtypes = [P, P]
+    L.urgym_flags_device.restype = P
+    L.urgym_flags_device.argtypes = [P]
+    L.urgym_get_stats.argtypes = [P, P]
+    L.urgym_get_rng.argtypes = [P, P, P]
+    L.urgym_set_rng.argtypes = [P, P, P]
+    L.urgym_contact_points.argtypes = [P, I, I, I, I, I, P, P]
     _lib = L
     return L
 
@@ -147,6 +162,42 @@ class Sim:
         out = np.zeros((self.n, 7))
         self._chk(self.L.urgym_link_state(self.h, int(link), ptr(out)), "urgym_link_state")
         return out
+
+    def set_reward_type(self, reward_type):
+        if reward_type not in ("dense", "sparse"):
+            raise ValueError(f"reward_type must be 'dense' or 'sparse', not {reward_type!r}")
+        self._chk(self.L.urgym_set_reward_type(self.h, int(reward_type == "sparse")), "urgym_set_reward_type")
+
+    def flags(self):
+        """UG_FLAG_* bits per env of the last step / reset call"""
+        f = np.zeros(self.n, np.uint8)
+        self._chk(self.L.urgym_get_flags(self.h, ptr(f)), "urgym_get_flags")
+        return f
+
+    def stats(self):
+        out = np.zeros((self.n, 8), np.int32)
+        self._chk(self.L.urgym_get_stats(self.h, ptr(out)), "urgym_get_stats")
+        return out
+
+    def get_rng(self):
+        """(MT19937 streams n x 625 uint32, elapsed episode steps n int32): checkpoint companion of get_state"""
+        mt = np.zeros((self.n, 625), np.uint32)
+        el = np.zeros(self.n, np.int32)
+        self._chk(self.L.urgym_get_rng(self.h, ptr(mt), ptr(el)), "urgym_get_rng")
+        return mt, el
+
+    def set_rng(self, mt, elapsed=None):
+        m = np.ascontiguousarray(mt, np.uint32).reshape(self.n, 625)
+        e = None if elapsed is None else np.ascontiguousarray(elapsed, np.int32).reshape(self.n)
+        self._chk(self.L.urgym_set_rng(self.h, ptr(m), ptr(e)), "urgym_set_rng")
+
+    def contact_points(self, body_a=-1, body_b=-1, link_a=-2, link_b=-2, max_pts=64):
+        """p.getContactPoints for every env: (n x max_pts x 24 tuples, n counts)"""
+        out = np.zeros((self.n, max_pts, CONTACT_FIELDS))
+        cnt = np.zeros(self.n, np.int32)
+        self._chk(self.L.urgym_contact_points(self.h, body_a, body_b, link_a, link_b, max_pts, ptr(out), ptr(cnt)),
+                  "urgym_contact_points")
+        return out, cnt
 
     def ik(self, target):
         t = np.ascontiguousarray(target, dtype=np.float64).reshape(self.n, 7)

@@ -55,11 +55,13 @@ UG_CONST double UG_GEAR_RATIO[5] = {1.0, -1.0, -1.0, 1.0, -1.0};
 /* variants: same scene and physics as their base task, different step/obs glue */
 #define UG_TASK_CUBESPUSHDIFF 4 /* env_cubes_push_diff_v0.py: obs = ee, cube - ee (x2) */
 #define UG_TASK_GOLFJOINTS 5    /* env_golf_joints_v0.py: joint-space action[6], obs = joints + Golf obs */
-#define UG_NTASK 6
-#define UG_BASE_TASK(t) ((t) == UG_TASK_CUBESPUSHDIFF ? UG_TASK_CUBESPUSH : ((t) == UG_TASK_GOLFJOINTS ? UG_TASK_GOLF : (t)))
+#define UG_TASK_TWOBALLS 6      /* env_two_balls_balance_v0.py: BallBalance robot + paddle, two balls r 0.003 */
+#define UG_NTASK 7
+#define UG_BASE_TASK(t) ((t) == UG_TASK_CUBESPUSHDIFF ? UG_TASK_CUBESPUSH : \
+                         ((t) == UG_TASK_GOLFJOINTS ? UG_TASK_GOLF : ((t) == UG_TASK_TWOBALLS ? UG_TASK_BALLBALANCE : (t))))
 #define UG_OBS_DIM(t) ((t) == 0 ? 6 : ((t) == 2 ? 17 : ((t) == 5 ? 15 : 9)))
 #define UG_ACT_DIM(t) ((t) == 2 ? 9 : ((t) == 5 ? 6 : 3))
-#define UG_NDRAW(t) ((t) == 1 || (t) == 4 ? 1 : 2)
+#define UG_NDRAW(t) ((t) == 1 || (t) == 4 ? 1 : ((t) == 6 ? 4 : 2))
 
 /* ---- shapes ---- */
 #define UG_SHAPE_BOX 0
@@ -82,6 +84,9 @@ UG_CONST double UG_GEAR_RATIO[5] = {1.0, -1.0, -1.0, 1.0, -1.0};
 #define UG_BB_PADDLE_MASS 0.1          /* :183 */
 #define UG_BB_BALL_R 0.02              /* :186 */
 #define UG_BB_BALL_MASS 0.01           /* :202 */
+/* TwoBallsBalance (env_two_balls_balance_v0.py): same paddle; create_balls(0.003) (:187) -> two spheres of
+ * radius 0.003, 0.01 kg (:213-233), ball 1 at +0.2 + r, ball 2 at +0.2 - r above the paddle */
+#define UG_TB_BALL_R 0.003
 
 /* CubesPush / CubesGrasp: cube.urdf x 0.04 (mass 1, lateral friction 1) [ext] */
 #define UG_CUBE_HALF 0.02

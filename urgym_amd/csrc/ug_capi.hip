@@ -9,6 +9,7 @@
 // per launch.  There is no CPU fallback: if this library is missing, nothing runs.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -69,6 +70,7 @@ __global__ void k_build_scene(Scene* s, int variant) {
     s->nobj = 0;
     s->ncol = 0;
     s->npair = 0;
+    s->sparse = 0;
     for (int o = 0; o < MAXOBJ; o++) s->oncol[o] = 0;
     for (int l = 1; l < UG_NL; l++) {
         Collider* c = &s->col[s->ncol++];
@@ -96,7 +98,10 @@ __global__ void k_build_scene(Scene* s, int variant) {
     int nrobot = s->ncol;
     int statics[4], nstat = 0;
     if (task == UG_TASK_BALLBALANCE) {
-        s->nobj = 2;
+        /* paddle, ball (env_ball_balance_v0.py:175-205); TwoBallsBalance: two balls of radius 0.003
+         * (env_two_balls_balance_v0.py:187, 212-235) */
+        const int two = variant == UG_TASK_TWOBALLS;
+        s->nobj = two ? 3 : 2;
         double hx = UG_BB_PADDLE_HX, hy = UG_BB_PADDLE_HY, hz = UG_BB_PADDLE_HZ, m = UG_BB_PADDLE_MASS;
         s->omass[0] = m;
         s->oinertia[0] = V(m / 12.0 * (4.0 * hy * hy + 4.0 * hz * hz), m / 12.0 * (4.0 * hx * hx + 4.0 * hz * hz),
@@ -105,17 +110,19 @@ __global__ void k_build_scene(Scene* s, int variant) {
         box_collider(c, hx, hy, hz, safe_margin(hx, hy, hz), UG_DEFAULT_FRICTION);
         c->owner = -2; c->ent = 1;
         s->ocol[0] = s->ncol++;
-        double r = UG_BB_BALL_R, mb = UG_BB_BALL_MASS;
-        s->omass[1] = mb;
-        double ib = 0.4 * mb * r * r;
-        s->oinertia[1] = V(ib, ib, ib);
-        c = &s->col[s->ncol];
-        box_collider(c, r, r, r, r, UG_DEFAULT_FRICTION);
-        c->kind = UG_SHAPE_SPHERE;
-        c->half[1] = c->half[2] = 0.0;
-        c->disc = ug_sqrt(3.0) * r;
-        c->owner = -3; c->ent = 2;
-        s->ocol[1] = s->ncol++;
+        double r = two ? UG_TB_BALL_R : UG_BB_BALL_R, mb = UG_BB_BALL_MASS;
+        for (int o = 1; o < s->nobj; o++) {
+            s->omass[o] = mb;
+            double ib = 0.4 * mb * r * r;
+            s->oinertia[o] = V(ib, ib, ib);
+            c = &s->col[s->ncol];
+            box_collider(c, r, r, r, r, UG_DEFAULT_FRICTION);
+            c->kind = UG_SHAPE_SPHERE;
+            c->half[1] = c->half[2] = 0.0;
+            c->disc = ug_sqrt(3.0) * r;
+            c->owner = -2 - o; c->ent = 1 + o;
+            s->ocol[o] = s->ncol++;
+        }
     }
     if (task == UG_TASK_CUBESPUSH || task == UG_TASK_CUBESGRASP) {
         s->nobj = task == UG_TASK_CUBESPUSH ? 2 : 1;
@@ -237,12 +244,12 @@ static __device__ int task_ndraw(int variant) { return UG_NDRAW(variant); }
 
 __global__ void __launch_bounds__(TEAM, 1) k_reset(const Scene* sc, double* S, uint32_t* mt, int* elapsed, double* ws,
                                                    int n, const uint8_t* mask, const double* draws, double* obs,
-                                                   int32_t* substeps) {
+                                                   int32_t* substeps, int* stats, uint8_t* flags) {
     const int i = blockIdx.x;
     if (i >= n) return;
     if (mask && !mask[i]) return;
     double* Si = S + (size_t)i * UG_STATE_DIM;
-    team_load(Si);
+    team_load(Si, stats + (size_t)i * UG_NSTAT);
     RunIO io;
     io.act = nullptr;
     io.obs = obs + (size_t)i * task_obs_dim(sc->variant);
@@ -253,7 +260,7 @@ __global__ void __launch_bounds__(TEAM, 1) k_reset(const Scene* sc, double* S, u
     PROF_T0(t_tot);
     int ns = team_run(sc, ws + (size_t)i * WS_DOUBLES, G_RESET, io);
     PROF_ADD(PF_TOTAL, t_tot);
-    team_store(Si);
+    team_store(Si, stats + (size_t)i * UG_NSTAT, flags + i);
     team_prof_flush();
     if (threadIdx.x == 0) {
         elapsed[i] = 0;
@@ -264,11 +271,12 @@ __global__ void __launch_bounds__(TEAM, 1) k_reset(const Scene* sc, double* S, u
 __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, uint32_t* mt, int* elapsed, double* ws,
                                                   int n, const float* act, double* obs, double* final_obs, double* rew,
                                                   uint8_t* term, uint8_t* trunc, uint8_t* succ, int32_t* substeps,
-                                                  int autoreset, int max_steps, const int* order, uint8_t* prio) {
+                                                  int autoreset, int max_steps, const int* order, uint8_t* prio,
+                                                  int* stats, uint8_t* flags) {
     if ((int)blockIdx.x >= n) return;
     const int i = order[blockIdx.x];
     double* Si = S + (size_t)i * UG_STATE_DIM;
-    team_load(Si);
+    team_load(Si, stats + (size_t)i * UG_NSTAT);
     const int O = task_obs_dim(sc->variant), A = task_act_dim(sc->variant);
     const int el = elapsed[i] + 1;
     RunIO io;
@@ -282,7 +290,7 @@ __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, ui
     PROF_T0(t_tot);
     int ns = team_run(sc, ws + (size_t)i * WS_DOUBLES, G_STEP, io);
     PROF_ADD(PF_TOTAL, t_tot);
-    team_store(Si);
+    team_store(Si, stats + (size_t)i * UG_NSTAT, flags + i);
     team_prof_flush();
     if (threadIdx.x == 0) {
         elapsed[i] = io.reset_done ? 0 : el;
@@ -325,13 +333,13 @@ __global__ void k_iota(int* order, uint8_t* prio, int n) {
     if (i < n) { order[i] = i; prio[i] = 0; }
 }
 
-__global__ void __launch_bounds__(TEAM, 1) k_substep(const Scene* sc, double* S, double* ws, int n) {
+__global__ void __launch_bounds__(TEAM, 1) k_substep(const Scene* sc, double* S, double* ws, int n, int* stats) {
     const int i = blockIdx.x;
     if (i >= n) return;
     double* Si = S + (size_t)i * UG_STATE_DIM;
-    team_load(Si);
+    team_load(Si, stats + (size_t)i * UG_NSTAT);
     team_substep(sc, ws + (size_t)i * WS_DOUBLES);
-    team_store(Si);
+    team_store(Si, stats + (size_t)i * UG_NSTAT, nullptr);
 }
 
 // getLinkState / calculateInverseKinematics queries: one env per lane (not on the step path)
@@ -357,6 +365,74 @@ __global__ void __launch_bounds__(WAVE) k_ik(const double* S, int n, const doubl
     for (int j = 0; j < NB; j++) qout[(size_t)i * NB + j] = qo[j];
 }
 
+/* p.getContactPoints(bodyA, bodyB, linkIndexA, linkIndexB) over each env's manifold cache (lane per env; a
+ * query, not on the step path).  Same definition as the oracle's ugo_contact_points: entity codes (0 robot,
+ * 1 + i object i, 10 table, 11 plane, 12 pitch, -1 any), links (robot link index, object base -1 / club parts
+ * 0, 1, -2 any), 24 doubles per point in pybullet's tuple order, forces = impulse / dt, friction directions
+ * btPlaneSpace1 of the normal, swapped tuple when the query's A is the pair's B side. */
+__device__ static int link_of_collider(const Scene* s, int ci) {
+    const Collider& c = s->col[ci];
+    if (c.ent == 0) return c.link;
+    if (c.ent >= 1 && c.ent <= MAXOBJ) return ci - s->ocol[c.ent - 1] - 1;
+    return -1;
+}
+__global__ void __launch_bounds__(WAVE) k_contacts(const Scene* sc, const double* S, int n, int bodyA, int bodyB,
+                                                   int linkA, int linkB, int max_pts, double* out, int32_t* count) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const EnvState& e = *(const EnvState*)(S + (size_t)i * UG_STATE_DIM);
+    Kin k;
+    fk(e.q, k);
+    int cnt = 0;
+    const int nm = (int)e.nman;
+    for (int m = 0; m < nm; m++) {
+        const StMan& M = e.man[m];
+        const PairDef& P = sc->pair[(int)M.pair];
+        const int ea = sc->col[P.a].ent, eb = sc->col[P.b].ent;
+        const int la = link_of_collider(sc, P.a), lb = link_of_collider(sc, P.b);
+        auto mt = [](int want, int have) { return want == -1 || want == have; };
+        auto ml = [](int want, int have) { return want == -2 || want == have; };
+        int swap;
+        if (mt(bodyA, ea) && mt(bodyB, eb) && ml(linkA, la) && ml(linkB, lb)) swap = 0;
+        else if (mt(bodyA, eb) && mt(bodyB, ea) && ml(linkA, lb) && ml(linkB, la)) swap = 1;
+        else continue;
+        const XF OA = owner_xf(e, k, sc->col[P.a].owner), OB = owner_xf(e, k, sc->col[P.b].owner);
+        const int np = (int)M.npts;
+        for (int j = 0; j < np; j++) {
+            const StPt& c = M.pt[j];
+            if (cnt < max_pts) {
+                double* o = out + ((size_t)i * max_pts + cnt) * 24;
+                v3 pA = xf_apply(OA, c.lpA), pB = xf_apply(OB, c.lpB);
+                v3 nn = c.n, t1, t2;
+                if (ug_fabs(nn.z) > 0.7071067811865475244) {
+                    double a = nn.y * nn.y + nn.z * nn.z, kk = 1.0 / ug_sqrt(a);
+                    t1 = V(0, -nn.z * kk, nn.y * kk);
+                    t2 = V(a * kk, -nn.x * t1.z, nn.x * t1.y);
+                } else {
+                    double a = nn.x * nn.x + nn.y * nn.y, kk = 1.0 / ug_sqrt(a);
+                    t1 = V(-nn.y * kk, nn.x * kk, 0);
+                    t2 = V(-nn.z * t1.y, nn.z * t1.x, a * kk);
+                }
+                if (swap) { v3 t = pA; pA = pB; pB = t; nn = vneg(nn); }
+                o[0] = 0.0;
+                o[1] = swap ? eb : ea; o[2] = swap ? ea : eb;
+                o[3] = swap ? lb : la; o[4] = swap ? la : lb;
+                o[5] = pA.x; o[6] = pA.y; o[7] = pA.z;
+                o[8] = pB.x; o[9] = pB.y; o[10] = pB.z;
+                o[11] = nn.x; o[12] = nn.y; o[13] = nn.z;
+                o[14] = c.dist;
+                o[15] = c.imp / UG_DT;
+                o[16] = c.imp1 / UG_DT;
+                o[17] = t1.x; o[18] = t1.y; o[19] = t1.z;
+                o[20] = c.imp2 / UG_DT;
+                o[21] = t2.x; o[22] = t2.y; o[23] = t2.z;
+            }
+            cnt++;
+        }
+    }
+    count[i] = cnt;
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -377,6 +453,8 @@ struct urgym_handle {
     int32_t* d_sub = nullptr;
     int* d_order = nullptr;   // k_step launch order (blockIdx -> env), from the previous step's priorities
     uint8_t* d_prio = nullptr;
+    int* d_stats = nullptr;   // UG_NSTAT event counters per env
+    uint8_t* d_flags = nullptr; // UG_FLAG_* of the last step / reset per env
     int autoreset = 0, max_steps = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
@@ -452,6 +530,10 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     HIPCHK(h, hipMalloc(&h->d_sub, sizeof(int32_t) * N));
     HIPCHK(h, hipMalloc(&h->d_order, sizeof(int) * N));
     HIPCHK(h, hipMalloc(&h->d_prio, N));
+    HIPCHK(h, hipMalloc(&h->d_stats, sizeof(int) * UG_NSTAT * N));
+    HIPCHK(h, hipMalloc(&h->d_flags, N));
+    HIPCHK(h, hipMemsetAsync(h->d_stats, 0, sizeof(int) * UG_NSTAT * N, h->stream));
+    HIPCHK(h, hipMemsetAsync(h->d_flags, 0, N, h->stream));
     k_iota<<<grid_of(n), WAVE, 0, h->stream>>>(h->d_order, h->d_prio, n);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipMemsetAsync(h->d_state, 0, sizeof(double) * UG_STATE_DIM * N, h->stream));
@@ -467,7 +549,7 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
 }
 
 urgym_handle* urgym_create(int task, int n, int dev, int precision, uint32_t seed, int env_offset) {
-    if (task < URGYM_TASK_BALLBALANCE || task > URGYM_TASK_GOLFJOINTS) {
+    if (task < URGYM_TASK_BALLBALANCE || task > URGYM_TASK_TWOBALLSBALANCE) {
         fail(nullptr, "urgym_create: unknown task " + std::to_string(task));
         return nullptr;
     }
@@ -488,7 +570,8 @@ void urgym_destroy(urgym_handle* h) {
     hipSetDevice(h->dev);
     if (h->stream) hipStreamSynchronize(h->stream);
     void* ptrs[] = {h->d_scene, h->d_state, h->d_ws, h->d_mt, h->d_elapsed, h->d_act, h->d_obs, h->d_final, h->d_rew,
-                    h->d_draws, h->d_aux, h->d_term, h->d_trunc, h->d_succ, h->d_mask, h->d_sub, h->d_order, h->d_prio};
+                    h->d_draws, h->d_aux, h->d_term, h->d_trunc, h->d_succ, h->d_mask, h->d_sub, h->d_order, h->d_prio,
+                    h->d_stats, h->d_flags};
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -523,7 +606,7 @@ int urgym_reset_device(urgym_handle* h, const uint8_t* d_mask, const double* d_d
     HIPCHK(h, hipSetDevice(h->dev));
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
     k_reset<<<h->n, TEAM, 0, h->stream>>>(h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->d_ws, h->n, d_mask,
-                                           d_draws, d_obs, nullptr);
+                                           d_draws, d_obs, nullptr, h->d_stats, h->d_flags);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     h->timed = true;
@@ -556,7 +639,7 @@ int urgym_step_device(urgym_handle* h, const float* d_act, double* d_obs, double
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
     k_step<<<h->n, TEAM, 0, h->stream>>>(h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->d_ws, h->n, d_act, d_obs,
                                           d_final, d_rew, d_term, d_trunc, d_succ, d_sub, h->autoreset, h->max_steps, h->d_order,
-                                          h->d_prio);
+                                          h->d_prio, h->d_stats, h->d_flags);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     k_order<<<1, ORDER_THREADS, 0, h->stream>>>(h->d_prio, h->d_order, h->n);
@@ -610,7 +693,7 @@ int urgym_set_state(urgym_handle* h, const double* state) {
 int urgym_substep(urgym_handle* h) {
     if (!h) return -1;
     HIPCHK(h, hipSetDevice(h->dev));
-    k_substep<<<h->n, TEAM, 0, h->stream>>>(h->d_scene, h->d_state, h->d_ws, h->n);
+    k_substep<<<h->n, TEAM, 0, h->stream>>>(h->d_scene, h->d_state, h->d_ws, h->n, h->d_stats);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
@@ -638,6 +721,72 @@ int urgym_ik(urgym_handle* h, const double* target, double* q_out) {
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipMemcpyAsync(q_out, d_q, sizeof(double) * NB * N, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int urgym_set_reward_type(urgym_handle* h, int sparse) {
+    if (!h) return -1;
+    const int v = sparse != 0;
+    HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipMemcpyAsync((char*)h->d_scene + offsetof(Scene, sparse), &v, sizeof(int), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int urgym_get_flags(urgym_handle* h, uint8_t* flags) {
+    if (!h || !flags) return -1;
+    HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipMemcpyAsync(flags, h->d_flags, (size_t)h->n, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+const uint8_t* urgym_flags_device(urgym_handle* h) { return h ? h->d_flags : nullptr; }
+
+int urgym_get_stats(urgym_handle* h, int32_t* stats) {
+    if (!h || !stats) return -1;
+    HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipMemcpyAsync(stats, h->d_stats, sizeof(int32_t) * UG_NSTAT * h->n, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int urgym_get_rng(urgym_handle* h, uint32_t* mt, int32_t* elapsed) {
+    if (!h || !mt) return -1;
+    HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipMemcpyAsync(mt, h->d_mt, sizeof(uint32_t) * UG_MT_WORDS * h->n, hipMemcpyDeviceToHost, h->stream));
+    if (elapsed) HIPCHK(h, hipMemcpyAsync(elapsed, h->d_elapsed, sizeof(int) * h->n, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int urgym_set_rng(urgym_handle* h, const uint32_t* mt, const int32_t* elapsed) {
+    if (!h || !mt) return -1;
+    HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipMemcpyAsync(h->d_mt, mt, sizeof(uint32_t) * UG_MT_WORDS * h->n, hipMemcpyHostToDevice, h->stream));
+    if (elapsed) HIPCHK(h, hipMemcpyAsync(h->d_elapsed, elapsed, sizeof(int) * h->n, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int urgym_contact_points(urgym_handle* h, int body_a, int body_b, int link_a, int link_b, int max_pts, double* out,
+                         int32_t* count) {
+    if (!h || !out || !count || max_pts <= 0) return -1;
+    size_t N = (size_t)h->n;
+    HIPCHK(h, hipSetDevice(h->dev));
+    double* d_out = nullptr;
+    int32_t* d_cnt = nullptr;
+    HIPCHK(h, hipMalloc(&d_out, sizeof(double) * 24 * (size_t)max_pts * N));
+    HIPCHK(h, hipMalloc(&d_cnt, sizeof(int32_t) * N));
+    HIPCHK(h, hipMemsetAsync(d_out, 0, sizeof(double) * 24 * (size_t)max_pts * N, h->stream));
+    k_contacts<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_scene, h->d_state, h->n, body_a, body_b, link_a, link_b,
+                                                    max_pts, d_out, d_cnt);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, sizeof(double) * 24 * (size_t)max_pts * N, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(count, d_cnt, sizeof(int32_t) * N, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    hipFree(d_out);
+    hipFree(d_cnt);
+    if (e != hipSuccess) return fail(h, std::string("urgym_contact_points: ") + hipGetErrorString(e));
     return 0;
 }
 

@@ -235,6 +235,7 @@ struct Scene {
     int oncol[MAXOBJ]; /* colliders of each object (consecutive) */
     int npair;
     PairDef pair[MAXPAIR];
+    int sparse; /* reward_type != 'dense' (urgym_set_reward_type) */
 };
 
 struct CPoint { v3 lpA, lpB, n; double dist, imp, imp1, imp2; };

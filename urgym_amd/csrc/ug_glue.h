@@ -29,19 +29,49 @@ UG_HD void ugg_union_center(const double* lo1, const double* hi1, const double* 
 /* random.uniform(a, b) = a + (b - a) * random() */
 UG_HD double ugg_uniform(double a, double b, double u) { return a + (b - a) * u; }
 
+/* ---- TwoBallsBalance (env_two_balls_balance_v0.py) ---- */
+/* create_balls (:212-223): ball 1 at the paddle + (U(-0.03, 0.03), U(-0.08, -0.045), 0.2 + r), ball 2 at the
+ * paddle + (U(-0.03, 0.03), U(-0.015, 0.02), 0.2 - r); draws in that order (b1x, b1y, b2x, b2y) */
+UG_HD void ugg_tb_balls(const double* paddle, double r, const double* u, double* b1, double* b2) {
+    b1[0] = paddle[0] + ugg_uniform(-0.03, 0.03, u[0]);
+    b1[1] = paddle[1] + ugg_uniform(-0.08, -0.045, u[1]);
+    b1[2] = paddle[2] + 0.2 + r;
+    b2[0] = paddle[0] + ugg_uniform(-0.03, 0.03, u[2]);
+    b2[1] = paddle[1] + ugg_uniform(-0.015, 0.02, u[3]);
+    b2[2] = paddle[2] + 0.2 - r;
+}
+/* reward_function (:148-151): 0 beyond 1, else 1 - x**2 */
+UG_HD double ugg_tb_rf(double x) { return x > 1.0 ? 0.0 : 1.0 - x * x; }
+/* step reward (:110-139): -|a_i| per action component, +1, then reward_function of |x|, |y| of each ball's
+ * world position.  numpy 1.26 promotion (setup.py pins numpy 1.26.4): the float32 action components enter a
+ * float64 sum (Python int 0 + numpy float32 scalar -> float64).  Returns terminated (a ball below the paddle). */
+UG_HD int ugg_tb_reward(const float* a, const double* b1, const double* b2, double paddle_z, double* reward) {
+    double r = 0.0;
+    for (int i = 0; i < 3; i++) r = r + -ug_fabs((double)a[i]);
+    r = r + 1.0;
+    r = r + ugg_tb_rf(ug_fabs(b1[0]));
+    r = r + ugg_tb_rf(ug_fabs(b1[1]));
+    r = r + ugg_tb_rf(ug_fabs(b2[0]));
+    r = r + ugg_tb_rf(ug_fabs(b2[1]));
+    *reward = r;
+    return b1[2] < paddle_z || b2[2] < paddle_z;
+}
+
 /* ---- CubesPush (env_cubes_push_v0.py) ---- */
 /* create_cubes (:240-246): second cube x = uniform(-0.1, 0.1) */
 UG_HD double ugg_cp_cube1_x(double u) { return ugg_uniform(-0.1, 0.1, u); }
-/* step reward (:129-150 with update_reward :152-165, dense): returns success */
+/* step reward (:129-150 with update_reward :152-165); sparse (reward_type != 'dense', :159) drops the
+ * distance shaping term; returns success */
 UG_HD int ugg_cp_reward(int table_contact, int touched, double c0x, double c0y, double c0z, double c1x, double c1y,
-                        double c1z, double* reward) {
+                        double c1z, int sparse, double* reward) {
     double r = 0.0;
     int success = 0;
     if (table_contact) {
         r -= 0.01;
     } else if (touched) {
         double dist = ug_norm3(c0x - c1x, c0y - c1y, c0z - c1z);
-        double ur = 0.0 + ugg_gdr(dist, 0.1, 0.5) / 10.0;
+        double ur = 0.0;
+        if (!sparse) ur += ugg_gdr(dist, 0.1, 0.5) / 10.0;
         if (dist < 0.05) { ur += 10.0; success = 1; }
         r = ur + 0.1;
     }
@@ -99,9 +129,10 @@ UG_HD void ugg_gf_ball_xy(double u0, double u1, double* x, double* y) {
     *x = 0.0 + ugg_uniform(-0.2, 0.2, u0);
     *y = -0.7 + ugg_uniform(-0.1, 0.1, u1);
 }
-/* step reward, termination precedence (:129-183); hole = pitch base position; returns success */
+/* step reward, termination precedence (:129-183); hole = pitch base position; sparse (reward_type != 'dense',
+ * :151, :163) drops both distance shaping terms; returns success */
 UG_HD int ugg_gf_reward(const double* ball, const double* hole, const double* stick, int in_fingers, int floor_contact,
-                        int touched, double* reward, int* terminated) {
+                        int touched, int sparse, double* reward, int* terminated) {
     double r = 0.0;
     int success = 0, term = 0;
     if (ug_norm3(hole[0] - ball[0], hole[1] - ball[1], hole[2] - ball[2]) < 0.05) { /* is_ball_in_hole :217-221 */
@@ -116,12 +147,16 @@ UG_HD int ugg_gf_reward(const double* ball, const double* hole, const double* st
         term = 1;
     } else {
         if (floor_contact) r -= 0.01;
-        double d = ug_norm3(stick[0] - ball[0], stick[1] - ball[1], stick[2] - ball[2]);
-        r += ugg_gdr(d, 0.1, 0.5) / 10.0;
+        if (!sparse) {
+            double d = ug_norm3(stick[0] - ball[0], stick[1] - ball[1], stick[2] - ball[2]);
+            r += ugg_gdr(d, 0.1, 0.5) / 10.0;
+        }
         if (touched) {
             r += 0.1;
-            double dh = ug_norm3(hole[0] - ball[0], hole[1] - ball[1], hole[2] - ball[2]);
-            r += ugg_gdr(dh, 0.1, 0.5) / 10.0;
+            if (!sparse) {
+                double dh = ug_norm3(hole[0] - ball[0], hole[1] - ball[1], hole[2] - ball[2]);
+                r += ugg_gdr(dh, 0.1, 0.5) / 10.0;
+            }
         }
     }
     r -= 0.1;

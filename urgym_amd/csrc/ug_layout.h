@@ -10,7 +10,7 @@
 #ifndef UG_LAYOUT_H
 #define UG_LAYOUT_H
 
-#define UG_MAXOBJ 2
+#define UG_MAXOBJ 3          /* paddle + 2 balls (TwoBallsBalance-v0); other tasks use 1-2 */
 #define UG_MAXMAN 16
 #define UG_PT_DOUBLES 13
 #define UG_MAN_DOUBLES (2 + 4 * UG_PT_DOUBLES)
@@ -21,12 +21,26 @@
 #define UG_F_MTARGET 24
 #define UG_F_MON 31
 #define UG_F_OACTIVE 38
-#define UG_F_OBJ 40          /* per object: pos3 quat4 v3 w3 */
+#define UG_F_OBJ (UG_F_OACTIVE + UG_MAXOBJ)   /* per object: pos3 quat4 v3 w3 */
 #define UG_OBJ_DOUBLES 13
-#define UG_F_NMAN 66
-#define UG_F_MAN 67          /* per manifold: pair, npts, 4 x (lpA3 lpB3 n3 dist imp imp1 imp2) */
-#define UG_F_TASK (UG_F_MAN + UG_MAXMAN * UG_MAN_DOUBLES)   /* approached, grasped, overflow, spare */
+#define UG_F_NMAN (UG_F_OBJ + UG_MAXOBJ * UG_OBJ_DOUBLES)
+#define UG_F_MAN (UG_F_NMAN + 1)   /* per manifold: pair, npts, 4 x (lpA3 lpB3 n3 dist imp imp1 imp2) */
+#define UG_F_TASK (UG_F_MAN + UG_MAXMAN * UG_MAN_DOUBLES)   /* approached, grasped, overflow (dropped contacts), spare */
 #define UG_STATE_DIM (UG_F_TASK + 4)
+
+/* per-env event counters (urgym_get_stats / ugo_get_stats), cumulative over the handle's life */
+#define UG_STAT_UNSTABLE 0   /* wait_until_stable loops that hit 480 substeps without settling (env_*:102-103) */
+#define UG_STAT_SPLIT 1      /* substeps whose solve ran the split-impulse (deep penetration) pass */
+#define UG_STAT_ROWCAP 2     /* substeps whose contact points exceeded the row capacity (points dropped) */
+#define UG_STAT_MANCAP 3     /* substeps whose manifolds exceeded the manifold capacity (manifolds dropped) */
+#define UG_STAT_NONFINITE 4  /* env-steps ended by the non-finite state guard */
+#define UG_STAT_SUBSTEPS 5   /* physics substeps run */
+#define UG_NSTAT 8
+/* per-env flags of the last step / reset call (urgym_get_flags; bit set = happened in that call, its same-step
+ * autoreset included) */
+#define UG_FLAG_UNSTABLE 1   /* a wait_until_stable loop did not settle ("did not stabilize" warning) */
+#define UG_FLAG_NONFINITE 2  /* the state became non-finite: the env was terminated (and reset by autoreset) */
+#define UG_FLAG_DROPPED 4    /* contacts were dropped at a capacity limit */
 
 #define UG_MT_WORDS 625      /* MT19937 state (624) + index, uint32, contiguous per env */
 

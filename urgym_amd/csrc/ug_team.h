@@ -35,10 +35,15 @@ namespace ugd {
 #define UG_NPROF 48 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
-/* per-env global workspace (L2-resident): old manifolds (collision), every row's J | M^-1 J^T (24 + 24
+/* a row's J and M^-1 J^T over the NVP = 32 dof slots (robot 12, objects 3 x 6, 2 zero pads) */
+#define RJ NVP              /* offset of M^-1 J^T in a workspace row */
+#define RS (2 * NVP)        /* workspace row stride (doubles) */
+#define KS (NVP / 4)        /* k-steps of the 16x16x4 MFMA Delassus tiles */
+static_assert(NV <= NVP, "dof slots exceed the padded row");
+/* per-env global workspace (L2-resident): old manifolds (collision), every row's J | M^-1 J^T (32 + 32
  * doubles, written lane-per-row by the row build), then the Delassus columns >= PREG (column-major) */
 #define WS_ROWS (UG_MAXMAN * UG_MAN_DOUBLES)
-#define WS_A (WS_ROWS + MAXROWS * 48)
+#define WS_A (WS_ROWS + MAXROWS * RS)
 #ifdef UG_DEBUG_DUMP /* development aid: team_pgs dumps A, w and impulses after the workspace proper */
 #define WS_DBG (WS_A + (MAXROWS - PREG) * MAXROWS)
 #define WS_DOUBLES (WS_DBG + MAXROWS * MAXROWS + 8 * MAXROWS)
@@ -91,6 +96,8 @@ struct Shared {
     int is[8];
     int ecnt[2 * MAXMAN]; /* team_enumerate: accepted points / rolling points per manifold */
     int anc[NB];          /* bit d set: dof d moves body b (moves(d, b)); filled by team_load */
+    int flags;            /* UG_FLAG_* of this launch (lane 0) */
+    int stats[UG_NSTAT];  /* the env's UG_STAT_* counters (lane 0), loaded / stored with the state */
     int bdepth[NB];       /* tree depth of body b (body_depth); filled by team_load */
 #ifdef UG_PROF
     unsigned long long prof[UG_NPROF];
@@ -844,16 +851,6 @@ __device__ __forceinline__ double ent_dot_v0(int ent, const double (&a)[NB], con
         if (i < 6 || ent == 0) s += a[i] * v0[o + i];
     return s;
 }
-/* dst[entity segment] = src[0 .. dofs) */
-__device__ __forceinline__ void put_seg_r(int ent, const double (&src)[NB], double (&dst)[NV]) {
-#pragma unroll
-    for (int i = 0; i < NB; i++) dst[i] = ent == 0 ? src[i] : dst[i];
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-        dst[NB + i] = ent == 1 ? src[i] : dst[NB + i];
-        dst[NB + 6 + i] = ent == 2 ? src[i] : dst[NB + 6 + i];
-    }
-}
 /* Jacobian of a point p on entity ent along d (ANG: angular component along d, rolling rows) and
  * M^-1 J^T of it; for an object only [0, 6) is set */
 template <bool ANG>
@@ -1115,12 +1112,12 @@ __device__ __forceinline__ static void build_row(const Scene* s, int pos, double
         }
     }
     r.invD = invD; r.rinv = invD == 0.0 ? 0.0 : 1.0 / invD; r.rhs = rhs; r.rhsPen = rhsPen; r.lo = lo; r.hi = hi; r.imp = imp; r.impPen = 0.0; r.fric = fric;
-    /* J | M^-1 J^T over the NV dof slots: limit / motor rows their robot part, gear rows the sum of both
-     * robot parts, contact rows each side's entity segment (put_seg_r semantics; zero elsewhere) */
+    /* J | M^-1 J^T over the NVP dof slots: limit / motor rows their robot part, gear rows the sum of both
+     * robot parts, contact rows each side's entity segment (zero elsewhere, pads included) */
     const int eA = kind <= 2 ? 0 : entA, eB = kind == 2 ? 0 : (kind <= 1 ? -1 : entB);
 #pragma unroll
-    for (int i = 0; i < NV; i++) {
-        const int ent = i < NB ? 0 : (i < NB + 6 ? 1 : 2);
+    for (int i = 0; i < NVP; i++) {
+        const int ent = i < NB ? 0 : (i < NV ? 1 + (i - NB) / 6 : -2);
         const int k = i < NB ? i : (i - NB) % 6;
         double j = 0.0, m = 0.0;
         if (kind == 2) {
@@ -1130,7 +1127,7 @@ __device__ __forceinline__ static void build_row(const Scene* s, int pos, double
             if (eB == ent) { j = JB[k]; m = MB[k]; }
         }
         wrow[i] = j;
-        wrow[24 + i] = m;
+        wrow[RJ + i] = m;
     }
     PROF_ADD(PF_RB3, t_rb3);
 }
@@ -1286,8 +1283,8 @@ __device__ __forceinline__ void sweep_warm(const double (&A0)[PREG], const doubl
     }
 }
 /* ---- Delassus rows on the matrix cores ----
- * A[i][p] = fma chain over the 24 dof slots of J_i[d] * M^-1J_p[d] is a 24-deep dot product, so a 16x16
- * tile of A is 6 chained v_mfma_f64_16x16x4_f64: their numerics are a k-ordered fma chain, bit-identical
+ * A[i][p] = fma chain over the 32 (padded) dof slots of J_i[d] * M^-1J_p[d] is a 32-deep dot product, so a
+ * 16x16 tile of A is KS = 8 chained v_mfma_f64_16x16x4_f64: their numerics are a k-ordered fma chain, bit-identical
  * to the oracle's rdot() (checked on MI355X: tools/micro/mfma64.hip, mfma_build.hip).  For the column
  * block PB (columns p = 16 PB + 0..15) the four row tiles of slot S are computed with the columns on the
  * A operand, so tile g leaves A[64 S + 16 g + m][16 PB + h + 4 r] in lane 16 h + m, register r; a 4x4
@@ -1309,23 +1306,23 @@ __device__ __forceinline__ void swap16_d(double& x, double& y) {
 /* the slot's row operands (J of rows 64 S + 16 g + (lane & 15), dof slots 4 ks + (lane >> 4)) are the same
  * for every column block: loaded once per slot into B; each block then loads only its 6 column operands */
 template <int PB>
-__device__ __forceinline__ void mfma_cols(gcdouble* rows, int n, int lane, double (&a)[6]) {
+__device__ __forceinline__ void mfma_cols(gcdouble* rows, int n, int lane, double (&a)[KS]) {
     const int p = 16 * PB + (lane & 15);
 #pragma unroll
-    for (int ks = 0; ks < 6; ks++) a[ks] = p < n ? rows[p * 48 + 24 + 4 * ks + (lane >> 4)] : 0.0;
+    for (int ks = 0; ks < KS; ks++) a[ks] = p < n ? rows[p * RS + RJ + 4 * ks + (lane >> 4)] : 0.0;
 }
 template <int PB, int S>
-__device__ __forceinline__ void mfma_block(gcdouble* rows, const double (&B)[6][4], const double (&a)[6], double invDr,
+__device__ __forceinline__ void mfma_block(gcdouble* rows, const double (&B)[KS][4], const double (&a)[KS], double invDr,
                                            double (&A)[PREG], gdouble* wsA, int n, int lane) {
     if constexpr (16 * PB < MAXROWS) {
         if (16 * PB < n) {
-            double an[6]; /* the next block's column operands, in flight during this block */
+            double an[KS]; /* the next block's column operands, in flight during this block */
             if (16 * PB + 16 < n) mfma_cols<PB + 1>(rows, n, lane, an);
             d4v acc[4];
 #pragma unroll
             for (int g = 0; g < 4; g++) acc[g] = d4v{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int ks = 0; ks < 6; ks++)
+            for (int ks = 0; ks < KS; ks++)
 #pragma unroll
                 for (int g = 0; g < 4; g++) acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], B[ks][g], acc[g], 0, 0, 0);
 #pragma unroll
@@ -1352,15 +1349,15 @@ __device__ __forceinline__ void mfma_block(gcdouble* rows, const double (&B)[6][
 template <int S>
 __device__ __forceinline__ void mfma_slot(gcdouble* rows, double invDr, double (&A)[PREG], gdouble* wsA, int n,
                                           int lane) {
-    double B[6][4];
+    double B[KS][4];
 #pragma unroll
-    for (int ks = 0; ks < 6; ks++)
+    for (int ks = 0; ks < KS; ks++)
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const int i = 64 * S + 16 * g + (lane & 15);
-            B[ks][g] = i < n ? rows[i * 48 + 4 * ks + (lane >> 4)] : 0.0;
+            B[ks][g] = i < n ? rows[i * RS + 4 * ks + (lane >> 4)] : 0.0;
         }
-    double a[6];
+    double a[KS];
     mfma_cols<0>(rows, n, lane, a);
     mfma_block<0, S>(rows, B, a, invDr, A, wsA, n, lane);
 }
@@ -1828,9 +1825,9 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     __builtin_amdgcn_wave_barrier();
     const int d = lane < NV ? lane : 0;
     double acc = 0.0, accs = 0.0;
-    for (int k = 0; k < n; k++) acc = __builtin_fma(rows[k * 48 + 24 + d], sh.rs[k].imp, acc);
+    for (int k = 0; k < n; k++) acc = __builtin_fma(rows[k * RS + RJ + d], sh.rs[k].imp, acc);
     if (split)
-        for (int k = nnc; k < fb; k++) accs = __builtin_fma(rows[k * 48 + 24 + d], sh.u.impx[k], accs);
+        for (int k = nnc; k < fb; k++) accs = __builtin_fma(rows[k * RS + RJ + d], sh.u.impx[k], accs);
     dv = lane < NV ? acc : 0.0;
     dvs = lane < NV ? accs : 0.0;
     __builtin_amdgcn_wave_barrier();
@@ -1846,11 +1843,18 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     serial_fk();
     __syncthreads();
     PROF_ADD(PF_FK, t_col);
+    const double ov0 = e.overflow;
     team_collide(s, ws);
+    const double ov1 = e.overflow;
+    if (lane == 0) {
+        sh.stats[UG_STAT_SUBSTEPS]++;
+        if (ov1 != ov0) { sh.stats[UG_STAT_MANCAP]++; sh.flags |= UG_FLAG_DROPPED; }
+    }
     PROF_ADD(PF_COLLIDE, t_col);
     PROF_T0(t_dyn);
     serial_pre(s);
     __syncthreads();
+    if (lane == 0 && e.overflow != ov1) { sh.stats[UG_STAT_ROWCAP]++; sh.flags |= UG_FLAG_DROPPED; }
     PROF_ADD(PF_DYN, t_dyn);
     PROF_T0(t_rows);
     const int n = uniform(sh.nrows), nnc = uniform(sh.nnc), nn = uniform(sh.nn);
@@ -1863,7 +1867,7 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     team_unit_solves();
     PROF_ADD(PF_UNIT, t_unit);
     PROF_T0(t_rowb);
-    for (int p = lane; p < n; p += TEAM) build_row(s, p, ws + WS_ROWS + p * 48);
+    for (int p = lane; p < n; p += TEAM) build_row(s, p, ws + WS_ROWS + p * RS);
     PROF_ADD(PF_ROWB, t_rowb);
     __threadfence_block();
     __syncthreads();
@@ -1871,6 +1875,7 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     PROF_T0(t_pgs);
     double dv, dvs;
     int split = team_pgs(ws, n, nnc, nn, dv, dvs);
+    if (lane == 0 && split) sh.stats[UG_STAT_SPLIT]++;
     PROF_ADD(PF_PGS, t_pgs);
     PROF_T0(t_int);
     if (lane < NVP) { sh.dvout[lane] = dv; sh.dvsout[lane] = dvs; }
@@ -2059,8 +2064,42 @@ __device__ static void cpd_obs(const EnvState& e, double* obs) {
         obs[3 + 3 * o] = e.obj[o].pos.x - pe.x; obs[4 + 3 * o] = e.obj[o].pos.y - pe.y; obs[5 + 3 * o] = e.obj[o].pos.z - pe.z;
     }
 }
+/* TwoBallsBalance obs (env_two_balls_balance_v0.py:157-163): paddle euler, paddle - ball 1, paddle - ball 2 */
+__device__ static void tb_obs(const EnvState& e, double* obs) {
+    v3 eu = euler_from_quat(e.obj[0].quat);
+    obs[0] = eu.x; obs[1] = eu.y; obs[2] = eu.z;
+    for (int b = 0; b < 2; b++) {
+        obs[3 + 3 * b] = e.obj[0].pos.x - e.obj[1 + b].pos.x;
+        obs[4 + 3 * b] = e.obj[0].pos.y - e.obj[1 + b].pos.y;
+        obs[5 + 3 * b] = e.obj[0].pos.z - e.obj[1 + b].pos.z;
+    }
+}
+/* non-finite state guard (oracle state_finite): q, qd and the active objects' state */
+__device__ static int state_finite(const Scene* s, const EnvState& e) {
+    for (int i = 0; i < NB; i++)
+        if (!__builtin_isfinite(e.q[i]) || !__builtin_isfinite(e.qd[i])) return 0;
+    for (int o = 0; o < s->nobj; o++) {
+        if (e.oactive[o] == 0.0) continue;
+        const double* v = &e.obj[o].pos.x;
+        for (int j = 0; j < UG_OBJ_DOUBLES; j++)
+            if (!__builtin_isfinite(v[j])) return 0;
+    }
+    return 1;
+}
+/* a reset of a non-finite state starts from a clean robot (oracle sanitize) */
+__device__ static void sanitize(const Scene* s, EnvState& e) {
+    if (state_finite(s, e)) return;
+    for (int i = 0; i < NB; i++) { e.q[i] = 0.0; e.qd[i] = 0.0; }
+    for (int m = 0; m < 7; m++) { e.mtarget[m] = 0.0; e.mon[m] = 0.0; }
+    for (int o = 0; o < MAXOBJ; o++) {
+        e.oactive[o] = 0.0;
+        e.obj[o].pos = V(0, 0, 0); e.obj[o].quat = Q(0, 0, 0, 0); e.obj[o].v = V(0, 0, 0); e.obj[o].w = V(0, 0, 0);
+    }
+    e.nman = 0.0;
+}
 __device__ static void task_obs(const Scene* s, const EnvState& e, double* obs) {
-    if (s->variant == UG_TASK_CUBESPUSHDIFF) cpd_obs(e, obs);
+    if (s->variant == UG_TASK_TWOBALLS) tb_obs(e, obs);
+    else if (s->variant == UG_TASK_CUBESPUSHDIFF) cpd_obs(e, obs);
     else if (s->task == UG_TASK_CUBESPUSH) cp_obs(e, obs);
     else if (s->task == UG_TASK_CUBESGRASP) cg_obs(e, obs);
     else if (s->variant == UG_TASK_GOLFJOINTS) { /* env_golf_joints_v0.py:228-235: arm joints, then the Golf obs */
@@ -2136,7 +2175,7 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
                 int table = robot_contact(e, s, static_collider(s, 10), 1, UG_NL - 1);
                 int touched = robot_contact(e, s, s->ocol[1], 9, 18);
                 io.succ = ugg_cp_reward(table, touched, e.obj[0].pos.x, e.obj[0].pos.y, e.obj[0].pos.z, e.obj[1].pos.x,
-                                        e.obj[1].pos.y, e.obj[1].pos.z, &io.rew);
+                                        e.obj[1].pos.y, e.obj[1].pos.z, s->sparse, &io.rew);
                 io.term = io.succ;
             } else if (task == UG_TASK_CUBESGRASP) { /* :160-192 */
                 v3 gc = gripper_center(e.q);
@@ -2156,11 +2195,23 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
                 v3 st = club_point(e, UG_GF_FOOT_Z);
                 double stick[3] = {st.x, st.y, st.z}, ball[3] = {e.obj[1].pos.x, e.obj[1].pos.y, e.obj[1].pos.z};
                 double hole[3] = {UG_GF_PITCH_X, UG_GF_PITCH_Y, UG_GF_PITCH_Z};
-                io.succ = ugg_gf_reward(ball, hole, stick, in_fingers, floor, touched, &io.rew, &io.term);
+                io.succ = ugg_gf_reward(ball, hole, stick, in_fingers, floor, touched, s->sparse, &io.rew, &io.term);
+            } else if (s->variant == UG_TASK_TWOBALLS) { /* env_two_balls_balance_v0.py:110-146 */
+                double b1[3] = {e.obj[1].pos.x, e.obj[1].pos.y, e.obj[1].pos.z};
+                double b2[3] = {e.obj[2].pos.x, e.obj[2].pos.y, e.obj[2].pos.z};
+                io.term = ugg_tb_reward(io.act, b1, b2, e.obj[0].pos.z, &io.rew);
+                io.succ = 0;
             } else { /* env_ball_balance_v0.py:119-134: reward 1, terminated when the ball falls below the paddle */
                 io.rew = 1.0;
                 io.term = e.obj[1].pos.z < e.obj[0].pos.z;
                 io.succ = 0;
+            }
+            if (!state_finite(s, e)) { /* end the episode, zero reward; the autoreset restarts from a clean state */
+                io.term = 1;
+                io.succ = 0;
+                io.rew = 0.0;
+                g_sh.flags |= UG_FLAG_NONFINITE;
+                g_sh.stats[UG_STAT_NONFINITE]++;
             }
             task_obs(s, e, io.obs);
             if (io.autoreset && (io.term || io.trunc)) {
@@ -2172,6 +2223,7 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
             *next = G_END;
             return L_NONE;
         case G_RESET: /* robot.reset(): reset_arm (rest pose) + 10 substeps */
+            sanitize(s, e);
             e.goal_approached = 0.0;
             e.goal_grasped = 0.0;
             for (int i = 0; i < 6; i++) { e.q[i] = UG_ARM_REST[i]; e.qd[i] = 0.0; }
@@ -2225,10 +2277,18 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
             v3 gc = gripper_center(e.q);
             v3 pose = V(pe.x, pe.y - 0.2, gc.z);
             place_object(e, 0, pose, Q(0, 0, 0, 1));
-            v3 bp = V(pose.x, pose.y, pose.z + 0.2 + UG_BB_BALL_R);
-            bp.x += io.dr.uniform(-0.03, 0.03);
-            bp.y += io.dr.uniform(-0.08, 0.02);
-            place_object(e, 1, bp, e.obj[0].quat);
+            if (s->variant == UG_TASK_TWOBALLS) { /* create_balls(0.003) (env_two_balls_balance_v0.py:212-235) */
+                double u[4], pd[3] = {pose.x, pose.y, pose.z}, b1[3], b2[3];
+                for (int k = 0; k < 4; k++) u[k] = io.dr.next();
+                ugg_tb_balls(pd, UG_TB_BALL_R, u, b1, b2);
+                place_object(e, 1, V(b1[0], b1[1], b1[2]), e.obj[0].quat);
+                place_object(e, 2, V(b2[0], b2[1], b2[2]), e.obj[0].quat);
+            } else {
+                v3 bp = V(pose.x, pose.y, pose.z + 0.2 + UG_BB_BALL_R);
+                bp.x += io.dr.uniform(-0.03, 0.03);
+                bp.y += io.dr.uniform(-0.08, 0.02);
+                place_object(e, 1, bp, e.obj[0].quat);
+            }
             close_gripper(e, 100.0);
             *next = G_RESET_DONE;
             return L_WAIT;
@@ -2278,7 +2338,12 @@ __device__ __forceinline__ static int team_run(const Scene* s, double* ws, int p
             __syncthreads();
             if (lane == 0) sh.is[0] = np_sum12(sh.a12) < UG_STABLE_EPS;
             __syncthreads();
-            if (uniform(sh.is[0]) || i + 1 == UG_STABLE_STEPS) break;
+            const int stable = uniform(sh.is[0]);
+            if (stable || i + 1 == UG_STABLE_STEPS) {
+                /* "did not stabilize" (env_ball_balance_v0.py:102-103): surfaced as a flag and a counter */
+                if (!stable && lane == 0) { sh.stats[UG_STAT_UNSTABLE]++; sh.flags |= UG_FLAG_UNSTABLE; }
+                break;
+            }
             pos = qn;
         }
     }
@@ -2286,10 +2351,12 @@ __device__ __forceinline__ static int team_run(const Scene* s, double* ws, int p
 }
 
 /* ---------------- state in/out (cooperative, canonical layout) ---------------- */
-__device__ static void team_load(const double* S) {
+__device__ static void team_load(const double* S, const int* stats) {
     Shared& sh = g_sh;
     double* dst = (double*)&sh.e;
     for (int i = threadIdx.x; i < UG_STATE_DIM; i += TEAM) dst[i] = S[i];
+    if (threadIdx.x < UG_NSTAT) sh.stats[threadIdx.x] = stats ? stats[threadIdx.x] : 0;
+    if (threadIdx.x == 0) sh.flags = 0;
     if (threadIdx.x < NB) {
         int m = 0;
         for (int b = threadIdx.x; b >= 0; b = UG_BODY_PARENT[b]) m |= 1 << b;
@@ -2319,15 +2386,17 @@ __device__ static int team_priority(const Scene* s, int nsub, int el_next, int m
     if (autoreset && max_steps > 0 && el_next >= max_steps) return 15;
     if (s->task == UG_TASK_BALLBALANCE && e.oactive[0] != 0.0 && e.oactive[1] != 0.0) {
         const m3 R = qmat(e.obj[0].quat);
-        const v3 r = vsub(e.obj[1].pos, e.obj[0].pos);
-        const v3 rv = vsub(e.obj[1].v, e.obj[0].v);
         const double T = 24.0 * UG_DT;
         double f = 0.0;
-        for (int k = 0; k < 2; k++) {
-            const v3 l = mtv(R, k ? vadd(r, vscale(rv, T)) : r);
-            double g = fmax(fabs(l.x) / UG_BB_PADDLE_HX, fabs(l.y) / UG_BB_PADDLE_HY);
-            if (l.z < UG_BB_PADDLE_HZ) g = fmax(g, 1.0);
-            f = fmax(f, g);
+        for (int o = 1; o < s->nobj; o++) {
+            const v3 r = vsub(e.obj[o].pos, e.obj[0].pos);
+            const v3 rv = vsub(e.obj[o].v, e.obj[0].v);
+            for (int k = 0; k < 2; k++) {
+                const v3 l = mtv(R, k ? vadd(r, vscale(rv, T)) : r);
+                double g = fmax(fabs(l.x) / UG_BB_PADDLE_HX, fabs(l.y) / UG_BB_PADDLE_HY);
+                if (l.z < UG_BB_PADDLE_HZ) g = fmax(g, 1.0);
+                f = fmax(f, g);
+            }
         }
         const int b = (int)(f * 10.0);
         return b > 14 ? 14 : (b < 0 ? 0 : b);
@@ -2337,8 +2406,11 @@ __device__ static int team_priority(const Scene* s, int nsub, int el_next, int m
     return b;
 }
 /* manifold slots beyond nman are written as (pair -1, zeros), as ugo_get_state does */
-__device__ static void team_store(double* S) {
+__device__ static void team_store(double* S, int* stats, uint8_t* flags) {
     const Shared& sh = g_sh;
+    __syncthreads();
+    if (stats && threadIdx.x < UG_NSTAT) stats[threadIdx.x] = sh.stats[threadIdx.x];
+    if (flags && threadIdx.x == 0) *flags = (uint8_t)sh.flags;
     const double* src = (const double*)&sh.e;
     int nm = (int)sh.e.nman;
     for (int i = threadIdx.x; i < UG_STATE_DIM; i += TEAM) {

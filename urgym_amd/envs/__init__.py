@@ -25,9 +25,10 @@ TASKS = {
     "URGym/Golf-v0": (3, 100),          # :40-44
     "URGym/CubesPushDiff-v0": (4, 50),  # :16-20  (variant of CubesPush: relative obs)
     "URGym/GolfJoints-v0": (5, 100),    # :46-50  (variant of Golf: joint-space action, joints in obs)
+    "URGym/TwoBallsBalance-v0": (6, 500),  # :34-38  (BallBalance scene with two balls)
 }
-UNSUPPORTED = {  # registered by the reference, not built yet
-    "URGym/Box-v0": 200, "URGym/TwoBallsBalance-v0": 500,
+UNSUPPORTED = {  # registered by the reference, not built (different scene / solver features)
+    "URGym/Box-v0": 200,
 }
 
 
@@ -35,6 +36,9 @@ def spaces_for(task):
     """observation_space / action_space exactly as the reference declares them."""
     if task == 0:  # env_ball_balance_v0.py:52-54
         obs = Box(low=np.array([-math.pi] * 3 + [-1.0] * 3), high=np.array([math.pi] * 3 + [1.0] * 3), dtype=np.float64)
+        act = Box(low=np.array([-0.1] * 3), high=np.array([+0.1] * 3), dtype=np.float32)
+    elif task == 6:  # env_two_balls_balance_v0.py:52-54
+        obs = Box(low=np.array([-math.pi] * 3 + [-1.0] * 6), high=np.array([math.pi] * 3 + [1.0] * 6), dtype=np.float64)
         act = Box(low=np.array([-0.1] * 3), high=np.array([+0.1] * 3), dtype=np.float32)
     elif task in (1, 3, 4):  # env_cubes_push_v0.py:58-60, env_golf_v0.py:58-60, env_cubes_push_diff_v0.py:58-62
         obs = Box(low=np.array([-1.0] * 9), high=np.array([1.0] * 9), dtype=np.float64)
@@ -95,5 +99,10 @@ def GolfJoints(camera=None, reward_type="dense", render_mode="human", **kw):
     return URGymEnv(5, max_episode_steps=None, camera=camera, reward_type=reward_type, render_mode=render_mode, **kw)
 
 
+def TwoBallsBalance(camera=None, reward_type="dense", render_mode="human", **kw):
+    """env_two_balls_balance_v0.TwoBallsBalance(camera, reward_type, render_mode) signature."""
+    return URGymEnv(6, max_episode_steps=None, camera=camera, reward_type=reward_type, render_mode=render_mode, **kw)
+
+
 __all__ = ["make", "TASKS", "URGymEnv", "URGymVectorEnv", "BallBalance", "CubesPush", "CubesGrasp", "Golf",
-           "CubesPushDiff", "GolfJoints", "spaces_for"]
+           "CubesPushDiff", "GolfJoints", "TwoBallsBalance", "spaces_for"]

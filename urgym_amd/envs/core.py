@@ -1,27 +1,61 @@
-"""gymnasium-compatible Env / VectorEnv over the batched C-ABI (urgym_amd._native.Sim)."""
+"""gymnasium-compatible Env / VectorEnv over the batched C-ABI (urgym_amd._native.Sim).
+
+When gymnasium is importable the classes subclass gymnasium.Env / gymnasium.vector.VectorEnv (the reference's
+envs are gymnasium.Env subclasses, env_ball_balance_v0.py:17); in this image it is absent and they stand alone
+with the same surface.  Constructor kwargs follow the reference (camera, reward_type, render_mode); what this
+build does not implement raises instead of being ignored.
+"""
 import numpy as np
 
-from .._native import Sim
+from .._native import FLAG_DROPPED, FLAG_NONFINITE, FLAG_UNSTABLE, Sim
+
+try:  # pragma: no cover - gymnasium is absent in this image
+    import gymnasium as _gym
+    _EnvBase = _gym.Env
+    _VecBase = _gym.vector.VectorEnv
+except Exception:  # pragma: no cover
+    _EnvBase = object
+    _VecBase = object
 
 
-class URGymVectorEnv:
+def _check_kwargs(camera, reward_type):
+    if camera is not None:
+        raise NotImplementedError("camera rendering is outside the hot-path scope (SURVEY.md 8(f)4)")
+    if reward_type not in ("dense", "sparse"):
+        raise ValueError(f"reward_type must be 'dense' or 'sparse', not {reward_type!r}")
+
+
+def _flag_info(flags):
+    """failure surfacing: only the events that happened, so the usual info stays the reference's"""
+    info = {}
+    if flags & FLAG_UNSTABLE:
+        info["unstable"] = True        # wait_until_stable hit 480 substeps ("did not stabilize")
+    if flags & FLAG_NONFINITE:
+        info["nonfinite"] = True       # state went non-finite: episode terminated, reward 0
+    if flags & FLAG_DROPPED:
+        info["contacts_dropped"] = True  # a contact capacity limit was hit
+    return info
+
+
+class URGymVectorEnv(_VecBase):
     """N envs of one task on one GPU, gymnasium 0.29 VectorEnv semantics:
     step() returns (obs, rewards, terminated, truncated, infos) with same-step
     autoreset -- a finished env is reset inside the same call and its terminal
     observation is in infos['final_observation'] (masked by '_final_observation').
+    infos also carries 'is_success', 'substeps' and the per-env failure flags
+    ('unstable', 'nonfinite', 'contacts_dropped').
     """
 
     def __init__(self, task, num_envs, max_episode_steps=None, device=0, seed=0, env_offset=0,
                  camera=None, reward_type="dense", render_mode="rgb_array"):
         from . import spaces_for
-        if camera is not None:
-            raise NotImplementedError("camera rendering is outside the hot-path scope")
-        if reward_type != "dense":
-            raise NotImplementedError("only reward_type='dense' is implemented")
+        _check_kwargs(camera, reward_type)
         self.task = task
         self.num_envs = num_envs
         self.single_observation_space, self.single_action_space = spaces_for(task)
         self.sim = Sim(task, num_envs, device=device, seed=seed, env_offset=env_offset)
+        self.sim.set_reward_type(reward_type)
+        self.reward_type = reward_type
         self.max_episode_steps = max_episode_steps or 0
         self.sim.set_autoreset(True, self.max_episode_steps)
         self.render_mode = render_mode  # 'human' GUI is not supported (documented deviation)
@@ -35,7 +69,10 @@ class URGymVectorEnv:
         term = out["terminated"].astype(bool)
         trunc = out["truncated"].astype(bool)
         done = term | trunc
-        infos = {"is_success": out["success"].astype(bool), "substeps": out["substeps"]}
+        flags = self.sim.flags()
+        infos = {"is_success": out["success"].astype(bool), "substeps": out["substeps"],
+                 "unstable": (flags & FLAG_UNSTABLE) != 0, "nonfinite": (flags & FLAG_NONFINITE) != 0,
+                 "contacts_dropped": (flags & FLAG_DROPPED) != 0}
         if done.any():
             fo = np.empty(self.num_envs, dtype=object)
             for i in np.nonzero(done)[0]:
@@ -48,18 +85,20 @@ class URGymVectorEnv:
         self.sim.close()
 
 
-class URGymEnv:
+class URGymEnv(_EnvBase):
     """Single env with the reference's surface: reset(*, seed, options) -> (obs, info),
-    step(a) -> (obs, float reward, bool terminated, bool truncated, info)."""
+    step(a) -> (obs, float reward, bool terminated, bool truncated, info).  max_episode_steps applies the
+    gymnasium TimeLimit truncation the registry adds (urgym/envs/__init__.py)."""
 
     def __init__(self, task, max_episode_steps=None, device=0, seed=0, camera=None, reward_type="dense",
                  render_mode="human"):
         from . import spaces_for
-        if camera is not None:
-            raise NotImplementedError("camera rendering is outside the hot-path scope")
+        _check_kwargs(camera, reward_type)
         self.task = task
         self.observation_space, self.action_space = spaces_for(task)
         self.sim = Sim(task, 1, device=device, seed=seed)
+        self.sim.set_reward_type(reward_type)
+        self.reward_type = reward_type
         self.max_episode_steps = max_episode_steps or 0
         self.sim.set_autoreset(False, 0)
         self._elapsed = 0
@@ -73,7 +112,9 @@ class URGymEnv:
         out = self.sim.step(np.asarray(action, dtype=np.float32).reshape(1, -1))
         self._elapsed += 1
         trunc = bool(self.max_episode_steps and self._elapsed >= self.max_episode_steps)
-        info = {} if self.task == 0 else {"is_success": bool(out["success"][0])}
+        # BallBalance / TwoBallsBalance return {} (env_ball_balance_v0.py:134); the others {'is_success': ...}
+        info = {} if self.task in (0, 6) else {"is_success": bool(out["success"][0])}
+        info.update(_flag_info(int(self.sim.flags()[0])))
         return out["obs"][0].copy(), float(out["reward"][0]), bool(out["terminated"][0]), trunc, info
 
     def close(self):
