@@ -1797,12 +1797,16 @@ static double np_sum12(const double* a) {
     for (int i = 8; i < 12; i++) r += a[i];
     return r;
 }
-/* wait_until_stable (env_ball_balance_v0.py:94-103): returns substeps taken */
+static int state_finite(const ugo_env* e);
+/* wait_until_stable (env_ball_balance_v0.py:94-103): returns substeps taken.  A state that went non-finite
+ * ends the loop at once (the step's non-finite guard then terminates the episode) instead of spinning the
+ * remaining substeps on NaNs. */
 static int wait_until_stable(ugo_env* e) {
     double pos[NB];
     memcpy(pos, e->q, sizeof(pos));
     for (int i = 0; i < UG_STABLE_STEPS; i++) {
         substep(e);
+        if (!state_finite(e)) return i + 1;
         double a[NB];
         for (int j = 0; j < NB; j++) a[j] = ug_fabs(pos[j] - e->q[j]);
         if (np_sum12(a) < UG_STABLE_EPS) return i + 1;
@@ -1952,9 +1956,14 @@ static void place_object(ugo_env* e, int o, v3 pos, q4 orn) {
 /* RobotBase.reset -> reset_arm (robot.py:89-98) + reset_gripper/open_gripper (robot.py:100-106) */
 static int robot_reset(ugo_env* e) {
     for (int i = 0; i < 6; i++) { e->q[i] = UG_ARM_REST[i]; e->qd[i] = 0.0; }
-    for (int i = 0; i < 10; i++) substep(e);
+    int n = 0;
+    while (n < 10) {
+        substep(e);
+        n++;
+        if (!state_finite(e)) break; /* as wait_until_stable: no substeps on NaNs */
+    }
     open_gripper(e, 100.0);
-    return 10;
+    return n;
 }
 
 /* ======================================================================== */

