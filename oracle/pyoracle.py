@@ -56,6 +56,8 @@ def lib():
         L.ugo_get_rng.argtypes = [P, P]
         L.ugo_set_rng.argtypes = [P, P]
         L.ugo_contact_points.argtypes = [P, I, I, I, I, P, I]
+        L.ugo_dynamics.argtypes = [P, P, D, P, P, P]
+        L.ugo_set_pgs_bullet.argtypes = [P, I]
         L.ugo_step.argtypes = [P, P, P, P, P, P]
         L.ugo_get_state.argtypes = [P, P]
         L.ugo_set_state.argtypes = [P, P]
@@ -150,6 +152,10 @@ class OracleEnv:
     def set_reward_type(self, reward_type):
         self.L.ugo_set_reward_type(self.h, int(reward_type == "sparse"))
 
+    def set_pgs_bullet(self, on):
+        """solve with Bullet's velocity-space PGS form (tests only)"""
+        self.L.ugo_set_pgs_bullet(self.h, int(on))
+
     def get_rng(self):
         out = np.zeros(625, np.uint32)
         self.L.ugo_get_rng(self.h, _p(out))
@@ -200,6 +206,16 @@ class OracleEnv:
         q = np.zeros(12)
         self.L.ugo_ik(self.h, _p(np.asarray(pos, np.float64)), _p(np.asarray(orn, np.float64)), _p(q))
         return q
+
+
+def dynamics(q, qd, g=-9.8):
+    """(M 12x12, C 12, body COMs 12x3) of the restatement's CRBA / RNEA at (q, qd)"""
+    M = np.zeros((12, 12))
+    C = np.zeros(12)
+    com = np.zeros((12, 3))
+    lib().ugo_dynamics(_p(np.ascontiguousarray(q, np.float64)), _p(np.ascontiguousarray(qd, np.float64)), g, _p(M),
+                       _p(C), _p(com))
+    return M, C, com
 
 
 def norm3(v):

@@ -271,6 +271,7 @@ struct ugo_env {
     int overflow;
     mt19937 rng;
     int sparse;            /* reward_type != 'dense' (ctor kwarg of every env, env_cubes_push_v0.py:42) */
+    int pgs_bullet;        /* tests only: solve with the velocity-space Bullet-shaped PGS (pgs_bullet) */
     int flags;             /* UG_FLAG_* of the last step / reset call */
     int stats[UG_NSTAT];   /* UG_STAT_* counters */
 };
@@ -1699,6 +1700,85 @@ static int pgs(rowset* rs, double* dv, double* dvs) {
     return 1;
 }
 
+/* ---- the same solve in Bullet's own form (tests only: bounds the row-space restatement's rounding) ----
+ * btMultiBodyConstraintSolver::resolveSingleConstraintRowGeneric [ext] keeps the velocity delta deltaV of
+ * every body and, per row, deltaImpulse = rhs - (J_A . deltaV_A + J_B . deltaV_B) * jacDiagABInv, then clamps
+ * by assigning the bound: sum = applied + delta; sum < lo -> delta = lo - applied, applied = lo (hi likewise),
+ * else applied = sum; deltaV += M^-1 J^T * delta.  Same row order, sweeps, friction bounds, residual and split
+ * pass as pgs(); deltaV itself is the solver output.  Plain sums (no fma), as Bullet's C++ in double. */
+static double solve_row_v(row* r, double* v, int pen) {
+    double imp = pen ? r->impPen : r->imp;
+    double dvn = 0.0;
+    for (int d = 0; d < UG_NVP; d++) dvn += r->J[d] * v[d];
+    double di = r->rhs - dvn * r->invD;
+    if (pen) di = r->rhsPen - dvn * r->invD;
+    double sum = imp + di;
+    if (sum < r->lo) { di = r->lo - imp; imp = r->lo; }
+    else if (sum > r->hi) { di = r->hi - imp; imp = r->hi; }
+    else imp = sum;
+    if (pen) r->impPen = imp; else r->imp = imp;
+    for (int d = 0; d < UG_NVP; d++) v[d] += r->MiJ[d] * di;
+    double rinv = r->invD == 0.0 ? 0.0 : 1.0 / r->invD;
+    return di * rinv;
+}
+static int pgs_bullet(rowset* rs, double* dv, double* dvs) {
+    row* R[MAXROWS];
+    int n = 0, pos_of[MAXROWS];
+    for (int j = 0; j < rs->nnc; j++) R[n++] = &rs->r[rs->idx_nc[j]];
+    for (int j = 0; j < rs->nn; j++) R[n++] = &rs->r[rs->idx_n[j]];
+    for (int j = 0; j < rs->nf; j++) R[n++] = &rs->r[rs->idx_f[j]];
+    for (int j = 0; j < rs->nr; j++) R[n++] = &rs->r[rs->idx_r[j]];
+    for (int p = 0; p < n; p++) pos_of[R[p] - rs->r] = p;
+    const int nnc = rs->nnc, fb = rs->nnc + rs->nn;
+    double v[UG_NVP];
+    memset(v, 0, sizeof(v));
+    for (int p = nnc; p < fb; p++) /* warm start: normals carry their scaled previous impulse */
+        for (int d = 0; d < UG_NVP; d++) v[d] += R[p]->MiJ[d] * R[p]->imp;
+    for (int it = 0; it < UG_PGS_ITERS; it++) {
+        double res = 0.0;
+        for (int j = 0; j < nnc; j++) {
+            int p = (it & 1) ? j : nnc - 1 - j;
+            double x = solve_row_v(R[p], v, 0);
+            x = x * x;
+            res = res > x ? res : x;
+        }
+        for (int p = nnc; p < fb; p++) {
+            double x = solve_row_v(R[p], v, 0);
+            x = x * x;
+            res = res > x ? res : x;
+        }
+        for (int p = fb; p < n; p++) {
+            row* f = R[p];
+            double tot = R[pos_of[f->nrow]]->imp;
+            if (tot > 0.0) {
+                f->lo = -(f->fric * tot);
+                f->hi = f->fric * tot;
+                double x = solve_row_v(f, v, 0);
+                x = x * x;
+                res = res > x ? res : x;
+            }
+        }
+        if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
+    }
+    for (int d = 0; d < UG_NVP; d++) dv[d] = v[d];
+    int any = 0;
+    for (int p = nnc; p < fb; p++)
+        if (R[p]->rhsPen != 0.0) any = 1;
+    if (!any) return 0;
+    memset(v, 0, sizeof(v));
+    for (int it = 0; it < UG_PGS_ITERS; it++) {
+        double res = 0.0;
+        for (int p = nnc; p < fb; p++) {
+            double x = solve_row_v(R[p], v, 1);
+            x = x * x;
+            res = res > x ? res : x;
+        }
+        if (res <= UG_RESIDUAL_THR || it >= UG_PGS_ITERS - 1) break;
+    }
+    for (int d = 0; d < UG_NVP; d++) dvs[d] = v[d];
+    return 1;
+}
+
 /* ======================================================================== */
 /* one p.stepSimulation()                                                    */
 /* ======================================================================== */
@@ -1749,7 +1829,7 @@ static void substep(ugo_env* e) {
     double dv[UG_NVP], dvs[UG_NVP];
     memset(dv, 0, sizeof(dv));
     memset(dvs, 0, sizeof(dvs));
-    int split = pgs(&rs, dv, dvs);
+    int split = e->pgs_bullet ? pgs_bullet(&rs, dv, dvs) : pgs(&rs, dv, dvs);
     if (split) e->stats[UG_STAT_SPLIT]++;
     for (int i = 0; i < rs.nn; i++) {
         const row* r = &rs.r[rs.idx_n[i]];
@@ -2451,9 +2531,19 @@ int ugo_contact_points(const ugo_env* e, int bodyA, int bodyB, int linkA, int li
     }
     return cnt;
 }
+/* the robot's equations of motion at (q, qd) for the dynamics known-answer tests: mass matrix M (NB x NB,
+ * CRBA), bias C (RNEA with qdd = 0: gravity g along z, Coriolis / gyroscopic, btMultiBody link damping) and
+ * the body COMs (NB x 3, world) */
+void ugo_dynamics(const double* q, const double* qd, double g, double* M, double* C, double* com) {
+    kin k;
+    fk(q, &k);
+    robot_dynamics(qd, &k, g, M, C);
+    for (int b = 0; b < NB; b++) { com[3 * b] = k.c[b].x; com[3 * b + 1] = k.c[b].y; com[3 * b + 2] = k.c[b].z; }
+}
 int ugo_flags(const ugo_env* e) { return e->flags; }
 void ugo_get_stats(const ugo_env* e, int32_t* out) { memcpy(out, e->stats, sizeof(e->stats)); }
 void ugo_set_reward_type(ugo_env* e, int sparse) { e->sparse = sparse != 0; }
+void ugo_set_pgs_bullet(ugo_env* e, int on) { e->pgs_bullet = on != 0; }
 /* checkpoint of the env's Python-random stream (624 words + index) */
 void ugo_get_rng(const ugo_env* e, uint32_t* mt625) {
     memcpy(mt625, e->rng.mt, 624 * sizeof(uint32_t));

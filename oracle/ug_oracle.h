@@ -44,9 +44,14 @@ int ugo_flags(const ugo_env* e);
 void ugo_get_stats(const ugo_env* e, int32_t* out);
 /* reward_type: 0 'dense', 1 'sparse' (ctor kwarg of every reference env) */
 void ugo_set_reward_type(ugo_env* e, int sparse);
+/* tests only: 1 = solve with Bullet's velocity-space PGS form (clamp-and-assign) instead of the row-space
+ * restatement the kernels reproduce; bounds the restatement's rounding against Bullet's arithmetic */
+void ugo_set_pgs_bullet(ugo_env* e, int on);
 /* Python-random stream checkpoint: 624 MT words + index */
 void ugo_get_rng(const ugo_env* e, uint32_t* mt625);
 void ugo_set_rng(ugo_env* e, const uint32_t* mt625);
+/* robot equations of motion at (q, qd): M (12 x 12), C (12), body COMs (12 x 3) -- dynamics KATs */
+void ugo_dynamics(const double* q, const double* qd, double g, double* M, double* C, double* com);
 /* p.getContactPoints over the manifold cache: 24 doubles per point (see ug_oracle.c); returns the count */
 int ugo_contact_points(const ugo_env* e, int bodyA, int bodyB, int linkA, int linkB, double* out, int max_pts);
 void ugo_set_state(ugo_env* e, const double* s);
