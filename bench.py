@@ -138,6 +138,8 @@ def main(argv=None):
     ap.add_argument("--task", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--backend", default="nccl", help="nccl (RCCL over xGMI); gloo only to rehearse several ranks "
+                                                      "on one GPU (returns gathered through host memory)")
     args = ap.parse_args(argv)
     rc = maybe_spawn(args, argv)
     if rc is not None:
@@ -149,16 +151,17 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gpu = local % max(torch.cuda.device_count(), 1)  # == local on a node with a GPU per rank
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        torch.cuda.set_device(gpu)
+        dist.init_process_group(args.backend, rank=rank, world_size=world)
         world = dist.get_world_size()
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", gpu)
 
     from urgym_amd._native import Sim
     n = args.envs
-    sim = Sim(args.task, n, device=local, seed=20241220, env_offset=rank * n)
+    sim = Sim(args.task, n, device=gpu, seed=20241220, env_offset=rank * n)
     sim.set_autoreset(True, MAX_STEPS[args.task])
     sim.reset()
     A, O = sim.act_dim, sim.obs_dim
@@ -226,7 +229,7 @@ def main(argv=None):
         dt = time.perf_counter() - t0
         kern_ms = [a.elapsed_time(b) for a, b in ev]
         vals = torch.tensor([dt, float(sub_tot.item()), float(res_tot.item()), float(np.mean(kern_ms))],
-                            dtype=torch.float64, device=dev)
+                            dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
         if world > 1:
             mx = vals.clone()
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -281,7 +284,8 @@ def main(argv=None):
         "data": "synthetic: uniform random actions (PCG64 seed 20241220+rank), per-env MT19937 reset draws",
         "config": {"workload": f"{TASK_NAMES[args.task]} x {n} envs per GPU, autoreset, max_episode_steps "
                                f"{MAX_STEPS[args.task]}", "envs_per_gpu": n, "total_envs": n * world,
-                   "parallelism": f"env-dp{world}", "world_size": world},
+                   "parallelism": f"env-dp{world}", "world_size": world,
+                   "backend": args.backend if world > 1 else None},
         "rep_values": [env_steps / x[0] for x in reps],
         "substeps_per_env_step": substeps / env_steps,
         "resets": int(resets),

@@ -1,0 +1,94 @@
+"""SB3-shaped VecEnv and device-resident rollouts (consumers training.py:24-41).
+CPU: the adapter's SB3 semantics with a scripted Sim (dones = terminated | truncated, terminal_observation,
+TimeLimit.truncated, is_success only where the reference reports it).  GPU: the adapter and the torch-tensor
+env against the host C-ABI path, bit for bit, and a device-side MLP policy rollout."""
+import numpy as np
+import pytest
+
+
+class FakeSim:
+    def __init__(self, task, n, **kw):
+        self.n, self.obs_dim, self.t = n, 9 if task != 0 else 6, 0
+
+    def set_reward_type(self, r):
+        self.rt = r
+
+    def set_autoreset(self, on, m):
+        self.max_steps = m
+
+    def reset(self):
+        return np.zeros((self.n, self.obs_dim))
+
+    def step(self, a):
+        self.t += 1
+        n = self.n
+        term = np.zeros(n, np.uint8)
+        trunc = np.zeros(n, np.uint8)
+        term[0] = 1
+        trunc[1] = 1
+        term[2] = trunc[2] = 1
+        return dict(obs=np.full((n, self.obs_dim), float(self.t)), final_obs=np.full((n, self.obs_dim), -1.0),
+                    reward=np.arange(n, dtype=np.float64), terminated=term, truncated=trunc,
+                    success=np.ones(n, np.uint8), substeps=np.ones(n, np.int32))
+
+    def close(self):
+        pass
+
+
+def test_sb3_semantics_cpu(monkeypatch):
+    import urgym_amd.vec as V
+    monkeypatch.setattr(V, "Sim", FakeSim)
+    env = V.URGymSB3VecEnv("URGym/CubesPush-v0", 4)
+    assert env.num_envs == 4 and env.action_space.shape == (3,) and env.observation_space.shape == (9,)
+    obs = env.reset()
+    assert obs.shape == (4, 9)
+    obs, rew, dones, infos = env.step(np.zeros((4, 3), np.float32))
+    assert dones.tolist() == [True, True, True, False] and rew.dtype == np.float32
+    assert infos[0]["TimeLimit.truncated"] is False and infos[1]["TimeLimit.truncated"] is True
+    assert infos[2]["TimeLimit.truncated"] is False                  # terminated wins (SB3 convention)
+    assert np.all(infos[0]["terminal_observation"] == -1.0) and "terminal_observation" not in infos[3]
+    assert all(i["is_success"] for i in infos)
+    bb = V.URGymSB3VecEnv("URGym/BallBalance-v0", 3)
+    bb.reset()
+    _, _, _, infos = bb.step(np.zeros((3, 3), np.float32))
+    assert "is_success" not in infos[3 - 1]                             # BallBalance info is {} (env_ball_balance_v0.py:134)
+    assert env.env_is_wrapped(object) == [False] * 4 and env.get_attr("task") == [1] * 4
+    with pytest.raises(NotImplementedError):
+        V.URGymSB3VecEnv("URGym/Box-v0", 2)
+
+
+@pytest.mark.gpu
+def test_sb3_adapter_and_torch_env_match_host_path(built):
+    import torch
+    from urgym_amd._native import Sim
+    from urgym_amd.vec import URGymSB3VecEnv, URGymTorchVecEnv
+    n, T, seed = 16, 6, 77
+    ref = Sim(1, n, seed=seed)
+    ref.set_autoreset(True, 50)
+    o_ref = ref.reset()
+    sb = URGymSB3VecEnv("URGym/CubesPush-v0", n, seed=seed)
+    tv = URGymTorchVecEnv("URGym/CubesPush-v0", n, seed=seed)
+    assert np.array_equal(sb.reset(), o_ref)
+    o_t = tv.reset()
+    tv.sync()
+    assert np.array_equal(o_t.cpu().numpy(), o_ref)
+    rng = np.random.default_rng(0)
+    for _ in range(T):
+        a = rng.uniform(-0.1, 0.1, (n, 3)).astype(np.float32)
+        r = ref.step(a)
+        obs, rew, dones, infos = sb.step(a)
+        with tv.stream_context():
+            ot, rt, tt, trt, ft = tv.step(torch.from_numpy(a).to(tv.device))
+        tv.sync()
+        assert np.array_equal(obs, r["obs"]) and np.array_equal(rew, r["reward"].astype(np.float32))
+        assert np.array_equal(dones, (r["terminated"] | r["truncated"]).astype(bool))
+        assert np.array_equal(ot.cpu().numpy(), r["obs"]) and np.array_equal(rt.cpu().numpy(), r["reward"])
+        assert np.array_equal(tt.cpu().numpy(), r["terminated"])
+    # a device-side MLP policy drives the batch with no host round trip per step
+    pol = torch.nn.Sequential(torch.nn.Linear(9, 32), torch.nn.Tanh(), torch.nn.Linear(32, 3)).to(tv.device)
+    with tv.stream_context():
+        rew, done = tv.rollout(pol, 5)
+    tv.sync()
+    assert torch.isfinite(rew).all() and rew.shape == (5,)
+    for e in (ref, sb, tv):
+        e.close()

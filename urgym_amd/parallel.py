@@ -61,8 +61,11 @@ def pack_returns(obs, reward, terminated, truncated):
 
 
 def gather_returns(obs, reward, terminated, truncated, group=None):
-    """All-gather every rank's returns; result is in global env-id order (rank-major)."""
+    """All-gather every rank's returns; result is in global env-id order (rank-major).  RCCL gathers HBM
+    buffers directly; under gloo (CPU tests, single-GPU rehearsals) the buffer goes through host memory."""
     buf = pack_returns(obs, reward, terminated, truncated)
+    if dist.get_backend(group) == "gloo" and buf.is_cuda:
+        buf = buf.cpu()
     world = dist.get_world_size(group)
     out = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(out, buf, group=group)
