@@ -6,6 +6,7 @@
 //   2  chunk-redundant chain: per 8-row chunk every lane runs the chunk's Gauss-Seidel chain on uniform copies
 //      (u by readlane at chunk start, bounds and the chunk's lower-triangular block of the Delassus matrix
 //      broadcast from LDS), then the bulk fma updates of its own rows (same operands, same order)
+//   3  variant 0 with the slot-1 columns pinned to AGPRs by an "a" asm constraint (A0 in VGPRs)
 // Usage: tools/micro/pgs2 (prints cycles per row update and a bit-exactness check against variant 0)
 #include "../../urgym_amd/csrc/ug_team.h"
 #include <cstdio>
@@ -125,9 +126,13 @@ __global__ void __launch_bounds__(64, 1) k(const double* in, double* out, unsign
         }
         __syncthreads();
     }
+    if (MODE == 3) { /* slot-1 columns pinned to AGPRs (A0 stays in VGPRs) */
+#pragma unroll
+        for (int p = 0; p < PREG; p++) asm volatile("" : "+a"(A1[p]));
+    }
     unsigned long long t0 = __builtin_readcyclecounter();
     for (int it = 0; it < 50; it++) {
-        if (MODE == 0) v0_rows<0>(A0, A1, lane, L, W);
+        if (MODE == 0 || MODE == 3) v0_rows<0>(A0, A1, lane, L, W);
         if (MODE == 1) { double a0, a1; colv<0>(A0, A1, a0, a1); v1_rows<0>(A0, A1, lane, L, W, a0, a1); }
         if (MODE == 2) v2_chunks<0>(A0, A1, lane, L, W, tri, bnd);
         asm volatile("" : "+v"(W[0]), "+v"(W[1]));
@@ -167,5 +172,6 @@ int main() {
     run<0>("0 production row_upd", d_in, d_out, d_c, blocks, ref);
     run<1>("1 pipelined column + critical slot first", d_in, d_out, d_c, blocks, ref);
     run<2>("2 chunk-redundant chain (LDS bounds/triangle)", d_in, d_out, d_c, blocks, ref);
+    run<3>("3 production row_upd, slot-1 columns in AGPRs", d_in, d_out, d_c, blocks, ref);
     return 0;
 }

@@ -127,7 +127,7 @@ __device__ unsigned long long g_prof[UG_NPROF];
 enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_TOTAL,
        PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN, PF_SWEEPS, PF_HULL,
        PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE, PF_FK, PF_LDL, PF_UNIT, PF_ROWB, PF_RB1, PF_RB2, PF_RB3, PF_MFMA, PF_WARM, PF_SW_NC, PF_SW_CT, PF_SW_FIN, PF_SW_FPREP, PF_SW_FR,
-       PF_SW_RES, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST };
+       PF_SW_RES, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST, PC_CHUNKS, PC_NNC, PC_NN };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -231,8 +231,8 @@ __device__ static inline void man_to_st(StMan& S, const Manifold& M) {
 /* ---------------- collision ---------------- */
 #define HB_FACE_UNROLL 12 /* covers hulls of up to 96 faces (the model's largest has 89) */
 /* hull (A, robot link) vs box (B): the whole wave.  Produces cand k (<= 4 points) in sh.u.cand. */
-__device__ __noinline__ static void team_reduce4(int n, int k);
-__device__ __noinline__ static void team_hull_box(const Collider& A, const Collider& B, const XF& TA, const XF& TB,
+__device__ __forceinline__ static void team_reduce4(int n, int k);
+__device__ __forceinline__ static void team_hull_box(const Collider& A, const Collider& B, const XF& TA, const XF& TB,
                                      double thr, int k) {
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
@@ -348,7 +348,7 @@ __device__ __noinline__ static void team_hull_box(const Collider& A, const Colli
 
 /* hull (A) vs hull (B) (oracle nc_hull_hull): lane per A vertex against B's planes, lane per B vertex against
  * A's planes; candidates in canonical order (A vertices, then B vertices; at most 64 kept), then reduce4 */
-__device__ __noinline__ static void team_hull_hull(const Collider& A, const Collider& B, const XF& TA, const XF& TB,
+__device__ __forceinline__ static void team_hull_hull(const Collider& A, const Collider& B, const XF& TA, const XF& TB,
                                                    double thr, int k) {
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
@@ -403,7 +403,7 @@ __device__ __noinline__ static void team_hull_hull(const Collider& A, const Coll
 }
 
 /* candidates sh.hc[0..n) -> at most 4 in sh.u.cand.c[k] (oracle reduce4: deepest, then farthest-spread) */
-__device__ __noinline__ static void team_reduce4(int n, int k) {
+__device__ __forceinline__ static void team_reduce4(int n, int k) {
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
     if (n <= 4) {
@@ -1238,7 +1238,10 @@ __device__ __forceinline__ void sweep_chunks(const double (&A0)[PREG], const dou
                                              int lane, int c_lo, int c_hi, Lrow& L, double (&W)[2]) {
     if constexpr (I < NCH) {
         constexpr int C = REV ? NCH - 1 - I : I;
-        if (C >= c_lo && C <= c_hi) chunk_rows<C, REV, 0, TWO>(A0, A1, wsA, lane, L, W);
+        if (C >= c_lo && C <= c_hi) {
+            chunk_rows<C, REV, 0, TWO>(A0, A1, wsA, lane, L, W);
+            PROF_CNT(PC_CHUNKS, 1);
+        }
         sweep_chunks<I + 1, REV, NCH, TWO>(A0, A1, wsA, lane, c_lo, c_hi, L, W);
     }
 }
@@ -1860,6 +1863,8 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     const int n = uniform(sh.nrows), nnc = uniform(sh.nnc), nn = uniform(sh.nn);
     PROF_CNT(PC_SUBSTEPS, 1);
     PROF_CNT(PC_ROWS, n);
+    PROF_CNT(PC_NNC, nnc);
+    PROF_CNT(PC_NN, nn);
     PROF_CNT(PC_OVL, sh.nov);
     PROF_CNT(PC_NMAN, (int)e.nman);
     /* rows: built lane-per-row into the workspace (J | M^-1 J^T) and LDS (scalars) */
