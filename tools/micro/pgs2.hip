@@ -7,6 +7,14 @@
 //      (u by readlane at chunk start, bounds and the chunk's lower-triangular block of the Delassus matrix
 //      broadcast from LDS), then the bulk fma updates of its own rows (same operands, same order)
 //   3  variant 0 with the slot-1 columns pinned to AGPRs by an "a" asm constraint (A0 in VGPRs)
+//   4  the production section structure (ug_team.h sweep_section): non-contact rows [0, 12) reversed on even
+//      sweeps, then [12 | 0, 33), then [33, 74), each section over whole CHUNK-row chunks with neutral rows
+//      (same row count per sweep as BallBalance in situ; records differ from variant 0 by design)
+//   5  one chunked section over all 74 rows (the chunk tests alone)
+//   7  variant 0 with an opaque always-true scalar test around every 8 rows (the cost of one chunk test)
+//   8  the same with one test per 16 rows
+//   6  variant 4 with switch dispatch: a jump into the section's first chunk, one exit compare per chunk
+//      (must equal variant 4 bit for bit)
 // Usage: tools/micro/pgs2 (prints cycles per row update and a bit-exactness check against variant 0)
 #include "../../urgym_amd/csrc/ug_team.h"
 #include <cstdio>
@@ -27,6 +35,23 @@ __device__ __forceinline__ void v0_rows(const double (&A0)[PREG], const double (
     if constexpr (P < NR) {
         row_upd<P, true>(A0, A1, nullptr, lane, L, W);
         v0_rows<P + 1>(A0, A1, lane, L, W);
+    }
+}
+template <int P, int K>
+__device__ __forceinline__ void v0_rows_n(const double (&A0)[PREG], const double (&A1)[PREG], int lane, Lrow& L,
+                                          double (&W)[2]) {
+    if constexpr (K > 0 && P < NR) {
+        row_upd<P, true>(A0, A1, nullptr, lane, L, W);
+        v0_rows_n<P + 1, K - 1>(A0, A1, lane, L, W);
+    }
+}
+/* variants 7 / 8: variant 0 with an opaque always-true test around every G rows */
+template <int P, int G>
+__device__ __forceinline__ void vg_rows(const double (&A0)[PREG], const double (&A1)[PREG], int lane, Lrow& L,
+                                        double (&W)[2], int on) {
+    if constexpr (P < NR) {
+        if (on > P) v0_rows_n<P, G>(A0, A1, lane, L, W);
+        vg_rows<P + G, G>(A0, A1, lane, L, W, on);
     }
 }
 /* variant 1: column of the next row in VGPRs before this row's clamp; critical slot first */
@@ -94,6 +119,41 @@ __device__ __forceinline__ void v2_chunks(const double (&A0)[PREG], const double
     }
 }
 
+/* chunk sequence [c_lo, c_hi] by a jump into the first chunk and one exit compare per chunk */
+#define SW_FWD(C) \
+    case C: \
+        chunk_rows<C, false, 0, true>(A0, A1, nullptr, lane, F, W); \
+        if (c_hi == C) break; \
+        [[fallthrough]];
+#define SW_REV(C) \
+    case C: \
+        chunk_rows<C, true, 0, true>(A0, A1, nullptr, lane, F, W); \
+        if (c_lo == C) break; \
+        [[fallthrough]];
+template <bool REV>
+__device__ __forceinline__ void sweep_section_sw(const double (&A0)[PREG], const double (&A1)[PREG], int lane, int a,
+                                                 int b, Lrow& L, double (&W)[2]) {
+    Lrow F = L;
+    bool in[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        const int p = lane + 64 * s;
+        in[s] = p >= a && p < b;
+        F.dlo[s] = in[s] ? L.dlo[s] : 0.0;
+        F.dhi[s] = in[s] ? L.dhi[s] : 0.0;
+    }
+    const int c_lo = a / CHUNK, c_hi = (b - 1) / CHUNK;
+    if (REV) {
+        switch (c_hi) { SW_REV(15) SW_REV(14) SW_REV(13) SW_REV(12) SW_REV(11) SW_REV(10) SW_REV(9) SW_REV(8)
+                        SW_REV(7) SW_REV(6) SW_REV(5) SW_REV(4) SW_REV(3) SW_REV(2) SW_REV(1) SW_REV(0) default: break; }
+    } else {
+        switch (c_lo) { SW_FWD(0) SW_FWD(1) SW_FWD(2) SW_FWD(3) SW_FWD(4) SW_FWD(5) SW_FWD(6) SW_FWD(7) SW_FWD(8)
+                        SW_FWD(9) SW_FWD(10) SW_FWD(11) SW_FWD(12) SW_FWD(13) SW_FWD(14) SW_FWD(15) default: break; }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; s++) L.dsv[s] = in[s] ? F.dsv[s] : L.dsv[s];
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(64, 1) k(const double* in, double* out, unsigned long long* cyc) {
     __shared__ double tri[NCH * 64];
@@ -135,6 +195,30 @@ __global__ void __launch_bounds__(64, 1) k(const double* in, double* out, unsign
         if (MODE == 0 || MODE == 3) v0_rows<0>(A0, A1, lane, L, W);
         if (MODE == 1) { double a0, a1; colv<0>(A0, A1, a0, a1); v1_rows<0>(A0, A1, lane, L, W, a0, a1); }
         if (MODE == 2) v2_chunks<0>(A0, A1, lane, L, W, tri, bnd);
+        if (MODE == 4) {
+            int nnc = 12, fb = 33, n = NR;
+            asm volatile("" : "+s"(nnc), "+s"(fb), "+s"(n));
+            if (!(it & 1)) sweep_section<true, (NCMAX + CHUNK - 1) / CHUNK, true>(A0, A1, nullptr, lane, 0, nnc, 0ull, 0ull, L, W);
+            sweep_section<false, MAXROWS / CHUNK, true>(A0, A1, nullptr, lane, (it & 1) ? 0 : nnc, fb, 0ull, 0ull, L, W);
+            sweep_section<false, MAXROWS / CHUNK, true>(A0, A1, nullptr, lane, fb, n, 0ull, 0ull, L, W);
+        }
+        if (MODE == 7 || MODE == 8) {
+            int on = 1000;
+            asm volatile("" : "+s"(on));
+            vg_rows<0, MODE == 7 ? 8 : 16>(A0, A1, lane, L, W, on);
+        }
+        if (MODE == 5) {
+            int n = NR;
+            asm volatile("" : "+s"(n));
+            sweep_section<false, MAXROWS / CHUNK, true>(A0, A1, nullptr, lane, 0, n, 0ull, 0ull, L, W);
+        }
+        if (MODE == 6) {
+            int nnc = 12, fb = 33, n = NR;
+            asm volatile("" : "+s"(nnc), "+s"(fb), "+s"(n));
+            if (!(it & 1)) sweep_section_sw<true>(A0, A1, lane, 0, nnc, L, W);
+            sweep_section_sw<false>(A0, A1, lane, (it & 1) ? 0 : nnc, fb, L, W);
+            sweep_section_sw<false>(A0, A1, lane, fb, n, L, W);
+        }
         asm volatile("" : "+v"(W[0]), "+v"(W[1]));
     }
     unsigned long long t1 = __builtin_readcyclecounter();
@@ -145,7 +229,8 @@ __global__ void __launch_bounds__(64, 1) k(const double* in, double* out, unsign
     if (lane == 0) cyc[blockIdx.x] = t1 - t0;
 }
 template <int MODE>
-void run(const char* name, double* d_in, double* d_out, unsigned long long* d_c, int blocks, double* ref) {
+void run(const char* name, double* d_in, double* d_out, unsigned long long* d_c, int blocks, double* ref,
+         double slots = NR) {
     for (int r = 0; r < 2; r++) { k<MODE><<<blocks, 64>>>(d_in, d_out, d_c); hipDeviceSynchronize(); }
     static unsigned long long c[1024];
     static double o[1024 * 64 * 4];
@@ -155,7 +240,7 @@ void run(const char* name, double* d_in, double* d_out, unsigned long long* d_c,
     for (int i = 0; i < blocks; i++) a += c[i];
     int same = ref ? memcmp(o, ref, sizeof(double) * blocks * 64 * 4) == 0 : 1;
     if (!ref) memcpy(ref = o, o, 0);
-    printf("%-46s blocks %4d: %6.1f cycles/row  %s\n", name, blocks, a / blocks / (50.0 * NR),
+    printf("%-46s blocks %4d: %6.1f cycles/row slot  %s\n", name, blocks, a / blocks / (50.0 * slots),
            ref ? (same ? "bit-exact vs variant 0" : "MISMATCH vs variant 0") : "");
 }
 int main() {
@@ -173,5 +258,14 @@ int main() {
     run<1>("1 pipelined column + critical slot first", d_in, d_out, d_c, blocks, ref);
     run<2>("2 chunk-redundant chain (LDS bounds/triangle)", d_in, d_out, d_c, blocks, ref);
     run<3>("3 production row_upd, slot-1 columns in AGPRs", d_in, d_out, d_c, blocks, ref);
+    run<7>("7 variant 0 + a test per 8 rows", d_in, d_out, d_c, blocks, ref);
+    run<8>("8 variant 0 + a test per 16 rows", d_in, d_out, d_c, blocks, ref);
+    run<5>("5 one chunked section [0, 74)", d_in, d_out, d_c, blocks, ref, 80);
+    static double ref4[1024 * 64 * 4];
+    k<4><<<blocks, 64>>>(d_in, d_out, d_c);
+    hipDeviceSynchronize();
+    hipMemcpy(ref4, d_out, sizeof(double) * blocks * 64 * 4, hipMemcpyDeviceToHost);
+    run<4>("4 production sections (92 slots/sweep avg)", d_in, d_out, d_c, blocks, ref4, 92);
+    run<6>("6 sections, switch dispatch (vs variant 4)", d_in, d_out, d_c, blocks, ref4, 92);
     return 0;
 }

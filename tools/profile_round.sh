@@ -11,10 +11,12 @@ mkdir -p $OUT
 timeout -k 10 240 python -c "import __graft_entry__ as g; g.build()" > $OUT/build.log 2>&1 || { echo BUILD_FAIL; exit 1; }
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --no-cpu-baseline "$@" > $OUT/trace.log 2>&1 || { echo TRACE_FAIL; exit 1; }
 echo TRACE_OK
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --no-cpu-baseline "$@" > $OUT/pmc_fetch.log 2>&1 || { echo PMC1_FAIL; exit 1; }
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py --no-cpu-baseline "$@" > $OUT/pmc_write.log 2>&1 || { echo PMC2_FAIL; exit 1; }
+# PMC passes on a short run of the same workload (traffic per launch does not depend on the step count)
+PMCARGS="--steps 20 --warmup 3 --reps 1"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --no-cpu-baseline "$@" $PMCARGS > $OUT/pmc_fetch.log 2>&1 || { echo PMC1_FAIL; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py --no-cpu-baseline "$@" $PMCARGS > $OUT/pmc_write.log 2>&1 || { echo PMC2_FAIL; exit 1; }
 echo PMC_OK
-python3 tools/pmc_traffic.py $OUT/pmc_fetch/run_counter_collection.csv $OUT/pmc_write/run_counter_collection.csv $OUT/traffic_k_step.json --steps 20 --warmup 3 "$@" > /dev/null && cp $OUT/traffic_k_step.json profiles/traffic_k_step.json && echo TRAFFIC_OK
+python3 tools/pmc_traffic.py $OUT/pmc_fetch/run_counter_collection.csv $OUT/pmc_write/run_counter_collection.csv $OUT/traffic_k_step.json "$@" > /dev/null && echo TRAFFIC_OK
 timeout -k 10 600 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err || { echo BENCH_FAIL; exit 1; }
 echo BENCH_OK
 
