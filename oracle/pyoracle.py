@@ -12,15 +12,17 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_build", "libugoracle.so")
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError("oracle not built: run `make -C oracle`")
-        L = ctypes.CDLL(LIB_PATH)
+def lib(path=None):
+    """the restatement's library (default: oracle/_build/libugoracle.so; tools/collision_fidelity.py passes the
+    paths of its fidelity builds)"""
+    path = path or LIB_PATH
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise RuntimeError(f"oracle library {path} not built: run `make -C oracle`")
+        L = ctypes.CDLL(path)
         P, D, I, U32 = ctypes.c_void_p, ctypes.c_double, ctypes.c_int, ctypes.c_uint32
         L.ugo_create.restype = P
         L.ugo_create.argtypes = [I, U32]
@@ -80,8 +82,8 @@ def lib():
         L.ugo_terminated.argtypes = [P]
         L.ugo_batch_step.restype = ctypes.c_long
         L.ugo_batch_step.argtypes = [P, I, P, P, P, P, P, P, I, I, P]
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
 def _p(a):
@@ -91,8 +93,8 @@ def _p(a):
 class OracleEnv:
     """One environment of the CPU restatement."""
 
-    def __init__(self, task, seed):
-        self.L = lib()
+    def __init__(self, task, seed, lib_path=None):
+        self.L = lib(lib_path)
         self.task = task
         self.h = self.L.ugo_create(task, seed)
         self.obs_dim = self.L.ugo_obs_dim(task)

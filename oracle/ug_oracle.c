@@ -14,7 +14,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#ifdef UG_MODEL_DATA /* collision-fidelity builds (tools/collision_fidelity.py) swap in their model header */
+#include UG_MODEL_DATA
+#else
 #include "../urgym_amd/csrc/model_data.h"
+#endif
 #include "../urgym_amd/csrc/scene_data.h"
 #include "../urgym_amd/csrc/ug_detmath.h"
 #include "../urgym_amd/csrc/ug_glue.h"
@@ -27,7 +31,9 @@
 #define MAXROWS 128
 #define MAXCOL 28
 #define MAXPAIR 160
+#ifndef MAXCAND
 #define MAXCAND 64
+#endif
 #define PT_DOUBLES UG_PT_DOUBLES
 #define MAN_DOUBLES UG_MAN_DOUBLES
 #define STATE_DIM UG_STATE_DIM
@@ -1030,6 +1036,7 @@ static void reduce4(candlist* L) {
     for (int s = 0; s < 4; s++) L->c[s] = sel[s];
     L->n = 4;
 }
+#ifndef UG_FIDELITY
 static void nc_hull_box(const xf* TA, const collider* A, const xf* TB, const collider* B, double thr, candlist* out) {
     m3 RAB = mtm(&TB->R, &TA->R);
     v3 pAB = mtv(&TB->R, vsub(TA->p, TB->p));
@@ -1156,6 +1163,10 @@ static void nc_hull_sphere(const xf* TA, const collider* A, const xf* TB, const 
     v3 nw = vneg(mv(&TA->R, V(F[0], F[1], F[2])));
     cand_add(out, nw, vadd(TB->p, vscale(nw, r)), depth);
 }
+
+#else
+#include "ug_fidelity.h"
+#endif
 
 /* btPersistentManifold [ext]: getCacheEntry / replaceContactPoint / addManifoldPoint / sortCachedPoints */
 static int sort_cached(const manifold* M, const cpoint* pt) {

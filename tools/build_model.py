@@ -40,7 +40,12 @@ from scipy.spatial import ConvexHull
 
 REF = os.environ.get("URGYM_REFERENCE", "/root/reference")
 URDF = os.path.join(REF, "urgym/urdf/ur5_robotiq_85.urdf")
-OUT = os.path.join(os.path.dirname(__file__), "..", "urgym_amd", "csrc", "model_data.h")
+OUT = os.environ.get("URGYM_MODEL_OUT",
+                     os.path.join(os.path.dirname(__file__), "..", "urgym_amd", "csrc", "model_data.h"))
+# collision-fidelity builds (tools/collision_fidelity.py; never the product): full hulls (URGYM_HULL_MAXV),
+# a finer club-disc prism (URGYM_CYL_SEG) and the vertex loop of every hull face (URGYM_HULL_POLYS=1)
+CYL_SEG = int(os.environ.get("URGYM_CYL_SEG", "16"))
+HULL_POLYS = os.environ.get("URGYM_HULL_POLYS", "0") == "1"
 MARGIN = 0.001  # gUrdfDefaultCollisionMargin [ext]
 
 
@@ -128,6 +133,21 @@ def hull_of(points):
     # plane as n.x <= off  (outward normal n, offset off = -d)
     planes = np.array([[p[0], p[1], p[2], -p[3]] for p in planes])
     return verts, planes, full
+
+
+def face_loops(verts, planes):
+    """vertex indices of each face, counter-clockwise about the outward normal (the face polygon)"""
+    loops = []
+    for p in planes:
+        n, off = p[:3], p[3]
+        on = np.where(np.abs(verts @ n - off) < 1e-6 * max(1.0, abs(off)) + 1e-9)[0]
+        c = verts[on].mean(0)
+        u = verts[on[0]] - c
+        u /= np.linalg.norm(u)
+        v = np.cross(n, u)
+        ang = np.arctan2((verts[on] - c) @ v, (verts[on] - c) @ u)
+        loops.append([int(i) for i in on[np.argsort(ang)]])
+    return loops
 
 
 def main():
@@ -329,6 +349,7 @@ def main():
     # collision shapes: flatten
     shp_link, shp_kind, shp_R, shp_P, shp_half, shp_v0, shp_nv, shp_f0, shp_nf = [], [], [], [], [], [], [], [], []
     V, F = [], []
+    FV, FV0, FVN = [], [], []  # face polygons (HULL_POLYS): global vertex indices, per-face start / count
     for i in range(19):
         for s in L[i]["shapes"]:
             T = T_body_link[i] @ s["T"]  # shape frame in body frame
@@ -345,12 +366,15 @@ def main():
                 lo, hi = vv.min(0), vv.max(0)
                 shp_half.append((hi - lo) / 2)  # unused for hulls except AABB sizing
                 shp_v0.append(len(V)); shp_nv.append(len(vv)); shp_f0.append(len(F)); shp_nf.append(len(s["planes"]))
+                if HULL_POLYS:
+                    for lp in face_loops(vv, s["planes"]):
+                        FV0.append(len(FV)); FVN.append(len(lp)); FV.extend(len(V) + i for i in lp)
                 V.extend(vv.tolist())
                 F.extend(s["planes"].tolist())
     # Golf club disc (env_golf_v0.py:293-305: GEOM_CYLINDER r 0.04, height 0.01, Z axis): a 16-sided prism
     # with the cylinder's safe margin (0.1 x min half extent) outside, so the outer extent is the cylinder's
     # (hull vertices on the circle of radius r - m; restated substitute for btCylinderShapeZ + GJK)
-    cyl_r, cyl_h, cyl_m, nseg = 0.04, 0.005, 0.0005, 16
+    cyl_r, cyl_h, cyl_m, nseg = 0.04, 0.005, 0.0005, CYL_SEG
     cyl_v0, cyl_f0 = len(V), len(F)
     rr, hh = cyl_r - cyl_m, cyl_h - cyl_m
     for zs in (-hh, hh):
@@ -363,6 +387,13 @@ def main():
         F.append([np.cos(th), np.sin(th), 0.0, apo])
     F.append([0.0, 0.0, 1.0, hh])
     F.append([0.0, 0.0, -1.0, hh])
+    if HULL_POLYS:  # side k joins bottom k, k+1 and top k+1, k (outward ccw), then top and bottom caps
+        for k in range(nseg):
+            k1 = (k + 1) % nseg
+            FV0.append(len(FV)); FVN.append(4)
+            FV.extend([cyl_v0 + k, cyl_v0 + k1, cyl_v0 + nseg + k1, cyl_v0 + nseg + k])
+        FV0.append(len(FV)); FVN.append(nseg); FV.extend(cyl_v0 + nseg + k for k in range(nseg))
+        FV0.append(len(FV)); FVN.append(nseg); FV.extend(cyl_v0 + k for k in reversed(range(nseg)))
     w("#define UG_CYL_V0 %d   /* golf club disc prism: 2 x %d vertices */" % (cyl_v0, nseg))
     w("#define UG_CYL_NV %d" % (2 * nseg))
     w("#define UG_CYL_F0 %d" % cyl_f0)
@@ -385,6 +416,13 @@ def main():
     arr("UG_SHAPE_NF", shp_nf, "int")
     arr("UG_HULL_V", V)
     arr("UG_HULL_F", F)
+    if HULL_POLYS:
+        assert len(FV0) == len(F)
+        w("#define UG_HULL_POLYS 1")
+        w("#define UG_NHULLFV %d" % len(FV))
+        arr("UG_HULL_FV", FV, "int")
+        arr("UG_HULL_FV0", FV0, "int")
+        arr("UG_HULL_FVN", FVN, "int")
     w("/* arm rest pose, robot.py:182-183 */")
     arr("UG_ARM_REST", [-1.5690622952052096, -1.5446774605904932, 1.343946009733127, -1.3708613585093699,
                         -1.5707970583733368, 0.0009377758247187636])
