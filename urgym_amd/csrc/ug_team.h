@@ -1238,7 +1238,7 @@ __device__ __forceinline__ void sweep_chunks(const double (&A0)[PREG], const dou
                                              int lane, int c_lo, int c_hi, Lrow& L, double (&W)[2]) {
     if constexpr (I < NCH) {
         constexpr int C = REV ? NCH - 1 - I : I;
-        if (C >= c_lo && C <= c_hi) {
+        if (__builtin_expect(C >= c_lo && C <= c_hi, 1)) { /* likely: the chunk body stays on the fall-through path */
             chunk_rows<C, REV, 0, TWO>(A0, A1, wsA, lane, L, W);
             PROF_CNT(PC_CHUNKS, 1);
         }
@@ -1720,8 +1720,12 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
 #endif
     /* the sweeps, specialised on whether slot 1 (rows 64..127) exists: with <= 64 rows the second u
      * register, its fma and its bookkeeping drop out of every row */
-    auto passes = [&](auto two_tag) -> int {
-        constexpr bool TWO = decltype(two_tag)::value;
+    auto passes = [&](auto span_tag) -> int {
+        /* SPAN: the row positions the sweep code covers (32, 64 or 128); every chunk position of a section
+         * costs one scalar test per sweep, so few-row solves (the resets' settling) get the short code */
+        constexpr int SPAN = decltype(span_tag)::value;
+        constexpr bool TWO = SPAN > 64;
+        constexpr int NCH_NC = (NCMAX + CHUNK - 1) / CHUNK < SPAN / CHUNK ? (NCMAX + CHUNK - 1) / CHUNK : SPAN / CHUNK;
         int split = 0;
         PROF_T0(t_sw);
         /* pass 0: the velocity solve; pass 1: the split-impulse pass (normals only, from zero) */
@@ -1759,11 +1763,11 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                 /* (even sweeps) non-contact rows reversed, then [s0, fb) */
                 PROF_T0(t_s1);
                 if (!pen && !(it & 1) && o_nnc > 0)
-                    sweep_section<true, (NCMAX + CHUNK - 1) / CHUNK, TWO>(A0, A1, o_wsA, lane, 0, o_nnc, 0ull, 0ull, L, W);
+                    sweep_section<true, NCH_NC, TWO>(A0, A1, o_wsA, lane, 0, o_nnc, 0ull, 0ull, L, W);
                 PROF_ADD(PF_SW_NC, t_s1);
                 PROF_T0(t_s2);
                 const int s0 = (pen || !(it & 1)) ? o_nnc : 0;
-                if (s0 < o_fb) sweep_section<false, TWO ? MAXROWS / CHUNK : 64 / CHUNK, TWO>(A0, A1, o_wsA, lane, s0, o_fb, 0ull, 0ull, L, W);
+                if (s0 < o_fb) sweep_section<false, SPAN / CHUNK, TWO>(A0, A1, o_wsA, lane, s0, o_fb, 0ull, 0ull, L, W);
                 PROF_ADD(PF_SW_CT, t_s2);
                 PROF_T0(t_s3);
                 const int f0 = pen ? o_nnc : 0;
@@ -1794,7 +1798,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                     __builtin_amdgcn_wave_barrier();
                     PROF_ADD(PF_SW_FPREP, t_s4);
                     PROF_T0(t_s5);
-                    sweep_section<false, TWO ? MAXROWS / CHUNK : 64 / CHUNK, TWO>(A0, A1, o_wsA, lane, o_fb, o_n, sk[0], sk[1], L, W);
+                    sweep_section<false, SPAN / CHUNK, TWO>(A0, A1, o_wsA, lane, o_fb, o_n, sk[0], sk[1], L, W);
                     row_finish<TWO>(L, pos_mask(0, o_fb, o_n, sk[0]), pos_mask(1, o_fb, o_n, sk[1]), lane, res);
                     PROF_ADD(PF_SW_FR, t_s5);
                 }
@@ -1818,7 +1822,9 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         }
         return split;
     };
-    const int split = n > 64 ? passes(std::true_type{}) : passes(std::false_type{});
+    const int split = n > 64   ? passes(std::integral_constant<int, 128>{})
+                      : n > 32 ? passes(std::integral_constant<int, 64>{})
+                               : passes(std::integral_constant<int, 32>{});
     /* dv[d] (dvs[d]) = fma chain over positions k of M^-1J_k[d] * impulse_k (lane d < NV) */
     __builtin_amdgcn_wave_barrier();
     if (split) {
