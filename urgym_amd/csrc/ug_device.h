@@ -27,7 +27,7 @@
 #define MAXROWS 128
 #define MAXCOL 28
 #define MAXPAIR 160
-#define MAXCAND 8   /* per-lane narrowphases emit <= 4 points */
+#define MAXCAND 4   /* per-pair narrowphases emit <= 4 points (box-box culls to 4) */
 
 #define DF __device__ static
 #define DFI __device__ static inline
@@ -240,6 +240,21 @@ struct Scene {
 
 struct CPoint { v3 lpA, lpB, n; double dist, imp, imp1, imp2; };
 struct Manifold { int pair, npts; CPoint pt[4]; };
+/* the lane-per-pair working manifold lives in LDS (team_collide: g_sh.pm[lane]); LDS-qualified values are
+ * moved field by field (plain aggregates have no address-space-qualified copy operations) */
+typedef __attribute__((address_space(3))) Manifold LManifold;
+typedef __attribute__((address_space(3))) CPoint LCPoint;
+typedef __attribute__((address_space(3))) v3 Lv3;
+__device__ static inline v3 ldv(const Lv3& a) { v3 r; r.x = a.x; r.y = a.y; r.z = a.z; return r; }
+__device__ static inline void stv(Lv3& d, v3 a) { d.x = a.x; d.y = a.y; d.z = a.z; }
+__device__ static inline void stpt(LCPoint& d, const CPoint& s) {
+    stv(d.lpA, s.lpA); stv(d.lpB, s.lpB); stv(d.n, s.n);
+    d.dist = s.dist; d.imp = s.imp; d.imp1 = s.imp1; d.imp2 = s.imp2;
+}
+__device__ static inline void cppt(LCPoint& d, const LCPoint& s) {
+    stv(d.lpA, ldv(s.lpA)); stv(d.lpB, ldv(s.lpB)); stv(d.n, ldv(s.n));
+    d.dist = s.dist; d.imp = s.imp; d.imp1 = s.imp1; d.imp2 = s.imp2;
+}
 
 /* ---------------- kinematics ---------------- */
 struct Kin {
@@ -432,9 +447,12 @@ DF void world_aabb(const XF& O, const Collider& c, v3& lo, v3& hi) {
 }
 
 struct Cand { v3 n, pB; double d; };
-struct CandList { int n; Cand c[MAXCAND]; };
+/* a pair's candidate slots: LDS (team_collide's u.cand.c[lane]), so the dynamically indexed list never goes
+ * to scratch memory */
+typedef __attribute__((address_space(3))) Cand LCand;
+struct CandList { int n; LCand* c; };
 DFI void cand_add(CandList& L, v3 n, v3 pB, double d) {
-    if (L.n < MAXCAND) { L.c[L.n].n = n; L.c[L.n].pB = pB; L.c[L.n].d = d; L.n++; }
+    if (L.n < MAXCAND) { stv(L.c[L.n].n, n); stv(L.c[L.n].pB, pB); L.c[L.n].d = d; L.n++; }
 }
 
 DF void nc_sphere_box(const XF& TA, const Collider& A, const XF& TB, const Collider& B, double thr, CandList& out) {
@@ -771,23 +789,23 @@ DF void nc_hull_sphere(const XF& TA, const Collider& A, const XF& TB, const Coll
     cand_add(out, nw, vadd(TB.p, vscale(nw, r)), depth);
 }
 
-DF int sort_cached(const Manifold& M, const CPoint& pt) {
+DF int sort_cached(const LManifold& M, const CPoint& pt) {
     int maxi = -1;
     double maxpen = pt.dist;
     for (int i = 0; i < 4; i++)
         if (M.pt[i].dist < maxpen) { maxi = i; maxpen = M.pt[i].dist; }
     double res[4] = {0, 0, 0, 0};
-    if (maxi != 0) { v3 a = vsub(pt.lpA, M.pt[1].lpA), b = vsub(M.pt[3].lpA, M.pt[2].lpA); v3 c = vcross(a, b); res[0] = vdot(c, c); }
-    if (maxi != 1) { v3 a = vsub(pt.lpA, M.pt[0].lpA), b = vsub(M.pt[3].lpA, M.pt[2].lpA); v3 c = vcross(a, b); res[1] = vdot(c, c); }
-    if (maxi != 2) { v3 a = vsub(pt.lpA, M.pt[0].lpA), b = vsub(M.pt[3].lpA, M.pt[1].lpA); v3 c = vcross(a, b); res[2] = vdot(c, c); }
-    if (maxi != 3) { v3 a = vsub(pt.lpA, M.pt[0].lpA), b = vsub(M.pt[2].lpA, M.pt[1].lpA); v3 c = vcross(a, b); res[3] = vdot(c, c); }
+    if (maxi != 0) { v3 a = vsub(pt.lpA, ldv(M.pt[1].lpA)), b = vsub(ldv(M.pt[3].lpA), ldv(M.pt[2].lpA)); v3 c = vcross(a, b); res[0] = vdot(c, c); }
+    if (maxi != 1) { v3 a = vsub(pt.lpA, ldv(M.pt[0].lpA)), b = vsub(ldv(M.pt[3].lpA), ldv(M.pt[2].lpA)); v3 c = vcross(a, b); res[1] = vdot(c, c); }
+    if (maxi != 2) { v3 a = vsub(pt.lpA, ldv(M.pt[0].lpA)), b = vsub(ldv(M.pt[3].lpA), ldv(M.pt[1].lpA)); v3 c = vcross(a, b); res[2] = vdot(c, c); }
+    if (maxi != 3) { v3 a = vsub(pt.lpA, ldv(M.pt[0].lpA)), b = vsub(ldv(M.pt[2].lpA), ldv(M.pt[1].lpA)); v3 c = vcross(a, b); res[3] = vdot(c, c); }
     int bi = -1;
     double bv = -1e300;
     for (int i = 0; i < 4; i++)
         if (ug_fabs(res[i]) > bv) { bv = ug_fabs(res[i]); bi = i; }
     return bi;
 }
-DF void manifold_add(Manifold& M, const XF& TA, const XF& TB, const Cand& c, double thr) {
+DF void manifold_add(LManifold& M, const XF& TA, const XF& TB, const Cand& c, double thr) {
     if (c.d > thr) return;
     v3 pA = vadd(c.pB, vscale(c.n, c.d));
     CPoint np;
@@ -799,40 +817,40 @@ DF void manifold_add(Manifold& M, const XF& TA, const XF& TB, const Cand& c, dou
     double shortest = thr * thr;
     int nearp = -1;
     for (int i = 0; i < M.npts; i++) {
-        v3 d = vsub(M.pt[i].lpA, np.lpA);
+        v3 d = vsub(ldv(M.pt[i].lpA), np.lpA);
         double x = vdot(d, d);
         if (x < shortest) { shortest = x; nearp = i; }
     }
     if (nearp >= 0) {
         np.imp = M.pt[nearp].imp; np.imp1 = M.pt[nearp].imp1; np.imp2 = M.pt[nearp].imp2;
-        M.pt[nearp] = np;
+        stpt(M.pt[nearp], np);
         return;
     }
     int ins = M.npts;
     if (ins == 4) ins = sort_cached(M, np);
     else M.npts++;
     if (ins < 0) ins = 0;
-    M.pt[ins] = np;
+    stpt(M.pt[ins], np);
 }
-DF void manifold_refresh(Manifold& M, const XF& TA, const XF& TB, double thr) {
+DF void manifold_refresh(LManifold& M, const XF& TA, const XF& TB, double thr) {
     for (int i = M.npts - 1; i >= 0; i--) {
-        CPoint& p = M.pt[i];
-        v3 pA = xf_apply(TA, p.lpA), pB = xf_apply(TB, p.lpB);
-        p.dist = vdot(vsub(pA, pB), p.n);
+        LCPoint& p = M.pt[i];
+        v3 pA = xf_apply(TA, ldv(p.lpA)), pB = xf_apply(TB, ldv(p.lpB));
+        p.dist = vdot(vsub(pA, pB), ldv(p.n));
     }
     for (int i = M.npts - 1; i >= 0; i--) {
-        CPoint& p = M.pt[i];
+        LCPoint& p = M.pt[i];
         int rm = 0;
         if (p.dist > thr) rm = 1;
         else {
-            v3 pA = xf_apply(TA, p.lpA), pB = xf_apply(TB, p.lpB);
-            v3 proj = vsub(pA, vscale(p.n, p.dist));
+            v3 pA = xf_apply(TA, ldv(p.lpA)), pB = xf_apply(TB, ldv(p.lpB));
+            v3 proj = vsub(pA, vscale(ldv(p.n), p.dist));
             v3 d = vsub(pB, proj);
             if (vdot(d, d) > thr * thr) rm = 1;
         }
         if (rm) {
             int last = M.npts - 1;
-            if (i != last) M.pt[i] = M.pt[last];
+            if (i != last) cppt(M.pt[i], M.pt[last]);
             M.npts--;
         }
     }

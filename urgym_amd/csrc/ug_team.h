@@ -51,7 +51,7 @@ static_assert(NV <= NVP, "dof slots exceed the padded row");
 #define WS_DOUBLES (WS_A + (MAXROWS - PREG) * MAXROWS)
 #endif
 
-#define MAXOV 40
+#define MAXOV 26 /* pairs per lane-per-pair pass: their working manifolds share LDS with the rows (Shared::pm) */
 
 /* ---------------- env state (canonical layout) ---------------- */
 struct StObj { v3 pos; q4 quat; v3 v, w; };
@@ -65,6 +65,7 @@ struct EnvState {
     double goal_approached, goal_grasped, overflow, spare;
 };
 static_assert(sizeof(EnvState) == UG_STATE_DIM * sizeof(double), "EnvState must match ug_layout.h");
+static_assert(sizeof(Manifold) * MAXOV <= 88 * MAXROWS, "working manifolds must fit in the rows' LDS");
 
 struct RowS {
     double invD, rinv, rhs, rhsPen, lo, hi, imp, impPen, fric; /* rinv = invD == 0 ? 0 : 1 / invD */
@@ -83,7 +84,10 @@ struct Shared {
     v3 lo[MAXCOL], hi[MAXCOL];
     int nov, ov[MAXPAIR];
     int nrows, nnc, nn, nf, split;
-    RowS rs[MAXROWS];
+    union {
+        RowS rs[MAXROWS];        /* row build .. impulse write-back */
+        Manifold pm[MAXOV];      /* collision: lane k's working manifold (rows are dead until the row build) */
+    };
     union {
         double mcol[NB + 5][NB]; /* row build: M^-1 e_d (d < NB) and M^-1 (ratio_g e_child_g) of gear g */
         struct { Cand c[MAXOV][4]; int n[MAXOV]; } cand;
@@ -95,6 +99,8 @@ struct Shared {
     double fs[8];
     int is[8];
     int ecnt[2 * MAXMAN]; /* team_enumerate: accepted points / rolling points per manifold */
+    int oldp[MAXMAN];     /* collision: pair ids of the previous manifolds (their records are in the workspace) */
+    int pmo[MAXOV];       /* collision: previous-manifold index of lane k's pair in this pass, -1 if none */
     int anc[NB];          /* bit d set: dof d moves body b (moves(d, b)); filled by team_load */
     int flags;            /* UG_FLAG_* of this launch (lane 0) */
     int stats[UG_NSTAT];  /* the env's UG_STAT_* counters (lane 0), loaded / stored with the state */
@@ -203,24 +209,16 @@ __device__ static inline int collider_active(const EnvState& e, const Collider& 
     if (c.owner <= -2 && c.owner > -100) return e.oactive[-2 - c.owner] != 0.0;
     return 1;
 }
-__device__ static inline void man_from_st(Manifold& M, const StMan& S) {
-    M.pair = (int)S.pair;
-    M.npts = (int)S.npts;
-    for (int p = 0; p < 4; p++) {
-        const StPt& s = S.pt[p];
-        M.pt[p].lpA = s.lpA; M.pt[p].lpB = s.lpB; M.pt[p].n = s.n;
-        M.pt[p].dist = s.dist; M.pt[p].imp = s.imp; M.pt[p].imp1 = s.imp1; M.pt[p].imp2 = s.imp2;
-    }
-}
-__device__ static inline void man_to_st(StMan& S, const Manifold& M) {
+__device__ static inline void man_to_st(StMan& S, const LManifold& M) {
     S.pair = (double)M.pair;
     S.npts = (double)M.npts;
     for (int p = 0; p < 4; p++) {
         StPt& s = S.pt[p];
         bool live = p < M.npts;
-        s.lpA = live ? M.pt[p].lpA : V(0, 0, 0);
-        s.lpB = live ? M.pt[p].lpB : V(0, 0, 0);
-        s.n = live ? M.pt[p].n : V(0, 0, 0);
+        const v3 a = ldv(M.pt[p].lpA), b = ldv(M.pt[p].lpB), n = ldv(M.pt[p].n);
+        s.lpA = live ? a : V(0, 0, 0);
+        s.lpB = live ? b : V(0, 0, 0);
+        s.n = live ? n : V(0, 0, 0);
         s.dist = live ? M.pt[p].dist : 0.0;
         s.imp = live ? M.pt[p].imp : 0.0;
         s.imp1 = live ? M.pt[p].imp1 : 0.0;
@@ -458,6 +456,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
     int nold = (int)e.nman;
     const double* src = (const double*)e.man;
     for (int i = lane; i < nold * UG_MAN_DOUBLES; i += TEAM) ws[i] = src[i];
+    if (lane < nold) sh.oldp[lane] = (int)e.man[lane].pair;
     __threadfence_block();
     __syncthreads();
     /* broadphase: ordered list of overlapping pairs */
@@ -502,53 +501,72 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         }
         PROF_ADD(PF_HULL, t_hull);
         PROF_T0(t_pairs);
-        /* lane per pair: remaining narrowphases, manifold update */
-        Manifold M;
-        M.npts = 0;
+        /* lane per pair: remaining narrowphases, manifold update.  The working manifold (g_sh.pm[lane]) and the
+         * candidate list (g_sh.u.cand.c[lane], where the hull pairs' candidates already are) live in LDS. */
+        /* previous manifolds of this pass's pairs: index lookup per lane (pair ids in LDS), then one cooperative
+         * copy of their points from the workspace into the working manifolds (all loads in flight together) */
+        PROF_T0(t_pl);
+        if (lane < cn) {
+            const int p = sh.ov[c0 + lane];
+            int mo = -1;
+            for (int m = 0; m < nold; m++)
+                if (sh.oldp[m] == p) { mo = m; break; }
+            sh.pmo[lane] = mo;
+            sh.pm[lane].pair = p;
+            sh.pm[lane].npts = mo >= 0 ? (int)ws[mo * UG_MAN_DOUBLES + 1] : 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        for (int i = lane; i < cn * 4 * UG_PT_DOUBLES; i += TEAM) {
+            const int k = i / (4 * UG_PT_DOUBLES), f = i - k * (4 * UG_PT_DOUBLES);
+            const int mo = sh.pmo[k];
+            if (mo >= 0) ((__attribute__((address_space(3))) double*)&sh.pm[k].pt[0].lpA.x)[f] = ws[mo * UG_MAN_DOUBLES + 2 + f];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        PROF_ADD(PF_PR_LOOK, t_pl);
         int has = 0;
         if (lane < cn) {
             int p = sh.ov[c0 + lane];
             const PairDef& P = s->pair[p];
             const Collider& A = s->col[P.a];
             const Collider& B = s->col[P.b];
-            M.pair = p;
-            PROF_T0(t_pl);
-            for (int m = 0; m < nold; m++) {
-                if ((int)ws[m * UG_MAN_DOUBLES] == p) {
-                    StMan tmp;
-                    double* t = (double*)&tmp;
-                    for (int i = 0; i < UG_MAN_DOUBLES; i++) t[i] = ws[m * UG_MAN_DOUBLES + i];
-                    man_from_st(M, tmp);
-                    break;
-                }
-            }
-            PROF_ADD(PF_PR_LOOK, t_pl);
+            LManifold& M = *(LManifold*)&sh.pm[lane];
             PROF_T0(t_pn);
             XF TA = shape_xf(sh.O[P.a], A), TB = shape_xf(sh.O[P.b], B);
             CandList L;
             L.n = 0;
+            L.c = (LCand*)&sh.u.cand.c[lane][0];
             if (A.kind == UG_SHAPE_HULL && (B.kind == UG_SHAPE_BOX || B.kind == UG_SHAPE_HULL)) {
-                for (int i = 0; i < sh.u.cand.n[lane]; i++) cand_add(L, sh.u.cand.c[lane][i].n, sh.u.cand.c[lane][i].pB, sh.u.cand.c[lane][i].d);
+                L.n = sh.u.cand.n[lane]; /* team_hull_box / team_hull_hull wrote them */
             } else if (A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_HULL) {
-                CandList L2;
-                L2.n = 0;
-                nc_hull_sphere(TB, B, TA, A, P.thr, L2);
-                for (int i = 0; i < L2.n; i++)
-                    cand_add(L, vneg(L2.c[i].n), vadd(L2.c[i].pB, vscale(L2.c[i].n, L2.c[i].d)), L2.c[i].d);
+                nc_hull_sphere(TB, B, TA, A, P.thr, L);
+                for (int i = 0; i < L.n; i++) { /* swapped roles: flip the normal, move the point onto the sphere */
+                    const v3 cn = ldv(L.c[i].n), cp = ldv(L.c[i].pB);
+                    stv(L.c[i].n, vneg(cn));
+                    stv(L.c[i].pB, vadd(cp, vscale(cn, L.c[i].d)));
+                }
             } else if (A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_BOX) nc_sphere_box(TA, A, TB, B, P.thr, L);
             else if (A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_SPHERE) nc_sphere_sphere(TA, A, TB, B, P.thr, L);
             else if (A.kind == UG_SHAPE_BOX && B.kind == UG_SHAPE_BOX) nc_box_box(TA, A, TB, B, P.thr, L);
             else if (A.kind == UG_SHAPE_HULL && B.kind == UG_SHAPE_SPHERE) nc_hull_sphere(TA, A, TB, B, P.thr, L);
             else if (A.kind == UG_SHAPE_BOX && B.kind == UG_SHAPE_SPHERE) {
-                CandList L2;
-                L2.n = 0;
-                nc_sphere_box(TB, B, TA, A, P.thr, L2);
-                for (int i = 0; i < L2.n; i++)
-                    cand_add(L, vneg(L2.c[i].n), vadd(L2.c[i].pB, vscale(L2.c[i].n, L2.c[i].d)), L2.c[i].d);
+                nc_sphere_box(TB, B, TA, A, P.thr, L);
+                for (int i = 0; i < L.n; i++) {
+                    const v3 cn = ldv(L.c[i].n), cp = ldv(L.c[i].pB);
+                    stv(L.c[i].n, vneg(cn));
+                    stv(L.c[i].pB, vadd(cp, vscale(cn, L.c[i].d)));
+                }
             }
             PROF_ADD(PF_PR_NP, t_pn);
             PROF_T0(t_pm);
-            for (int i = 0; i < L.n; i++) manifold_add(M, sh.O[P.a], sh.O[P.b], L.c[i], P.thr);
+            for (int i = 0; i < L.n; i++) {
+                Cand c;
+                c.n = ldv(L.c[i].n);
+                c.pB = ldv(L.c[i].pB);
+                c.d = L.c[i].d;
+                manifold_add(M, sh.O[P.a], sh.O[P.b], c, P.thr);
+            }
             if (M.npts) manifold_refresh(M, sh.O[P.a], sh.O[P.b], P.thr);
             has = M.npts > 0;
             PROF_ADD(PF_PR_MAN, t_pm);
@@ -558,7 +576,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         unsigned long long hm = ballot(has);
         if (has) {
             int pos = nnew + lane_prefix(hm);
-            if (pos < MAXMAN) man_to_st(e.man[pos], M);
+            if (pos < MAXMAN) man_to_st(e.man[pos], *(const LManifold*)&sh.pm[lane]);
         }
         nnew += __popcll(hm);
         __syncthreads();
