@@ -1472,6 +1472,8 @@ __device__ __noinline__ static void team_robot_dynamics(double g_) {
     SV Vbb;
     Vbb.w = V(0, 0, 0);
     Vbb.v = V(0, 0, 0);
+    /* the damping inertia in world axes does not depend on the parent: formed before the level loop */
+    const m3 Dw = inertia_world(k.R[b], &UG_BODY_DAMPI[6 * b]);
     for (int L = 0; L < NB; L++) {
         if (own && depth == L) {
             const int p = UG_BODY_PARENT[b];
@@ -1491,12 +1493,12 @@ __device__ __noinline__ static void team_robot_dynamics(double g_) {
             f.w = vadd(IA.w, vadd(vcross(Vb.w, IV.w), vcross(Vb.v, IV.v)));
             f.v = vadd(IA.v, vcross(Vb.w, IV.v));
             double wn = vlen(Vb.w);
-            m3 D = inertia_world(k.R[b], &UG_BODY_DAMPI[6 * b]);
-            v3 tau = vscale(mv(D, Vb.w), UG_ANG_DAMP + UG_ANG_DAMP * wn);
+            v3 tau = vscale(mv(Dw, Vb.w), UG_ANG_DAMP + UG_ANG_DAMP * wn);
             f.w = vadd(f.w, tau);
             Vbb = Vb;
         }
         __syncthreads();
+        if (ballot(depth > L) == 0ull) break; /* no deeper bodies */
     }
     /* 5. link damping: lane l computes link l's force and torque; body b adds its links in link order */
     if (lane >= 1 && lane < UG_NL) {
@@ -1555,25 +1557,48 @@ __device__ __noinline__ static void serial_pre(const Scene* s) {
     team_robot_dynamics(s->gravity);
     PROF_ADD(PF_RDYN, t_rd);
     PROF_T0(t_ldl);
+    {
+        /* LDL^T of the mass matrix, wave-parallel: lane i < NB owns row i.  Step j: every lane forms
+         * t = a[j] - sum_k (a[k] * L_jk) * D_k (k ascending; L_jk broadcast from lane j), which on lane j is
+         * ldlt()'s diagonal d and on lanes i > j its s; then a[j] = d (lane j) or s / d (i > j).  The same
+         * operations in the same order as ldlt_r() / the oracle's ldlt(), one division per step instead of
+         * one per element. */
+        const bool own = lane < NB;
+        double a[NB], D[NB];
+#pragma unroll
+        for (int c = 0; c < NB; c++) a[c] = own ? sh.LDL[lane * NB + c] : 0.0;
+#pragma unroll
+        for (int j = 0; j < NB; j++) {
+            double t = a[j];
+#pragma unroll
+            for (int k2 = 0; k2 < j; k2++) t -= a[k2] * readlane_d(a[k2], j) * D[k2];
+            const double d = readlane_d(t, j);
+            D[j] = d;
+            a[j] = lane == j ? d : (lane > j ? t / d : a[j]);
+        }
+        if (own) {
+#pragma unroll
+            for (int c = 0; c < NB; c++) sh.LDL[lane * NB + c] = a[c];
+        }
+        if (lane < NVP) sh.v0[lane] = 0.0; /* inactive objects' and padding slots stay 0 */
+        __syncthreads();
+    }
     if (lane == 0) {
         double C[NB];
 #pragma unroll
         for (int i = 0; i < NB; i++) C[i] = sh.u.dyn.C[i];
-        /* LDL^T and the qdd solve with the matrix in registers (compile-time indices, same order) */
+        /* the qdd solve with the factored matrix in registers (compile-time indices, same order) */
         double A[NB * NB];
 #pragma unroll
         for (int i = 0; i < NB * NB; i++) A[i] = sh.LDL[i];
-        ldlt_r(A);
-#pragma unroll
-        for (int i = 0; i < NB * NB; i++) sh.LDL[i] = A[i];
         double qdd[NB];
 #pragma unroll
         for (int i = 0; i < NB; i++) qdd[i] = -C[i];
         ldlt_solve_r(A, qdd);
-        for (int i = 0; i < NVP; i++) sh.v0[i] = 0.0;
         for (int i = 0; i < NB; i++) { e.qd[i] = e.qd[i] + qdd[i] * dt; sh.v0[i] = e.qd[i]; }
-        for (int o = 0; o < s->nobj; o++) {
-            if (e.oactive[o] == 0.0) continue;
+    } else if (lane <= s->nobj) { /* free bodies, one lane each (independent of the robot solve) */
+        const int o = lane - 1;
+        if (e.oactive[o] != 0.0) {
             StObj& ob = e.obj[o];
             v3 v = ob.v;
             double vn = vlen(v);
