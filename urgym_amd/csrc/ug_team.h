@@ -1284,6 +1284,15 @@ __device__ __forceinline__ void sweep_section(const double (&A0)[PREG], const do
 #pragma unroll
     for (int s = 0; s < (TWO ? 2 : 1); s++) L.dsv[s] = in[s] ? F.dsv[s] : L.dsv[s];
 }
+/* rows P0, P0 + STEP, ... (NR of them) straight, no chunk tests and no neutral rows (the contact-free solve) */
+template <int P, int STEP, int K>
+__device__ __forceinline__ void straight_rows(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA,
+                                              int lane, Lrow& L, double (&W)[2]) {
+    if constexpr (K > 0) {
+        row_upd<P, false>(A0, A1, wsA, lane, L, W);
+        straight_rows<P + STEP, STEP, K - 1>(A0, A1, wsA, lane, L, W);
+    }
+}
 /* warm start: normal rows [nnc, fb) with a carried impulse, w += A[:, P] * impulse */
 template <int P>
 __device__ __forceinline__ void sweep_warm(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA,
@@ -1865,9 +1874,34 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         }
         return split;
     };
-    const int split = n > 64   ? passes(std::integral_constant<int, 128>{})
-                      : n > 32 ? passes(std::integral_constant<int, 64>{})
-                               : passes(std::integral_constant<int, 32>{});
+    /* contact-free solve of the 7 motor + 5 gear rows (free-space motion: most of a reset's settling): the
+     * sweeps as straight 12-row sequences, reversed on even sweeps, forward on odd ones -- the general
+     * path's order without chunk tests or neutral rows; no normal rows, so no warm start and no split pass */
+    auto passes_free12 = [&]() -> int {
+        PROF_T0(t_sw);
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            L.dlo[s] = L.lo[s] - L.imp[s];
+            L.dhi[s] = L.hi[s] - L.imp[s];
+        }
+        for (int it = 0; it < UG_PGS_ITERS; it++) {
+            double res = 0.0;
+            gcdouble* o_wsA = wsAr;
+            asm volatile("" : "+s"(o_wsA));
+            if (!(it & 1)) straight_rows<11, -1, 12>(A0, A1, o_wsA, lane, L, W);
+            else straight_rows<0, 1, 12>(A0, A1, o_wsA, lane, L, W);
+            row_finish<false>(L, pos_mask(0, 0, 12, 0ull), 0ull, lane, res);
+            PROF_CNT(PC_ITERS, 1);
+            if (ballot(!(res <= UG_RESIDUAL_THR)) == 0ull || it >= UG_PGS_ITERS - 1) break;
+        }
+        PROF_ADD(PF_SWEEPS, t_sw);
+        if (lane < 12) g_sh.rs[lane].imp = L.imp[0];
+        return 0;
+    };
+    const int split = (n == 12 && nnc == 12) ? passes_free12()
+                      : n > 64             ? passes(std::integral_constant<int, 128>{})
+                      : n > 32             ? passes(std::integral_constant<int, 64>{})
+                                           : passes(std::integral_constant<int, 32>{});
     /* dv[d] (dvs[d]) = fma chain over positions k of M^-1J_k[d] * impulse_k (lane d < NV) */
     __builtin_amdgcn_wave_barrier();
     if (split) {
