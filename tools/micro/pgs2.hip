@@ -13,6 +13,7 @@
 //   5  one chunked section over all 74 rows (the chunk tests alone)
 //   7  variant 0 with an opaque always-true scalar test around every 8 rows (the cost of one chunk test)
 //   8  the same with one test per 16 rows
+//   9  variant 4 with an 80-position span (10 chunk positions per section instead of 16)
 //   6  variant 4 with switch dispatch: a jump into the section's first chunk, one exit compare per chunk
 //      (must equal variant 4 bit for bit)
 // Usage: tools/micro/pgs2 (prints cycles per row update and a bit-exactness check against variant 0)
@@ -207,6 +208,13 @@ __global__ void __launch_bounds__(64, 1) k(const double* in, double* out, unsign
             asm volatile("" : "+s"(on));
             vg_rows<0, MODE == 7 ? 8 : 16>(A0, A1, lane, L, W, on);
         }
+        if (MODE == 9) {
+            int nnc = 12, fb = 33, n = NR;
+            asm volatile("" : "+s"(nnc), "+s"(fb), "+s"(n));
+            if (!(it & 1)) sweep_section<true, (NCMAX + CHUNK - 1) / CHUNK, true>(A0, A1, nullptr, lane, 0, nnc, 0ull, 0ull, L, W);
+            sweep_section<false, 80 / CHUNK, true>(A0, A1, nullptr, lane, (it & 1) ? 0 : nnc, fb, 0ull, 0ull, L, W);
+            sweep_section<false, 80 / CHUNK, true>(A0, A1, nullptr, lane, fb, n, 0ull, 0ull, L, W);
+        }
         if (MODE == 5) {
             int n = NR;
             asm volatile("" : "+s"(n));
@@ -267,5 +275,6 @@ int main() {
     hipMemcpy(ref4, d_out, sizeof(double) * blocks * 64 * 4, hipMemcpyDeviceToHost);
     run<4>("4 production sections (92 slots/sweep avg)", d_in, d_out, d_c, blocks, ref4, 92);
     run<6>("6 sections, switch dispatch (vs variant 4)", d_in, d_out, d_c, blocks, ref4, 92);
+    run<9>("9 sections, 80-position span (vs variant 4)", d_in, d_out, d_c, blocks, ref4, 92);
     return 0;
 }

@@ -27,6 +27,7 @@
 #include <utility>
 
 #include "ug_device.h"
+#include "prio_model.h"
 #include "ug_glue.h"
 
 namespace ugd {
@@ -2479,35 +2480,49 @@ __device__ static void team_prof_flush() {
     if (threadIdx.x < UG_NPROF) atomicAdd(&g_prof[threadIdx.x], sh.prof[threadIdx.x]);
 #endif
 }
+/* BallBalance / TwoBalls reset predictor (scheduling only): ball i in the paddle frame -> the logit of "this
+ * env ends its episode in the next env-step", a 14 -> 16 (ReLU) -> 1 MLP (prio_model.h, tools/fit_priority.py)
+ * over the ball's paddle-frame offset, velocities and in-plane gravity and the log times of an edge-roll +
+ * free-fall estimate */
+__device__ static double bb_reset_logit(const EnvState& e, const m3& R, int o) {
+    const v3 l = mtv(R, vsub(e.obj[o].pos, e.obj[0].pos));
+    const v3 lv = mtv(R, vsub(e.obj[o].v, e.obj[0].v));
+    const v3 gl = mtv(R, V(0.0, 0.0, -9.81));
+    const double sx = l.x < 0.0 ? -1.0 : (l.x > 0.0 ? 1.0 : 0.0), sy = l.y < 0.0 ? -1.0 : (l.y > 0.0 ? 1.0 : 0.0);
+    const double fx = fabs(l.x) / UG_BB_PADDLE_HX, fy = fabs(l.y) / UG_BB_PADDLE_HY;
+    const double vx = lv.x * sx, vy = lv.y * sy;
+    const double dz = e.obj[o].pos.z - e.obj[0].pos.z, bvz = e.obj[o].v.z;
+    const double tf = dz < 0.0 ? 0.0 : (bvz + sqrt(bvz * bvz + 2.0 * 9.81 * dz)) / 9.81;
+    const double tex = fx >= 1.0 ? 0.0 : (1.0 - fx) * UG_BB_PADDLE_HX / fmax(vx, 0.05);
+    const double tey = fy >= 1.0 ? 0.0 : (1.0 - fy) * UG_BB_PADDLE_HY / fmax(vy, 0.05);
+    const double x[UG_PM_IN] = {fx, fy, l.z, vx, vy, lv.z, dz, bvz, gl.x * sx, gl.y * sy,
+                                log(fmin(tex, tey) + tf + 1e-3), log(tex + 1e-3), log(tey + 1e-3), log(tf + 1e-3)};
+    double z[UG_PM_IN];
+    for (int i = 0; i < UG_PM_IN; i++) z[i] = (x[i] - UG_PM_MU[i]) / UG_PM_SD[i];
+    double out = UG_PM_B2;
+    for (int h = 0; h < UG_PM_HID; h++) {
+        double a = UG_PM_B1[h];
+        for (int i = 0; i < UG_PM_IN; i++) a += z[i] * UG_PM_W1[i * UG_PM_HID + h];
+        out += fmax(a, 0.0) * UG_PM_W2[h];
+    }
+    return out;
+}
 /* Launch-order priority of an env for the next k_step (0..15, higher runs first).  The launch time is the
  * longest env chain, and an env-step that ends its episode carries a ~170-substep autoreset: envs likely
  * to end next step are dispatched first so their reset overlaps the other envs' steps.  Scheduling only --
  * every env computes the same thing whatever its position in the launch.  Predicted truncation: 15;
- * BallBalance / TwoBalls: the predicted time until a ball falls below the paddle (time to roll to the
- * paddle's edge at its outward paddle-frame speed, then free fall from its height over the paddle), in
- * 20 ms buckets (tools/predict_fit.py: on random-action BallBalance x 4096, 1.3 of ~270 resets per step
- * rank outside the first 1024 launch slots, against 5.8 for a position-extrapolation score);
- * otherwise the env's last substep count (longest first). */
+ * BallBalance / TwoBalls: the reset predictor's logit in 15 levels (held-out random-action BallBalance x 4096:
+ * 0.44 of ~270 resets per step ranked outside the first 1024 launch slots, against 1.1 for an edge-roll +
+ * free-fall time and 5.8 for a position-extrapolation score); otherwise the env's last substep count. */
 __device__ static int team_priority(const Scene* s, int nsub, int el_next, int max_steps, int autoreset) {
     const EnvState& e = g_sh.e;
     if (autoreset && max_steps > 0 && el_next >= max_steps) return 15;
     if (s->task == UG_TASK_BALLBALANCE && e.oactive[0] != 0.0) {
         const m3 R = qmat(e.obj[0].quat);
-        const double g = fabs(s->gravity) > 0.0 ? fabs(s->gravity) : 9.81;
-        double tmin = 1e30;
-        for (int o = 1; o < s->nobj; o++) {
-            if (e.oactive[o] == 0.0) continue;
-            const v3 l = mtv(R, vsub(e.obj[o].pos, e.obj[0].pos));
-            const v3 lv = mtv(R, vsub(e.obj[o].v, e.obj[0].v));
-            const double fx = fabs(l.x) / UG_BB_PADDLE_HX, fy = fabs(l.y) / UG_BB_PADDLE_HY;
-            const double vx = l.x < 0.0 ? -lv.x : lv.x, vy = l.y < 0.0 ? -lv.y : lv.y;
-            const double tex = fx >= 1.0 ? 0.0 : (1.0 - fx) * UG_BB_PADDLE_HX / fmax(vx, 0.05);
-            const double tey = fy >= 1.0 ? 0.0 : (1.0 - fy) * UG_BB_PADDLE_HY / fmax(vy, 0.05);
-            const double dz = e.obj[o].pos.z - e.obj[0].pos.z, vz = e.obj[o].v.z;
-            const double tf = dz < 0.0 ? 0.0 : (vz + sqrt(vz * vz + 2.0 * g * dz)) / g;
-            tmin = fmin(tmin, fmin(tex, tey) + tf);
-        }
-        const double b = 14.0 - floor(tmin / 0.02);
+        double lg = -1e300;
+        for (int o = 1; o < s->nobj; o++)
+            if (e.oactive[o] != 0.0) lg = fmax(lg, bb_reset_logit(e, R, o));
+        const double b = floor((lg - UG_PM_L0) / UG_PM_DL);
         return b > 14.0 ? 14 : (b < 0.0 ? 0 : (int)b);
     }
     int b = 0;
