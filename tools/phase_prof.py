@@ -23,7 +23,7 @@ NAMES = ["collide", "dyn+enum", "rows", "pgs", "pgs_setup", "integrate", "glue",
          "hullbox_vertices", "hullbox_corners", "hullbox_reduce", "fk", "lane0_ldl_objects", "unit_solves",
          "row_build", "rb_jacobians", "rb_solves", "rb_scalars", "pgs_mfma",
          "pgs_warm", "sw_nc", "sw_contact", "sw_finish", "sw_fric_prep", "sw_fric", "sw_res",
-         "pr_lookup", "pr_narrow", "pr_manifold", "pr_store", "chunks", "nnc", "nn"]
+         "pr_lookup", "pr_narrow", "pr_manifold", "pr_store", "chunks", "nnc", "nn", "n_le64", "n_65_80", "n_81_96"]
 
 
 def main():
@@ -39,7 +39,7 @@ def main():
     sim.sync()
     rc = sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     assert rc == 0, "library not built with -DUG_PROF"
-    r = {k: float(v) for k, v in zip(NAMES, buf[:45])}
+    r = {k: float(v) for k, v in zip(NAMES, buf[:48])}
     print("reset (cycles per substep):", json.dumps({k: round(r[k] / max(r["substeps"], 1), 1) for k in NAMES}))
     rng = np.random.default_rng(1)
     for _ in range(a.steps):
@@ -47,7 +47,7 @@ def main():
     sim.sync()
     sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     es = a.envs * a.steps
-    d = {k: float(v) for k, v in zip(NAMES, buf[:45])}
+    d = {k: float(v) for k, v in zip(NAMES, buf[:48])}
     out = {"per_env_step_cycles": {k: d[k] / es for k in NAMES[:8]},
            "substeps_per_env_step": d["substeps"] / es,
            "rows_per_substep": d["nrows"] / max(d["substeps"], 1),
@@ -60,6 +60,7 @@ def main():
     out["pgs_sweep_cycles_per_row_update"] = d["pgs_sweeps"] / max(d["nrows"] * d["pgs_iters"] / max(d["substeps"], 1), 1)
     out["pgs_sweep_cycles_per_row_slot"] = d["pgs_sweeps"] / max(8 * d["chunks"], 1)  # chunk rows incl. neutral
     out["row_slots_per_sweep"] = 8 * d["chunks"] / max(d["pgs_iters"], 1)
+    out["substep_fraction_rows_le64_65to80_81to96"] = [d[k] / max(d["substeps"], 1) for k in ("n_le64", "n_65_80", "n_81_96")]
     out["nc_normal_friction_rows_per_substep"] = [d["nnc"] / max(d["substeps"], 1), d["nn"] / max(d["substeps"], 1),
                                                   (d["nrows"] - d["nnc"] - d["nn"]) / max(d["substeps"], 1)]
     for k in ("dyn+enum", "rows", "pgs", "pgs_setup", "pgs_sweeps", "hull_narrowphase", "robot_dynamics",

@@ -134,7 +134,7 @@ __device__ unsigned long long g_prof[UG_NPROF];
 enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_TOTAL,
        PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN, PF_SWEEPS, PF_HULL,
        PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE, PF_FK, PF_LDL, PF_UNIT, PF_ROWB, PF_RB1, PF_RB2, PF_RB3, PF_MFMA, PF_WARM, PF_SW_NC, PF_SW_CT, PF_SW_FIN, PF_SW_FPREP, PF_SW_FR,
-       PF_SW_RES, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST, PC_CHUNKS, PC_NNC, PC_NN };
+       PF_SW_RES, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST, PC_CHUNKS, PC_NNC, PC_NN, PC_N64, PC_N80, PC_N96 };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -1900,7 +1900,8 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         return 0;
     };
     const int split = (n == 12 && nnc == 12) ? passes_free12()
-                      : n > 64             ? passes(std::integral_constant<int, 128>{})
+                      : n > 96             ? passes(std::integral_constant<int, 128>{})
+                      : n > 64             ? passes(std::integral_constant<int, 96>{})
                       : n > 32             ? passes(std::integral_constant<int, 64>{})
                                            : passes(std::integral_constant<int, 32>{});
     /* dv[d] (dvs[d]) = fma chain over positions k of M^-1J_k[d] * impulse_k (lane d < NV) */
@@ -1949,6 +1950,9 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     PROF_CNT(PC_ROWS, n);
     PROF_CNT(PC_NNC, nnc);
     PROF_CNT(PC_NN, nn);
+    PROF_CNT(PC_N64, n <= 64);
+    PROF_CNT(PC_N80, n > 64 && n <= 80);
+    PROF_CNT(PC_N96, n > 80 && n <= 96);
     PROF_CNT(PC_OVL, sh.nov);
     PROF_CNT(PC_NMAN, (int)e.nman);
     /* rows: built lane-per-row into the workspace (J | M^-1 J^T) and LDS (scalars) */
