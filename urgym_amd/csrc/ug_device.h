@@ -862,16 +862,74 @@ DFI double np_sum12(const double* a) {
     return r;
 }
 DFI double gripper_angle(double L) { return 0.715 - ug_asin((L - 0.010) / 0.1143); }
+/* ik_solve's kinematics: the 6 arm bodies only (their axes / points and the EE link frame are all the IK
+ * reads), compile-time body indices so everything stays in registers; the same operations as fk() and
+ * link_frame() for those bodies */
+constexpr int kBodyParentIK[NB] = UG_BODY_PARENT_INIT;
+#define UG_IK_NB 6 /* arm bodies 0..5; the EE link (UG_EE_LINK) is fixed to body 5 (UG_LINK_BODY) */
+#define UG_IK_EE_BODY 5
+struct ArmKin { m3 R[UG_IK_NB]; v3 p[UG_IK_NB]; v3 a[UG_IK_NB]; };
+DFI void fk_arm(const double (&q)[NB], ArmKin& k) {
+#pragma unroll
+    for (int b = 0; b < UG_IK_NB; b++) {
+        const int pb = kBodyParentIK[b];
+        m3 Rpb = mload(&UG_BODY_R[9 * b]);
+        v3 Ppb = V(UG_BODY_P[3 * b], UG_BODY_P[3 * b + 1], UG_BODY_P[3 * b + 2]);
+        v3 ax = V(UG_BODY_AXIS[3 * b], UG_BODY_AXIS[3 * b + 1], UG_BODY_AXIS[3 * b + 2]);
+        m3 Rj = axis_angle(ax, q[b]);
+        m3 Rp;
+        v3 pp;
+        if (pb < 0) { Rp = mident(); pp = V(0, 0, 0); }
+        else { Rp = k.R[pb < 0 ? 0 : pb]; pp = k.p[pb < 0 ? 0 : pb]; }
+        m3 Rtmp = mm(Rp, Rpb);
+        k.R[b] = mm(Rtmp, Rj);
+        k.p[b] = vadd(pp, mv(Rp, Ppb));
+        k.a[b] = mv(Rtmp, ax);
+    }
+}
+/* ldlt() / ldlt_solve() of a fixed size with compile-time indices (same operations, same order) */
+template <int N>
+DFI void ldlt_n(double (&A)[N * N]) {
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        double d = A[j * N + j];
+#pragma unroll
+        for (int k2 = 0; k2 < j; k2++) d -= A[j * N + k2] * A[j * N + k2] * A[k2 * N + k2];
+        A[j * N + j] = d;
+#pragma unroll
+        for (int i = j + 1; i < N; i++) {
+            double s = A[i * N + j];
+#pragma unroll
+            for (int k2 = 0; k2 < j; k2++) s -= A[i * N + k2] * A[j * N + k2] * A[k2 * N + k2];
+            A[i * N + j] = s / d;
+        }
+    }
+}
+template <int N>
+DFI void ldlt_solve_n(const double (&A)[N * N], double (&x)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; i++)
+#pragma unroll
+        for (int k2 = 0; k2 < i; k2++) x[i] -= A[i * N + k2] * x[k2];
+#pragma unroll
+    for (int i = 0; i < N; i++) x[i] = x[i] / A[i * N + i];
+#pragma unroll
+    for (int i = N - 1; i >= 0; i--)
+#pragma unroll
+        for (int k2 = i + 1; k2 < N; k2++) x[i] -= A[k2 * N + i] * x[k2];
+}
 DF void ik_solve(const double* q0, v3 tp, q4 to, double* qout) {
     double q[NB];
+#pragma unroll
     for (int i = 0; i < NB; i++) q[i] = q0[i];
     double diff = 1e30;
+    const m3 Rl = mload(&UG_LINK_COMR[9 * UG_EE_LINK]);
+    const v3 Pl = V(UG_LINK_COMP[3 * UG_EE_LINK], UG_LINK_COMP[3 * UG_EE_LINK + 1], UG_LINK_COMP[3 * UG_EE_LINK + 2]);
     for (int it = 0; it < UG_IK_ITERS && diff > UG_IK_RESIDUAL; it++) {
-        Kin k;
-        fk(q, k);
-        m3 Re;
-        v3 pe;
-        link_frame(k, UG_EE_LINK, 1, Re, pe);
+        ArmKin k;
+        fk_arm(q, k);
+        const m3 Re = mm(k.R[UG_IK_EE_BODY], Rl); /* link_frame(k, UG_EE_LINK, 1, ...) */
+        const v3 pe = vadd(k.p[UG_IK_EE_BODY], mv(k.R[UG_IK_EE_BODY], Pl));
         q4 oe = mquat(Re);
         diff = vlen(vsub(pe, tp));
         double ds[6];
@@ -893,31 +951,40 @@ DF void ik_solve(const double* q0, v3 tp, q4 to, double* qout) {
         ds[4] = 1.0 * ((double)angle * axis.y);
         ds[5] = 1.0 * ((double)angle * axis.z);
         double J[6][6];
+#pragma unroll
         for (int d = 0; d < 6; d++) {
             v3 jl = vcross(k.a[d], vsub(pe, k.p[d]));
             J[0][d] = jl.x; J[1][d] = jl.y; J[2][d] = jl.z;
             J[3][d] = k.a[d].x; J[4][d] = k.a[d].y; J[5][d] = k.a[d].z;
         }
         double U[36], rhs[6];
+#pragma unroll
         for (int i = 0; i < 6; i++) {
+#pragma unroll
             for (int j = 0; j < 6; j++) {
                 double sum = 0.0;
+#pragma unroll
                 for (int r = 0; r < 6; r++) sum += J[r][i] * J[r][j];
                 U[i * 6 + j] = sum;
             }
             U[i * 6 + i] += UG_IK_DAMPING;
             double sr = 0.0;
+#pragma unroll
             for (int r = 0; r < 6; r++) sr += J[r][i] * ds[r];
             rhs[i] = sr;
         }
-        ldlt(U, 6);
-        ldlt_solve(U, 6, rhs);
+        ldlt_n<6>(U);
+        ldlt_solve_n<6>(U, rhs);
         double mx = 0.0;
+#pragma unroll
         for (int i = 0; i < 6; i++) mx = ug_fabs(rhs[i]) > mx ? ug_fabs(rhs[i]) : mx;
         if (mx > UG_IK_MAXANGLE)
+#pragma unroll
             for (int i = 0; i < 6; i++) rhs[i] *= UG_IK_MAXANGLE / mx;
+#pragma unroll
         for (int i = 0; i < 6; i++) q[i] = rhs[i] + q[i];
     }
+#pragma unroll
     for (int i = 0; i < NB; i++) qout[i] = q[i];
 }
 
