@@ -1482,34 +1482,42 @@ __device__ __noinline__ static void team_robot_dynamics(double g_) {
     SV Vbb;
     Vbb.w = V(0, 0, 0);
     Vbb.v = V(0, 0, 0);
-    /* the damping inertia in world axes does not depend on the parent: formed before the level loop */
+    /* the damping inertia in world axes does not depend on the parent: formed up front */
     const m3 Dw = inertia_world(k.R[b], &UG_BODY_DAMPI[6 * b]);
-    for (int L = 0; L < NB; L++) {
-        if (own && depth == L) {
-            const int p = UG_BODY_PARENT[b];
-            SV Vp, Ap;
-            if (p < 0) { Vp.w = V(0, 0, 0); Vp.v = V(0, 0, 0); Ap.w = V(0, 0, 0); Ap.v = V(0, 0, -g); }
-            else { Vp = w.Vb[p]; Ap = w.Ab[p]; }
-            const SV Sb = w.S[b];
-            SV vj; vj.w = vscale(Sb.w, qd[b]); vj.v = vscale(Sb.v, qd[b]);
-            SV Vb, Ab;
-            Vb.w = vadd(Vp.w, vj.w); Vb.v = vadd(Vp.v, vj.v);
-            Ab.w = vadd(Ap.w, vcross(Vb.w, vj.w));
-            Ab.v = vadd(Ap.v, vadd(vcross(Vb.w, vj.v), vcross(Vb.v, vj.w)));
-            w.Vb[b] = Vb;
-            w.Ab[b] = Ab;
-            SV IA = spatial_inertia_mul(m, h, Jb, Ab);
-            SV IV = spatial_inertia_mul(m, h, Jb, Vb);
-            f.w = vadd(IA.w, vadd(vcross(Vb.w, IV.w), vcross(Vb.v, IV.v)));
-            f.v = vadd(IA.v, vcross(Vb.w, IV.v));
-            double wn = vlen(Vb.w);
-            v3 tau = vscale(mv(Dw, Vb.w), UG_ANG_DAMP + UG_ANG_DAMP * wn);
-            f.w = vadd(f.w, tau);
-            Vbb = Vb;
+    /* RNEA forward as a per-lane ancestor walk: lane b recomputes the velocity / acceleration recursion
+     * along its own root-to-b path (ancestor indices ascend with depth), the same operations on the same
+     * inputs as the body-by-body pass, without a barrier per tree level */
+    (void)depth;
+    if (own) {
+        const int am = g_sh.anc[b];
+        SV Vp, Ap;
+        Vp.w = V(0, 0, 0); Vp.v = V(0, 0, 0); Ap.w = V(0, 0, 0); Ap.v = V(0, 0, -g);
+#pragma unroll
+        for (int j = 0; j < NB; j++) {
+            if ((am >> j) & 1) {
+                const SV Sj = w.S[j];
+                SV vj; vj.w = vscale(Sj.w, qd[j]); vj.v = vscale(Sj.v, qd[j]);
+                SV Vj, Aj;
+                Vj.w = vadd(Vp.w, vj.w); Vj.v = vadd(Vp.v, vj.v);
+                Aj.w = vadd(Ap.w, vcross(Vj.w, vj.w));
+                Aj.v = vadd(Ap.v, vadd(vcross(Vj.w, vj.v), vcross(Vj.v, vj.w)));
+                Vp = Vj;
+                Ap = Aj;
+            }
         }
-        __syncthreads();
-        if (ballot(depth > L) == 0ull) break; /* no deeper bodies */
+        const SV Vb = Vp, Ab = Ap;
+        w.Vb[b] = Vb;
+        w.Ab[b] = Ab;
+        SV IA = spatial_inertia_mul(m, h, Jb, Ab);
+        SV IV = spatial_inertia_mul(m, h, Jb, Vb);
+        f.w = vadd(IA.w, vadd(vcross(Vb.w, IV.w), vcross(Vb.v, IV.v)));
+        f.v = vadd(IA.v, vcross(Vb.w, IV.v));
+        double wn = vlen(Vb.w);
+        v3 tau = vscale(mv(Dw, Vb.w), UG_ANG_DAMP + UG_ANG_DAMP * wn);
+        f.w = vadd(f.w, tau);
+        Vbb = Vb;
     }
+    __syncthreads();
     /* 5. link damping: lane l computes link l's force and torque; body b adds its links in link order */
     if (lane >= 1 && lane < UG_NL) {
         const int l = lane, bl = UG_LINK_BODY[l];
