@@ -754,7 +754,8 @@ DF void nc_box_box(const XF& TA, const Collider& A, const XF& TB, const Collider
  * semantics).  Planes are fetched HP_BATCH at a time with every load issued before the first use: the
  * per-face loop would otherwise wait one memory latency per face. */
 #define HP_BATCH 8
-DFI void hull_plane_max(const Collider& A, v3 y, double& smax, int& fm) {
+template <class C> /* a Collider, or any type with the hull range fields nf / f0 */
+DFI void hull_plane_max(const C& A, v3 y, double& smax, int& fm) {
     const int nf = A.nf, f0 = A.f0;
     for (int b = 0; b < nf; b += HP_BATCH) {
         double F[HP_BATCH][4];

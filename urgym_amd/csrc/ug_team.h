@@ -68,6 +68,17 @@ struct EnvState {
 static_assert(sizeof(EnvState) == UG_STATE_DIM * sizeof(double), "EnvState must match ug_layout.h");
 static_assert(sizeof(Manifold) * MAXOV <= 88 * MAXROWS, "working manifolds must fit in the rows' LDS");
 
+/* the collider fields the wave narrowphases read, and a pair's shape transforms: formed lane-per-pair once
+ * per collision pass (team_collide), read back uniformly by the hull pair loop */
+struct HullArg { int nv, v0, nf, f0; double margin; double half[3]; };
+struct PairInfo { XF TA, TB; HullArg A, B; double thr; int a, b, ka, kb; };
+__device__ __forceinline__ static HullArg hull_arg(const Collider& c) {
+    HullArg h;
+    h.nv = c.nv; h.v0 = c.v0; h.nf = c.nf; h.f0 = c.f0; h.margin = c.margin;
+    h.half[0] = c.half[0]; h.half[1] = c.half[1]; h.half[2] = c.half[2];
+    return h;
+}
+
 struct RowS {
     double invD, rinv, rhs, rhsPen, lo, hi, imp, impPen, fric; /* rinv = invD == 0 ? 0 : 1 / invD */
     int kind; /* 0 limit, 1 motor, 2 gear, 3 normal, 4/5 friction dir 1/2, 6/7 rolling axis 1/2 */
@@ -88,6 +99,7 @@ struct Shared {
     union {
         RowS rs[MAXROWS];        /* row build .. impulse write-back */
         Manifold pm[MAXOV];      /* collision: lane k's working manifold (rows are dead until the row build) */
+        PairInfo pinfo[MAXOV];   /* collision: pair k's transforms and collider fields (before pm is written) */
     };
     union {
         double mcol[NB + 5][NB]; /* row build: M^-1 e_d (d < NB) and M^-1 (ratio_g e_child_g) of gear g */
@@ -231,7 +243,7 @@ __device__ static inline void man_to_st(StMan& S, const LManifold& M) {
 #define HB_FACE_UNROLL 12 /* covers hulls of up to 96 faces (the model's largest has 89) */
 /* hull (A, robot link) vs box (B): the whole wave.  Produces cand k (<= 4 points) in sh.u.cand. */
 __device__ __forceinline__ static void team_reduce4(int n, int k);
-__device__ __forceinline__ static void team_hull_box(const Collider& A, const Collider& B, const XF& TA, const XF& TB,
+__device__ __forceinline__ static void team_hull_box(const HullArg& A, const HullArg& B, const XF& TA, const XF& TB,
                                      double thr, int k) {
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
@@ -347,7 +359,7 @@ __device__ __forceinline__ static void team_hull_box(const Collider& A, const Co
 
 /* hull (A) vs hull (B) (oracle nc_hull_hull): lane per A vertex against B's planes, lane per B vertex against
  * A's planes; candidates in canonical order (A vertices, then B vertices; at most 64 kept), then reduce4 */
-__device__ __forceinline__ static void team_hull_hull(const Collider& A, const Collider& B, const XF& TA, const XF& TB,
+__device__ __forceinline__ static void team_hull_hull(const HullArg& A, const HullArg& B, const XF& TA, const XF& TB,
                                                    double thr, int k) {
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
@@ -486,19 +498,32 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         int cn = nov - c0 < MAXOV ? nov - c0 : MAXOV;
         /* hull-box pairs of this chunk: cooperative narrowphase */
         PROF_T0(t_hull);
-        for (int k = 0; k < cn; k++) {
-            const PairDef& P = s->pair[sh.ov[c0 + k]];
+        /* every pair's transforms and collider fields at once (lane per pair: one load latency for the pass),
+         * then the hull pairs in pair order, each reading its record uniformly from LDS */
+        int hk = 0;
+        if (lane < cn) {
+            const int p = sh.ov[c0 + lane];
+            const PairDef& P = s->pair[p];
             const Collider& A = s->col[P.a];
             const Collider& B = s->col[P.b];
-            if (A.kind == UG_SHAPE_HULL && B.kind == UG_SHAPE_BOX) {
-                XF TA = shape_xf(sh.O[P.a], A), TB = shape_xf(sh.O[P.b], B);
-                team_hull_box(A, B, TA, TB, P.thr, k);
-                PROF_CNT(PC_HULL, 1);
-            } else if (A.kind == UG_SHAPE_HULL && B.kind == UG_SHAPE_HULL) {
-                XF TA = shape_xf(sh.O[P.a], A), TB = shape_xf(sh.O[P.b], B);
-                team_hull_hull(A, B, TA, TB, P.thr, k);
-                PROF_CNT(PC_HULL, 1);
-            }
+            PairInfo pi;
+            pi.TA = shape_xf(sh.O[P.a], A);
+            pi.TB = shape_xf(sh.O[P.b], B);
+            pi.A = hull_arg(A);
+            pi.B = hull_arg(B);
+            pi.thr = P.thr;
+            pi.a = P.a; pi.b = P.b; pi.ka = A.kind; pi.kb = B.kind;
+            sh.pinfo[lane] = pi;
+            hk = A.kind == UG_SHAPE_HULL && (B.kind == UG_SHAPE_BOX || B.kind == UG_SHAPE_HULL);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        for (unsigned long long hm = ballot(hk); hm != 0ull; hm &= hm - 1ull) {
+            const int k = __builtin_ctzll(hm);
+            const PairInfo pi = sh.pinfo[k];
+            if (pi.kb == UG_SHAPE_BOX) team_hull_box(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k);
+            else team_hull_hull(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k);
+            PROF_CNT(PC_HULL, 1);
         }
         PROF_ADD(PF_HULL, t_hull);
         PROF_T0(t_pairs);
@@ -507,6 +532,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         /* previous manifolds of this pass's pairs: index lookup per lane (pair ids in LDS), then one cooperative
          * copy of their points from the workspace into the working manifolds (all loads in flight together) */
         PROF_T0(t_pl);
+        __builtin_amdgcn_wave_barrier(); /* the pair records (sh.pinfo) are dead from here: pm reuses their LDS */
         if (lane < cn) {
             const int p = sh.ov[c0 + lane];
             int mo = -1;
