@@ -496,15 +496,20 @@ DF void nc_sphere_sphere(const XF& TA, const Collider& A, const XF& TB, const Co
     cand_add(out, n, vadd(TB.p, vscale(n, B.half[0])), dist);
 }
 
-DF int intersect_rect_quad(const double h[2], double p[8], double ret[16]) {
+/* box-box working arrays: one LDS slot per box-box lane (team_collide), so the dynamically indexed clip
+ * buffers never go to scratch memory */
+typedef __attribute__((address_space(3))) double ldouble;
+typedef __attribute__((address_space(3))) int lint;
+struct BoxScratch { double quad[8], ret[16], buffer[16], dep[8], ang[8], pt[24]; int avail[8], iret[8]; };
+typedef __attribute__((address_space(3))) BoxScratch LBoxScratch;
+DF int intersect_rect_quad(const double h[2], ldouble* p, ldouble* ret, ldouble* buffer) {
     int nq = 4, nr = 0;
-    double buffer[16];
-    double* q = p;
-    double* r = ret;
+    ldouble* q = p;
+    ldouble* r = ret;
     for (int dir = 0; dir <= 1; dir++) {
         for (int sign = -1; sign <= 1; sign += 2) {
-            double* pq = q;
-            double* pr = r;
+            ldouble* pq = q;
+            ldouble* pr = r;
             nr = 0;
             for (int i = nq; i > 0; i--) {
                 if (sign * pq[dir] < h[dir]) {
@@ -512,7 +517,7 @@ DF int intersect_rect_quad(const double h[2], double p[8], double ret[16]) {
                     pr += 2; nr++;
                     if (nr & 8) { q = r; goto done; }
                 }
-                double* nextq = (i > 1) ? pq + 2 : q;
+                ldouble* nextq = (i > 1) ? pq + 2 : q;
                 if ((sign * pq[dir] < h[dir]) ^ (sign * nextq[dir] < h[dir])) {
                     pr[1 - dir] = pq[1 - dir] + (nextq[1 - dir] - pq[1 - dir]) / (nextq[dir] - pq[dir]) * (sign * h[dir] - pq[dir]);
                     pr[dir] = sign * h[dir];
@@ -531,7 +536,7 @@ done:
         for (int i = 0; i < nr * 2; i++) ret[i] = q[i];
     return nr;
 }
-DF void cull_points(int n, const double p[], int m, int i0, int iret[]) {
+DF void cull_points(int n, const ldouble* p, int m, int i0, lint* iret, ldouble* A, lint* avail) {
     double a, cx, cy, qq;
     if (n == 1) { cx = p[0]; cy = p[1]; }
     else if (n == 2) { cx = 0.5 * (p[0] + p[2]); cy = 0.5 * (p[1] + p[3]); }
@@ -549,9 +554,7 @@ DF void cull_points(int n, const double p[], int m, int i0, int iret[]) {
         cx = a * (cx + qq * (p[n * 2 - 2] + p[0]));
         cy = a * (cy + qq * (p[n * 2 - 1] + p[1]));
     }
-    double A[8];
     for (int i = 0; i < n; i++) A[i] = ug_atan2(p[i * 2 + 1] - cy, p[i * 2] - cx);
-    int avail[8];
     for (int i = 0; i < n; i++) avail[i] = 1;
     avail[i0] = 0;
     iret[0] = i0;
@@ -577,7 +580,8 @@ DFI double col_dotv(const m3& A, int i, v3 v) { return A.m[i] * v.x + A.m[3 + i]
 DFI double vget(v3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
 DFI void vsetc(v3& v, int i, double x) { if (i == 0) v.x = x; else if (i == 1) v.y = x; else v.z = x; }
 
-DF void nc_box_box(const XF& TA, const Collider& A, const XF& TB, const Collider& B, double thr, CandList& out) {
+DF void nc_box_box(const XF& TA, const Collider& A, const XF& TB, const Collider& B, double thr, CandList& out,
+                   LBoxScratch& S) {
     (void)thr;
     const double fudge = 1.05;
     const m3& R1 = TA.R;
@@ -693,7 +697,7 @@ DF void nc_box_box(const XF& TA, const Collider& A, const XF& TB, const Collider
     if (codeN == 0) { code1 = 1; code2 = 2; }
     else if (codeN == 1) { code1 = 0; code2 = 2; }
     else { code1 = 0; code2 = 1; }
-    double quad[8];
+    ldouble* quad = S.quad;
     double c1 = col_dotv(*Ra, code1, center), c2 = col_dotv(*Ra, code2, center);
     double m11 = col_dot(*Ra, code1, *Rb, a1), m12 = col_dot(*Ra, code1, *Rb, a2);
     double m21 = col_dot(*Ra, code2, *Rb, a1), m22 = col_dot(*Ra, code2, *Rb, a2);
@@ -705,11 +709,11 @@ DF void nc_box_box(const XF& TA, const Collider& A, const XF& TB, const Collider
         quad[6] = c1 + k1 - k3; quad[7] = c2 + k2 - k4;
     }
     double rect[2] = {Sa[code1], Sa[code2]};
-    double ret[16];
-    int n = intersect_rect_quad(rect, quad, ret);
+    ldouble* ret = S.ret;
+    int n = intersect_rect_quad(rect, quad, ret, S.buffer);
     if (n < 1) return;
-    v3 point[8];
-    double dep[8];
+    ldouble* pt = S.pt;
+    ldouble* dep = S.dep;
     double det1 = 1.0 / (m11 * m22 - m12 * m21);
     m11 *= det1; m12 *= det1; m21 *= det1; m22 *= det1;
     int cnum = 0;
@@ -718,8 +722,9 @@ DF void nc_box_box(const XF& TA, const Collider& A, const XF& TB, const Collider
     for (int j = 0; j < n; j++) {
         double k1 = m22 * (ret[j * 2] - c1) - m12 * (ret[j * 2 + 1] - c2);
         double k2 = -m21 * (ret[j * 2] - c1) + m11 * (ret[j * 2 + 1] - c2);
-        point[cnum] = vadd(vadd(center, vscale(rba1, k1)), vscale(rba2, k2));
-        dep[cnum] = Sa[codeN] - vdot(normal2, point[cnum]);
+        const v3 pc = vadd(vadd(center, vscale(rba1, k1)), vscale(rba2, k2));
+        pt[3 * cnum] = pc.x; pt[3 * cnum + 1] = pc.y; pt[3 * cnum + 2] = pc.z;
+        dep[cnum] = Sa[codeN] - vdot(normal2, pc);
         if (dep[cnum] >= 0) {
             ret[cnum * 2] = ret[j * 2];
             ret[cnum * 2 + 1] = ret[j * 2 + 1];
@@ -731,7 +736,7 @@ DF void nc_box_box(const XF& TA, const Collider& A, const XF& TB, const Collider
     if (maxc > cnum) maxc = cnum;
     if (cnum <= maxc) {
         for (int j = 0; j < cnum; j++) {
-            v3 pw = vadd(point[j], pa);
+            v3 pw = vadd(V(pt[3 * j], pt[3 * j + 1], pt[3 * j + 2]), pa);
             if (code >= 4) pw = vsub(pw, vscale(normal, dep[j]));
             cand_add(out, vneg(normal), pw, -dep[j]);
         }
@@ -740,12 +745,13 @@ DF void nc_box_box(const XF& TA, const Collider& A, const XF& TB, const Collider
         double maxdepth = dep[0];
         for (int i = 1; i < cnum; i++)
             if (dep[i] > maxdepth) { maxdepth = dep[i]; i1 = i; }
-        int iret[8];
-        cull_points(cnum, ret, maxc, i1, iret);
+        lint* iret = S.iret;
+        cull_points(cnum, ret, maxc, i1, iret, S.ang, S.avail);
         for (int j = 0; j < maxc; j++) {
-            v3 pw = vadd(point[iret[j]], pa);
-            if (code >= 4) pw = vsub(pw, vscale(normal, dep[iret[j]]));
-            cand_add(out, vneg(normal), pw, -dep[iret[j]]);
+            const int ij = iret[j];
+            v3 pw = vadd(V(pt[3 * ij], pt[3 * ij + 1], pt[3 * ij + 2]), pa);
+            if (code >= 4) pw = vsub(pw, vscale(normal, dep[ij]));
+            cand_add(out, vneg(normal), pw, -dep[ij]);
         }
     }
 }

@@ -53,6 +53,7 @@ static_assert(NV <= NVP, "dof slots exceed the padded row");
 #endif
 
 #define MAXOV 26 /* pairs per lane-per-pair pass: their working manifolds share LDS with the rows (Shared::pm) */
+#define NBOXSLOT 5 /* box-box pairs run per round, one LDS clip-buffer slot each (they share the hull candidates' LDS) */
 
 /* ---------------- env state (canonical layout) ---------------- */
 struct StObj { v3 pos; q4 quat; v3 v, w; };
@@ -107,7 +108,10 @@ struct Shared {
         double impx[MAXROWS]; /* PGS: row impulses gathered through LDS (after the Delassus build) */
         DynWork dyn;          /* serial_pre: robot_dynamics work arrays */
     } u;
-    Cand hc[64];
+    union {
+        Cand hc[64];              /* hull narrowphase candidates */
+        BoxScratch bs[NBOXSLOT];  /* lane-per-pair box-box clip buffers (after the hull pairs of the pass) */
+    };
     double a12[NB];
     double fs[8];
     int is[8];
@@ -553,17 +557,18 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         __builtin_amdgcn_wave_barrier();
         PROF_ADD(PF_PR_LOOK, t_pl);
         int has = 0;
+        int isbb = 0; /* box-box pairs run below in rounds of NBOXSLOT lanes, each with an LDS clip-buffer slot */
         if (lane < cn) {
             int p = sh.ov[c0 + lane];
             const PairDef& P = s->pair[p];
             const Collider& A = s->col[P.a];
             const Collider& B = s->col[P.b];
-            LManifold& M = *(LManifold*)&sh.pm[lane];
             PROF_T0(t_pn);
             XF TA = shape_xf(sh.O[P.a], A), TB = shape_xf(sh.O[P.b], B);
             CandList L;
             L.n = 0;
             L.c = (LCand*)&sh.u.cand.c[lane][0];
+            isbb = A.kind == UG_SHAPE_BOX && B.kind == UG_SHAPE_BOX;
             if (A.kind == UG_SHAPE_HULL && (B.kind == UG_SHAPE_BOX || B.kind == UG_SHAPE_HULL)) {
                 L.n = sh.u.cand.n[lane]; /* team_hull_box / team_hull_hull wrote them */
             } else if (A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_HULL) {
@@ -575,7 +580,6 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
                 }
             } else if (A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_BOX) nc_sphere_box(TA, A, TB, B, P.thr, L);
             else if (A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_SPHERE) nc_sphere_sphere(TA, A, TB, B, P.thr, L);
-            else if (A.kind == UG_SHAPE_BOX && B.kind == UG_SHAPE_BOX) nc_box_box(TA, A, TB, B, P.thr, L);
             else if (A.kind == UG_SHAPE_HULL && B.kind == UG_SHAPE_SPHERE) nc_hull_sphere(TA, A, TB, B, P.thr, L);
             else if (A.kind == UG_SHAPE_BOX && B.kind == UG_SHAPE_SPHERE) {
                 nc_sphere_box(TB, B, TA, A, P.thr, L);
@@ -585,7 +589,34 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
                     stv(L.c[i].pB, vadd(cp, vscale(cn, L.c[i].d)));
                 }
             }
+            sh.u.cand.n[lane] = L.n;
             PROF_ADD(PF_PR_NP, t_pn);
+        }
+        PROF_T0(t_bb);
+        for (unsigned long long bbm = ballot(isbb); bbm != 0ull;) {
+            unsigned long long round = 0ull, rest = bbm;
+            for (int t = 0; t < NBOXSLOT && rest != 0ull; t++) { round |= rest & (0ull - rest); rest &= rest - 1ull; }
+            if ((round >> lane) & 1ull) {
+                const int slot = __popcll(round & ((1ull << lane) - 1ull));
+                const PairDef& P = s->pair[sh.ov[c0 + lane]];
+                const Collider& A = s->col[P.a];
+                const Collider& B = s->col[P.b];
+                const XF TA = shape_xf(sh.O[P.a], A), TB = shape_xf(sh.O[P.b], B);
+                CandList L;
+                L.n = 0;
+                L.c = (LCand*)&sh.u.cand.c[lane][0];
+                nc_box_box(TA, A, TB, B, P.thr, L, *(LBoxScratch*)&sh.bs[slot]);
+                sh.u.cand.n[lane] = L.n;
+            }
+            bbm = rest;
+        }
+        PROF_ADD(PF_PR_NP, t_bb);
+        if (lane < cn) {
+            const PairDef& P = s->pair[sh.ov[c0 + lane]];
+            LManifold& M = *(LManifold*)&sh.pm[lane];
+            CandList L;
+            L.n = sh.u.cand.n[lane];
+            L.c = (LCand*)&sh.u.cand.c[lane][0];
             PROF_T0(t_pm);
             for (int i = 0; i < L.n; i++) {
                 Cand c;
