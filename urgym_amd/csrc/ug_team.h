@@ -106,6 +106,7 @@ struct Shared {
         double mcol[NB + 5][NB]; /* row build: M^-1 e_d (d < NB) and M^-1 (ratio_g e_child_g) of gear g */
         struct { Cand c[MAXOV][4]; int n[MAXOV]; } cand;
         double impx[MAXROWS]; /* PGS: row impulses gathered through LDS (after the Delassus build) */
+        m3 rj[NB];            /* FK: each body's joint rotation (axis_angle), shared for the ancestor walks */
         DynWork dyn;          /* serial_pre: robot_dynamics work arrays */
     } u;
     union {
@@ -1734,37 +1735,45 @@ __device__ __noinline__ static void serial_post(const Scene* s, int split) {
         }
     }
 }
-/* fk() wave-parallel: lane b < NB forms its joint rotation, then the tree is composed one level at a
- * time (same operations as fk(), parent frames read from LDS) */
+/* fk() wave-parallel: lane b < NB forms its joint rotation, then composes its own root-to-body chain
+ * (same operations and order as fk() along that path) */
 __device__ __noinline__ static void serial_fk() {
     Kin& k = g_sh.kin;
     const int lane = threadIdx.x;
     const bool own = lane < NB;
     const int b = own ? lane : 0;
-    const int pb = UG_BODY_PARENT[b];
-    const m3 Rpb = mload(&UG_BODY_R[9 * b]);
-    const v3 Ppb = V(UG_BODY_P[3 * b], UG_BODY_P[3 * b + 1], UG_BODY_P[3 * b + 2]);
-    const v3 ax = V(UG_BODY_AXIS[3 * b], UG_BODY_AXIS[3 * b + 1], UG_BODY_AXIS[3 * b + 2]);
-    const v3 com = V(UG_BODY_COM[3 * b], UG_BODY_COM[3 * b + 1], UG_BODY_COM[3 * b + 2]);
-    const m3 Rj = axis_angle(ax, g_sh.e.q[b]);
-    const int depth = own ? g_sh.bdepth[b] : -1; /* body_depth(b), cached in LDS */
-    for (int L = 0; L < NB; L++) {
-        if (depth == L) {
-            m3 Rp;
-            v3 pp;
-            if (pb < 0) { Rp = mident(); pp = V(0, 0, 0); }
-            else { Rp = k.R[pb]; pp = k.p[pb]; }
-            const m3 Rtmp = mm(Rp, Rpb);
-            const m3 R = mm(Rtmp, Rj);
-            const v3 p = vadd(pp, mv(Rp, Ppb));
-            k.R[b] = R;
-            k.p[b] = p;
-            k.a[b] = mv(Rtmp, ax);
-            k.c[b] = vadd(p, mv(R, com));
-        }
-        __syncthreads();
-        if (ballot(depth > L) == 0ull) break;
+    /* each body's joint rotation once (lane per body), shared through LDS; then every lane walks its own
+     * root-to-body path (ancestor indices ascend with depth) with fk()'s operations, no barrier per level */
+    if (own) {
+        const v3 ax = V(UG_BODY_AXIS[3 * b], UG_BODY_AXIS[3 * b + 1], UG_BODY_AXIS[3 * b + 2]);
+        g_sh.u.rj[b] = axis_angle(ax, g_sh.e.q[b]);
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    if (own) {
+        const int am = g_sh.anc[b];
+        m3 Rp = mident();
+        v3 pp = V(0, 0, 0);
+        m3 Rtmp = Rp;
+#pragma unroll
+        for (int j = 0; j < NB; j++) {
+            if ((am >> j) & 1) {
+                const m3 Rpb = mload(&UG_BODY_R[9 * j]);
+                const v3 Ppb = V(UG_BODY_P[3 * j], UG_BODY_P[3 * j + 1], UG_BODY_P[3 * j + 2]);
+                Rtmp = mm(Rp, Rpb);
+                const m3 R = mm(Rtmp, g_sh.u.rj[j]);
+                pp = vadd(pp, mv(Rp, Ppb));
+                Rp = R;
+            }
+        }
+        const v3 ax = V(UG_BODY_AXIS[3 * b], UG_BODY_AXIS[3 * b + 1], UG_BODY_AXIS[3 * b + 2]);
+        const v3 com = V(UG_BODY_COM[3 * b], UG_BODY_COM[3 * b + 1], UG_BODY_COM[3 * b + 2]);
+        k.R[b] = Rp;
+        k.p[b] = pp;
+        k.a[b] = mv(Rtmp, ax);
+        k.c[b] = vadd(pp, mv(Rp, com));
+    }
+    __syncthreads();
 }
 
 #ifdef UG_DEBUG_DUMP
