@@ -1687,6 +1687,10 @@ static int pgs(rowset* rs, double* dv, double* dvs) {
         for (int k = 0; k < n; k++) s = fma(R[k]->MiJ[d], R[k]->imp, s);
         dv[d] = s;
     }
+#ifdef UG_ROWHIST /* development aid (tools/row_hist.py): the row layout and sweep count of every solve */
+    extern int dprintf(int, const char*, ...);
+    dprintf(2, "ROWS %d %d %d %d %d %d\n", n, nnc, rs->nn, rs->nf, rs->nr, g_dbg[5]);
+#endif
     /* split-impulse pass for deep penetrations (rhsPenetration rows, normals only, from zero) */
     int any = 0;
     for (int p = nnc; p < fb; p++)

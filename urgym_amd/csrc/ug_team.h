@@ -33,7 +33,7 @@
 namespace ugd {
 
 #define TEAM 64
-#define UG_NPROF 48 /* phase accumulators of the -DUG_PROF build */
+#define UG_NPROF 56 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* a row's J and M^-1 J^T over the NVP = 32 dof slots (robot 12, objects 3 x 6, 2 zero pads) */
@@ -151,7 +151,8 @@ __device__ unsigned long long g_prof[UG_NPROF];
 enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_TOTAL,
        PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN, PF_SWEEPS, PF_HULL,
        PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE, PF_FK, PF_LDL, PF_UNIT, PF_ROWB, PF_RB1, PF_RB2, PF_RB3, PF_MFMA, PF_WARM, PF_SW_NC, PF_SW_CT, PF_SW_FIN, PF_SW_FPREP, PF_SW_FR,
-       PF_SW_RES, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST, PC_CHUNKS, PC_NNC, PC_NN, PC_N64, PC_N80, PC_N96 };
+       PF_SW_RES, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST, PC_CHUNKS, PC_NNC, PC_NN, PC_N64, PC_N80, PC_N96,
+       PC_FREE, PF_FREE_COL, PF_FREE_DYN, PF_FREE_ROWS, PF_FREE_PGS, PF_FREE_INT };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -2058,6 +2059,16 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     serial_post(s, split);
     __syncthreads();
     PROF_ADD(PF_INTEG, t_int);
+#ifdef UG_PROF
+    if (n == 12 && nnc == 12) { /* contact-free substeps (most of a reset's settling) on their own */
+        PROF_CNT(PC_FREE, 1);
+        PROF_CNT(PF_FREE_COL, t_dyn - t_col);
+        PROF_CNT(PF_FREE_DYN, t_rows - t_dyn);
+        PROF_CNT(PF_FREE_ROWS, t_pgs - t_rows);
+        PROF_CNT(PF_FREE_PGS, t_int - t_pgs);
+        PROF_ADD(PF_FREE_INT, t_int);
+    }
+#endif
 }
 
 /* ---------------- robot control + BallBalance glue (lane 0 unless noted) ---------------- */
