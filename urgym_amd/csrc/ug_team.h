@@ -1345,12 +1345,12 @@ __device__ __forceinline__ void sweep_section(const double (&A0)[PREG], const do
     for (int s = 0; s < (TWO ? 2 : 1); s++) L.dsv[s] = in[s] ? F.dsv[s] : L.dsv[s];
 }
 /* rows P0, P0 + STEP, ... (NR of them) straight, no chunk tests and no neutral rows (the contact-free solve) */
-template <int P, int STEP, int K>
+template <int P, int STEP, int K, bool TWO = false>
 __device__ __forceinline__ void straight_rows(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA,
                                               int lane, Lrow& L, double (&W)[2]) {
     if constexpr (K > 0) {
-        row_upd<P, false>(A0, A1, wsA, lane, L, W);
-        straight_rows<P + STEP, STEP, K - 1>(A0, A1, wsA, lane, L, W);
+        row_upd<P, TWO>(A0, A1, wsA, lane, L, W);
+        straight_rows<P + STEP, STEP, K - 1, TWO>(A0, A1, wsA, lane, L, W);
     }
 }
 /* warm start: normal rows [nnc, fb) with a carried impulse, w += A[:, P] * impulse */
@@ -1393,21 +1393,41 @@ __device__ __forceinline__ void swap16_d(double& x, double& y) {
     x = __hiloint2double(h[0], l[0]);
     y = __hiloint2double(h[1], l[1]);
 }
+/* solve position -> row index.  The general layout is the identity over [0, n).  The fixed layout (team_pgs
+ * passes_fl) keeps the non-contact and normal rows at [0, fb) and moves the friction rows to [FL_F0, FL_F0 + n - fb),
+ * so that every section starts at a compile-time position; the positions in between are pads (-1: zero J, zero
+ * bounds, so a zero column and a neutral row). */
+#define FL_NNC 12 /* non-contact rows of the fixed layout (7 motors + 5 gears) */
+#define FL_F0 40  /* first friction position: normals at [12, 40) (at most 28) */
+#define FL_NF 56  /* friction positions [40, 96): at most 56 rows */
+struct PosMap {
+    int n, fb, fl;
+    __device__ __forceinline__ int q(int p) const {
+        if (!fl) return p < n ? p : -1;
+        if (p < fb) return p;
+        if (p < FL_F0) return -1;
+        const int r = fb + (p - FL_F0);
+        return r < n ? r : -1;
+    }
+    /* positions the Delassus build covers: the fixed layout's straight sweeps read every column up to 96,
+     * so all of them are built (pad columns zero) */
+    __device__ __forceinline__ int npos() const { return fl ? FL_F0 + FL_NF : n; }
+};
 /* the slot's row operands (J of rows 64 S + 16 g + (lane & 15), dof slots 4 ks + (lane >> 4)) are the same
  * for every column block: loaded once per slot into B; each block then loads only its 6 column operands */
 template <int PB>
-__device__ __forceinline__ void mfma_cols(gcdouble* rows, int n, int lane, double (&a)[KS]) {
-    const int p = 16 * PB + (lane & 15);
+__device__ __forceinline__ void mfma_cols(gcdouble* rows, const PosMap& pm, int lane, double (&a)[KS]) {
+    const int q = pm.q(16 * PB + (lane & 15));
 #pragma unroll
-    for (int ks = 0; ks < KS; ks++) a[ks] = p < n ? rows[p * RS + RJ + 4 * ks + (lane >> 4)] : 0.0;
+    for (int ks = 0; ks < KS; ks++) a[ks] = q >= 0 ? rows[q * RS + RJ + 4 * ks + (lane >> 4)] : 0.0;
 }
 template <int PB, int S>
 __device__ __forceinline__ void mfma_block(gcdouble* rows, const double (&B)[KS][4], const double (&a)[KS], double invDr,
-                                           double (&A)[PREG], gdouble* wsA, int n, int lane) {
+                                           double (&A)[PREG], gdouble* wsA, const PosMap& pm, int n, int lane) {
     if constexpr (16 * PB < MAXROWS) {
         if (16 * PB < n) {
             double an[KS]; /* the next block's column operands, in flight during this block */
-            if (16 * PB + 16 < n) mfma_cols<PB + 1>(rows, n, lane, an);
+            if (16 * PB + 16 < n) mfma_cols<PB + 1>(rows, pm, lane, an);
             d4v acc[4];
 #pragma unroll
             for (int g = 0; g < 4; g++) acc[g] = d4v{0.0, 0.0, 0.0, 0.0};
@@ -1432,24 +1452,25 @@ __device__ __forceinline__ void mfma_block(gcdouble* rows, const double (&B)[KS]
                     else wsA[(P - PREG) * MAXROWS + 64 * S + lane] = x;
                 }
             }
-            mfma_block<PB + 1, S>(rows, B, an, invDr, A, wsA, n, lane);
+            mfma_block<PB + 1, S>(rows, B, an, invDr, A, wsA, pm, n, lane);
         }
     }
 }
 template <int S>
-__device__ __forceinline__ void mfma_slot(gcdouble* rows, double invDr, double (&A)[PREG], gdouble* wsA, int n,
-                                          int lane) {
+__device__ __forceinline__ void mfma_slot(gcdouble* rows, double invDr, double (&A)[PREG], gdouble* wsA,
+                                          const PosMap& pm, int lane) {
+    const int n = pm.npos();
     double B[KS][4];
 #pragma unroll
     for (int ks = 0; ks < KS; ks++)
 #pragma unroll
         for (int g = 0; g < 4; g++) {
-            const int i = 64 * S + 16 * g + (lane & 15);
-            B[ks][g] = i < n ? rows[i * RS + 4 * ks + (lane >> 4)] : 0.0;
+            const int q = pm.q(64 * S + 16 * g + (lane & 15));
+            B[ks][g] = q >= 0 ? rows[q * RS + 4 * ks + (lane >> 4)] : 0.0;
         }
     double a[KS];
-    mfma_cols<0>(rows, n, lane, a);
-    mfma_block<0, S>(rows, B, a, invDr, A, wsA, n, lane);
+    mfma_cols<0>(rows, pm, lane, a);
+    mfma_block<0, S>(rows, B, a, invDr, A, wsA, pm, n, lane);
 }
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
 template <typename T>
@@ -1805,9 +1826,21 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     double A0[PREG], A1[PREG];
     /* scaled Delassus rows on the matrix cores (mfma_block); slot 1 only when rows >= 64 exist */
     PROF_T0(t_mf);
-    mfma_slot<0>(rows, lane < n ? sh.rs[lane].invD : 0.0, A0, wsA, n, lane);
-    if (n > 64) {
-        mfma_slot<1>(rows, lane + 64 < n ? sh.rs[lane + 64].invD : 0.0, A1, wsA, n, lane);
+    /* the fixed layout: 12 non-contact rows, 16..28 normals, at most 56 friction rows (BallBalance's contact
+     * solves, in steps and in resets) */
+#ifdef UG_DEBUG_DUMP
+    const PosMap pm{n, fb, 0};
+#else
+    const PosMap pm{n, fb, nnc == FL_NNC && nn >= 16 && fb <= FL_F0 && n - fb <= FL_NF};
+#endif
+    const int npos = pm.npos();
+    {
+        const int q0 = pm.q(lane);
+        mfma_slot<0>(rows, q0 >= 0 ? sh.rs[q0].invD : 0.0, A0, wsA, pm, lane);
+    }
+    if (npos > 64) {
+        const int q1 = pm.q(lane + 64);
+        mfma_slot<1>(rows, q1 >= 0 ? sh.rs[q1].invD : 0.0, A1, wsA, pm, lane);
     } else {
 #pragma unroll
         for (int j = 0; j < PREG; j++) A1[j] = 0.0;
@@ -1821,9 +1854,9 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     int nrow[2];
 #pragma unroll
     for (int s = 0; s < 2; s++) {
-        const int p = lane + 64 * s;
-        const bool in = p < n;
-        const RowS& r = sh.rs[in ? p : 0];
+        const int q = pm.q(lane + 64 * s);
+        const bool in = q >= 0;
+        const RowS& r = sh.rs[in ? q : 0];
         L.rhs[s] = in ? r.rhs : 0.0;
         L.invD[s] = in ? r.invD : 0.0;
         L.rinv[s] = in ? r.rinv : 0.0;
@@ -1974,7 +2007,86 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         if (lane < 12) g_sh.rs[lane].imp = L.imp[0];
         return 0;
     };
-    const int split = (n == 12 && nnc == 12) ? passes_free12()
+    /* the fixed layout's sweeps as straight row sequences (no chunk tests, no section copies): even sweeps the
+     * non-contact rows reversed then the normal positions [12, 40), odd sweeps [0, 40) forward; then the friction
+     * positions [40, 96).  Pads are neutral (zero bounds and column); only the section's own rows finish. */
+    auto passes_fl = [&]() -> int {
+        const int nf = n - fb;
+        int split = 0;
+        PROF_T0(t_sw);
+#pragma nounroll
+        for (int pass = 0; pass < 2; pass++) {
+            const int pen = pass;
+            if (pen) {
+                int anypen = 0;
+#pragma unroll
+                for (int s = 0; s < 2; s++) {
+                    const int p = lane + 64 * s;
+                    anypen |= p >= nnc && p < fb && rhsPen[s] != 0.0;
+                }
+                split = ballot(anypen) != 0ull;
+                if (!split) break;
+#pragma unroll
+                for (int s = 0; s < 2; s++) {
+                    L.rhs[s] = rhsPen[s];
+                    L.imp[s] = 0.0;
+                }
+                W[0] = L.rhs[0];
+                W[1] = L.rhs[1];
+            }
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                L.dlo[s] = L.lo[s] - L.imp[s];
+                L.dhi[s] = L.hi[s] - L.imp[s];
+            }
+            for (int it = 0; it < UG_PGS_ITERS; it++) {
+                double res = 0.0;
+                gcdouble* o_wsA = wsAr;
+                asm volatile("" : "+s"(o_wsA));
+                if (pen || !(it & 1)) {
+                    if (!pen) straight_rows<FL_NNC - 1, -1, FL_NNC, true>(A0, A1, o_wsA, lane, L, W);
+                    straight_rows<FL_NNC, 1, FL_F0 - FL_NNC, true>(A0, A1, o_wsA, lane, L, W);
+                } else {
+                    straight_rows<0, 1, FL_F0, true>(A0, A1, o_wsA, lane, L, W);
+                }
+                row_finish<false>(L, pos_mask(0, pen ? nnc : 0, fb, 0ull), 0ull, lane, res);
+                if (!pen && nf > 0) {
+                    g_sh.u.impx[lane] = L.imp[0];
+                    __builtin_amdgcn_wave_barrier();
+                    unsigned long long sk[2];
+#pragma unroll
+                    for (int s = 0; s < 2; s++) {
+                        const int p = lane + 64 * s;
+                        const bool isf = p >= FL_F0 && p < FL_F0 + nf;
+                        const double tot = g_sh.u.impx[isf ? nrow[s] : 0];
+                        const bool skip = isf && !(tot > 0.0);
+                        L.lo[s] = isf ? -(fric[s] * tot) : L.lo[s];
+                        L.hi[s] = isf ? fric[s] * tot : L.hi[s];
+                        L.dlo[s] = skip ? 0.0 : L.lo[s] - L.imp[s];
+                        L.dhi[s] = skip ? 0.0 : L.hi[s] - L.imp[s];
+                        sk[s] = ballot(skip);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    straight_rows<FL_F0, 1, FL_NF, true>(A0, A1, o_wsA, lane, L, W);
+                    row_finish<true>(L, pos_mask(0, FL_F0, FL_F0 + nf, sk[0]), pos_mask(1, FL_F0, FL_F0 + nf, sk[1]),
+                                     lane, res);
+                }
+                PROF_CNT(PC_ITERS, 1);
+                if (ballot(!(res <= UG_RESIDUAL_THR)) == 0ull || it >= UG_PGS_ITERS - 1) break;
+            }
+            if (!pen) {
+                PROF_ADD(PF_SWEEPS, t_sw);
+#pragma unroll
+                for (int s = 0; s < 2; s++) {
+                    const int q = pm.q(lane + 64 * s);
+                    if (q >= 0) g_sh.rs[q].imp = L.imp[s];
+                }
+            }
+        }
+        return split;
+    };
+    const int split = pm.fl                 ? passes_fl()
+                      : (n == 12 && nnc == 12) ? passes_free12()
                       : n > 96             ? passes(std::integral_constant<int, 128>{})
                       : n > 64             ? passes(std::integral_constant<int, 96>{})
                       : n > 32             ? passes(std::integral_constant<int, 64>{})
