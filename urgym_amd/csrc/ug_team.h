@@ -1261,7 +1261,14 @@ __device__ __forceinline__ double writelane_d(double old, double x) {
  * forms the clamped increment of its own row, lane (P & 63)'s is broadcast, applied to w and recorded in
  * that lane (the impulse itself is advanced after the section).  W holds each row's unclamped increment
  * u = rhs - (J dv) / D and A0 / A1 the negated, 1/D-scaled Delassus rows.  Chain: max, min, readlane, fma. */
-template <int P, bool TWO>
+/* lane L of the result := x (that lane's own value), other lanes keep old: a row's record by a select on a
+ * constant lane mask (inverse ballot), since lane L's own clamped value is the broadcast one -- cheaper than
+ * v_writelane of the broadcast value where the masks stay in SGPRs (tools/micro/pgs3.hip) */
+template <int L>
+__device__ __forceinline__ double own_lane_sel(double old, double x) {
+    return __builtin_amdgcn_inverse_ballot_w64(1ull << L) ? x : old;
+}
+template <int P, bool TWO, bool SEL = false>
 __device__ __forceinline__ void row_upd(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA, int lane,
                                         Lrow& L, double (&W)[2]) {
     constexpr int s = P >> 6, O = P & 63;
@@ -1271,7 +1278,8 @@ __device__ __forceinline__ void row_upd(const double (&A0)[PREG], const double (
     double d = readlane_d(dn, O);
     W[0] = __builtin_fma(a0, d, W[0]);
     if (TWO) W[1] = __builtin_fma(a1, d, W[1]); /* slot 1 exists only with more than 64 rows */
-    L.dsv[s] = writelane_d<O>(L.dsv[s], d);
+    if constexpr (SEL) L.dsv[s] = own_lane_sel<O>(L.dsv[s], dn);
+    else L.dsv[s] = writelane_d<O>(L.dsv[s], d);
 }
 /* after a section: the lanes whose row was solved advance their impulse by the recorded increment and
  * fold (delta / D)^2 into their residual */
@@ -1345,12 +1353,12 @@ __device__ __forceinline__ void sweep_section(const double (&A0)[PREG], const do
     for (int s = 0; s < (TWO ? 2 : 1); s++) L.dsv[s] = in[s] ? F.dsv[s] : L.dsv[s];
 }
 /* rows P0, P0 + STEP, ... (NR of them) straight, no chunk tests and no neutral rows (the contact-free solve) */
-template <int P, int STEP, int K, bool TWO = false>
+template <int P, int STEP, int K, bool TWO = false, bool SEL = false>
 __device__ __forceinline__ void straight_rows(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA,
                                               int lane, Lrow& L, double (&W)[2]) {
     if constexpr (K > 0) {
-        row_upd<P, TWO>(A0, A1, wsA, lane, L, W);
-        straight_rows<P + STEP, STEP, K - 1, TWO>(A0, A1, wsA, lane, L, W);
+        row_upd<P, TWO, SEL>(A0, A1, wsA, lane, L, W);
+        straight_rows<P + STEP, STEP, K - 1, TWO, SEL>(A0, A1, wsA, lane, L, W);
     }
 }
 /* warm start: normal rows [nnc, fb) with a carried impulse, w += A[:, P] * impulse */
@@ -1997,8 +2005,9 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
             double res = 0.0;
             gcdouble* o_wsA = wsAr;
             asm volatile("" : "+s"(o_wsA));
-            if (!(it & 1)) straight_rows<11, -1, 12>(A0, A1, o_wsA, lane, L, W);
-            else straight_rows<0, 1, 12>(A0, A1, o_wsA, lane, L, W);
+            /* 12 lane masks stay in SGPRs: the records by lane select (the fixed layout's 64 would spill) */
+            if (!(it & 1)) straight_rows<11, -1, 12, false, true>(A0, A1, o_wsA, lane, L, W);
+            else straight_rows<0, 1, 12, false, true>(A0, A1, o_wsA, lane, L, W);
             row_finish<false>(L, pos_mask(0, 0, 12, 0ull), 0ull, lane, res);
             PROF_CNT(PC_ITERS, 1);
             if (ballot(!(res <= UG_RESIDUAL_THR)) == 0ull || it >= UG_PGS_ITERS - 1) break;
