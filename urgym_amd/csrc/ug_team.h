@@ -33,7 +33,7 @@
 namespace ugd {
 
 #define TEAM 64
-#define UG_NPROF 56 /* phase accumulators of the -DUG_PROF build */
+#define UG_NPROF 60 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* a row's J and M^-1 J^T over the NVP = 32 dof slots (robot 12, objects 3 x 6, 2 zero pads) */
@@ -152,7 +152,8 @@ enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_
        PC_SUBSTEPS = 8, PC_ROWS, PC_ITERS, PC_OVL, PC_HULL, PC_NMAN, PF_SWEEPS, PF_HULL,
        PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE, PF_FK, PF_LDL, PF_UNIT, PF_ROWB, PF_RB1, PF_RB2, PF_RB3, PF_MFMA, PF_WARM, PF_SW_NC, PF_SW_CT, PF_SW_FIN, PF_SW_FPREP, PF_SW_FR,
        PF_SW_RES, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST, PC_CHUNKS, PC_NNC, PC_NN, PC_N64, PC_N80, PC_N96,
-       PC_FREE, PF_FREE_COL, PF_FREE_DYN, PF_FREE_ROWS, PF_FREE_PGS, PF_FREE_INT };
+       PC_FREE, PF_FREE_COL, PF_FREE_DYN, PF_FREE_ROWS, PF_FREE_PGS, PF_FREE_INT,
+       PF_FREE_PSETUP, PF_FREE_PSWEEP, PF_FREE_PPOST };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -1821,6 +1822,49 @@ __device__ __forceinline__ void dump_A(const double (&A0)[PREG], const double (&
 /* PGS: Delassus rows, warm start (normals), sweeps (residual early-out), the split-impulse pass; returns
  * whether the split pass ran (dvs valid).  Impulses are written back to sh.rs[].imp.  Its own function:
  * the 2 x PREG register rows of A get a register allocation of their own. */
+/* a[i] of a small constant table by an unrolled select (immediates, no constant-memory load) */
+template <typename T, int N>
+__device__ __forceinline__ T csel(const T (&a)[N], int i) {
+    T v = a[0];
+#pragma unroll
+    for (int g = 1; g < N; g++) v = i == g ? a[g] : v;
+    return v;
+}
+/* the scaled Delassus rows of a motor / gear solve (n = nnc = 12): A[i][P] = the k-ordered fma chain of J_i . M^-1 J_P^T
+ * over the dof slots (what the matrix cores compute, mfma_block), with J_i's one or two non-zero entries
+ * (motor: 1 at its dof; gear: 1 at the finger dof, the ratio at the child dof) -- the zero terms of the chain
+ * leave it unchanged -- then scaled -(A / D_i).  Branch-free, every LDS read independent. */
+__device__ __forceinline__ void nc_direct_A(double (&A0)[PREG], int lane) {
+    const int i = lane < 12 ? lane : 0;
+    const RowS& r = g_sh.rs[i];
+    const bool gear = r.kind == 2;
+    const int ra = r.a;
+    const int k1 = gear ? UG_FINGER_DOF : (ra < 6 ? ra : UG_FINGER_DOF);
+    const int k2 = gear ? csel(UG_GEAR_CHILD, ra) : k1;
+    const double j2 = gear ? csel(UG_GEAR_RATIO, ra) : 0.0;
+    const double invD = lane < 12 ? r.invD : 0.0;
+    int kP[12], aP[12];
+#pragma unroll
+    for (int P = 0; P < 12; P++) {
+        kP[P] = __builtin_amdgcn_readfirstlane(g_sh.rs[P].kind);
+        aP[P] = __builtin_amdgcn_readfirstlane(g_sh.rs[P].a);
+    }
+#pragma unroll
+    for (int P = 0; P < PREG; P++) {
+        if (P < 12) {
+            const bool gP = kP[P] == 2;
+            const int r1 = gP ? UG_FINGER_DOF : (aP[P] < 6 ? aP[P] : UG_FINGER_DOF);
+            const int r2 = gP ? NB + aP[P] : r1;
+            const double x11 = g_sh.u.mcol[r1][k1], x21 = g_sh.u.mcol[r2][k1];
+            const double x12 = g_sh.u.mcol[r1][k2], x22 = g_sh.u.mcol[r2][k2];
+            const double m1 = gP ? x11 + x21 : x11, m2 = gP ? x12 + x22 : x12;
+            const double c1 = __builtin_fma(1.0, m1, 0.0), c2 = __builtin_fma(j2, m2, 0.0);
+            const double raw = !gear ? c1 : (k1 < k2 ? __builtin_fma(j2, m2, c1) : __builtin_fma(1.0, m1, c2));
+            const double x = -(raw * invD);
+            A0[P] = lane < 12 ? x : 0.0;
+        }
+    }
+}
 __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int nn_, double& dv, double& dvs) {
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
@@ -1842,16 +1886,25 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     const PosMap pm{n, fb, nnc == FL_NNC && nn >= 16 && fb <= FL_F0 && n - fb <= FL_NF};
 #endif
     const int npos = pm.npos();
-    {
+    /* the contact-free solve of 7 motor + 5 gear rows: its Delassus rows straight from the shared unit solves
+     * in LDS (team_unit_solves), no workspace round trip */
+#ifdef UG_DEBUG_DUMP
+    const bool direct = false; /* the dump reads every column */
+#else
+    const bool direct = n == 12 && nnc == 12 && ballot(lane < 12 && sh.rs[lane].kind == 0) == 0ull;
+#endif
+    if (direct) {
+        nc_direct_A(A0, lane); /* columns 0..11 only: the 12-row sweeps read nothing else of A0 / A1 */
+    } else {
         const int q0 = pm.q(lane);
         mfma_slot<0>(rows, q0 >= 0 ? sh.rs[q0].invD : 0.0, A0, wsA, pm, lane);
-    }
-    if (npos > 64) {
-        const int q1 = pm.q(lane + 64);
-        mfma_slot<1>(rows, q1 >= 0 ? sh.rs[q1].invD : 0.0, A1, wsA, pm, lane);
-    } else {
+        if (npos > 64) {
+            const int q1 = pm.q(lane + 64);
+            mfma_slot<1>(rows, q1 >= 0 ? sh.rs[q1].invD : 0.0, A1, wsA, pm, lane);
+        } else {
 #pragma unroll
-        for (int j = 0; j < PREG; j++) A1[j] = 0.0;
+            for (int j = 0; j < PREG; j++) A1[j] = 0.0;
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -1878,7 +1931,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     }
     double W[2] = {L.rhs[0], L.rhs[1]}; /* u */
     PROF_T0(t_wm);
-    sweep_warm<0>(A0, A1, wsAr, lane, nnc, fb, L, W);
+    if (nn > 0) sweep_warm<0>(A0, A1, wsAr, lane, nnc, fb, L, W);
     PROF_ADD(PF_WARM, t_wm);
     PROF_ADD(PF_SPLIT, t_setup);
 #ifdef UG_DEBUG_DUMP
@@ -1995,6 +2048,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
      * sweeps as straight 12-row sequences, reversed on even sweeps, forward on odd ones -- the general
      * path's order without chunk tests or neutral rows; no normal rows, so no warm start and no split pass */
     auto passes_free12 = [&]() -> int {
+        PROF_CNT(PF_FREE_PSETUP, __builtin_readcyclecounter() - t_setup);
         PROF_T0(t_sw);
 #pragma unroll
         for (int s = 0; s < 2; s++) {
@@ -2013,6 +2067,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
             if (ballot(!(res <= UG_RESIDUAL_THR)) == 0ull || it >= UG_PGS_ITERS - 1) break;
         }
         PROF_ADD(PF_SWEEPS, t_sw);
+        PROF_ADD(PF_FREE_PSWEEP, t_sw);
         if (lane < 12) g_sh.rs[lane].imp = L.imp[0];
         return 0;
     };
@@ -2094,6 +2149,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         }
         return split;
     };
+    PROF_T0(t_post);
     const int split = pm.fl                 ? passes_fl()
                       : (n == 12 && nnc == 12) ? passes_free12()
                       : n > 96             ? passes(std::integral_constant<int, 128>{})
@@ -2109,12 +2165,29 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     __builtin_amdgcn_wave_barrier();
     const int d = lane < NV ? lane : 0;
     double acc = 0.0, accs = 0.0;
-    for (int k = 0; k < n; k++) acc = __builtin_fma(rows[k * RS + RJ + d], sh.rs[k].imp, acc);
+    if (direct) { /* the 12 rows' M^-1 J^T at dof slot d from the unit solves, every LDS read up front */
+        double m[12], im[12];
+#pragma unroll
+        for (int k = 0; k < 12; k++) {
+            const int kk = __builtin_amdgcn_readfirstlane(sh.rs[k].kind), ka = __builtin_amdgcn_readfirstlane(sh.rs[k].a);
+            const bool g = kk == 2;
+            const int r1 = g ? UG_FINGER_DOF : (ka < 6 ? ka : UG_FINGER_DOF), r2 = g ? NB + ka : r1;
+            const int dd = lane < NB ? lane : 0;
+            const double x1 = sh.u.mcol[r1][dd], x2 = sh.u.mcol[r2][dd];
+            m[k] = lane < NB ? (g ? x1 + x2 : x1) : 0.0;
+            im[k] = sh.rs[k].imp;
+        }
+#pragma unroll
+        for (int k = 0; k < 12; k++) acc = __builtin_fma(m[k], im[k], acc);
+    } else {
+        for (int k = 0; k < n; k++) acc = __builtin_fma(rows[k * RS + RJ + d], sh.rs[k].imp, acc);
+    }
     if (split)
         for (int k = nnc; k < fb; k++) accs = __builtin_fma(rows[k * RS + RJ + d], sh.u.impx[k], accs);
     dv = lane < NV ? acc : 0.0;
     dvs = lane < NV ? accs : 0.0;
     __builtin_amdgcn_wave_barrier();
+    if (direct) PROF_ADD(PF_FREE_PPOST, t_post);
     return split;
 }
 
