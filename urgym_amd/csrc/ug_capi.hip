@@ -275,6 +275,9 @@ __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, ui
                                                   int* stats, uint8_t* flags) {
     if ((int)blockIdx.x >= n) return;
     const int i = order[blockIdx.x];
+#ifdef UG_PROF
+    const unsigned long long bt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     double* Si = S + (size_t)i * UG_STATE_DIM;
     team_load(Si, stats + (size_t)i * UG_NSTAT);
     const int O = task_obs_dim(sc->variant), A = task_act_dim(sc->variant);
@@ -300,6 +303,15 @@ __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, ui
         if (succ) succ[i] = (uint8_t)io.succ;
         if (substeps) substeps[i] = ns;
         prio[i] = (uint8_t)team_priority(sc, ns, elapsed[i] + 1, max_steps, autoreset);
+#ifdef UG_PROF
+        if (blockIdx.x < UG_BT_MAX) {
+            unsigned long long* bt = &g_btime[4 * blockIdx.x];
+            bt[0] = bt0;
+            bt[1] = __builtin_amdgcn_s_memrealtime();
+            bt[2] = (unsigned long long)i;
+            bt[3] = (unsigned long long)ns | ((unsigned long long)io.reset_done << 16);
+        }
+#endif
     }
 }
 
@@ -792,11 +804,17 @@ int urgym_contact_points(urgym_handle* h, int body_a, int body_b, int link_a, in
 
 // Phase cycle counters of the team kernels (only a -DUG_PROF build records them):
 // out16 receives the UG_NPROF (60) accumulators (ug_team.h PF_* / PC_*); reset != 0 zeroes them.
+// reset == 2 instead copies the last k_step's block timeline (UG_BT_MAX x 4 words: start / end s_memrealtime,
+// env, substeps | reset << 16), tools/timeline.py.
 int urgym_debug_prof(urgym_handle* h, unsigned long long* out16, int reset) {
 #ifdef UG_PROF
     if (!h || !out16) return -1;
     HIPCHK(h, hipSetDevice(h->dev));
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (reset == 2) {
+        HIPCHK(h, hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_btime), sizeof(unsigned long long) * 4 * UG_BT_MAX));
+        return 0;
+    }
     HIPCHK(h, hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * UG_NPROF));
     if (reset) {
         unsigned long long z[UG_NPROF] = {0};

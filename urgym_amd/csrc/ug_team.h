@@ -134,6 +134,8 @@ static __shared__ Shared g_sh;
 /* phase timers (build with -DUG_PROF; read back with urgym_debug_prof) */
 #ifdef UG_PROF
 __device__ unsigned long long g_prof[UG_NPROF];
+#define UG_BT_MAX 8192
+__device__ unsigned long long g_btime[4 * UG_BT_MAX]; /* k_step block timeline (urgym_debug_prof reset == 2) */
 #define PROF_T0(v) unsigned long long v = __builtin_readcyclecounter()
 #define PROF_ADD(k, v)                                                   \
     do {                                                                 \
