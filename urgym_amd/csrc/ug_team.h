@@ -1405,24 +1405,26 @@ __device__ __forceinline__ void swap16_d(double& x, double& y) {
     y = __hiloint2double(h[1], l[1]);
 }
 /* solve position -> row index.  The general layout is the identity over [0, n).  The fixed layout (team_pgs
- * passes_fl) keeps the non-contact and normal rows at [0, fb) and moves the friction rows to [FL_F0, FL_F0 + n - fb),
+ * passes_fl) keeps the non-contact and normal rows at [0, fb) and moves the friction rows to [f0, f0 + n - fb),
  * so that every section starts at a compile-time position; the positions in between are pads (-1: zero J, zero
  * bounds, so a zero column and a neutral row). */
 #define FL_NNC 12 /* non-contact rows of the fixed layout (7 motors + 5 gears) */
 #define FL_F0 40  /* first friction position: normals at [12, 40) (at most 28) */
 #define FL_NF 56  /* friction positions [40, 96): at most 56 rows */
+#define FL_F0S 36 /* the short variant (at most 24 normals): friction at [36, 84) */
+#define FL_NFS 48
 struct PosMap {
-    int n, fb, fl;
+    int n, fb, fl; /* fl: the fixed layout's first friction position (FL_F0 or FL_F0S), 0 for the identity */
     __device__ __forceinline__ int q(int p) const {
         if (!fl) return p < n ? p : -1;
         if (p < fb) return p;
-        if (p < FL_F0) return -1;
-        const int r = fb + (p - FL_F0);
+        if (p < fl) return -1;
+        const int r = fb + (p - fl);
         return r < n ? r : -1;
     }
     /* positions the Delassus build covers: the fixed layout's straight sweeps read every column up to 96,
      * so all of them are built (pad columns zero) */
-    __device__ __forceinline__ int npos() const { return fl ? FL_F0 + FL_NF : n; }
+    __device__ __forceinline__ int npos() const { return fl ? fl + 2 * (fl - FL_NNC) : n; }
 };
 /* the slot's row operands (J of rows 64 S + 16 g + (lane & 15), dof slots 4 ks + (lane >> 4)) are the same
  * for every column block: loaded once per slot into B; each block then loads only its 6 column operands */
@@ -1885,7 +1887,8 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
 #ifdef UG_DEBUG_DUMP
     const PosMap pm{n, fb, 0};
 #else
-    const PosMap pm{n, fb, nnc == FL_NNC && nn >= 16 && fb <= FL_F0 && n - fb <= FL_NF};
+    const bool flok = nnc == FL_NNC && nn >= 16 && fb <= FL_F0 && n - fb <= FL_NF;
+    const PosMap pm{n, fb, !flok ? 0 : (fb <= FL_F0S && n - fb <= FL_NFS) ? FL_F0S : FL_F0};
 #endif
     const int npos = pm.npos();
     /* the contact-free solve of 7 motor + 5 gear rows: its Delassus rows straight from the shared unit solves
@@ -2076,7 +2079,8 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     /* the fixed layout's sweeps as straight row sequences (no chunk tests, no section copies): even sweeps the
      * non-contact rows reversed then the normal positions [12, 40), odd sweeps [0, 40) forward; then the friction
      * positions [40, 96).  Pads are neutral (zero bounds and column); only the section's own rows finish. */
-    auto passes_fl = [&]() -> int {
+    auto passes_fl = [&](auto f0_tag) -> int {
+        constexpr int F0 = decltype(f0_tag)::value, NF = 2 * (F0 - FL_NNC);
         const int nf = n - fb;
         int split = 0;
         PROF_T0(t_sw);
@@ -2111,9 +2115,9 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                 asm volatile("" : "+s"(o_wsA));
                 if (pen || !(it & 1)) {
                     if (!pen) straight_rows<FL_NNC - 1, -1, FL_NNC, true>(A0, A1, o_wsA, lane, L, W);
-                    straight_rows<FL_NNC, 1, FL_F0 - FL_NNC, true>(A0, A1, o_wsA, lane, L, W);
+                    straight_rows<FL_NNC, 1, F0 - FL_NNC, true>(A0, A1, o_wsA, lane, L, W);
                 } else {
-                    straight_rows<0, 1, FL_F0, true>(A0, A1, o_wsA, lane, L, W);
+                    straight_rows<0, 1, F0, true>(A0, A1, o_wsA, lane, L, W);
                 }
                 row_finish<false>(L, pos_mask(0, pen ? nnc : 0, fb, 0ull), 0ull, lane, res);
                 if (!pen && nf > 0) {
@@ -2123,7 +2127,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
 #pragma unroll
                     for (int s = 0; s < 2; s++) {
                         const int p = lane + 64 * s;
-                        const bool isf = p >= FL_F0 && p < FL_F0 + nf;
+                        const bool isf = p >= F0 && p < F0 + nf;
                         const double tot = g_sh.u.impx[isf ? nrow[s] : 0];
                         const bool skip = isf && !(tot > 0.0);
                         L.lo[s] = isf ? -(fric[s] * tot) : L.lo[s];
@@ -2133,8 +2137,8 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                         sk[s] = ballot(skip);
                     }
                     __builtin_amdgcn_wave_barrier();
-                    straight_rows<FL_F0, 1, FL_NF, true>(A0, A1, o_wsA, lane, L, W);
-                    row_finish<true>(L, pos_mask(0, FL_F0, FL_F0 + nf, sk[0]), pos_mask(1, FL_F0, FL_F0 + nf, sk[1]),
+                    straight_rows<F0, 1, NF, true>(A0, A1, o_wsA, lane, L, W);
+                    row_finish<true>(L, pos_mask(0, F0, F0 + nf, sk[0]), pos_mask(1, F0, F0 + nf, sk[1]),
                                      lane, res);
                 }
                 PROF_CNT(PC_ITERS, 1);
@@ -2152,7 +2156,8 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         return split;
     };
     PROF_T0(t_post);
-    const int split = pm.fl                 ? passes_fl()
+    const int split = pm.fl == FL_F0S         ? passes_fl(std::integral_constant<int, FL_F0S>{})
+                      : pm.fl                 ? passes_fl(std::integral_constant<int, FL_F0>{})
                       : (n == 12 && nnc == 12) ? passes_free12()
                       : n > 96             ? passes(std::integral_constant<int, 128>{})
                       : n > 64             ? passes(std::integral_constant<int, 96>{})
