@@ -1428,24 +1428,24 @@ struct PosMap {
 };
 /* the slot's row operands (J of rows 64 S + 16 g + (lane & 15), dof slots 4 ks + (lane >> 4)) are the same
  * for every column block: loaded once per slot into B; each block then loads only its 6 column operands */
-template <int PB>
+template <int PB, int K>
 __device__ __forceinline__ void mfma_cols(gcdouble* rows, const PosMap& pm, int lane, double (&a)[KS]) {
     const int q = pm.q(16 * PB + (lane & 15));
 #pragma unroll
-    for (int ks = 0; ks < KS; ks++) a[ks] = q >= 0 ? rows[q * RS + RJ + 4 * ks + (lane >> 4)] : 0.0;
+    for (int ks = 0; ks < K; ks++) a[ks] = q >= 0 ? rows[q * RS + RJ + 4 * ks + (lane >> 4)] : 0.0;
 }
-template <int PB, int S>
+template <int PB, int S, int K>
 __device__ __forceinline__ void mfma_block(gcdouble* rows, const double (&B)[KS][4], const double (&a)[KS], double invDr,
                                            double (&A)[PREG], gdouble* wsA, const PosMap& pm, int n, int lane) {
     if constexpr (16 * PB < MAXROWS) {
         if (16 * PB < n) {
             double an[KS]; /* the next block's column operands, in flight during this block */
-            if (16 * PB + 16 < n) mfma_cols<PB + 1>(rows, pm, lane, an);
+            if (16 * PB + 16 < n) mfma_cols<PB + 1, K>(rows, pm, lane, an);
             d4v acc[4];
 #pragma unroll
             for (int g = 0; g < 4; g++) acc[g] = d4v{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int ks = 0; ks < KS; ks++)
+            for (int ks = 0; ks < K; ks++)
 #pragma unroll
                 for (int g = 0; g < 4; g++) acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], B[ks][g], acc[g], 0, 0, 0);
 #pragma unroll
@@ -1465,25 +1465,27 @@ __device__ __forceinline__ void mfma_block(gcdouble* rows, const double (&B)[KS]
                     else wsA[(P - PREG) * MAXROWS + 64 * S + lane] = x;
                 }
             }
-            mfma_block<PB + 1, S>(rows, B, an, invDr, A, wsA, pm, n, lane);
+            mfma_block<PB + 1, S, K>(rows, B, an, invDr, A, wsA, pm, n, lane);
         }
     }
 }
-template <int S>
+/* K: the k-steps that can hold a non-zero (4 K >= NB + 6 nobj; the dof slots beyond are zero in every row,
+ * and a chain of exact zero terms on an accumulator that is never -0 changes nothing) */
+template <int S, int K>
 __device__ __forceinline__ void mfma_slot(gcdouble* rows, double invDr, double (&A)[PREG], gdouble* wsA,
                                           const PosMap& pm, int lane) {
     const int n = pm.npos();
     double B[KS][4];
 #pragma unroll
-    for (int ks = 0; ks < KS; ks++)
+    for (int ks = 0; ks < K; ks++)
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const int q = pm.q(64 * S + 16 * g + (lane & 15));
             B[ks][g] = q >= 0 ? rows[q * RS + 4 * ks + (lane >> 4)] : 0.0;
         }
     double a[KS];
-    mfma_cols<0>(rows, pm, lane, a);
-    mfma_block<0, S>(rows, B, a, invDr, A, wsA, pm, n, lane);
+    mfma_cols<0, K>(rows, pm, lane, a);
+    mfma_block<0, S, K>(rows, B, a, invDr, A, wsA, pm, n, lane);
 }
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
 template <typename T>
@@ -1869,11 +1871,11 @@ __device__ __forceinline__ void nc_direct_A(double (&A0)[PREG], int lane) {
         }
     }
 }
-__device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int nn_, double& dv, double& dvs) {
+__device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int nn_, int nobj_, double& dv, double& dvs) {
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
     /* arguments of a non-kernel function arrive in VGPRs: make the uniform ones scalar again */
-    const int n = uniform(n_), nnc = uniform(nnc_), nn = uniform(nn_);
+    const int n = uniform(n_), nnc = uniform(nnc_), nn = uniform(nn_), nobj = uniform(nobj_);
     double* ws = uniform_ptr(ws_);
     const int fb = nnc + nn;
     PROF_T0(t_setup);
@@ -1901,11 +1903,14 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     if (direct) {
         nc_direct_A(A0, lane); /* columns 0..11 only: the 12-row sweeps read nothing else of A0 / A1 */
     } else {
-        const int q0 = pm.q(lane);
-        mfma_slot<0>(rows, q0 >= 0 ? sh.rs[q0].invD : 0.0, A0, wsA, pm, lane);
+        const int q0 = pm.q(lane), q1 = pm.q(lane + 64);
+        const double i0 = q0 >= 0 ? sh.rs[q0].invD : 0.0, i1 = q1 >= 0 ? sh.rs[q1].invD : 0.0;
+        const bool k6 = nobj <= (4 * 6 - NB) / 6; /* the object dofs end within k-step 5 */
+        if (k6) mfma_slot<0, 6>(rows, i0, A0, wsA, pm, lane);
+        else mfma_slot<0, KS>(rows, i0, A0, wsA, pm, lane);
         if (npos > 64) {
-            const int q1 = pm.q(lane + 64);
-            mfma_slot<1>(rows, q1 >= 0 ? sh.rs[q1].invD : 0.0, A1, wsA, pm, lane);
+            if (k6) mfma_slot<1, 6>(rows, i1, A1, wsA, pm, lane);
+            else mfma_slot<1, KS>(rows, i1, A1, wsA, pm, lane);
         } else {
 #pragma unroll
             for (int j = 0; j < PREG; j++) A1[j] = 0.0;
@@ -2243,7 +2248,7 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     PROF_ADD(PF_ROWS, t_rows);
     PROF_T0(t_pgs);
     double dv, dvs;
-    int split = team_pgs(ws, n, nnc, nn, dv, dvs);
+    int split = team_pgs(ws, n, nnc, nn, s->nobj, dv, dvs);
     if (lane == 0 && split) sh.stats[UG_STAT_SPLIT]++;
     PROF_ADD(PF_PGS, t_pgs);
     PROF_T0(t_int);
