@@ -8,7 +8,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 240 python -c "import __graft_entry__ as g; g.build()" > $OUT/build.log 2>&1 || { echo BUILD_FAIL; exit 1; }
+# the libraries are built beforehand on the CPU side (__graft_entry__.build()) and travel with the tree
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --no-cpu-baseline "$@" > $OUT/trace.log 2>&1 || { echo TRACE_FAIL; exit 1; }
 echo TRACE_OK
 # PMC passes on a short run of the same workload (traffic per launch does not depend on the step count)
