@@ -1284,6 +1284,27 @@ __device__ __forceinline__ void row_upd(const double (&A0)[PREG], const double (
     if constexpr (SEL) L.dsv[s] = own_lane_sel<O>(L.dsv[s], dn);
     else L.dsv[s] = writelane_d<O>(L.dsv[s], d);
 }
+/* the fixed layout's row update: the slot-1 column of row P is read from A1[P + OFS] (passes_fl packs the
+ * first part's slot-1 columns into the upper half-wave of the friction columns' registers) */
+template <int P, int OFS>
+__device__ __forceinline__ void row_upd_fl(const double (&A0)[PREG], const double (&A1)[PREG], Lrow& L,
+                                           double (&W)[2]) {
+    constexpr int s = P >> 6, O = P & 63;
+    const double a0 = A0[P], a1 = A1[P + OFS];
+    double dn = __builtin_fmin(__builtin_fmax(W[s], L.dlo[s]), L.dhi[s]);
+    double d = readlane_d(dn, O);
+    W[0] = __builtin_fma(a0, d, W[0]);
+    W[1] = __builtin_fma(a1, d, W[1]);
+    L.dsv[s] = writelane_d<O>(L.dsv[s], d);
+}
+template <int P, int STEP, int K, int OFS>
+__device__ __forceinline__ void straight_rows_fl(const double (&A0)[PREG], const double (&A1)[PREG], Lrow& L,
+                                                 double (&W)[2]) {
+    if constexpr (K > 0) {
+        row_upd_fl<P, OFS>(A0, A1, L, W);
+        straight_rows_fl<P + STEP, STEP, K - 1, OFS>(A0, A1, L, W);
+    }
+}
 /* after a section: the lanes whose row was solved advance their impulse by the recorded increment and
  * fold (delta / D)^2 into their residual */
 template <bool TWO>
@@ -2086,9 +2107,22 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
      * positions [40, 96).  Pads are neutral (zero bounds and column); only the section's own rows finish. */
     auto passes_fl = [&](auto f0_tag) -> int {
         constexpr int F0 = decltype(f0_tag)::value, NF = 2 * (F0 - FL_NNC);
+        static_assert(F0 <= NF && F0 + NF - 64 <= 32, "slot 1 must fit a half-wave for the packing");
         const int nf = n - fb;
         int split = 0;
         PROF_T0(t_sw);
+        /* slot 1 holds at most 32 rows (positions 64 .. F0 + NF - 1): the first part's slot-1 columns A1[k]
+         * (k < F0) move into the upper half-wave of the friction columns' registers A1[F0 + k], halving the
+         * slot-1 registers.  u of slot 1 then lives in two half-wave copies: the lower one is current during
+         * the friction rows, the upper one (lanes 32..63 = rows 64..95) during the first part; each section
+         * starts by copying the current one over the other (v_permlane32_swap), so every element still sees
+         * the same fma chain in the same order. */
+#pragma unroll
+        for (int k = 0; k < F0; k++) {
+            double x = A1[F0 + k], y = A1[k];
+            swap32_d(x, y); /* x: lower half its own column, upper half column k's lower half */
+            A1[F0 + k] = x;
+        }
 #pragma nounroll
         for (int pass = 0; pass < 2; pass++) {
             const int pen = pass;
@@ -2116,13 +2150,21 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
             }
             for (int it = 0; it < UG_PGS_ITERS; it++) {
                 double res = 0.0;
-                gcdouble* o_wsA = wsAr;
-                asm volatile("" : "+s"(o_wsA));
+                {
+                    double x = W[1], y = W[1];
+                    swap32_d(x, y); /* upper copy := lower */
+                    W[1] = x;
+                }
                 if (pen || !(it & 1)) {
-                    if (!pen) straight_rows<FL_NNC - 1, -1, FL_NNC, true>(A0, A1, o_wsA, lane, L, W);
-                    straight_rows<FL_NNC, 1, F0 - FL_NNC, true>(A0, A1, o_wsA, lane, L, W);
+                    if (!pen) straight_rows_fl<FL_NNC - 1, -1, FL_NNC, F0>(A0, A1, L, W);
+                    straight_rows_fl<FL_NNC, 1, F0 - FL_NNC, F0>(A0, A1, L, W);
                 } else {
-                    straight_rows<0, 1, F0, true>(A0, A1, o_wsA, lane, L, W);
+                    straight_rows_fl<0, 1, F0, F0>(A0, A1, L, W);
+                }
+                {
+                    double x = W[1], y = W[1];
+                    swap32_d(x, y); /* lower copy := upper */
+                    W[1] = y;
                 }
                 row_finish<false>(L, pos_mask(0, pen ? nnc : 0, fb, 0ull), 0ull, lane, res);
                 if (!pen && nf > 0) {
@@ -2142,7 +2184,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                         sk[s] = ballot(skip);
                     }
                     __builtin_amdgcn_wave_barrier();
-                    straight_rows<F0, 1, NF, true>(A0, A1, o_wsA, lane, L, W);
+                    straight_rows_fl<F0, 1, NF, 0>(A0, A1, L, W);
                     row_finish<true>(L, pos_mask(0, F0, F0 + nf, sk[0]), pos_mask(1, F0, F0 + nf, sk[1]),
                                      lane, res);
                 }
