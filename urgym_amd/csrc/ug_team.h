@@ -1455,7 +1455,7 @@ __device__ __forceinline__ void mfma_cols(gcdouble* rows, const PosMap& pm, int 
 #pragma unroll
     for (int ks = 0; ks < K; ks++) a[ks] = q >= 0 ? rows[q * RS + RJ + 4 * ks + (lane >> 4)] : 0.0;
 }
-template <int PB, int S, int K>
+template <int PB, int S, int K, int G>
 __device__ __forceinline__ void mfma_block(gcdouble* rows, const double (&B)[KS][4], const double (&a)[KS], double invDr,
                                            double (&A)[PREG], gdouble* wsA, const PosMap& pm, int n, int lane) {
     if constexpr (16 * PB < MAXROWS) {
@@ -1468,7 +1468,7 @@ __device__ __forceinline__ void mfma_block(gcdouble* rows, const double (&B)[KS]
 #pragma unroll
             for (int ks = 0; ks < K; ks++)
 #pragma unroll
-                for (int g = 0; g < 4; g++) acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], B[ks][g], acc[g], 0, 0, 0);
+                for (int g = 0; g < G; g++) acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], B[ks][g], acc[g], 0, 0, 0);
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 double v[4] = {acc[0][r], acc[1][r], acc[2][r], acc[3][r]};
@@ -1486,13 +1486,15 @@ __device__ __forceinline__ void mfma_block(gcdouble* rows, const double (&B)[KS]
                     else wsA[(P - PREG) * MAXROWS + 64 * S + lane] = x;
                 }
             }
-            mfma_block<PB + 1, S, K>(rows, B, an, invDr, A, wsA, pm, n, lane);
+            mfma_block<PB + 1, S, K, G>(rows, B, an, invDr, A, wsA, pm, n, lane);
         }
     }
 }
 /* K: the k-steps that can hold a non-zero (4 K >= NB + 6 nobj; the dof slots beyond are zero in every row,
  * and a chain of exact zero terms on an accumulator that is never -0 changes nothing) */
-template <int S, int K>
+/* G: the row tiles of the slot that can hold a row (the fixed layout's slot 1 has at most 32 rows: tiles 2
+ * and 3 are pads, their accumulators stay zero) */
+template <int S, int K, int G = 4>
 __device__ __forceinline__ void mfma_slot(gcdouble* rows, double invDr, double (&A)[PREG], gdouble* wsA,
                                           const PosMap& pm, int lane) {
     const int n = pm.npos();
@@ -1500,13 +1502,13 @@ __device__ __forceinline__ void mfma_slot(gcdouble* rows, double invDr, double (
 #pragma unroll
     for (int ks = 0; ks < K; ks++)
 #pragma unroll
-        for (int g = 0; g < 4; g++) {
+        for (int g = 0; g < G; g++) {
             const int q = pm.q(64 * S + 16 * g + (lane & 15));
             B[ks][g] = q >= 0 ? rows[q * RS + 4 * ks + (lane >> 4)] : 0.0;
         }
     double a[KS];
     mfma_cols<0, K>(rows, pm, lane, a);
-    mfma_block<0, S, K>(rows, B, a, invDr, A, wsA, pm, n, lane);
+    mfma_block<0, S, K, G>(rows, B, a, invDr, A, wsA, pm, n, lane);
 }
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
 template <typename T>
@@ -1930,7 +1932,9 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         if (k6) mfma_slot<0, 6>(rows, i0, A0, wsA, pm, lane);
         else mfma_slot<0, KS>(rows, i0, A0, wsA, pm, lane);
         if (npos > 64) {
-            if (k6) mfma_slot<1, 6>(rows, i1, A1, wsA, pm, lane);
+            if (pm.fl && k6) mfma_slot<1, 6, 2>(rows, i1, A1, wsA, pm, lane);
+            else if (pm.fl) mfma_slot<1, KS, 2>(rows, i1, A1, wsA, pm, lane);
+            else if (k6) mfma_slot<1, 6>(rows, i1, A1, wsA, pm, lane);
             else mfma_slot<1, KS>(rows, i1, A1, wsA, pm, lane);
         } else {
 #pragma unroll
