@@ -1024,7 +1024,7 @@ __device__ __forceinline__ void object_jac_sel(const Scene* sc, const EnvState& 
  * Jacobians (robot parts unsolved; limit / motor / gear rows take the shared unit solves), (2) the LDL
  * solves of the robot parts, once for all lanes that need one, (3) per kind, dots, rhs and bounds.  Every
  * row's arithmetic is the oracle's (build_rows in oracle/ug_oracle.c). */
-__device__ __forceinline__ static void build_row(const Scene* s, int pos, double* wrow) {
+__device__ __forceinline__ static void build_row(const Scene* s, int pos, double* wrow, bool store_j = true) {
     Shared& sh = g_sh;
     const EnvState& e = sh.e;
     const double dt = UG_DT;
@@ -1196,6 +1196,7 @@ __device__ __forceinline__ static void build_row(const Scene* s, int pos, double
     /* J | M^-1 J^T over the NVP dof slots: limit / motor rows their robot part, gear rows the sum of both
      * robot parts, contact rows each side's entity segment (zero elsewhere, pads included) */
     const int eA = kind <= 2 ? 0 : entA, eB = kind == 2 ? 0 : (kind <= 1 ? -1 : entB);
+    if (store_j) {
 #pragma unroll
     for (int i = 0; i < NVP; i++) {
         const int ent = i < NB ? 0 : (i < NV ? 1 + (i - NB) / 6 : -2);
@@ -1209,6 +1210,7 @@ __device__ __forceinline__ static void build_row(const Scene* s, int pos, double
         }
         wrow[i] = j;
         wrow[RJ + i] = m;
+    }
     }
     PROF_ADD(PF_RB3, t_rb3);
 }
@@ -2287,7 +2289,14 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     team_unit_solves();
     PROF_ADD(PF_UNIT, t_unit);
     PROF_T0(t_rowb);
-    for (int p = lane; p < n; p += TEAM) build_row(s, p, ws + WS_ROWS + p * RS);
+    /* the motor / gear solve (team_pgs's direct path) reads its Delassus rows and M^-1 J^T from the unit
+     * solves in LDS: its J | M^-1 J^T stay out of the workspace */
+#ifdef UG_DEBUG_DUMP
+    const bool nc_direct = false;
+#else
+    const bool nc_direct = n == 12 && nnc == 12 && ballot(lane < 12 && sh.rs[lane].kind == 0) == 0ull;
+#endif
+    for (int p = lane; p < n; p += TEAM) build_row(s, p, ws + WS_ROWS + p * RS, !nc_direct);
     PROF_ADD(PF_ROWB, t_rowb);
     __threadfence_block();
     __syncthreads();
