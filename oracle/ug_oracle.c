@@ -1299,6 +1299,14 @@ static void collide(ugo_env* e, const kin* k) {
             for (int i = 0; i < L2.n; i++)
                 cand_add(&L, vneg(L2.c[i].n), vadd(L2.c[i].pB, vscale(L2.c[i].n, L2.c[i].d)), L2.c[i].d);
         }
+#ifdef UG_ROWHIST /* development aid (tools/row_hist.py): every overlapping pair, its candidates and the deepest */
+        {
+            extern int dprintf(int, const char*, ...);
+            double dm = 1e9;
+            for (int i = 0; i < L.n; i++) dm = L.c[i].d < dm ? L.c[i].d : dm;
+            dprintf(2, "PAIR %d %d %d %d %d %d %.6f\n", p, a, b, A->kind, B->kind, L.n, dm);
+        }
+#endif
         /* manifold frames = owner frames */
         for (int i = 0; i < L.n; i++) manifold_add(&M, &O[a], &O[b], &L.c[i], P->thr);
         if (M.npts) manifold_refresh(&M, &O[a], &O[b], P->thr);

@@ -45,11 +45,14 @@ static_assert(NV <= NVP, "dof slots exceed the padded row");
  * doubles, written lane-per-row by the row build), then the Delassus columns >= PREG (column-major) */
 #define WS_ROWS (UG_MAXMAN * UG_MAN_DOUBLES)
 #define WS_A (WS_ROWS + MAXROWS * RS)
+/* hull-box pairs' corner certificates: per pair, the face that last maximised each box corner's plane
+ * distance (8 bytes; a hint only -- team_hull_box proves with it or scans every face) */
+#define WS_HC (WS_A + (MAXROWS - PREG) * MAXROWS)
 #ifdef UG_DEBUG_DUMP /* development aid: team_pgs dumps A, w and impulses after the workspace proper */
-#define WS_DBG (WS_A + (MAXROWS - PREG) * MAXROWS)
+#define WS_DBG (WS_HC + MAXPAIR)
 #define WS_DOUBLES (WS_DBG + MAXROWS * MAXROWS + 8 * MAXROWS)
 #else
-#define WS_DOUBLES (WS_A + (MAXROWS - PREG) * MAXROWS)
+#define WS_DOUBLES (WS_HC + MAXPAIR)
 #endif
 
 #define MAXOV 26 /* pairs per lane-per-pair pass: their working manifolds share LDS with the rows (Shared::pm) */
@@ -253,7 +256,7 @@ __device__ static inline void man_to_st(StMan& S, const LManifold& M) {
 /* hull (A, robot link) vs box (B): the whole wave.  Produces cand k (<= 4 points) in sh.u.cand. */
 __device__ __forceinline__ static void team_reduce4(int n, int k);
 __device__ __forceinline__ static void team_hull_box(const HullArg& A, const HullArg& B, const XF& TA, const XF& TB,
-                                     double thr, int k) {
+                                     double thr, int k, unsigned char* hcert) {
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
     PROF_T0(t_hv);
@@ -305,9 +308,22 @@ __device__ __forceinline__ static void team_hull_box(const HullArg& A, const Hul
     v3 y = vadd(mv(RBA, cl), pBA);
     double smax = -1e300;
     int fm = 0x7fffffff;
+    const int nf = A.nf;
+    /* certificate: a corner is rejected (smax - margin >= thr) as soon as one face's plane distance, formed
+     * with the scan's own expression, clears it -- the scan's max is at least that value and the subtraction
+     * is monotone.  The faces that maximised the corners last time usually still do: when all 8 corners are
+     * rejected by them the face scan is skipped, with the same (empty) corner result. */
+    bool certified = false;
+    if (nf > 0) {
+        int fc = hcert[c];
+        fc = fc < nf ? fc : nf - 1;
+        const double* F = &UG_HULL_F[4 * (A.f0 + fc)];
+        const double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
+        certified = ballot(j == 0 && sd - mA >= thr) == 0x0101010101010101ull;
+    }
+    if (!certified) {
     /* the first HB_FACE_UNROLL x 8 faces with every plane load issued up front (clamped index, predicated
      * update: one load latency instead of one per face); faces beyond that (none in this model) in a loop */
-    const int nf = A.nf;
     {
         double F[HB_FACE_UNROLL][4];
 #pragma unroll
@@ -340,6 +356,8 @@ __device__ __forceinline__ static void team_hull_box(const HullArg& A, const Hul
         if (!better(smax, fm, w, jj, true)) { smax = w; fm = jj; }
         w = dpp<0x141>(smax); jj = dppi<0x141>(fm);
         if (!better(smax, fm, w, jj, true)) { smax = w; fm = jj; }
+    }
+    if (j == 0 && fm != 0x7fffffff) hcert[c] = (unsigned char)fm;
     }
     int cvalid = 0;
     Cand cc;
@@ -530,7 +548,8 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         for (unsigned long long hm = ballot(hk); hm != 0ull; hm &= hm - 1ull) {
             const int k = __builtin_ctzll(hm);
             const PairInfo pi = sh.pinfo[k];
-            if (pi.kb == UG_SHAPE_BOX) team_hull_box(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k);
+            if (pi.kb == UG_SHAPE_BOX)
+                team_hull_box(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k, (unsigned char*)(ws + WS_HC) + 8 * sh.ov[c0 + k]);
             else team_hull_hull(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k);
             PROF_CNT(PC_HULL, 1);
         }
