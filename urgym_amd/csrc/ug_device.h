@@ -840,25 +840,36 @@ DF void manifold_add(LManifold& M, const XF& TA, const XF& TB, const Cand& c, do
     stpt(M.pt[ins], np);
 }
 DF void manifold_refresh(LManifold& M, const XF& TA, const XF& TB, double thr) {
-    for (int i = M.npts - 1; i >= 0; i--) {
-        LCPoint& p = M.pt[i];
-        v3 pA = xf_apply(TA, ldv(p.lpA)), pB = xf_apply(TB, ldv(p.lpB));
-        p.dist = vdot(vsub(pA, pB), ldv(p.n));
-    }
-    for (int i = M.npts - 1; i >= 0; i--) {
-        LCPoint& p = M.pt[i];
-        int rm = 0;
-        if (p.dist > thr) rm = 1;
-        else {
-            v3 pA = xf_apply(TA, ldv(p.lpA)), pB = xf_apply(TB, ldv(p.lpB));
-            v3 proj = vsub(pA, vscale(ldv(p.n), p.dist));
-            v3 d = vsub(pB, proj);
-            if (vdot(d, d) > thr * thr) rm = 1;
+    /* the world points of the first pass are kept (registers, compile-time slots) for the removal pass: the
+     * removal pass visits slots in descending order and a removal only overwrites the slot just visited, so
+     * every slot it reads still holds its original point */
+    const int n0 = M.npts;
+    v3 wA[4], wB[4];
+#pragma unroll
+    for (int i = 3; i >= 0; i--) {
+        if (i < n0) {
+            LCPoint& p = M.pt[i];
+            wA[i] = xf_apply(TA, ldv(p.lpA));
+            wB[i] = xf_apply(TB, ldv(p.lpB));
+            p.dist = vdot(vsub(wA[i], wB[i]), ldv(p.n));
         }
-        if (rm) {
-            int last = M.npts - 1;
-            if (i != last) cppt(M.pt[i], M.pt[last]);
-            M.npts--;
+    }
+#pragma unroll
+    for (int i = 3; i >= 0; i--) {
+        if (i < n0) {
+            LCPoint& p = M.pt[i];
+            int rm = 0;
+            if (p.dist > thr) rm = 1;
+            else {
+                v3 proj = vsub(wA[i], vscale(ldv(p.n), p.dist));
+                v3 d = vsub(wB[i], proj);
+                if (vdot(d, d) > thr * thr) rm = 1;
+            }
+            if (rm) {
+                int last = M.npts - 1;
+                if (i != last) cppt(M.pt[i], M.pt[last]);
+                M.npts--;
+            }
         }
     }
 }

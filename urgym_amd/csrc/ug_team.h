@@ -458,10 +458,11 @@ __device__ __forceinline__ static void team_reduce4(int n, int k) {
     wave_best(v, idx, false);
     int sel[4];
     sel[0] = idx;
+    double md = 1e300; /* squared distance to the nearest selected point, folded in one point per round (a min:
+                        * the same value as the oracle's scan over all selected points) */
     for (int s = 1; s < 4; s++) {
-        double md = 1e300;
-        for (int t = 0; t < s; t++) {
-            const Cand& st = sh.hc[sel[t]];
+        {
+            const Cand& st = sh.hc[sel[s - 1]];
             v3 dd = vsub(mine.pB, st.pB);
             double x = vdot(dd, dd);
             if (x < md) md = x;
