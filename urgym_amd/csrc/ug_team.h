@@ -1293,18 +1293,41 @@ template <int L>
 __device__ __forceinline__ double own_lane_sel(double old, double x) {
     return __builtin_amdgcn_inverse_ballot_w64(1ull << L) ? x : old;
 }
+/* w + a * (lane O's x) with the broadcast folded into the fma: DP-ALU DPP row_newbcast (gfx90a+) hands every
+ * 16-lane row the value of its own lane O, so it serves rows held in lanes 0..15 (the contact-free 12-row
+ * solve) and takes the two v_readlane and the SGPR hop off the row chain.  s_nop 1: the two wait states a DPP
+ * read of a VGPR the previous VALU op wrote needs. */
+template <int O>
+__device__ __forceinline__ double clamp_fma_bcast16(double a, double dlo, double dhi, double& w) {
+    static_assert(O >= 0 && O < 16, "row_newbcast reaches the lanes of one 16-lane row");
+    double dn;
+    /* the clamp in the same block: v_max_f64 / v_min_f64 are what fmax / fmin compile to, and an fmax of an
+     * asm result would cost a canonicalising v_max first */
+    asm("v_max_f64 %0, %1, %2\n\t"
+        "v_min_f64 %0, %0, %3\n\t"
+        "s_nop 1\n\t"
+        "v_fmac_f64_dpp %1, %0, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf"
+        : "=&v"(dn), "+v"(w)
+        : "v"(dlo), "v"(dhi), "v"(a), "i"(O));
+    return dn;
+}
 template <int P, bool TWO, bool SEL = false>
 __device__ __forceinline__ void row_upd(const double (&A0)[PREG], const double (&A1)[PREG], gcdouble* wsA, int lane,
                                         Lrow& L, double (&W)[2]) {
     constexpr int s = P >> 6, O = P & 63;
     double a0, a1;
     colA<P>(A0, A1, wsA, lane, a0, a1);
-    double dn = __builtin_fmin(__builtin_fmax(W[s], L.dlo[s]), L.dhi[s]);
-    double d = readlane_d(dn, O);
-    W[0] = __builtin_fma(a0, d, W[0]);
-    if (TWO) W[1] = __builtin_fma(a1, d, W[1]); /* slot 1 exists only with more than 64 rows */
-    if constexpr (SEL) L.dsv[s] = own_lane_sel<O>(L.dsv[s], dn);
-    else L.dsv[s] = writelane_d<O>(L.dsv[s], d);
+    if constexpr (SEL) { /* rows in lanes 0..15, one slot: broadcast inside the fma, record by lane select */
+        static_assert(!TWO && P < 16, "the DPP row update serves one slot of at most 16 rows");
+        const double dn = clamp_fma_bcast16<O>(a0, L.dlo[0], L.dhi[0], W[0]);
+        L.dsv[s] = own_lane_sel<O>(L.dsv[s], dn);
+    } else {
+        double dn = __builtin_fmin(__builtin_fmax(W[s], L.dlo[s]), L.dhi[s]);
+        double d = readlane_d(dn, O);
+        W[0] = __builtin_fma(a0, d, W[0]);
+        if (TWO) W[1] = __builtin_fma(a1, d, W[1]); /* slot 1 exists only with more than 64 rows */
+        L.dsv[s] = writelane_d<O>(L.dsv[s], d);
+    }
 }
 /* the fixed layout's row update: the slot-1 column of row P is read from A1[P + OFS] (passes_fl packs the
  * first part's slot-1 columns into the upper half-wave of the friction columns' registers) */
