@@ -158,7 +158,7 @@ enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_
        PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE, PF_FK, PF_LDL, PF_UNIT, PF_ROWB, PF_RB1, PF_RB2, PF_RB3, PF_MFMA, PF_WARM, PF_SW_NC, PF_SW_CT, PF_SW_FIN, PF_SW_FPREP, PF_SW_FR,
        PF_SW_RES, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST, PC_CHUNKS, PC_NNC, PC_NN, PC_N64, PC_N80, PC_N96,
        PC_FREE, PF_FREE_COL, PF_FREE_DYN, PF_FREE_ROWS, PF_FREE_PGS, PF_FREE_INT,
-       PF_FREE_PSETUP, PF_FREE_PSWEEP, PF_FREE_PPOST };
+       PF_FREE_PSETUP, PF_FREE_PSWEEP, PF_FREE_PPOST, PF_PR_BB, PF_HS };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -479,6 +479,304 @@ __device__ __forceinline__ static void team_reduce4(int n, int k) {
     __syncthreads();
 }
 
+/* box (A) vs box (B) (oracle nc_box_box: ODE dBoxBox2 as btBoxBoxDetector), the whole wave per pair.  The same
+ * operations on the same values as the serial routine, spread over lanes:
+ *   - the 15 separating-axis tests in lanes 0..14 (any positive separation ends the pair, as the serial early
+ *     return does whichever test it is), then the serial selection order -- faces by strict max, edges by the
+ *     fudge-weighted test -- replayed on the broadcast values;
+ *   - the face case's rectangle-quad clipping (intersectRectQuad2) one polygon vertex per lane per pass: each
+ *     vertex emits [itself if inside][the crossing if its edge crosses], prefix sums give the serial emission
+ *     order, and the serial cap at 8 points keeps the first 8 items and ends the clipping;
+ *   - the contact points one per lane (kept ones compacted in order); cullPoints: the centroid as the serial
+ *     chain, the angles one point per lane, each pick an arg-min whose ties go to the lower index (the serial
+ *     scan's first minimum).
+ * Writes cand k (0..4 points). */
+/* column / element picks by selects: run-time indices into register-resident matrices made team_box_box read wrong
+ * values (measured: the face normal and clip frame came out of the wrong column), so every pick is explicit */
+__device__ __forceinline__ v3 colsel(const m3& A, int i) {
+    return i == 0 ? V(A.m[0], A.m[3], A.m[6]) : i == 1 ? V(A.m[1], A.m[4], A.m[7]) : V(A.m[2], A.m[5], A.m[8]);
+}
+__device__ __forceinline__ double sel3(const double (&a)[3], int i) { return i == 0 ? a[0] : i == 1 ? a[1] : a[2]; }
+__device__ __forceinline__ m3 msel(bool c, const m3& a, const m3& b) {
+    m3 r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.m[i] = c ? a.m[i] : b.m[i];
+    return r;
+}
+#ifdef UG_BB_CHECK
+static __shared__ int g_bbdbg[8];
+#endif
+__device__ __forceinline__ static void team_box_box(const XF& TA, const double (&Ah)[3], const XF& TB,
+                                                    const double (&Bh)[3], int k) {
+    Shared& sh = g_sh;
+    const int lane = threadIdx.x;
+    const double fudge = 1.05;
+    const m3& R1 = TA.R;
+    const m3& R2 = TB.R;
+    const v3 p1 = TA.p, p2 = TB.p;
+    const v3 p = vsub(p2, p1);
+    const v3 pp = mtv(R1, p);
+    const double R11 = col_dot(R1, 0, R2, 0), R12 = col_dot(R1, 0, R2, 1), R13 = col_dot(R1, 0, R2, 2);
+    const double R21 = col_dot(R1, 1, R2, 0), R22 = col_dot(R1, 1, R2, 1), R23 = col_dot(R1, 1, R2, 2);
+    const double R31 = col_dot(R1, 2, R2, 0), R32 = col_dot(R1, 2, R2, 1), R33 = col_dot(R1, 2, R2, 2);
+    const double Q11 = ug_fabs(R11), Q12 = ug_fabs(R12), Q13 = ug_fabs(R13);
+    const double Q21 = ug_fabs(R21), Q22 = ug_fabs(R22), Q23 = ug_fabs(R23);
+    const double Q31 = ug_fabs(R31), Q32 = ug_fabs(R32), Q33 = ug_fabs(R33);
+    /* lane t: test t (code t + 1) */
+    double e1 = 0.0, x2 = 0.0, n1 = 0.0, n2 = 0.0, n3 = 0.0;
+    switch (lane) {
+    case 0: e1 = pp.x; x2 = (Ah[0] + Bh[0] * Q11 + Bh[1] * Q12 + Bh[2] * Q13); break;
+    case 1: e1 = pp.y; x2 = (Ah[1] + Bh[0] * Q21 + Bh[1] * Q22 + Bh[2] * Q23); break;
+    case 2: e1 = pp.z; x2 = (Ah[2] + Bh[0] * Q31 + Bh[1] * Q32 + Bh[2] * Q33); break;
+    case 3: e1 = col_dotv(R2, 0, p); x2 = (Ah[0] * Q11 + Ah[1] * Q21 + Ah[2] * Q31 + Bh[0]); break;
+    case 4: e1 = col_dotv(R2, 1, p); x2 = (Ah[0] * Q12 + Ah[1] * Q22 + Ah[2] * Q32 + Bh[1]); break;
+    case 5: e1 = col_dotv(R2, 2, p); x2 = (Ah[0] * Q13 + Ah[1] * Q23 + Ah[2] * Q33 + Bh[2]); break;
+    case 6: e1 = pp.z * R21 - pp.y * R31; x2 = (Ah[1] * Q31 + Ah[2] * Q21 + Bh[1] * Q13 + Bh[2] * Q12); n1 = 0; n2 = -R31; n3 = R21; break;
+    case 7: e1 = pp.z * R22 - pp.y * R32; x2 = (Ah[1] * Q32 + Ah[2] * Q22 + Bh[0] * Q13 + Bh[2] * Q11); n1 = 0; n2 = -R32; n3 = R22; break;
+    case 8: e1 = pp.z * R23 - pp.y * R33; x2 = (Ah[1] * Q33 + Ah[2] * Q23 + Bh[0] * Q12 + Bh[1] * Q11); n1 = 0; n2 = -R33; n3 = R23; break;
+    case 9: e1 = pp.x * R31 - pp.z * R11; x2 = (Ah[0] * Q31 + Ah[2] * Q11 + Bh[1] * Q23 + Bh[2] * Q22); n1 = R31; n2 = 0; n3 = -R11; break;
+    case 10: e1 = pp.x * R32 - pp.z * R12; x2 = (Ah[0] * Q32 + Ah[2] * Q12 + Bh[0] * Q23 + Bh[2] * Q21); n1 = R32; n2 = 0; n3 = -R12; break;
+    case 11: e1 = pp.x * R33 - pp.z * R13; x2 = (Ah[0] * Q33 + Ah[2] * Q13 + Bh[0] * Q22 + Bh[1] * Q21); n1 = R33; n2 = 0; n3 = -R13; break;
+    case 12: e1 = pp.y * R11 - pp.x * R21; x2 = (Ah[0] * Q21 + Ah[1] * Q11 + Bh[1] * Q33 + Bh[2] * Q32); n1 = -R21; n2 = R11; n3 = 0; break;
+    case 13: e1 = pp.y * R12 - pp.x * R22; x2 = (Ah[0] * Q22 + Ah[1] * Q12 + Bh[0] * Q33 + Bh[2] * Q31); n1 = -R22; n2 = R12; n3 = 0; break;
+    case 14: e1 = pp.y * R13 - pp.x * R23; x2 = (Ah[0] * Q23 + Ah[1] * Q13 + Bh[0] * Q32 + Bh[1] * Q31); n1 = -R23; n2 = R13; n3 = 0; break;
+    default: break;
+    }
+    const bool test = lane < 15;
+    const double s2 = ug_fabs(e1) - x2;
+    if (ballot(test && s2 > 0) != 0ull) { /* a separating axis: no contact */
+        if (lane == 0) sh.u.cand.n[k] = 0;
+        __syncthreads();
+        return;
+    }
+    double l = 0.0, s2n = 0.0;
+    v3 nc = V(0, 0, 0);
+    if (lane >= 6 && lane < 15) {
+        l = ug_sqrt((n1) * (n1) + (n2) * (n2) + (n3) * (n3));
+        if (l > 0) {
+            s2n = s2 / l;
+            nc = V((n1) / l, (n2) / l, (n3) / l);
+        }
+    }
+    const unsigned long long neg = ballot(test && e1 < 0), lpos = ballot(lane >= 6 && lane < 15 && l > 0);
+    double s = -1e300;
+    int nR = -1, tsel = -1, invert_normal = 0, code = 0;
+    for (int t = 0; t < 6; t++) {
+        const double v = readlane_d(s2, t);
+        if (v > s) { s = v; nR = t; invert_normal = (int)((neg >> t) & 1ull); code = t + 1; }
+    }
+    for (int t = 6; t < 15; t++) {
+        if ((lpos >> t) & 1ull) {
+            const double v = readlane_d(s2n, t);
+            if (v * fudge > s) { s = v; nR = -1; tsel = t; invert_normal = (int)((neg >> t) & 1ull); code = t + 1; }
+        }
+    }
+    int nout = 0;
+    if (code) {
+        v3 normal;
+        if (nR >= 0) { /* column nR % 3 of R1 (nR < 3) or R2, by selects (no dynamic register indexing) */
+            const m3& Rn = nR < 3 ? R1 : R2;
+            const int c = nR % 3;
+            normal = c == 0 ? V(Rn.m[0], Rn.m[3], Rn.m[6]) : c == 1 ? V(Rn.m[1], Rn.m[4], Rn.m[7]) : V(Rn.m[2], Rn.m[5], Rn.m[8]);
+        } else {
+            normal = mv(R1, V(readlane_d(nc.x, tsel), readlane_d(nc.y, tsel), readlane_d(nc.z, tsel)));
+        }
+        if (invert_normal) normal = vneg(normal);
+        const double depth = -s;
+        if (code > 6) { /* edge-edge: one point (uniform arithmetic; lane 0 stores it) */
+            v3 pa = p1;
+            for (int j = 0; j < 3; j++) {
+                double sign = (col_dotv(R1, j, normal) > 0) ? 1.0 : -1.0;
+                pa = vadd(pa, V(sign * Ah[j] * R1.m[j], sign * Ah[j] * R1.m[3 + j], sign * Ah[j] * R1.m[6 + j]));
+            }
+            v3 pb = p2;
+            for (int j = 0; j < 3; j++) {
+                double sign = (col_dotv(R2, j, normal) > 0) ? -1.0 : 1.0;
+                pb = vadd(pb, V(sign * Bh[j] * R2.m[j], sign * Bh[j] * R2.m[3 + j], sign * Bh[j] * R2.m[6 + j]));
+            }
+            const int ia = (code - 7) / 3, ib = (code - 7) % 3;
+            const v3 ua = colsel(R1, ia);
+            const v3 ub = colsel(R2, ib);
+            const v3 pd = vsub(pb, pa);
+            double uaub = vdot(ua, ub), q1 = vdot(ua, pd), q2 = -vdot(ub, pd);
+            double d = 1.0 - uaub * uaub, beta;
+            if (d <= 0.0001) { beta = 0; }
+            else { d = 1.0 / d; beta = (uaub * q1 + q2) * d; }
+            pb = vadd(pb, vscale(ub, beta));
+            if (lane == 0) {
+                Cand c;
+                c.n = vneg(normal);
+                c.pB = pb;
+                c.d = -depth;
+                sh.u.cand.c[k][0] = c;
+            }
+            nout = 1;
+        } else { /* face: clip the incident face against the reference face's rectangle */
+            const m3 Ra = msel(code <= 3, R1, R2);
+            const m3 Rb = msel(code <= 3, R2, R1);
+            const v3 pa = code <= 3 ? p1 : p2, pb = code <= 3 ? p2 : p1;
+            const double Sa[3] = {code <= 3 ? Ah[0] : Bh[0], code <= 3 ? Ah[1] : Bh[1], code <= 3 ? Ah[2] : Bh[2]};
+            const double Sb[3] = {code <= 3 ? Bh[0] : Ah[0], code <= 3 ? Bh[1] : Ah[1], code <= 3 ? Bh[2] : Ah[2]};
+            const v3 normal2 = code <= 3 ? normal : vneg(normal);
+            const v3 nr = mtv(Rb, normal2);
+            const v3 anr = V(ug_fabs(nr.x), ug_fabs(nr.y), ug_fabs(nr.z));
+            int lanr, a1, a2;
+            if (anr.y > anr.x) {
+                if (anr.y > anr.z) { a1 = 0; lanr = 1; a2 = 2; }
+                else { a1 = 0; a2 = 1; lanr = 2; }
+            } else {
+                if (anr.x > anr.z) { lanr = 0; a1 = 1; a2 = 2; }
+                else { a1 = 0; a2 = 1; lanr = 2; }
+            }
+            v3 center;
+            const v3 rbl = colsel(Rb, lanr);
+            if (vget(nr, lanr) < 0) center = vadd(vsub(pb, pa), vscale(rbl, sel3(Sb, lanr)));
+            else center = vsub(vsub(pb, pa), vscale(rbl, sel3(Sb, lanr)));
+            const int codeN = code <= 3 ? code - 1 : code - 4;
+            int code1, code2;
+            if (codeN == 0) { code1 = 1; code2 = 2; }
+            else if (codeN == 1) { code1 = 0; code2 = 2; }
+            else { code1 = 0; code2 = 1; }
+            /* col_dotv / col_dot with the columns picked first: the same products and sums in the same order */
+            const v3 ra1 = colsel(Ra, code1), ra2 = colsel(Ra, code2), rb1 = colsel(Rb, a1), rb2 = colsel(Rb, a2);
+            const double c1 = vdot(ra1, center), c2 = vdot(ra2, center);
+            double m11 = vdot(ra1, rb1), m12 = vdot(ra1, rb2);
+            double m21 = vdot(ra2, rb1), m22 = vdot(ra2, rb2);
+            const double Sba1 = sel3(Sb, a1), Sba2 = sel3(Sb, a2);
+            /* the quad, vertex per lane (lanes 0..3) */
+            double qx, qy;
+            {
+                const double k1 = m11 * Sba1, k2 = m21 * Sba1, k3 = m12 * Sba2, k4 = m22 * Sba2;
+                const double x0 = c1 - k1 - k3, y0 = c2 - k2 - k4, x1 = c1 - k1 + k3, y1 = c2 - k2 + k4;
+                const double x2q = c1 + k1 + k3, y2q = c2 + k2 + k4, x3 = c1 + k1 - k3, y3 = c2 + k2 - k4;
+                qx = lane == 0 ? x0 : lane == 1 ? x1 : lane == 2 ? x2q : x3;
+                qy = lane == 0 ? y0 : lane == 1 ? y1 : lane == 2 ? y2q : y3;
+            }
+            const double rect0 = sel3(Sa, code1), rect1 = sel3(Sa, code2);
+            ldouble* buf = (ldouble*)&sh.bs[0].buffer[0]; /* one pass's output points (x, y), at most 8 */
+            int nq = 4;
+            bool capped = false;
+            for (int pass = 0; pass < 4 && !capped; pass++) {
+                const int dir = pass >> 1;
+                const double sgn = (pass & 1) ? 1.0 : -1.0, hd = dir ? rect1 : rect0;
+                const int nj = lane + 1 < nq ? lane + 1 : 0;
+                const double nx = __shfl(qx, nj), ny = __shfl(qy, nj);
+                const bool live = lane < nq;
+                const double qd = dir ? qy : qx, qo = dir ? qx : qy, nd = dir ? ny : nx, no = dir ? nx : ny;
+                const bool in = live && sgn * qd < hd;
+                const bool cross = live && ((sgn * qd < hd) ^ (sgn * nd < hd));
+                const unsigned long long bi = ballot(in), bc = ballot(cross);
+                const unsigned long long below = (1ull << lane) - 1ull;
+                const int pin = __popcll(bi & below) + __popcll(bc & below), pcr = pin + (in ? 1 : 0);
+                const int total = __popcll(bi) + __popcll(bc);
+                __builtin_amdgcn_wave_barrier();
+                if (in && pin < 8) { buf[2 * pin] = qx; buf[2 * pin + 1] = qy; }
+                if (cross && pcr < 8) {
+                    const double ix = qo + (no - qo) / (nd - qd) * (sgn * hd - qd);
+                    buf[2 * pcr + 1 - dir] = ix;
+                    buf[2 * pcr + dir] = sgn * hd;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                nq = total < 8 ? total : 8;
+                capped = total >= 8;
+                qx = lane < nq ? buf[2 * lane] : 0.0;
+                qy = lane < nq ? buf[2 * lane + 1] : 0.0;
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (nq >= 1) {
+                const double det1 = 1.0 / (m11 * m22 - m12 * m21);
+                m11 *= det1; m12 *= det1; m21 *= det1; m22 *= det1;
+                const v3 rba1 = rb1, rba2 = rb2;
+                const bool live = lane < nq;
+                const double k1 = m22 * (qx - c1) - m12 * (qy - c2);
+                const double k2 = -m21 * (qx - c1) + m11 * (qy - c2);
+                const v3 pc = vadd(vadd(center, vscale(rba1, k1)), vscale(rba2, k2));
+                const double dep = sel3(Sa, codeN) - vdot(normal2, pc);
+                const bool keep = live && dep >= 0;
+                const unsigned long long km = ballot(keep);
+                const int cnum = __popcll(km), cpos = __popcll(km & ((1ull << lane) - 1ull));
+                v3 pw = vadd(pc, pa);
+                if (code >= 4) pw = vsub(pw, vscale(normal, dep));
+                if (cnum >= 1 && cnum <= 4) {
+                    if (keep) {
+                        Cand c;
+                        c.n = vneg(normal);
+                        c.pB = pw;
+                        c.d = -dep;
+                        sh.u.cand.c[k][cpos] = c;
+                    }
+                    nout = cnum;
+                } else if (cnum > 4) { /* cullPoints to 4, starting from the deepest */
+                    double dv = keep ? dep : 0.0;
+                    int di = keep ? cpos : 0x7fffffff;
+                    wave_best(dv, di, true);
+                    const int i0 = di;
+                    ldouble* kp = (ldouble*)&sh.bs[0].ret[0]; /* the kept clip points (x, y) in order */
+                    __builtin_amdgcn_wave_barrier();
+                    if (keep) { kp[2 * cpos] = qx; kp[2 * cpos + 1] = qy; }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                    const int n = cnum;
+                    double a = 0, cx = 0, cy = 0, qq;
+                    for (int i = 0; i < n - 1; i++) {
+                        qq = kp[i * 2] * kp[i * 2 + 3] - kp[i * 2 + 2] * kp[i * 2 + 1];
+                        a += qq;
+                        cx += qq * (kp[i * 2] + kp[i * 2 + 2]);
+                        cy += qq * (kp[i * 2 + 1] + kp[i * 2 + 3]);
+                    }
+                    qq = kp[n * 2 - 2] * kp[1] - kp[0] * kp[n * 2 - 1];
+                    if (ug_fabs(a + qq) > 2.220446049250313e-16) a = 1.0 / (3.0 * (a + qq));
+                    else a = 1e30;
+                    cx = a * (cx + qq * (kp[n * 2 - 2] + kp[0]));
+                    cy = a * (cy + qq * (kp[n * 2 - 1] + kp[1]));
+                    const double ang = keep ? ug_atan2(qy - cy, qx - cx) : 0.0;
+                    /* the angles by kept index: lane cpos of the kept set holds point cpos */
+                    ldouble* A = (ldouble*)&sh.bs[0].ang[0];
+                    __builtin_amdgcn_wave_barrier();
+                    if (keep) A[cpos] = ang;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                    const double Ai = lane < n ? A[lane] : 0.0;
+                    const double Ai0 = A[i0];
+                    unsigned long long avail = (n == 64 ? ~0ull : ((1ull << n) - 1ull)) & ~(1ull << i0);
+                    int iret[4];
+                    iret[0] = i0;
+                    const int m = 4;
+                    for (int j = 1; j < m; j++) {
+                        double aj = (double)j * (2.0 * UG_PI / m) + Ai0;
+                        if (aj > UG_PI) aj -= 2.0 * UG_PI;
+                        double diff = ug_fabs(Ai - aj);
+                        if (diff > UG_PI) diff = 2.0 * UG_PI - diff;
+                        const bool av = (avail >> lane) & 1ull;
+                        int idx = av && diff < 1e9 ? lane : 0x7fffffff;
+                        double dd = av ? diff : 0.0;
+                        wave_best(dd, idx, false);
+                        iret[j] = idx == 0x7fffffff ? i0 : idx;
+                        avail &= ~(1ull << iret[j]);
+                    }
+                    if (keep) {
+                        const int slot = cpos == iret[0] ? 0 : cpos == iret[1] ? 1 : cpos == iret[2] ? 2 : cpos == iret[3] ? 3 : -1;
+                        if (slot >= 0) {
+                            Cand c;
+                            c.n = vneg(normal);
+                            c.pB = pw;
+                            c.d = -dep;
+                            sh.u.cand.c[k][slot] = c;
+                        }
+                    }
+                    nout = m;
+                }
+            }
+        }
+    }
+    if (lane == 0) sh.u.cand.n[k] = nout;
+#ifdef UG_BB_CHECK
+    if (lane == 0) { g_bbdbg[0] = code; g_bbdbg[1] = tsel; g_bbdbg[2] = nR; }
+#endif
+    __syncthreads();
+}
+
 /* performDiscreteCollisionDetection (oracle collide()), team version.  ws: this env's global workspace. */
 __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
     Shared& sh = g_sh;
@@ -618,24 +916,39 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
             PROF_ADD(PF_PR_NP, t_pn);
         }
         PROF_T0(t_bb);
-        for (unsigned long long bbm = ballot(isbb); bbm != 0ull;) {
-            unsigned long long round = 0ull, rest = bbm;
-            for (int t = 0; t < NBOXSLOT && rest != 0ull; t++) { round |= rest & (0ull - rest); rest &= rest - 1ull; }
-            if ((round >> lane) & 1ull) {
-                const int slot = __popcll(round & ((1ull << lane) - 1ull));
-                const PairDef& P = s->pair[sh.ov[c0 + lane]];
-                const Collider& A = s->col[P.a];
-                const Collider& B = s->col[P.b];
-                const XF TA = shape_xf(sh.O[P.a], A), TB = shape_xf(sh.O[P.b], B);
+        /* box-box pairs: the whole wave per pair (team_box_box) */
+        for (unsigned long long bbm = ballot(isbb); bbm != 0ull; bbm &= bbm - 1ull) {
+            const int kb = __builtin_ctzll(bbm);
+            const PairDef& P = s->pair[sh.ov[c0 + kb]];
+            const Collider& A = s->col[P.a];
+            const Collider& B = s->col[P.b];
+            const XF TA = shape_xf(sh.O[P.a], A), TB = shape_xf(sh.O[P.b], B);
+            const double Ah[3] = {A.half[0], A.half[1], A.half[2]}, Bh[3] = {B.half[0], B.half[1], B.half[2]};
+            team_box_box(TA, Ah, TB, Bh, kb);
+#ifdef UG_BB_CHECK /* development aid: the serial routine beside the team one, mismatches printed */
+            if (lane == 0) {
                 CandList L;
                 L.n = 0;
-                L.c = (LCand*)&sh.u.cand.c[lane][0];
-                nc_box_box(TA, A, TB, B, P.thr, L, *(LBoxScratch*)&sh.bs[slot]);
-                sh.u.cand.n[lane] = L.n;
+                L.c = (LCand*)&sh.bs[2];
+                nc_box_box(TA, A, TB, B, P.thr, L, *(LBoxScratch*)&sh.bs[1]);
+                int same = L.n == sh.u.cand.n[kb];
+                for (int i = 0; same && i < L.n; i++) {
+                    const v3 an = ldv(L.c[i].n), ap = ldv(L.c[i].pB), bn = sh.u.cand.c[kb][i].n, bp = sh.u.cand.c[kb][i].pB;
+                    same = an.x == bn.x && an.y == bn.y && an.z == bn.z && ap.x == bp.x && ap.y == bp.y && ap.z == bp.z &&
+                           L.c[i].d == sh.u.cand.c[kb][i].d;
+                }
+                if (!same) {
+                    printf("BBCHK pair %d-%d serial n %d team n %d code %d tsel %d nR %d | s0 %.17g %.17g %.17g d %.17g | t0 %.17g %.17g %.17g d %.17g\n",
+                           P.a, P.b, L.n, sh.u.cand.n[kb], g_bbdbg[0], g_bbdbg[1], g_bbdbg[2],
+                           L.n ? ldv(L.c[0].pB).x : 0.0, L.n ? ldv(L.c[0].pB).y : 0.0, L.n ? ldv(L.c[0].pB).z : 0.0, L.n ? L.c[0].d : 0.0,
+                           sh.u.cand.c[kb][0].pB.x, sh.u.cand.c[kb][0].pB.y, sh.u.cand.c[kb][0].pB.z, sh.u.cand.c[kb][0].d);
+                }
             }
-            bbm = rest;
+            __syncthreads();
+#endif
         }
         PROF_ADD(PF_PR_NP, t_bb);
+        PROF_ADD(PF_PR_BB, t_bb);
         if (lane < cn) {
             const PairDef& P = s->pair[sh.ov[c0 + lane]];
             LManifold& M = *(LManifold*)&sh.pm[lane];
