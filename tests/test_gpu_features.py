@@ -309,3 +309,72 @@ def test_long_horizon_through_truncation(mods, task, max_steps, n, T):
     sim, ref, outs = run_parity(Sim, OracleEnv, task, n, T, max_steps)
     assert any(o["truncated"].any() for o in outs)
     print("stats", task, sim.stats().sum(0).tolist())
+
+
+def _quat_axis_angle(ax, ang):
+    ax = np.asarray(ax, np.float64) / np.linalg.norm(ax)
+    s = np.sin(ang / 2.0)
+    return np.array([ax[0] * s, ax[1] * s, ax[2] * s, np.cos(ang / 2.0)])
+
+
+def _quat_mul(a, b):
+    ax, ay, az, aw = a
+    bx, by, bz, bw = b
+    return np.array([aw * bx + ax * bw + ay * bz - az * by, aw * by - ax * bz + ay * bw + az * bx,
+                     aw * bz + ax * by - ay * bx + az * bw, aw * bw - ax * bx - ay * by - az * bz])
+
+
+def test_box_box_clip_cull_and_edge_paths(mods):
+    """The box-box narrowphase's rare branches (ug_team.h team_box_box vs the oracle's serial dBoxBox2): a cube
+    stacked on a cube rotated about z (octagonal clip polygon -> 8 points -> cullPoints), at 0 degrees (4
+    points), tilted so an edge or a corner leads (edge-edge / single-point contacts), and offset to the edge of
+    the lower cube (partial clips).  Three substeps from each crafted state, bit-identical to the oracle."""
+    Sim, OracleEnv = mods
+    n = 25
+    sim = Sim(1, n, seed=SEED)
+    sim.reset()
+    st = sim.get_state().copy()
+    rng = np.random.default_rng(7)
+    h = 0.02
+    for i in range(n):
+        o0, o1 = LY.obj(0), LY.obj(1)
+        c0 = np.array([0.10, -0.60, h - 1e-5])  # resting on the table, away from the gripper
+        st[i, o0:o0 + 3] = c0
+        st[i, o0 + 3:o0 + 7] = [0.0, 0.0, 0.0, 1.0]
+        st[i, o0 + 7:o0 + 13] = 0.0
+        kind = i % 5
+        if kind == 0:    # rotated about z: octagon, cull to 4
+            q = _quat_axis_angle([0, 0, 1], np.pi / 4 + 0.05 * rng.standard_normal())
+            c1 = c0 + np.array([0.0, 0.0, 2 * h - 0.0008])
+        elif kind == 1:  # aligned: 4 corner points, no clipping
+            q = _quat_axis_angle([0, 0, 1], 0.02 * rng.standard_normal())
+            c1 = c0 + np.array([0.003 * rng.standard_normal(), 0.003 * rng.standard_normal(), 2 * h - 0.0006])
+        elif kind == 2:  # tilted 45 degrees about x and rotated about z: an edge leads, crossing the top face edge
+            q = _quat_mul(_quat_axis_angle([0, 0, 1], 0.6 + 0.1 * rng.standard_normal()), _quat_axis_angle([1, 0, 0], np.pi / 4))
+            c1 = c0 + np.array([h * 0.9, 0.0, h + h * np.sqrt(2.0) - 0.0007])
+        elif kind == 3:  # offset over the edge of the lower cube: a partial clip
+            q = _quat_axis_angle([0, 0, 1], 0.3 + 0.1 * rng.standard_normal())
+            c1 = c0 + np.array([1.3 * h, 0.7 * h, 2 * h - 0.0005])
+        else:            # both on an edge, the edges crossed: an edge-edge contact
+            r2 = np.sqrt(2.0)
+            c0 = np.array([0.10, -0.60, h * r2 - 1e-5])
+            st[i, o0:o0 + 3] = c0
+            st[i, o0 + 3:o0 + 7] = _quat_axis_angle([0, 1, 0], np.pi / 4)
+            q = _quat_mul(_quat_axis_angle([0, 0, 1], 0.1 * rng.standard_normal()), _quat_axis_angle([1, 0, 0], np.pi / 4))
+            c1 = c0 + np.array([0.002 * rng.standard_normal(), 0.002 * rng.standard_normal(), 2 * h * r2 - 0.0007])
+        st[i, o1:o1 + 3] = c1
+        st[i, o1 + 3:o1 + 7] = q / np.linalg.norm(q)
+        st[i, o1 + 7:o1 + 13] = 0.0
+    sim.set_state(st)
+    ref = {i: OracleEnv(1, SEED + i) for i in range(n)}
+    for i, r in ref.items():
+        r.set_state(st[i])
+    npts = 0
+    for k in range(3):
+        sim.substep()
+        got = sim.get_state()
+        for i, r in ref.items():
+            r.substep()
+            assert np.array_equal(got[i], r.get_state()), (k, i)
+        npts += int(got[:, LY.F_NMAN].sum())
+    assert npts > 0
