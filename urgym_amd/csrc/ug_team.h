@@ -1664,18 +1664,20 @@ __device__ __forceinline__ void straight_rows_fl(const double (&A0)[PREG], const
     }
 }
 /* after a section: the lanes whose row was solved advance their impulse by the recorded increment and
- * fold (delta / D)^2 into their residual */
+ * flag a (delta / D)^2 above the residual threshold.  The sweep's convergence test (the largest (delta / D)^2
+ * of the sweep <= threshold, oracle pgs()) is then "no row flagged": the same decision as folding a running
+ * max and comparing it (NaN included: a NaN square is flagged, as a NaN max fails the test), without the
+ * max / select chain in front of the wave-wide test. */
 template <bool TWO>
 __device__ __forceinline__ void row_finish(Lrow& L, unsigned long long m0, unsigned long long m1, int lane,
-                                           double& res) {
+                                           bool& bad) {
 #pragma unroll
     for (int s = 0; s < (TWO ? 2 : 1); s++) {
         const bool did = (((s ? m1 : m0) >> lane) & 1ull) != 0ull;
         const double dn = L.dsv[s];
         double x = dn * L.rinv[s];
         x = x * x;
-        double r2 = res > x ? res : x;
-        res = did ? r2 : res;
+        bad = bad | (did & !(x <= UG_RESIDUAL_THR));
         L.imp[s] = did ? L.imp[s] + dn : L.imp[s];
         L.dlo[s] = L.lo[s] - L.imp[s];
         L.dhi[s] = L.hi[s] - L.imp[s];
@@ -2370,7 +2372,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                 L.dhi[s] = L.hi[s] - L.imp[s];
             }
             for (int it = 0; it < UG_PGS_ITERS; it++) {
-                double res = 0.0;
+                bool bad = false;
                 /* opaque per-sweep copies: keeps the per-chunk scalar tests inside the loop */
                 int o_n = n, o_nnc = nnc, o_fb = fb;
                 gcdouble* o_wsA = wsAr;
@@ -2386,7 +2388,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                 PROF_ADD(PF_SW_CT, t_s2);
                 PROF_T0(t_s3);
                 const int f0 = pen ? o_nnc : 0;
-                row_finish<TWO>(L, pos_mask(0, f0, o_fb, 0ull), pos_mask(1, f0, o_fb, 0ull), lane, res);
+                row_finish<TWO>(L, pos_mask(0, f0, o_fb, 0ull), pos_mask(1, f0, o_fb, 0ull), lane, bad);
                 PROF_ADD(PF_SW_FIN, t_s3);
                 /* friction and rolling rows: bounds +-mu * (their normal's impulse, final for this sweep),
                  * skipped while it is not positive.  A skipped row is made neutral (sweep_section):
@@ -2414,12 +2416,12 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                     PROF_ADD(PF_SW_FPREP, t_s4);
                     PROF_T0(t_s5);
                     sweep_section<false, SPAN / CHUNK, TWO>(A0, A1, o_wsA, lane, o_fb, o_n, sk[0], sk[1], L, W);
-                    row_finish<TWO>(L, pos_mask(0, o_fb, o_n, sk[0]), pos_mask(1, o_fb, o_n, sk[1]), lane, res);
+                    row_finish<TWO>(L, pos_mask(0, o_fb, o_n, sk[0]), pos_mask(1, o_fb, o_n, sk[1]), lane, bad);
                     PROF_ADD(PF_SW_FR, t_s5);
                 }
                 PROF_CNT(PC_ITERS, 1);
                 PROF_T0(t_s6);
-                if (ballot(!(res <= UG_RESIDUAL_THR)) == 0ull || it >= UG_PGS_ITERS - 1) break;
+                if (ballot(bad) == 0ull || it >= UG_PGS_ITERS - 1) break;
                 PROF_ADD(PF_SW_RES, t_s6);
             }
             if (!pen) {
@@ -2449,15 +2451,15 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
             L.dhi[s] = L.hi[s] - L.imp[s];
         }
         for (int it = 0; it < UG_PGS_ITERS; it++) {
-            double res = 0.0;
+            bool bad = false;
             gcdouble* o_wsA = wsAr;
             asm volatile("" : "+s"(o_wsA));
             /* 12 lane masks stay in SGPRs: the records by lane select (the fixed layout's 64 would spill) */
             if (!(it & 1)) straight_rows<11, -1, 12, false, true>(A0, A1, o_wsA, lane, L, W);
             else straight_rows<0, 1, 12, false, true>(A0, A1, o_wsA, lane, L, W);
-            row_finish<false>(L, pos_mask(0, 0, 12, 0ull), 0ull, lane, res);
+            row_finish<false>(L, pos_mask(0, 0, 12, 0ull), 0ull, lane, bad);
             PROF_CNT(PC_ITERS, 1);
-            if (ballot(!(res <= UG_RESIDUAL_THR)) == 0ull || it >= UG_PGS_ITERS - 1) break;
+            if (ballot(bad) == 0ull || it >= UG_PGS_ITERS - 1) break;
         }
         PROF_ADD(PF_SWEEPS, t_sw);
         PROF_ADD(PF_FREE_PSWEEP, t_sw);
@@ -2511,7 +2513,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                 L.dhi[s] = L.hi[s] - L.imp[s];
             }
             for (int it = 0; it < UG_PGS_ITERS; it++) {
-                double res = 0.0;
+                bool bad = false;
                 {
                     double x = W[1], y = W[1];
                     swap32_d(x, y); /* upper copy := lower */
@@ -2528,7 +2530,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                     swap32_d(x, y); /* lower copy := upper */
                     W[1] = y;
                 }
-                row_finish<false>(L, pos_mask(0, pen ? nnc : 0, fb, 0ull), 0ull, lane, res);
+                row_finish<false>(L, pos_mask(0, pen ? nnc : 0, fb, 0ull), 0ull, lane, bad);
                 if (!pen && nf > 0) {
                     g_sh.u.impx[lane] = L.imp[0];
                     __builtin_amdgcn_wave_barrier();
@@ -2548,10 +2550,10 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                     __builtin_amdgcn_wave_barrier();
                     straight_rows_fl<F0, 1, NF, 0>(A0, A1, L, W);
                     row_finish<true>(L, pos_mask(0, F0, F0 + nf, sk[0]), pos_mask(1, F0, F0 + nf, sk[1]),
-                                     lane, res);
+                                     lane, bad);
                 }
                 PROF_CNT(PC_ITERS, 1);
-                if (ballot(!(res <= UG_RESIDUAL_THR)) == 0ull || it >= UG_PGS_ITERS - 1) break;
+                if (ballot(bad) == 0ull || it >= UG_PGS_ITERS - 1) break;
             }
             if (!pen) {
                 PROF_ADD(PF_SWEEPS, t_sw);
