@@ -2,7 +2,7 @@
 """Per-phase cycle breakdown of the team kernels (development aid).
 
 Needs the instrumented library: hipcc ... -DUG_PROF -o urgym_amd/_lib/liburgym_prof.so
-(tools/build_prof.sh).  Runs BallBalance x N envs with autoreset for K steps and prints
+(tools/build_prof.sh).  Runs a task (default BallBalance) x N envs with autoreset for K steps and prints
 cycles per phase per env-step, plus substeps / rows / PGS iterations per substep.
 """
 import argparse
@@ -31,10 +31,13 @@ NAMES = ["collide", "dyn+enum", "rows", "pgs", "pgs_setup", "integrate", "glue",
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--task", type=int, default=0)
     ap.add_argument("--steps", type=int, default=5)
     a = ap.parse_args()
     from urgym_amd._native import Sim
-    sim = Sim(0, a.envs, seed=20241220)
+    sim = Sim(a.task, a.envs, seed=20241220)
+    from urgym_amd.envs import spaces_for
+    _, asp = spaces_for(a.task)
     sim.set_autoreset(True, 500)
     buf = np.zeros(60, np.uint64)
     sim.reset()
@@ -47,7 +50,7 @@ def main():
           **{k + "_cycles": round(r[k] / max(r["free_substeps"], 1), 1) for k in NAMES[-10:-2]}}))
     rng = np.random.default_rng(1)
     for _ in range(a.steps):
-        sim.step(rng.uniform(-0.1, 0.1, size=(a.envs, 3)).astype(np.float32))
+        sim.step(rng.uniform(asp.low, asp.high, size=(a.envs, len(asp.low))).astype(np.float32))
     sim.sync()
     sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     es = a.envs * a.steps

@@ -19,7 +19,8 @@ fd, path = tempfile.mkstemp()
 saved = os.dup(2)
 os.dup2(fd, 2)
 marks = []
-env = OracleEnv(0, 20241220, lib_path=os.path.join(ROOT, "oracle/_dev/libugoracle_rowhist.so"))
+task = int(os.environ.get("UG_TASK", "0"))
+env = OracleEnv(task, 20241220, lib_path=os.path.join(ROOT, "oracle/_dev/libugoracle_rowhist.so"))
 rng = np.random.default_rng(0)
 for e in range(eps):
     marks.append(("reset", os.lseek(fd, 0, os.SEEK_CUR)))

@@ -1794,18 +1794,29 @@ __device__ __forceinline__ void swap16_d(double& x, double& y) {
 #define FL_NF 56  /* friction positions [40, 96): at most 56 rows */
 #define FL_F0S 36 /* the short variant (at most 24 normals): friction at [36, 84) */
 #define FL_NFS 48
+/* the single-slot fixed layout (CubesPush / CubesGrasp contact solves, BallBalance's early reset contacts): at
+ * most FS_NC non-contact rows (motors, gears, violated limits) at [0, nnc), pads to FS_NC, at most
+ * FS_F0 - FS_NC normals, pads to FS_F0, at most FS_NF friction rows; 50 positions, all in slot 0 */
+#define FS_NC 20
+#define FS_F0 30
+#define FS_NF 20
 struct PosMap {
-    int n, fb, fl; /* fl: the fixed layout's first friction position (FL_F0 or FL_F0S), 0 for the identity */
+    int n, fb, fl; /* fl: the fixed layout's first friction position (FL_F0, FL_F0S or FS_F0), 0 for the identity */
+    int nc, nb;    /* the fixed layouts: non-contact rows [0, nc) at positions [0, nc), normals from position nb */
+    int np;        /* positions the sweeps cover */
     __device__ __forceinline__ int q(int p) const {
         if (!fl) return p < n ? p : -1;
-        if (p < fb) return p;
-        if (p < fl) return -1;
+        if (p < nb) return p < nc ? p : -1;
+        if (p < fl) {
+            const int r = nc + (p - nb);
+            return r < fb ? r : -1;
+        }
         const int r = fb + (p - fl);
         return r < n ? r : -1;
     }
-    /* positions the Delassus build covers: the fixed layout's straight sweeps read every column up to 96,
+    /* positions the Delassus build covers: the fixed layouts' straight sweeps read every column they span,
      * so all of them are built (pad columns zero) */
-    __device__ __forceinline__ int npos() const { return fl ? fl + 2 * (fl - FL_NNC) : n; }
+    __device__ __forceinline__ int npos() const { return fl ? np : n; }
 };
 /* the slot's row operands (J of rows 64 S + 16 g + (lane & 15), dof slots 4 ks + (lane >> 4)) are the same
  * for every column block: loaded once per slot into B; each block then loads only its 6 column operands */
@@ -2270,10 +2281,15 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     /* the fixed layout: 12 non-contact rows, 16..28 normals, at most 56 friction rows (BallBalance's contact
      * solves, in steps and in resets) */
 #ifdef UG_DEBUG_DUMP
-    const PosMap pm{n, fb, 0};
+    const PosMap pm{n, fb, 0, nnc, nnc, n};
 #else
     const bool flok = nnc == FL_NNC && nn >= 16 && fb <= FL_F0 && n - fb <= FL_NF;
-    const PosMap pm{n, fb, !flok ? 0 : (fb <= FL_F0S && n - fb <= FL_NFS) ? FL_F0S : FL_F0};
+    const int flf0 = (fb <= FL_F0S && n - fb <= FL_NFS) ? FL_F0S : FL_F0;
+    /* the single-slot layout: few normals (CubesPush 8, CubesGrasp 4-6), up to 20 non-contact rows */
+    const bool fsok = !flok && nnc <= FS_NC && nn >= 3 && nn <= FS_F0 - FS_NC && n - fb <= FS_NF;
+    const PosMap pm = flok ? PosMap{n, fb, flf0, nnc, nnc, flf0 + 2 * (flf0 - FL_NNC)}
+                      : fsok ? PosMap{n, fb, FS_F0, nnc, FS_NC, FS_F0 + FS_NF}
+                             : PosMap{n, fb, 0, nnc, nnc, n};
 #endif
     const int npos = pm.npos();
     /* the contact-free solve of 7 motor + 5 gear rows: its Delassus rows straight from the shared unit solves
@@ -2326,7 +2342,10 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     }
     double W[2] = {L.rhs[0], L.rhs[1]}; /* u */
     PROF_T0(t_wm);
-    if (nn > 0) sweep_warm<0>(A0, A1, wsAr, lane, nnc, fb, L, W);
+    if (nn > 0) { /* the normals' positions: [nnc, fb), or [FS_NC, FS_NC + nn) in the single-slot layout */
+        const int wb = pm.fl ? pm.nb : nnc;
+        sweep_warm<0>(A0, A1, wsAr, lane, wb, wb + nn, L, W);
+    }
     PROF_ADD(PF_WARM, t_wm);
     PROF_ADD(PF_SPLIT, t_setup);
 #ifdef UG_DEBUG_DUMP
@@ -2566,8 +2585,75 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         }
         return split;
     };
+    /* the single-slot fixed layout (FS_*): even sweeps the non-contact positions reversed then the normal
+     * positions, odd sweeps [0, FS_F0) forward, then the friction positions -- the general path's row order with
+     * neutral pads and no chunk tests; one u register (all positions < 64) */
+    auto passes_fs = [&]() -> int {
+        constexpr int NC = FS_NC, F0 = FS_F0, NF = FS_NF;
+        const int nf = n - fb;
+        int split = 0;
+        PROF_T0(t_sw);
+#pragma nounroll
+        for (int pass = 0; pass < 2; pass++) {
+            const int pen = pass;
+            if (pen) {
+                const int anypen = lane >= NC && lane < F0 && rhsPen[0] != 0.0;
+                split = ballot(anypen) != 0ull;
+                if (!split) break;
+#pragma unroll
+                for (int s = 0; s < 2; s++) {
+                    L.rhs[s] = rhsPen[s];
+                    L.imp[s] = 0.0;
+                }
+                W[0] = L.rhs[0];
+                W[1] = L.rhs[1];
+            }
+#pragma unroll
+            for (int s = 0; s < 2; s++) {
+                L.dlo[s] = L.lo[s] - L.imp[s];
+                L.dhi[s] = L.hi[s] - L.imp[s];
+            }
+            for (int it = 0; it < UG_PGS_ITERS; it++) {
+                bool bad = false;
+                gcdouble* o_wsA = wsAr;
+                asm volatile("" : "+s"(o_wsA));
+                if (pen || !(it & 1)) {
+                    if (!pen) straight_rows<NC - 1, -1, NC>(A0, A1, o_wsA, lane, L, W);
+                    straight_rows<NC, 1, F0 - NC>(A0, A1, o_wsA, lane, L, W);
+                } else {
+                    straight_rows<0, 1, F0>(A0, A1, o_wsA, lane, L, W);
+                }
+                row_finish<false>(L, pos_mask(0, pen ? NC : 0, F0, 0ull), 0ull, lane, bad);
+                if (!pen && nf > 0) {
+                    g_sh.u.impx[lane] = L.imp[0];
+                    __builtin_amdgcn_wave_barrier();
+                    const bool isf = lane >= F0 && lane < F0 + nf;
+                    /* the friction row's normal: row nrow sits at position NC + (nrow - nnc) */
+                    const double tot = g_sh.u.impx[isf ? NC + (nrow[0] - nnc) : 0];
+                    const bool skip = isf && !(tot > 0.0);
+                    L.lo[0] = isf ? -(fric[0] * tot) : L.lo[0];
+                    L.hi[0] = isf ? fric[0] * tot : L.hi[0];
+                    L.dlo[0] = skip ? 0.0 : L.lo[0] - L.imp[0];
+                    L.dhi[0] = skip ? 0.0 : L.hi[0] - L.imp[0];
+                    const unsigned long long sk = ballot(skip);
+                    __builtin_amdgcn_wave_barrier();
+                    straight_rows<F0, 1, NF>(A0, A1, o_wsA, lane, L, W);
+                    row_finish<false>(L, pos_mask(0, F0, F0 + nf, sk), 0ull, lane, bad);
+                }
+                PROF_CNT(PC_ITERS, 1);
+                if (ballot(bad) == 0ull || it >= UG_PGS_ITERS - 1) break;
+            }
+            if (!pen) {
+                PROF_ADD(PF_SWEEPS, t_sw);
+                const int q = pm.q(lane);
+                if (q >= 0) g_sh.rs[q].imp = L.imp[0];
+            }
+        }
+        return split;
+    };
     PROF_T0(t_post);
-    const int split = pm.fl == FL_F0S         ? passes_fl(std::integral_constant<int, FL_F0S>{})
+    const int split = pm.fl == FS_F0          ? passes_fs()
+                      : pm.fl == FL_F0S       ? passes_fl(std::integral_constant<int, FL_F0S>{})
                       : pm.fl                 ? passes_fl(std::integral_constant<int, FL_F0>{})
                       : (n == 12 && nnc == 12) ? passes_free12()
                       : n > 96             ? passes(std::integral_constant<int, 128>{})
@@ -2576,9 +2662,10 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                                            : passes(std::integral_constant<int, 32>{});
     /* dv[d] (dvs[d]) = fma chain over positions k of M^-1J_k[d] * impulse_k (lane d < NV) */
     __builtin_amdgcn_wave_barrier();
-    if (split) {
-        sh.u.impx[lane] = L.imp[0];
-        sh.u.impx[64 + lane] = L.imp[1];
+    if (split) { /* the split impulses by row (the accumulation below reads rows [nnc, fb)) */
+        const int q0 = pm.q(lane), q1 = pm.q(64 + lane);
+        if (q0 >= 0) sh.u.impx[q0] = L.imp[0];
+        if (q1 >= 0) sh.u.impx[q1] = L.imp[1];
     }
     __builtin_amdgcn_wave_barrier();
     const int d = lane < NV ? lane : 0;
