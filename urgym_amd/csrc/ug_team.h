@@ -1800,6 +1800,16 @@ __device__ __forceinline__ void swap16_d(double& x, double& y) {
 #define FS_NC 20
 #define FS_F0 30
 #define FS_NF 20
+/* the two-slot layout for Golf's contact solves (13 non-contact rows with the club's limit row, up to 28
+ * normals, friction + rolling rows up to 52): non-contact rows at [0, nnc), pads to 16, normals from 16,
+ * friction from 44, 96 positions */
+#define FG_NC 16
+#define FG_F0 44
+#define FG_NF 52
+template <int NC_, int F0_, int NF_>
+struct FLShape {
+    static constexpr int NC = NC_, F0 = F0_, NF = NF_;
+};
 struct PosMap {
     int n, fb, fl; /* fl: the fixed layout's first friction position (FL_F0, FL_F0S or FS_F0), 0 for the identity */
     int nc, nb;    /* the fixed layouts: non-contact rows [0, nc) at positions [0, nc), normals from position nb */
@@ -2287,8 +2297,10 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     const int flf0 = (fb <= FL_F0S && n - fb <= FL_NFS) ? FL_F0S : FL_F0;
     /* the single-slot layout: few normals (CubesPush 8, CubesGrasp 4-6), up to 20 non-contact rows */
     const bool fsok = !flok && nnc <= FS_NC && nn >= 3 && nn <= FS_F0 - FS_NC && n - fb <= FS_NF;
+    const bool fgok = !flok && !fsok && nnc <= FG_NC && nn >= 16 && nn <= FG_F0 - FG_NC && n - fb <= FG_NF;
     const PosMap pm = flok ? PosMap{n, fb, flf0, nnc, nnc, flf0 + 2 * (flf0 - FL_NNC)}
                       : fsok ? PosMap{n, fb, FS_F0, nnc, FS_NC, FS_F0 + FS_NF}
+                      : fgok ? PosMap{n, fb, FG_F0, nnc, FG_NC, FG_F0 + FG_NF}
                              : PosMap{n, fb, 0, nnc, nnc, n};
 #endif
     const int npos = pm.npos();
@@ -2488,8 +2500,8 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     /* the fixed layout's sweeps as straight row sequences (no chunk tests, no section copies): even sweeps the
      * non-contact rows reversed then the normal positions [12, 40), odd sweeps [0, 40) forward; then the friction
      * positions [40, 96).  Pads are neutral (zero bounds and column); only the section's own rows finish. */
-    auto passes_fl = [&](auto f0_tag) -> int {
-        constexpr int F0 = decltype(f0_tag)::value, NF = 2 * (F0 - FL_NNC);
+    auto passes_fl = [&](auto shape) -> int {
+        constexpr int NC = decltype(shape)::NC, F0 = decltype(shape)::F0, NF = decltype(shape)::NF;
         static_assert(F0 <= NF && F0 + NF - 64 <= 32, "slot 1 must fit a half-wave for the packing");
         const int nf = n - fb;
         int split = 0;
@@ -2514,7 +2526,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
 #pragma unroll
                 for (int s = 0; s < 2; s++) {
                     const int p = lane + 64 * s;
-                    anypen |= p >= nnc && p < fb && rhsPen[s] != 0.0;
+                    anypen |= p >= pm.nb && p < pm.nb + nn && rhsPen[s] != 0.0;
                 }
                 split = ballot(anypen) != 0ull;
                 if (!split) break;
@@ -2539,8 +2551,8 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                     W[1] = x;
                 }
                 if (pen || !(it & 1)) {
-                    if (!pen) straight_rows_fl<FL_NNC - 1, -1, FL_NNC, F0>(A0, A1, L, W);
-                    straight_rows_fl<FL_NNC, 1, F0 - FL_NNC, F0>(A0, A1, L, W);
+                    if (!pen) straight_rows_fl<NC - 1, -1, NC, F0>(A0, A1, L, W);
+                    straight_rows_fl<NC, 1, F0 - NC, F0>(A0, A1, L, W);
                 } else {
                     straight_rows_fl<0, 1, F0, F0>(A0, A1, L, W);
                 }
@@ -2549,7 +2561,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                     swap32_d(x, y); /* lower copy := upper */
                     W[1] = y;
                 }
-                row_finish<false>(L, pos_mask(0, pen ? nnc : 0, fb, 0ull), 0ull, lane, bad);
+                row_finish<false>(L, pos_mask(0, pen ? pm.nb : 0, pm.nb + nn, 0ull), 0ull, lane, bad);
                 if (!pen && nf > 0) {
                     g_sh.u.impx[lane] = L.imp[0];
                     __builtin_amdgcn_wave_barrier();
@@ -2558,7 +2570,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                     for (int s = 0; s < 2; s++) {
                         const int p = lane + 64 * s;
                         const bool isf = p >= F0 && p < F0 + nf;
-                        const double tot = g_sh.u.impx[isf ? nrow[s] : 0];
+                        const double tot = g_sh.u.impx[isf ? pm.nb + (nrow[s] - nnc) : 0]; /* the normal's position */
                         const bool skip = isf && !(tot > 0.0);
                         L.lo[s] = isf ? -(fric[s] * tot) : L.lo[s];
                         L.hi[s] = isf ? fric[s] * tot : L.hi[s];
@@ -2653,8 +2665,9 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     };
     PROF_T0(t_post);
     const int split = pm.fl == FS_F0          ? passes_fs()
-                      : pm.fl == FL_F0S       ? passes_fl(std::integral_constant<int, FL_F0S>{})
-                      : pm.fl                 ? passes_fl(std::integral_constant<int, FL_F0>{})
+                      : pm.fl == FG_F0        ? passes_fl(FLShape<FG_NC, FG_F0, FG_NF>{})
+                      : pm.fl == FL_F0S       ? passes_fl(FLShape<FL_NNC, FL_F0S, FL_NFS>{})
+                      : pm.fl                 ? passes_fl(FLShape<FL_NNC, FL_F0, FL_NF>{})
                       : (n == 12 && nnc == 12) ? passes_free12()
                       : n > 96             ? passes(std::integral_constant<int, 128>{})
                       : n > 64             ? passes(std::integral_constant<int, 96>{})
