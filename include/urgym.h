@@ -101,8 +101,10 @@ int urgym_set_reward_type(urgym_handle* h, int sparse);
  * SURVEY.md 5).  flags: n_envs bytes, UG_FLAG_* bits (urgym_amd/csrc/ug_layout.h) of the last step / reset call:
  * 1 a wait_until_stable loop hit 480 substeps unsettled, 2 the state went non-finite (the env was terminated with
  * reward 0 and, with autoreset, reset from a clean state), 4 contacts were dropped at a capacity limit.
+ * A reset (urgym_reset, or a step's autoreset) whose settling ends non-finite also sets bit 2 and counts; envs
+ * masked out of urgym_reset get flags 0 (nothing happened to them in that call).
  * stats: n_envs x 8 int32 cumulative counters (UG_STAT_*: unstable waits, split-impulse substeps, row-capacity
- * substeps, manifold-capacity substeps, non-finite terminations, substeps). */
+ * substeps, manifold-capacity substeps, non-finite terminations or resets, substeps). */
 int urgym_get_flags(urgym_handle* h, uint8_t* flags);
 const uint8_t* urgym_flags_device(urgym_handle* h);
 int urgym_get_stats(urgym_handle* h, int32_t* stats);
@@ -117,7 +119,13 @@ int urgym_set_rng(urgym_handle* h, const uint32_t* mt, const int32_t* elapsed);
  * the robot link index / -1 object base (Golf club parts 0, 1) / -2 any.  out: n_envs x max_pts x 24 doubles,
  * pybullet's tuple (flag, bodyA, bodyB, linkA, linkB, positionOnA[3], positionOnB[3], contactNormalOnB[3],
  * distance, normalForce, lateralFriction1, lateralFrictionDir1[3], lateralFriction2, lateralFrictionDir2[3]);
- * count: n_envs matching points (may exceed max_pts; only max_pts are written). */
+ * count: n_envs matching points (may exceed max_pts; only max_pts are written).
+ * Filters apply in pybullet's order: body_a alone decides the orientation (no swap when it is -1 or names the
+ * pair's A side; A/B fields exchanged and the normal negated when it names the B side), then body_b, link_a and
+ * link_b filter in that orientation.  A pair's A side: the robot link (robot pairs), the object (object-static
+ * pairs), the sphere or else the lower-numbered object (object-object pairs).
+ * Deviation: positions are the points' body-local anchors under the current poses; Bullet reports the world
+ * points of the last narrowphase, taken before that substep's integration (one substep's motion apart). */
 int urgym_contact_points(urgym_handle* h, int body_a, int body_b, int link_a, int link_b, int max_pts, double* out,
                          int32_t* count);
 

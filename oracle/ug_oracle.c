@@ -2454,14 +2454,21 @@ static void sanitize(ugo_env* e) {
 static int reset_impl(ugo_env* e, const double* draws, double* obs) {
     sanitize(e);
     e->goal_approached = e->goal_grasped = 0;
-    if (e->sc.variant == UG_TASK_TWOBALLS) return tb_reset(e, draws, obs);
-    switch (e->sc.task) {
-        case UG_TASK_BALLBALANCE: return bb_reset(e, draws, obs);
-        case UG_TASK_CUBESPUSH: return cp_reset(e, draws, obs);
-        case UG_TASK_CUBESGRASP: return cg_reset(e, draws, obs);
-        case UG_TASK_GOLF: return gf_reset(e, draws, obs);
+    int n = -1;
+    if (e->sc.variant == UG_TASK_TWOBALLS) n = tb_reset(e, draws, obs);
+    else switch (e->sc.task) {
+        case UG_TASK_BALLBALANCE: n = bb_reset(e, draws, obs); break;
+        case UG_TASK_CUBESPUSH: n = cp_reset(e, draws, obs); break;
+        case UG_TASK_CUBESGRASP: n = cg_reset(e, draws, obs); break;
+        case UG_TASK_GOLF: n = gf_reset(e, draws, obs); break;
     }
-    return -1;
+    /* a reset whose settling went non-finite is surfaced like a step's (flag + counter); its observation is
+     * returned as computed */
+    if (!state_finite(e)) {
+        e->flags |= UG_FLAG_NONFINITE;
+        e->stats[UG_STAT_NONFINITE]++;
+    }
+    return n;
 }
 int ugo_reset(ugo_env* e, double* obs) { return ugo_reset_draws(e, NULL, obs); }
 int ugo_reset_draws(ugo_env* e, const double* draws, double* obs) {
@@ -2494,9 +2501,12 @@ int ugo_step(ugo_env* e, const float* action, double* obs, double* reward, uint8
  * flag 0, bodyA, bodyB, linkA, linkB, positionOnA[3], positionOnB[3], contactNormalOnB[3], distance,
  * normalForce, lateralFriction1, lateralFrictionDir1[3], lateralFriction2, lateralFrictionDir2[3]; forces are
  * the last solve's impulses / dt, the friction directions btPlaneSpace1 of the normal (the solver's rows),
- * world positions from the points' body-local anchors with the current poses.  When the query's A matches the
- * pair's B side the tuple is swapped (A/B fields exchanged, normal negated).  Returns the number of matching
- * points (at most max_pts written). */
+ * world positions from the points' body-local anchors with the current poses (a deviation: Bullet reports the
+ * narrowphase's world points, taken before that substep's integration).  Filters as pybullet applies them
+ * (PhysicsServerCommandProcessor's contact query): the tuple is swapped (A/B fields exchanged, normal negated)
+ * when bodyA names the pair's B side, then bodyB / linkA / linkB filter that orientation; a pair's A side is the
+ * robot link for robot pairs, the object for object-static pairs, the sphere (else the lower object) for
+ * object-object pairs.  Returns the number of matching points (at most max_pts written). */
 static int link_of_collider(const scene* s, int ci) {
     const collider* c = &s->col[ci];
     if (c->ent == 0) return c->link;
@@ -2515,10 +2525,16 @@ int ugo_contact_points(const ugo_env* e, int bodyA, int bodyB, int linkA, int li
         const pairdef* P = &s->pair[M->pair];
         const int ea = s->col[P->a].ent, eb = s->col[P->b].ent;
         const int la = link_of_collider(s, P->a), lb = link_of_collider(s, P->b);
-        int swap;
-        if (match(bodyA, ea) && match(bodyB, eb) && match_link(linkA, la) && match_link(linkB, lb)) swap = 0;
-        else if (match(bodyA, eb) && match(bodyB, ea) && match_link(linkA, lb) && match_link(linkB, la)) swap = 1;
-        else continue;
+        /* pybullet's filter order: the orientation comes from bodyA alone (no swap without a bodyA filter, or
+         * when it names the pair's A side), then bodyB and the link filters apply in that orientation */
+        int swap = 0;
+        if (bodyA != -1) {
+            if (bodyA == ea) swap = 0;
+            else if (bodyA == eb) swap = 1;
+            else continue;
+        }
+        if (!match(bodyB, swap ? ea : eb) || !match_link(linkA, swap ? lb : la) || !match_link(linkB, swap ? la : lb))
+            continue;
         xf OA = owner_xf(e, &k, s->col[P->a].owner), OB = owner_xf(e, &k, s->col[P->b].owner);
         for (int j = 0; j < M->npts; j++) {
             const cpoint* c = &M->pt[j];

@@ -1,0 +1,119 @@
+"""The failure branches, driven on purpose: crafted states that overflow the manifold
+capacity (16) and the row capacity (128), run a wait_until_stable loop into its 480-substep cap ("did not stabilize",
+env_ball_balance_v0.py:102-103), and trigger the split-impulse pass (penetration deeper than 0.04).  Each case runs
+one env-step on the GPU and in the CPU restatement from the same crafted state: every output, the flags, the event
+counters and the final state are bit-identical, and the counter the case targets is > 0.
+
+The states were found with the restatement (arm folded into the table; a CubesGrasp joint move across the whole
+pan range against the joint's current motion; a cube 3 cm inside the table)."""
+import numpy as np
+import pytest
+
+from urgym_amd import layout as LY
+
+pytestmark = pytest.mark.gpu
+
+SEED = 20241220
+UNSTABLE, SPLIT, ROWCAP, MANCAP, NONFINITE, SUBSTEPS = range(6)
+FLAG_UNSTABLE, FLAG_DROPPED = 1, 4
+
+
+@pytest.fixture(scope="module")
+def mods(built):
+    from urgym_amd._native import Sim
+    from oracle.pyoracle import OracleEnv
+    return Sim, OracleEnv
+
+
+def crafted_step(Sim, OracleEnv, task, edits, action):
+    """reset n = len(edits) envs, apply edit k to env k's state on both sides, one env-step with `action`;
+    returns (GPU outputs, flags, stat increments)"""
+    n = len(edits)
+    sim = Sim(task, n, seed=SEED)
+    sim.set_autoreset(False, 0)
+    sim.reset()
+    st = sim.get_state()
+    ref = [OracleEnv(task, SEED + i) for i in range(n)]
+    for i, (r, edit) in enumerate(zip(ref, edits)):
+        r.reset()
+        assert np.array_equal(st[i], r.get_state()), i
+        edit(st[i])
+        r.set_state(st[i])
+    sim.set_state(st)
+    s0 = sim.stats().copy()
+    acts = np.repeat(np.asarray(action, np.float32)[None, :], n, 0)
+    out = sim.step(acts)
+    fl = sim.flags()
+    d = sim.stats() - s0
+    got = sim.get_state()
+    for i, r in enumerate(ref):
+        o, rew, term, succ, ns = r.step(acts[i])
+        assert np.array_equal(out["obs"][i], o) and out["reward"][i] == rew, i
+        assert bool(out["terminated"][i]) == term and bool(out["success"][i]) == succ, i
+        assert out["substeps"][i] == ns, (i, out["substeps"][i], ns)
+        assert fl[i] == r.flags(), (i, fl[i], r.flags())
+        assert np.array_equal(sim.stats()[i], r.stats()), (i, sim.stats()[i], r.stats())
+        assert np.array_equal(got[i], r.get_state()), i
+        assert np.all(np.isfinite(got[i]))
+    sim.close()
+    return out, fl, d
+
+
+def _fold(q1, q2):
+    def edit(s):
+        s[LY.F_Q + 1] = q1
+        s[LY.F_Q + 2] = q2
+        s[LY.F_QD:LY.F_QD + 12] = 0.0
+    return edit
+
+
+POSES = [(-0.5, 1.5), (0.0, 1.5), (0.5, 0.0), (1.0, 1.5), (0.5, 2.5)]
+
+
+@pytest.mark.parametrize("task", [0, 1])
+def test_manifold_and_row_capacity_overflow(mods, task):
+    """the arm folded into the table: more than 16 touching pairs and more than 128 contact rows.  The capacity
+    counters and the DROPPED flag fire (and, for the deepest poses, the 480 cap and the split pass too), equal to
+    the restatement's."""
+    Sim, OracleEnv = mods
+    out, fl, d = crafted_step(Sim, OracleEnv, task, [_fold(*p) for p in POSES], np.zeros(3))
+    assert (d[:, MANCAP] > 0).sum() >= 3 and (d[:, ROWCAP] > 0).sum() >= 4, d.tolist()
+    assert np.all((fl & FLAG_DROPPED) != 0), fl.tolist()
+    assert (d[:, SPLIT] > 0).all() and (d[:, UNSTABLE] > 0).any(), d.tolist()
+    assert np.array_equal((d[:, UNSTABLE] > 0), (fl & FLAG_UNSTABLE) != 0)
+
+
+def test_wait_until_stable_hits_the_480_cap(mods):
+    """CubesGrasp 'joint' move: the pan joint at -3.1 rad turning away at 2 rad/s is sent to +3.1 rad; at the
+    3.15 rad/s velocity limit the move outlasts 480 substeps, so wait_until_stable gives up (UNSTABLE flag and
+    counter, exactly 480 substeps); the control env (same move from rest at -3.0) settles before the cap."""
+    Sim, OracleEnv = mods
+
+    def edit(q0, qd0):
+        def e(s):
+            s[LY.F_Q + 0] = q0
+            s[LY.F_QD + 0] = qd0
+        return e
+
+    probe = Sim(2, 1, seed=SEED)
+    probe.reset()
+    q = probe.get_state()[0, LY.F_Q:LY.F_Q + 6].copy()
+    probe.close()
+    action = np.array([1.0, 0.0, 3.1] + list(q[1:6]) + [0.0], np.float32)  # random.choices -> always the move
+    out, fl, d = crafted_step(Sim, OracleEnv, 2, [edit(-3.1, -2.0), edit(-3.0, 0.0)], action)
+    assert d[0, UNSTABLE] == 1 and (fl[0] & FLAG_UNSTABLE) and out["substeps"][0] == 480, (d.tolist(), fl.tolist())
+    assert d[1, UNSTABLE] == 0 and not (fl[1] & FLAG_UNSTABLE) and out["substeps"][1] < 480
+
+
+def test_split_impulse_on_deep_penetration(mods):
+    """CubesPush: a cube pushed 3 cm into the table (penetration 0.05 > 0.04) is resolved with the split-impulse
+    pass (btSequentialImpulseConstraintSolver's split path [ext]); the counter fires and the result is exact."""
+    Sim, OracleEnv = mods
+
+    def sink(dz):
+        def e(s):
+            s[LY.obj(0) + 2] = dz
+        return e
+
+    out, fl, d = crafted_step(Sim, OracleEnv, 1, [sink(-0.03), sink(0.019)], np.zeros(3))
+    assert d[0, SPLIT] >= 1 and d[1, SPLIT] == 0, d.tolist()

@@ -92,3 +92,75 @@ def test_sb3_adapter_and_torch_env_match_host_path(built):
     assert torch.isfinite(rew).all() and rew.shape == (5,)
     for e in (ref, sb, tv):
         e.close()
+
+
+@pytest.mark.gpu
+def test_sb3_adapter_matches_oracle_through_truncation(built):
+    """URGymSB3VecEnv against the CPU restatement: obs, float32 rewards, dones, infos'
+    terminal_observation / TimeLimit.truncated / is_success, across CubesGrasp's 20-step limit, every value
+    bit-identical to what SB3's DummyVecEnv over the reference env would return (training.py:25-41)."""
+    from oracle.pyoracle import OracleEnv
+    from urgym_amd.vec import URGymSB3VecEnv
+    n, T, seed = 8, 23, 99
+    env = URGymSB3VecEnv("URGym/CubesGrasp-v0", n, seed=seed)
+    ref = [OracleEnv(2, seed + i) for i in range(n)]
+    obs = env.reset()
+    for i, r in enumerate(ref):
+        assert np.array_equal(obs[i], r.reset()[0]), i
+    el = np.zeros(n, int)
+    rng = np.random.default_rng(1)
+    lo = np.array([0, 0] + [-np.pi] * 6 + [0])
+    hi = np.array([1, 1] + [np.pi] * 6 + [1])
+    saw = {"trunc": 0, "term": 0}
+    for t in range(T):
+        a = rng.uniform(lo, hi, size=(n, 9)).astype(np.float32)
+        obs, rew, dones, infos = env.step(a)
+        assert rew.dtype == np.float32 and dones.dtype == bool and len(infos) == n
+        for i, r in enumerate(ref):
+            o, rw, term, succ, _ = r.step(a[i])
+            el[i] += 1
+            trunc = el[i] >= 20
+            assert rew[i] == np.float32(rw), (t, i)
+            assert dones[i] == (term or trunc), (t, i)
+            assert infos[i]["is_success"] == succ, (t, i)
+            if term or trunc:
+                assert np.array_equal(infos[i]["terminal_observation"], o), (t, i)
+                assert infos[i]["TimeLimit.truncated"] == (trunc and not term), (t, i)
+                saw["trunc" if trunc and not term else "term"] += 1
+                o, _ = r.reset()
+                el[i] = 0
+            else:
+                assert "terminal_observation" not in infos[i] and "TimeLimit.truncated" not in infos[i]
+            assert np.array_equal(obs[i], o), (t, i)
+    assert saw["trunc"] > 0
+    env.close()
+
+
+@pytest.mark.gpu
+def test_torch_env_orders_itself_against_the_callers_stream(built):
+    """URGymTorchVecEnv used from torch's current stream, outside stream_context: actions
+    made on the caller's stream are read only after they exist, outputs are readable on the caller's stream
+    without a manual sync -- equal to the host C-ABI path step by step."""
+    import torch
+    from urgym_amd._native import Sim
+    from urgym_amd.vec import URGymTorchVecEnv
+    n, T, seed = 64, 5, 5
+    ref = Sim(0, n, seed=seed)
+    ref.set_autoreset(True, 500)
+    o_ref = ref.reset()
+    tv = URGymTorchVecEnv("URGym/BallBalance-v0", n, seed=seed)
+    o = tv.reset().clone()  # a clone on the caller's stream, after the reset kernel
+    assert np.array_equal(o.cpu().numpy(), o_ref)
+    rng = np.random.default_rng(0)
+    for _ in range(T):
+        a = rng.uniform(-0.1, 0.1, (n, 3)).astype(np.float32)
+        big = torch.randn(2048, 2048, device=tv.device)  # keep the caller's stream busy before the actions exist
+        big = big @ big
+        ta = torch.from_numpy(a).to(tv.device) + 0.0 * big[0, 0]
+        ot, rt, tt, trt, _ = tv.step(ta)
+        got_o, got_r = ot.clone(), rt.clone()  # on the caller's stream
+        del ta
+        r = ref.step(a)
+        assert np.array_equal(got_o.cpu().numpy(), r["obs"]) and np.array_equal(got_r.cpu().numpy(), r["reward"])
+    tv.close()
+    ref.close()

@@ -11,7 +11,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("URGYM_LIB") or os.path.join(_HERE, "_lib", "liburgym.so")
 
-# C-ABI symbols declared in include/urgym.h (checked by tests/test_capi_symbols.py)
+# C-ABI symbols declared in include/urgym.h (tests/test_capi.py checks that the library exports each one)
 SYMBOLS = [
     "urgym_create", "urgym_destroy", "urgym_last_error", "urgym_obs_dim", "urgym_act_dim", "urgym_state_dim",
     "urgym_num_envs", "urgym_set_autoreset", "urgym_reset", "urgym_num_draws", "urgym_step", "urgym_step_device",

@@ -247,7 +247,10 @@ __global__ void __launch_bounds__(TEAM, 1) k_reset(const Scene* sc, double* S, u
                                                    int32_t* substeps, int* stats, uint8_t* flags) {
     const int i = blockIdx.x;
     if (i >= n) return;
-    if (mask && !mask[i]) return;
+    if (mask && !mask[i]) { /* nothing happened to a masked-out env in this call */
+        if (threadIdx.x == 0) flags[i] = 0;
+        return;
+    }
     double* Si = S + (size_t)i * UG_STATE_DIM;
     team_load(Si, stats + (size_t)i * UG_NSTAT);
     RunIO io;
@@ -381,7 +384,9 @@ __global__ void __launch_bounds__(WAVE) k_ik(const double* S, int n, const doubl
  * query, not on the step path).  Same definition as the oracle's ugo_contact_points: entity codes (0 robot,
  * 1 + i object i, 10 table, 11 plane, 12 pitch, -1 any), links (robot link index, object base -1 / club parts
  * 0, 1, -2 any), 24 doubles per point in pybullet's tuple order, forces = impulse / dt, friction directions
- * btPlaneSpace1 of the normal, swapped tuple when the query's A is the pair's B side. */
+ * btPlaneSpace1 of the normal; the tuple is swapped when bodyA names the pair's B side, and bodyB / linkA /
+ * linkB filter in that orientation (pybullet's order).  Positions use the current poses (Bullet: the
+ * narrowphase's world points, before that substep's integration -- a documented deviation). */
 __device__ static int link_of_collider(const Scene* s, int ci) {
     const Collider& c = s->col[ci];
     if (c.ent == 0) return c.link;
@@ -404,10 +409,13 @@ __global__ void __launch_bounds__(WAVE) k_contacts(const Scene* sc, const double
         const int la = link_of_collider(sc, P.a), lb = link_of_collider(sc, P.b);
         auto mt = [](int want, int have) { return want == -1 || want == have; };
         auto ml = [](int want, int have) { return want == -2 || want == have; };
-        int swap;
-        if (mt(bodyA, ea) && mt(bodyB, eb) && ml(linkA, la) && ml(linkB, lb)) swap = 0;
-        else if (mt(bodyA, eb) && mt(bodyB, ea) && ml(linkA, lb) && ml(linkB, la)) swap = 1;
-        else continue;
+        int swap = 0; /* pybullet's order: orientation from bodyA alone, then the other filters */
+        if (bodyA != -1) {
+            if (bodyA == ea) swap = 0;
+            else if (bodyA == eb) swap = 1;
+            else continue;
+        }
+        if (!mt(bodyB, swap ? ea : eb) || !ml(linkA, swap ? lb : la) || !ml(linkB, swap ? la : lb)) continue;
         const XF OA = owner_xf(e, k, sc->col[P.a].owner), OB = owner_xf(e, k, sc->col[P.b].owner);
         const int np = (int)M.npts;
         for (int j = 0; j < np; j++) {

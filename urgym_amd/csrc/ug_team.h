@@ -3193,6 +3193,10 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
         case G_RESET_DONE:
             e.goal_approached = 0.0;
             e.goal_grasped = 0.0;
+            if (!state_finite(s, e)) { /* a reset that settled into a non-finite state: surfaced (oracle reset_impl) */
+                g_sh.flags |= UG_FLAG_NONFINITE;
+                g_sh.stats[UG_STAT_NONFINITE]++;
+            }
             task_obs(s, e, io.obs);
             io.reset_done = 1;
             *next = G_END;

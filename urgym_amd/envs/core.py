@@ -18,6 +18,31 @@ except Exception:  # pragma: no cover
     _VecBase = object
 
 
+def _batched(space, n):
+    """gymnasium's batch_space for the stand-in Box (the batched space a VectorEnv consumer reads)"""
+    from ..spaces import Box
+    return Box(np.tile(space.low, (n,) + (1,) * space.low.ndim), np.tile(space.high, (n,) + (1,) * space.high.ndim),
+               dtype=space.dtype)
+
+
+def _init_vector_base(env, num_envs, obs_space, act_space):
+    """Run the base VectorEnv's constructor when gymnasium is present (0.29: VectorEnv.__init__(num_envs, obs,
+    act) batches the spaces; 1.x: no constructor arguments, the batched spaces are set here); with the stand-in
+    base the batched spaces are built the same way."""
+    if _VecBase is object:
+        env.observation_space, env.action_space = _batched(obs_space, num_envs), _batched(act_space, num_envs)
+        return
+    try:  # pragma: no cover - gymnasium is absent in this image
+        _VecBase.__init__(env, num_envs, obs_space, act_space)
+    except TypeError:  # pragma: no cover
+        from gymnasium.vector.utils import batch_space
+        _VecBase.__init__(env)
+        env.observation_space = batch_space(obs_space, num_envs)
+        env.action_space = batch_space(act_space, num_envs)
+    env.num_envs = num_envs
+    env.single_observation_space, env.single_action_space = obs_space, act_space
+
+
 def _check_kwargs(camera, reward_type):
     if camera is not None:
         raise NotImplementedError("camera rendering is outside the hot-path scope (SURVEY.md 8(f)4)")
@@ -53,12 +78,13 @@ class URGymVectorEnv(_VecBase):
         self.task = task
         self.num_envs = num_envs
         self.single_observation_space, self.single_action_space = spaces_for(task)
+        _init_vector_base(self, num_envs, self.single_observation_space, self.single_action_space)
         self.sim = Sim(task, num_envs, device=device, seed=seed, env_offset=env_offset)
         self.sim.set_reward_type(reward_type)
         self.reward_type = reward_type
         self.max_episode_steps = max_episode_steps or 0
         self.sim.set_autoreset(True, self.max_episode_steps)
-        self.render_mode = render_mode  # 'human' GUI is not supported (documented deviation)
+        self.render_mode = render_mode  # accepted; there is no GUI ('human' opens no window: documented deviation)
 
     def reset(self, *, seed=None, options=None):
         obs = self.sim.reset()
@@ -94,6 +120,8 @@ class URGymEnv(_EnvBase):
                  render_mode="human"):
         from . import spaces_for
         _check_kwargs(camera, reward_type)
+        if _EnvBase is not object:  # pragma: no cover - gymnasium is absent in this image
+            _EnvBase.__init__(self)
         self.task = task
         self.observation_space, self.action_space = spaces_for(task)
         self.sim = Sim(task, 1, device=device, seed=seed)
@@ -102,7 +130,7 @@ class URGymEnv(_EnvBase):
         self.max_episode_steps = max_episode_steps or 0
         self.sim.set_autoreset(False, 0)
         self._elapsed = 0
-        self.render_mode = render_mode
+        self.render_mode = render_mode  # accepted; 'human' opens no GUI window (documented deviation)
 
     def reset(self, *, seed=None, options=None):
         self._elapsed = 0

@@ -30,9 +30,13 @@ class URGymSB3VecEnv(_SB3VecEnv):
         if env_id in UNSUPPORTED:
             raise NotImplementedError(f"{env_id} is outside this build's hot-path scope (SURVEY.md 8(f))")
         self.task, self.max_episode_steps = TASKS[env_id]
-        self.num_envs = num_envs
-        self.observation_space, self.action_space = spaces_for(self.task)
         self.render_mode = None
+        obs_space, act_space = spaces_for(self.task)
+        if _SB3VecEnv is not object:  # pragma: no cover - SB3 is absent in this image
+            # SB3's constructor sets num_envs / spaces / reset_infos / _seeds / _options / render_mode
+            _SB3VecEnv.__init__(self, num_envs, obs_space, act_space)
+        self.num_envs = num_envs
+        self.observation_space, self.action_space = obs_space, act_space
         self.sim = Sim(self.task, num_envs, device=device, seed=seed, env_offset=env_offset)
         self.sim.set_reward_type(reward_type)
         self.sim.set_autoreset(True, self.max_episode_steps)
@@ -121,34 +125,56 @@ class URGymTorchVecEnv:
         self.substeps = torch.zeros(n, dtype=torch.int32, device=self.device)
         self.low = torch.as_tensor(np.asarray(self.action_space.low), dtype=torch.float32, device=self.device)
         self.high = torch.as_tensor(np.asarray(self.action_space.high), dtype=torch.float32, device=self.device)
+        # the buffers were zero-filled on the caller's stream; the handle's stream is non-blocking
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
 
     def stream_context(self):
         """with env.stream_context(): torch work (the policy) is ordered with the env kernels"""
         return self.torch.cuda.stream(self.stream)
 
+    def _enter(self):
+        """order the env stream after the caller's current stream (actions produced there); returns it"""
+        cur = self.torch.cuda.current_stream(self.device)
+        if cur != self.stream:
+            self.stream.wait_stream(cur)
+        return cur
+
+    def _leave(self, cur):
+        """order the caller's current stream after the env kernels, so it may read the outputs directly"""
+        if cur != self.stream:
+            cur.wait_stream(self.stream)
+
     def reset(self):
         import ctypes
         v = ctypes.c_void_p
+        cur = self._enter()
         self.sim._chk(self.sim.L.urgym_reset_device(self.sim.h, None, None, v(self.obs.data_ptr())), "urgym_reset_device")
+        self._leave(cur)
         return self.obs
 
     def step(self, actions):
-        """actions: (n, act_dim) float32 CUDA tensor, ordered before this call on the env stream.  Returns the
-        device buffers (obs, reward, terminated, truncated, final_obs) -- overwritten by the next step."""
-        a = actions.to(dtype=self.torch.float32).contiguous()
+        """actions: (n, act_dim) CUDA tensor from any stream of the env's device (the env stream waits for the
+        caller's current stream).  Returns the device buffers (obs, reward, terminated, truncated, final_obs),
+        ordered before later work on the caller's current stream and overwritten by the next step."""
+        cur = self._enter()
+        with self.stream_context():  # the float32 copy (if any) is made on the env stream
+            a = actions.to(dtype=self.torch.float32).contiguous()
+        if a.data_ptr() == actions.data_ptr():
+            a.record_stream(self.stream)  # the caller's tensor: not reused before the kernel has read it
         self.sim.step_device(a.data_ptr(), self.obs.data_ptr(), self.final_obs.data_ptr(), self.reward.data_ptr(),
                              self.terminated.data_ptr(), self.truncated.data_ptr(), self.success.data_ptr(),
                              self.substeps.data_ptr())
-        self._last_actions = a  # keep the action buffer alive until the kernel has read it
+        self._leave(cur)
         return self.obs, self.reward, self.terminated, self.truncated, self.final_obs
 
     def rollout(self, policy, steps):
         """Run `policy(obs) -> actions` (a torch module / function on the device) for `steps` batched env steps
         on the env stream; returns per-step reward sums and done counts (tensors on the device)."""
         torch = self.torch
-        rew = torch.zeros(steps, dtype=torch.float64, device=self.device)
-        done = torch.zeros(steps, dtype=torch.int64, device=self.device)
+        cur = self._enter()
         with self.stream_context():
+            rew = torch.zeros(steps, dtype=torch.float64, device=self.device)
+            done = torch.zeros(steps, dtype=torch.int64, device=self.device)
             obs = self.obs
             for t in range(steps):
                 with torch.no_grad():
@@ -157,6 +183,7 @@ class URGymTorchVecEnv:
                 obs, r, term, trunc, _ = self.step(act)
                 rew[t] = r.sum()
                 done[t] = (term | trunc).sum()
+        self._leave(cur)
         return rew, done
 
     def sync(self):
