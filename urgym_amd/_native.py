@@ -36,6 +36,13 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"liburgym.so not built ({LIB_PATH}); run __graft_entry__.build() -- no CPU fallback exists")
+    # torch, when installed, is loaded first: it bundles its own HIP runtime, and importing it after this library
+    # has initialised the /opt/rocm runtime leaves torch.cuda unavailable in the process (measured on MI355X,
+    # tools/gpu_diag.sh); the other order works, and the device tensors / streams of vec.py need torch's side
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is part of this image
+        pass
     L = ctypes.CDLL(LIB_PATH)
     P, I, D, U32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_uint32
     L.urgym_create.restype = P

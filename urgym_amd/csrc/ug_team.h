@@ -493,6 +493,7 @@ __device__ __forceinline__ static void team_reduce4(int n, int k) {
  * Writes cand k (0..4 points). */
 /* column / element picks by selects: run-time indices into register-resident matrices made team_box_box read wrong
  * values (measured: the face normal and clip frame came out of the wrong column), so every pick is explicit */
+#ifndef UG_BB_DYNIDX
 __device__ __forceinline__ v3 colsel(const m3& A, int i) {
     return i == 0 ? V(A.m[0], A.m[3], A.m[6]) : i == 1 ? V(A.m[1], A.m[4], A.m[7]) : V(A.m[2], A.m[5], A.m[8]);
 }
@@ -503,6 +504,11 @@ __device__ __forceinline__ m3 msel(bool c, const m3& a, const m3& b) {
     for (int i = 0; i < 9; i++) r.m[i] = c ? a.m[i] : b.m[i];
     return r;
 }
+#else /* investigation build (tools/bb_dynidx.sh): the run-time-indexed picks the selects replaced */
+__device__ __forceinline__ v3 colsel(const m3& A, int i) { return V(A.m[i], A.m[3 + i], A.m[6 + i]); }
+__device__ __forceinline__ double sel3(const double (&a)[3], int i) { return a[i]; }
+__device__ __forceinline__ m3 msel(bool c, const m3& a, const m3& b) { return c ? a : b; }
+#endif
 #ifdef UG_BB_CHECK
 static __shared__ int g_bbdbg[8];
 #endif
@@ -577,7 +583,11 @@ __device__ __forceinline__ static void team_box_box(const XF& TA, const double (
         if (nR >= 0) { /* column nR % 3 of R1 (nR < 3) or R2, by selects (no dynamic register indexing) */
             const m3& Rn = nR < 3 ? R1 : R2;
             const int c = nR % 3;
+#ifndef UG_BB_DYNIDX
             normal = c == 0 ? V(Rn.m[0], Rn.m[3], Rn.m[6]) : c == 1 ? V(Rn.m[1], Rn.m[4], Rn.m[7]) : V(Rn.m[2], Rn.m[5], Rn.m[8]);
+#else
+            normal = V(Rn.m[c], Rn.m[3 + c], Rn.m[6 + c]);
+#endif
         } else {
             normal = mv(R1, V(readlane_d(nc.x, tsel), readlane_d(nc.y, tsel), readlane_d(nc.z, tsel)));
         }
@@ -773,6 +783,18 @@ __device__ __forceinline__ static void team_box_box(const XF& TA, const double (
     if (lane == 0) sh.u.cand.n[k] = nout;
 #ifdef UG_BB_CHECK
     if (lane == 0) { g_bbdbg[0] = code; g_bbdbg[1] = tsel; g_bbdbg[2] = nR; }
+#ifdef UG_BB_DYNIDX /* every lane's view of the picked values (a lane whose index disagrees would show here) */
+    {
+        const v3 n0 = nR >= 0 ? V((nR < 3 ? R1 : R2).m[nR % 3], (nR < 3 ? R1 : R2).m[3 + nR % 3], (nR < 3 ? R1 : R2).m[6 + nR % 3]) : V(0, 0, 0);
+        const v3 n1 = nR >= 0 ? (nR % 3 == 0 ? V((nR < 3 ? R1 : R2).m[0], (nR < 3 ? R1 : R2).m[3], (nR < 3 ? R1 : R2).m[6])
+                                : nR % 3 == 1 ? V((nR < 3 ? R1 : R2).m[1], (nR < 3 ? R1 : R2).m[4], (nR < 3 ? R1 : R2).m[7])
+                                              : V((nR < 3 ? R1 : R2).m[2], (nR < 3 ? R1 : R2).m[5], (nR < 3 ? R1 : R2).m[8]))
+                              : V(0, 0, 0);
+        if (n0.x != n1.x || n0.y != n1.y || n0.z != n1.z)
+            printf("BBIDX lane %d code %d nR %d tsel %d dyn (%.17g %.17g %.17g) sel (%.17g %.17g %.17g)\n", lane, code, nR,
+                   tsel, n0.x, n0.y, n0.z, n1.x, n1.y, n1.z);
+    }
+#endif
 #endif
     __syncthreads();
 }
