@@ -46,11 +46,11 @@ def cpu_model():
     return "unknown"
 
 
-def _oracle_sample(task, n, threads, seconds):
+def _oracle_sample(task, n, threads, seconds, flags=0):
     import ctypes
     from oracle.pyoracle import OracleEnv, lib as olib
     from urgym_amd.envs import spaces_for
-    envs = [OracleEnv(task, 20241220 + i) for i in range(n)]
+    envs = [OracleEnv(task, 20241220 + i, flags=flags) for i in range(n)]
     for e in envs:
         e.reset()
     arr = (ctypes.c_void_p * n)(*[e.h for e in envs])
@@ -71,15 +71,15 @@ def _oracle_sample(task, n, threads, seconds):
     return steps, substeps, time.perf_counter() - t0
 
 
-def cpu_baseline(task, seconds=10.0, seconds_1core=5.0):
+def cpu_baseline(task, seconds=10.0, seconds_1core=5.0, flags=0):
     """CPU restatement (oracle/, test infrastructure) timed on this host's cores: bounded samples of the same
     workload (same task, random actions, autoreset) -- all cores with OpenMP (one env per thread at a time,
     4 envs per thread) and the 1-env / 1-core analogue of config A."""
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     os.environ["OMP_NUM_THREADS"] = str(threads)
     n = 4 * threads
-    steps, substeps, dt = _oracle_sample(task, n, threads, seconds)
-    s1, sub1, dt1 = _oracle_sample(task, 1, 1, seconds_1core)
+    steps, substeps, dt = _oracle_sample(task, n, threads, seconds, flags)
+    s1, sub1, dt1 = _oracle_sample(task, 1, 1, seconds_1core, flags)
     return {"value": steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(),
             "sample": f"{TASK_NAMES[task]} x {n} envs, {steps} env-steps incl. autoresets ({substeps} substeps) in "
@@ -136,6 +136,9 @@ def main(argv=None):
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--task", type=int, default=0)
+    ap.add_argument("--geometry", choices=("lod", "full"), default="lod",
+                    help="robot collision hulls: lod (<= 48 vertices, default) or full (every vertex of PyBullet's mesh hull, "
+                         "URGYM_FLAG_FULL_GEOMETRY)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL over xGMI); gloo only to rehearse several ranks "
@@ -159,9 +162,10 @@ def main(argv=None):
         world = dist.get_world_size()
     dev = torch.device("cuda", gpu)
 
-    from urgym_amd._native import Sim
+    from urgym_amd._native import GEOM_FULL, Sim
     n = args.envs
-    sim = Sim(args.task, n, device=gpu, seed=20241220, env_offset=rank * n)
+    geom_flags = GEOM_FULL if args.geometry == "full" else 0
+    sim = Sim(args.task, n, device=gpu, seed=20241220, env_offset=rank * n, flags=geom_flags)
     sim.set_autoreset(True, MAX_STEPS[args.task])
     sim.reset()
     A, O = sim.act_dim, sim.obs_dim
@@ -284,7 +288,7 @@ def main(argv=None):
         "data": "synthetic: uniform random actions (PCG64 seed 20241220+rank), per-env MT19937 reset draws",
         "config": {"workload": f"{TASK_NAMES[args.task]} x {n} envs per GPU, autoreset, max_episode_steps "
                                f"{MAX_STEPS[args.task]}", "envs_per_gpu": n, "total_envs": n * world,
-                   "parallelism": f"env-dp{world}", "world_size": world,
+                   "parallelism": f"env-dp{world}", "world_size": world, "geometry": args.geometry,
                    "backend": args.backend if world > 1 else None},
         "rep_values": [env_steps / x[0] for x in reps],
         "substeps_per_env_step": substeps / env_steps,
@@ -292,7 +296,7 @@ def main(argv=None):
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.task, args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(args.task, args.cpu_seconds, flags=geom_flags)
     if rank == 0:
         print(json.dumps(line), flush=True)
     sim.close()

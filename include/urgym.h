@@ -41,6 +41,14 @@ typedef struct urgym_handle urgym_handle;
 urgym_handle* urgym_create(int task_id, int n_envs, int device_ordinal, int precision, uint32_t seed,
                            int env_offset);
 
+/* urgym_create with creation flags (0 = urgym_create).  URGYM_FLAG_FULL_GEOMETRY: the robot's mesh colliders are
+ * PyBullet's convex hulls of all mesh vertices (URDF2Bullet: btConvexHullShape + optimizeConvexHull, up to 865
+ * vertices / 1306 faces per link) instead of the default <= 48-vertex collision LOD; same contact algorithm.
+ * Slower (more vertices and faces per hull pair); parity: bit-identical to the CPU restatement's same mode. */
+#define URGYM_FLAG_FULL_GEOMETRY 1 /* == UG_GEOM_FULL (urgym_amd/csrc/ug_layout.h) */
+urgym_handle* urgym_create_ex(int task_id, int n_envs, int device_ordinal, int precision, uint32_t seed,
+                              int env_offset, int flags);
+
 /* Replaces: Env.close() -> p.disconnect (env_ball_balance_v0.py:172-173). */
 void urgym_destroy(urgym_handle* h);
 

@@ -26,6 +26,8 @@ def lib(path=None):
         P, D, I, U32 = ctypes.c_void_p, ctypes.c_double, ctypes.c_int, ctypes.c_uint32
         L.ugo_create.restype = P
         L.ugo_create.argtypes = [I, U32]
+        L.ugo_create_ex.restype = P
+        L.ugo_create_ex.argtypes = [I, U32, I]
         L.ugo_destroy.argtypes = [P]
         L.ugo_obs_dim.argtypes = [I]
         L.ugo_act_dim.argtypes = [I]
@@ -93,10 +95,11 @@ def _p(a):
 class OracleEnv:
     """One environment of the CPU restatement."""
 
-    def __init__(self, task, seed, lib_path=None):
+    def __init__(self, task, seed, lib_path=None, flags=0):
+        """flags: 1 = full geometry (UG_GEOM_FULL / URGYM_FLAG_FULL_GEOMETRY)"""
         self.L = lib(lib_path)
         self.task = task
-        self.h = self.L.ugo_create(task, seed)
+        self.h = self.L.ugo_create_ex(task, seed, flags)
         self.obs_dim = self.L.ugo_obs_dim(task)
         self.act_dim = self.L.ugo_act_dim(task)
         self.state_dim = self.L.ugo_state_dim()

@@ -40,7 +40,7 @@ int ugo_fid_box_box(const double* ha, const double* Ra, const double* pa, const 
     fp_box(&g_fpA, &TA, &A);
     fp_box(&g_fpB, &TB, &B);
     static candlist L;
-    L.n = 0;
+    cand_init(&L, MAXCAND);
     fp_hull_hull(&g_fpA, &g_fpB, 0.0, 0.0, thr, &L);
     int n = L.n < max_pts ? L.n : max_pts;
     for (int i = 0; i < n; i++) {
@@ -367,7 +367,7 @@ int ugo_fid_box_box(const double* ha, const double* Ra, const double* pa, const 
     fp_box(&g_fpA, &TA, &A);
     fp_box(&g_fpB, &TB, &B);
     static candlist L;
-    L.n = 0;
+    cand_init(&L, MAXCAND);
     fp_hull_hull(&g_fpA, &g_fpB, 0.0, 0.0, thr, &L);
     int n = L.n < max_pts ? L.n : max_pts;
     for (int i = 0; i < n; i++) {

@@ -32,8 +32,9 @@
 #define MAXCOL 28
 #define MAXPAIR 160
 #ifndef MAXCAND
-#define MAXCAND 64
+#define MAXCAND 1024 /* candidate storage: a full hull's vertices + the box corners (UG_FULL_HULL_MAXV + 8) */
 #endif
+#define LOD_MAXCAND 64 /* candidates a hull pair keeps with the LOD hulls (the kernels' LDS list) */
 #define PT_DOUBLES UG_PT_DOUBLES
 #define MAN_DOUBLES UG_MAN_DOUBLES
 #define STATE_DIM UG_STATE_DIM
@@ -240,6 +241,7 @@ typedef struct {
     int owner;        /* >=0 robot body, -1 fixed robot base, -2-i object i, -100 static */
     int ent;          /* 0 robot, 1+i object i, 10+s static s */
     int link;         /* pybullet link index for robot colliders, -1 otherwise */
+    int full;         /* full-geometry mode (URGYM_FLAG_FULL_GEOMETRY): hull pairs keep every candidate */
 } collider;
 
 typedef struct { int a, b; double thr, friction, restitution, rolling; } pairdef;
@@ -247,6 +249,7 @@ typedef struct { int a, b; double thr, friction, restitution, rolling; } pairdef
 typedef struct {
     int task;    /* base task: scene and physics */
     int variant; /* the env id's task (a variant shares its base task's scene) */
+    int full;    /* full-geometry mode: robot hulls with every vertex and face of the mesh's convex hull */
     double gravity;
     int nobj;
     double omass[MAXOBJ];
@@ -319,9 +322,10 @@ static void add_pair(scene* s, int a, int b) {
     p->rolling = r;
 }
 
-static void build_scene(scene* s, int variant) {
+static void build_scene(scene* s, int variant, int flags) {
     memset(s, 0, sizeof(*s));
     const int task = UG_BASE_TASK(variant);
+    s->full = (flags & UG_GEOM_FULL) != 0;
     s->task = task;
     s->variant = variant;
     s->gravity = task == UG_TASK_CUBESGRASP ? -10.0 : -9.8; /* env_cubes_grasp_v0.py:43 vs :59 */
@@ -337,6 +341,9 @@ static void build_scene(scene* s, int variant) {
         c->half[0] = UG_SHAPE_HALF[3 * si]; c->half[1] = UG_SHAPE_HALF[3 * si + 1]; c->half[2] = UG_SHAPE_HALF[3 * si + 2];
         c->margin = UG_URDF_MARGIN;
         c->v0 = UG_SHAPE_V0[si]; c->nv = UG_SHAPE_NV[si]; c->f0 = UG_SHAPE_F0[si]; c->nf = UG_SHAPE_NF[si];
+        if (s->full) { /* PyBullet's hull of all mesh vertices instead of the collision LOD */
+            c->v0 = UG_SHAPE_FV0[si]; c->nv = UG_SHAPE_FNV[si]; c->f0 = UG_SHAPE_FF0[si]; c->nf = UG_SHAPE_FNF[si];
+        }
         c->R = mload(&UG_SHAPE_R[9 * si]);
         c->P = V(UG_SHAPE_P[3 * si], UG_SHAPE_P[3 * si + 1], UG_SHAPE_P[3 * si + 2]);
         c->aR = mload(&UG_LINK_COMR[9 * l]);
@@ -348,6 +355,7 @@ static void build_scene(scene* s, int variant) {
         c->owner = UG_LINK_BODY[l];
         c->ent = 0;
         c->link = l;
+        c->full = s->full;
     }
     int nrobot = s->ncol;
     int statics[4], nstat = 0;
@@ -700,9 +708,13 @@ static void world_aabb(const xf* O, const collider* c, v3* lo, v3* hi) {
 
 /* contact candidate: normal on B (world, B->A), point on B (world), signed distance */
 typedef struct { v3 n, pB; double d; } cand;
-typedef struct { int n; cand c[MAXCAND]; } candlist;
+typedef struct { int n, cap; cand c[MAXCAND]; } candlist;
+static void cand_init(candlist* L, int cap) {
+    L->n = 0;
+    L->cap = cap < MAXCAND ? cap : MAXCAND;
+}
 static void cand_add(candlist* L, v3 n, v3 pB, double d) {
-    if (L->n < MAXCAND) { L->c[L->n].n = n; L->c[L->n].pB = pB; L->c[L->n].d = d; L->n++; }
+    if (L->n < L->cap) { L->c[L->n].n = n; L->c[L->n].pB = pB; L->c[L->n].d = d; L->n++; }
 }
 
 /* btSphereBoxCollisionAlgorithm::getSphereDistance [ext]: sphere A, box B */
@@ -1042,8 +1054,8 @@ static void nc_hull_box(const xf* TA, const collider* A, const xf* TB, const col
     v3 pAB = mtv(&TB->R, vsub(TA->p, TB->p));
     v3 h = V(B->half[0], B->half[1], B->half[2]);
     double mA = A->margin;
-    candlist L;
-    L.n = 0;
+    static _Thread_local candlist L;
+    cand_init(&L, A->full ? MAXCAND : LOD_MAXCAND);
     for (int i = 0; i < A->nv; i++) {
         const double* vv = &UG_HULL_V[3 * (A->v0 + i)];
         v3 x = vadd(mv(&RAB, V(vv[0], vv[1], vv[2])), pAB);
@@ -1099,8 +1111,8 @@ static void nc_hull_box(const xf* TA, const collider* A, const xf* TB, const col
  * against A's planes, deepest + farthest-spread 4 points */
 static void nc_hull_hull(const xf* TA, const collider* A, const xf* TB, const collider* B, double thr, candlist* out) {
     double mA = A->margin, mB = B->margin;
-    candlist L;
-    L.n = 0;
+    static _Thread_local candlist L;
+    cand_init(&L, A->full ? MAXCAND : LOD_MAXCAND);
     /* A vertex x in B's frame: max over B's faces of n.x - d */
     m3 RAB = mtm(&TB->R, &TA->R);
     v3 pAB = mtv(&TB->R, vsub(TA->p, TB->p));
@@ -1276,7 +1288,7 @@ static void collide(ugo_env* e, const kin* k) {
         const collider* B = &s->col[b];
         xf TA = shape_xf(&O[a], A), TB = shape_xf(&O[b], B);
         candlist L;
-        L.n = 0;
+        cand_init(&L, LOD_MAXCAND);
         if (A->kind == UG_SHAPE_SPHERE && B->kind == UG_SHAPE_BOX) nc_sphere_box(&TA, A, &TB, B, P->thr, &L);
         else if (A->kind == UG_SHAPE_SPHERE && B->kind == UG_SHAPE_SPHERE) nc_sphere_sphere(&TA, A, &TB, B, P->thr, &L);
         else if (A->kind == UG_SHAPE_BOX && B->kind == UG_SHAPE_BOX) nc_box_box(&TA, A, &TB, B, P->thr, &L);
@@ -1286,7 +1298,7 @@ static void collide(ugo_env* e, const kin* k) {
         else if (A->kind == UG_SHAPE_SPHERE && B->kind == UG_SHAPE_HULL) {
             /* hull-sphere with swapped roles: flip normal, move the point onto the sphere */
             candlist L2;
-            L2.n = 0;
+            cand_init(&L2, LOD_MAXCAND);
             nc_hull_sphere(&TB, B, &TA, A, P->thr, &L2);
             for (int i = 0; i < L2.n; i++)
                 cand_add(&L, vneg(L2.c[i].n), vadd(L2.c[i].pB, vscale(L2.c[i].n, L2.c[i].d)), L2.c[i].d);
@@ -1294,7 +1306,7 @@ static void collide(ugo_env* e, const kin* k) {
         else if (A->kind == UG_SHAPE_BOX && B->kind == UG_SHAPE_SPHERE) {
             /* sphere-box with swapped roles: flip normal, move the point onto the sphere */
             candlist L2;
-            L2.n = 0;
+            cand_init(&L2, LOD_MAXCAND);
             nc_sphere_box(&TB, B, &TA, A, P->thr, &L2);
             for (int i = 0; i < L2.n; i++)
                 cand_add(&L, vneg(L2.c[i].n), vadd(L2.c[i].pB, vscale(L2.c[i].n, L2.c[i].d)), L2.c[i].d);
@@ -2416,9 +2428,11 @@ static int gf_step(ugo_env* e, const float* a, double* obs, double* rew, uint8_t
 /* ======================================================================== */
 /* public API                                                                */
 /* ======================================================================== */
-ugo_env* ugo_create(int task, uint32_t seed) {
+ugo_env* ugo_create(int task, uint32_t seed) { return ugo_create_ex(task, seed, 0); }
+/* flags: UG_GEOM_FULL (urgym_create_ex's URGYM_FLAG_FULL_GEOMETRY) -- the full-geometry mode */
+ugo_env* ugo_create_ex(int task, uint32_t seed, int flags) {
     ugo_env* e = (ugo_env*)calloc(1, sizeof(ugo_env));
-    build_scene(&e->sc, task);
+    build_scene(&e->sc, task, flags);
     mt_seed(&e->rng, seed);
     return e;
 }

@@ -110,16 +110,8 @@ def decimate(verts, maxv):
     return verts[sorted(sel)]
 
 
-def hull_of(points):
-    h = ConvexHull(points)
-    full = points[h.vertices]
-    verts = decimate(full, MAXV)
-    h = ConvexHull(verts)
-    verts = verts[h.vertices]
-    # report how far the dropped vertices lie outside the LOD hull
-    out = np.max(full @ h.equations[:, :3].T + h.equations[:, 3], axis=1).max()
-    print("  hull %d -> %d verts, max outside %.4f m" % (len(full), len(verts), out))
-    # merge coplanar facets into faces (unique planes)
+def hull_planes(h):
+    """the hull's facets with coplanar ones merged (unique planes), as n.x <= off (outward normal n, off = -d)"""
     planes = []
     for eq in h.equations:
         n, d = eq[:3], eq[3]
@@ -130,9 +122,25 @@ def hull_of(points):
                 break
         if not dup:
             planes.append(eq)
-    # plane as n.x <= off  (outward normal n, offset off = -d)
-    planes = np.array([[p[0], p[1], p[2], -p[3]] for p in planes])
-    return verts, planes, full
+    return np.array([[p[0], p[1], p[2], -p[3]] for p in planes])
+
+
+def hull_of(points):
+    """(LOD vertices, LOD planes, full hull vertices, full hull planes): the collision LOD of the product's default
+    geometry, and the convex hull of all mesh vertices that PyBullet builds (optimizeConvexHull) for the full mode"""
+    h = ConvexHull(points)
+    full = points[h.vertices]
+    verts = decimate(full, MAXV)
+    h = ConvexHull(verts)
+    verts = verts[h.vertices]
+    # report how far the dropped vertices lie outside the LOD hull
+    out = np.max(full @ h.equations[:, :3].T + h.equations[:, 3], axis=1).max()
+    print("  hull %d -> %d verts, max outside %.4f m" % (len(full), len(verts), out))
+    planes = hull_planes(h)
+    hf = ConvexHull(full)
+    fverts = full[hf.vertices]
+    fplanes = planes if len(fverts) == len(verts) and np.array_equal(fverts, verts) else hull_planes(hf)
+    return verts, planes, fverts, fplanes
 
 
 def face_loops(verts, planes):
@@ -206,8 +214,9 @@ def main():
                 scale = np.array([float(v) for v in m.get("scale", "1 1 1").split()])
                 pts = read_stl(fn) if fn.endswith(".stl") else read_dae(fn)
                 pts = pts * scale
-                verts, planes, full = hull_of(pts)
-                shapes.append(dict(kind="hull", T=Tc, verts=verts, planes=planes, full=full, file=os.path.basename(fn)))
+                verts, planes, full, fplanes = hull_of(pts)
+                shapes.append(dict(kind="hull", T=Tc, verts=verts, planes=planes, full=full, fplanes=fplanes,
+                                   file=os.path.basename(fn)))
         # compound AABB in inertial frame (child AABB includes margin; compound margin 0)
         Tinv = np.linalg.inv(Ti)
         lo = np.full(3, np.inf)
@@ -394,6 +403,20 @@ def main():
             FV.extend([cyl_v0 + k, cyl_v0 + k1, cyl_v0 + nseg + k1, cyl_v0 + nseg + k])
         FV0.append(len(FV)); FVN.append(nseg); FV.extend(cyl_v0 + nseg + k for k in range(nseg))
         FV0.append(len(FV)); FVN.append(nseg); FV.extend(cyl_v0 + k for k in reversed(range(nseg)))
+    # the full hulls (every vertex of PyBullet's convex hull of the mesh, every merged face) after the LOD data and
+    # the prism, for the full-geometry mode (URGYM_FLAG_FULL_GEOMETRY): per-shape offsets into the same arrays
+    shp_fv0, shp_fnv, shp_ff0, shp_fnf = [], [], [], []
+    for i in range(19):
+        for sh in L[i]["shapes"]:
+            if sh["kind"] == "box":
+                shp_fv0.append(0); shp_fnv.append(0); shp_ff0.append(0); shp_fnf.append(0)
+            else:
+                shp_fv0.append(len(V)); shp_fnv.append(len(sh["full"])); shp_ff0.append(len(F)); shp_fnf.append(len(sh["fplanes"]))
+                if HULL_POLYS:
+                    for lp in face_loops(sh["full"], sh["fplanes"]):
+                        FV0.append(len(FV)); FVN.append(len(lp)); FV.extend(len(V) + k for k in lp)
+                V.extend(sh["full"].tolist())
+                F.extend(sh["fplanes"].tolist())
     w("#define UG_CYL_V0 %d   /* golf club disc prism: 2 x %d vertices */" % (cyl_v0, nseg))
     w("#define UG_CYL_NV %d" % (2 * nseg))
     w("#define UG_CYL_F0 %d" % cyl_f0)
@@ -414,6 +437,13 @@ def main():
     arr("UG_SHAPE_NV", shp_nv, "int")
     arr("UG_SHAPE_F0", shp_f0, "int")
     arr("UG_SHAPE_NF", shp_nf, "int")
+    w("/* full-geometry mode: the same shapes' full hulls (offsets into UG_HULL_V / UG_HULL_F) */")
+    w("#define UG_FULL_HULL_MAXV %d" % max(shp_fnv))
+    w("#define UG_FULL_HULL_MAXF %d" % max(shp_fnf))
+    arr("UG_SHAPE_FV0", shp_fv0, "int")
+    arr("UG_SHAPE_FNV", shp_fnv, "int")
+    arr("UG_SHAPE_FF0", shp_ff0, "int")
+    arr("UG_SHAPE_FNF", shp_fnf, "int")
     arr("UG_HULL_V", V)
     arr("UG_HULL_F", F)
     if HULL_POLYS:

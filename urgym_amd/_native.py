@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("URGYM_LIB") or os.path.join(_HERE, "_lib", "liburgym.
 
 # C-ABI symbols declared in include/urgym.h (tests/test_capi.py checks that the library exports each one)
 SYMBOLS = [
-    "urgym_create", "urgym_destroy", "urgym_last_error", "urgym_obs_dim", "urgym_act_dim", "urgym_state_dim",
+    "urgym_create", "urgym_create_ex", "urgym_destroy", "urgym_last_error", "urgym_obs_dim", "urgym_act_dim", "urgym_state_dim",
     "urgym_num_envs", "urgym_set_autoreset", "urgym_reset", "urgym_num_draws", "urgym_step", "urgym_step_device",
     "urgym_reset_device", "urgym_sync", "urgym_stream", "urgym_get_state", "urgym_set_state", "urgym_substep",
     "urgym_link_state", "urgym_ik", "urgym_last_kernel_ms", "urgym_debug_prof", "urgym_debug_workspace",
@@ -23,6 +23,7 @@ SYMBOLS = [
 
 # UG_FLAG_* / UG_STAT_* (urgym_amd/csrc/ug_layout.h)
 FLAG_UNSTABLE, FLAG_NONFINITE, FLAG_DROPPED = 1, 2, 4
+GEOM_FULL = 1  # urgym_create_ex flag URGYM_FLAG_FULL_GEOMETRY
 STAT_NAMES = ["unstable_waits", "split_substeps", "row_capacity_substeps", "manifold_capacity_substeps",
               "nonfinite_terminations", "substeps", "reserved6", "reserved7"]
 CONTACT_FIELDS = 24  # pybullet getContactPoints tuple, flattened
@@ -47,6 +48,8 @@ def lib():
     P, I, D, U32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_uint32
     L.urgym_create.restype = P
     L.urgym_create.argtypes = [I, I, I, I, U32, I]
+    L.urgym_create_ex.restype = P
+    L.urgym_create_ex.argtypes = [I, I, I, I, U32, I, I]
     L.urgym_destroy.argtypes = [P]
     L.urgym_last_error.restype = ctypes.c_char_p
     L.urgym_last_error.argtypes = [P]
@@ -91,11 +94,13 @@ def ptr(a):
 class Sim:
     """One handle = n_envs environments of one task on one GPU."""
 
-    def __init__(self, task, n_envs, device=0, seed=0, env_offset=0):
+    def __init__(self, task, n_envs, device=0, seed=0, env_offset=0, flags=0):
+        """flags: GEOM_FULL = full geometry (robot hulls with every mesh-hull vertex / face)"""
         self.L = lib()
         self.task = task
         self.n = n_envs
-        self.h = self.L.urgym_create(task, n_envs, device, 64, seed & 0xFFFFFFFF, env_offset)
+        self.flags = flags
+        self.h = self.L.urgym_create_ex(task, n_envs, device, 64, seed & 0xFFFFFFFF, env_offset, flags)
         if not self.h:
             raise RuntimeError("urgym_create failed: " + self.L.urgym_last_error(None).decode())
         self.obs_dim = self.L.urgym_obs_dim(task)

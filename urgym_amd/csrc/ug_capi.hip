@@ -61,11 +61,12 @@ __device__ static void add_pair(Scene* s, int a, int b) {
     if (r > UG_MAX_FRICTION) r = UG_MAX_FRICTION;
     p->rolling = r;
 }
-__global__ void k_build_scene(Scene* s, int variant) {
+__global__ void k_build_scene(Scene* s, int variant, int flags) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const int task = UG_BASE_TASK(variant);
     s->task = task;
     s->variant = variant;
+    s->full = (flags & UG_GEOM_FULL) != 0;
     s->gravity = task == UG_TASK_CUBESGRASP ? -10.0 : -9.8;
     s->nobj = 0;
     s->ncol = 0;
@@ -81,6 +82,9 @@ __global__ void k_build_scene(Scene* s, int variant) {
         c->half[0] = UG_SHAPE_HALF[3 * si]; c->half[1] = UG_SHAPE_HALF[3 * si + 1]; c->half[2] = UG_SHAPE_HALF[3 * si + 2];
         c->margin = UG_URDF_MARGIN;
         c->v0 = UG_SHAPE_V0[si]; c->nv = UG_SHAPE_NV[si]; c->f0 = UG_SHAPE_F0[si]; c->nf = UG_SHAPE_NF[si];
+        if (s->full) { /* PyBullet's hull of all mesh vertices instead of the collision LOD (oracle build_scene) */
+            c->v0 = UG_SHAPE_FV0[si]; c->nv = UG_SHAPE_FNV[si]; c->f0 = UG_SHAPE_FF0[si]; c->nf = UG_SHAPE_FNF[si];
+        }
         c->R = mload(&UG_SHAPE_R[9 * si]);
         c->P = V(UG_SHAPE_P[3 * si], UG_SHAPE_P[3 * si + 1], UG_SHAPE_P[3 * si + 2]);
         c->aR = mload(&UG_LINK_COMR[9 * l]);
@@ -459,7 +463,7 @@ __global__ void __launch_bounds__(WAVE) k_contacts(const Scene* sc, const double
 static std::string g_create_error;
 
 struct urgym_handle {
-    int task = 0, n = 0, dev = 0;
+    int task = 0, n = 0, dev = 0, flags = 0;
     hipStream_t stream = nullptr;
     Scene* d_scene = nullptr;
     double* d_state = nullptr;
@@ -524,7 +528,7 @@ int urgym_num_draws(int task) { return UG_NDRAW(task); }
 int urgym_num_envs(const urgym_handle* h) { return h ? h->n : 0; }
 const char* urgym_last_error(const urgym_handle* h) { return h ? h->err.c_str() : g_create_error.c_str(); }
 
-static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed, int env_offset) {
+static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed, int env_offset, int flags) {
     HIPCHK(h, hipSetDevice(dev));
     HIPCHK(h, hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     HIPCHK(h, hipEventCreate(&h->ev0));
@@ -562,13 +566,21 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     std::vector<uint32_t> host(UG_MT_WORDS * N);
     for (int i = 0; i < n; i++) mt_seed_host(host.data() + (size_t)i * UG_MT_WORDS, seed + (uint32_t)env_offset + (uint32_t)i);
     HIPCHK(h, hipMemcpyAsync(h->d_mt, host.data(), sizeof(uint32_t) * host.size(), hipMemcpyHostToDevice, h->stream));
-    k_build_scene<<<1, 1, 0, h->stream>>>(h->d_scene, task);
+    k_build_scene<<<1, 1, 0, h->stream>>>(h->d_scene, task, flags);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
 }
 
 urgym_handle* urgym_create(int task, int n, int dev, int precision, uint32_t seed, int env_offset) {
+    return urgym_create_ex(task, n, dev, precision, seed, env_offset, 0);
+}
+
+urgym_handle* urgym_create_ex(int task, int n, int dev, int precision, uint32_t seed, int env_offset, int flags) {
+    if (flags & ~URGYM_FLAG_FULL_GEOMETRY) {
+        fail(nullptr, "urgym_create_ex: unknown flags " + std::to_string(flags));
+        return nullptr;
+    }
     if (task < URGYM_TASK_BALLBALANCE || task > URGYM_TASK_TWOBALLSBALANCE) {
         fail(nullptr, "urgym_create: unknown task " + std::to_string(task));
         return nullptr;
@@ -576,8 +588,8 @@ urgym_handle* urgym_create(int task, int n, int dev, int precision, uint32_t see
     if (n <= 0) { fail(nullptr, "urgym_create: n_envs must be > 0"); return nullptr; }
     if (precision != 64) { fail(nullptr, "urgym_create: only precision=64 (FP64) is supported"); return nullptr; }
     urgym_handle* h = new urgym_handle();
-    h->task = task; h->n = n; h->dev = dev;
-    if (create_impl(h, task, n, dev, seed, env_offset) != 0) {
+    h->task = task; h->n = n; h->dev = dev; h->flags = flags;
+    if (create_impl(h, task, n, dev, seed, env_offset, flags) != 0) {
         g_create_error = h->err;
         urgym_destroy(h);
         return nullptr;

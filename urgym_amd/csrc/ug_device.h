@@ -236,6 +236,7 @@ struct Scene {
     int npair;
     PairDef pair[MAXPAIR];
     int sparse; /* reward_type != 'dense' (urgym_set_reward_type) */
+    int full;   /* full-geometry mode (UG_GEOM_FULL): robot hulls with every vertex and face */
 };
 
 struct CPoint { v3 lpA, lpB, n; double dist, imp, imp1, imp2; };

@@ -42,6 +42,10 @@
 #define UG_FLAG_NONFINITE 2  /* the state became non-finite: the env was terminated (and reset by autoreset) */
 #define UG_FLAG_DROPPED 4    /* contacts were dropped at a capacity limit */
 
+/* creation flags (urgym_create_ex / ugo_create_ex) */
+#define UG_GEOM_FULL 1       /* full geometry: robot hulls with every vertex / face of the mesh's convex hull (PyBullet's
+                              * optimizeConvexHull of all mesh vertices) instead of the <= 48-vertex collision LOD */
+
 #define UG_MT_WORDS 625      /* MT19937 state (624) + index, uint32, contiguous per env */
 
 #endif

@@ -33,6 +33,8 @@
 namespace ugd {
 
 #define TEAM 64
+typedef __attribute__((address_space(1))) const double gcdouble;
+typedef __attribute__((address_space(1))) double gdouble;
 #define UG_NPROF 60 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
@@ -48,11 +50,17 @@ static_assert(NV <= NVP, "dof slots exceed the padded row");
 /* hull-box pairs' corner certificates: per pair, the face that last maximised each box corner's plane
  * distance (8 bytes; a hint only -- team_hull_box proves with it or scans every face) */
 #define WS_HC (WS_A + (MAXROWS - PREG) * MAXROWS)
+/* full-geometry mode (UG_GEOM_FULL): a hull pair's candidates (FC_MAX x 7 doubles: n, pB, d), and the corner
+ * certificates as 16-bit face indices (the full hulls have up to UG_FULL_HULL_MAXF faces) */
+#define FC_MAX 1024
+static_assert(UG_FULL_HULL_MAXV + 64 + 8 <= FC_MAX, "a full hull pair's candidates must fit the workspace list");
+#define WS_FC (WS_HC + MAXPAIR)
+#define WS_HC2 (WS_FC + 7 * FC_MAX)
 #ifdef UG_DEBUG_DUMP /* development aid: team_pgs dumps A, w and impulses after the workspace proper */
-#define WS_DBG (WS_HC + MAXPAIR)
+#define WS_DBG (WS_HC2 + 2 * MAXPAIR)
 #define WS_DOUBLES (WS_DBG + MAXROWS * MAXROWS + 8 * MAXROWS)
 #else
-#define WS_DOUBLES (WS_HC + MAXPAIR)
+#define WS_DOUBLES (WS_HC2 + 2 * MAXPAIR)
 #endif
 
 #define MAXOV 26 /* pairs per lane-per-pair pass: their working manifolds share LDS with the rows (Shared::pm) */
@@ -479,6 +487,248 @@ __device__ __forceinline__ static void team_reduce4(int n, int k) {
     __syncthreads();
 }
 
+/* ---- full-geometry mode (UG_GEOM_FULL): hulls with more vertices than lanes (up to UG_FULL_HULL_MAXV) and more
+ * candidates than the LDS list holds.  Same arithmetic as the LOD functions above and as the oracle's nc_hull_box /
+ * nc_hull_hull with every candidate kept (collider.full): vertices in chunks of 64 lanes, candidates in canonical
+ * order (vertices by index, then corners / the other hull's vertices) in the env's global workspace, reduce4 over
+ * that list (per-lane strided scans, then the wave-wide arg-min / arg-max with ties to the lower index). */
+__device__ __forceinline__ void gc_put(gdouble* gc, int i, const Cand& c) {
+    gdouble* o = gc + 7 * i;
+    o[0] = c.n.x; o[1] = c.n.y; o[2] = c.n.z; o[3] = c.pB.x; o[4] = c.pB.y; o[5] = c.pB.z; o[6] = c.d;
+}
+__device__ __forceinline__ Cand gc_get(const gdouble* gc, int i) {
+    const gdouble* o = gc + 7 * i;
+    Cand c;
+    c.n = V(o[0], o[1], o[2]);
+    c.pB = V(o[3], o[4], o[5]);
+    c.d = o[6];
+    return c;
+}
+__device__ __forceinline__ void gc_publish() { /* the wave's workspace stores, visible to its later loads */
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+}
+/* candidates gc[0..n) -> at most 4 in sh.u.cand.c[k] (oracle reduce4) */
+__device__ __noinline__ static void team_reduce4_g(int n, int k, gdouble* gc) {
+    Shared& sh = g_sh;
+    const int lane = threadIdx.x;
+    if (n <= 4) {
+        if (lane < n) sh.u.cand.c[k][lane] = gc_get(gc, lane);
+        if (lane == 0) sh.u.cand.n[k] = n;
+        __syncthreads();
+        return;
+    }
+    /* deepest: the first minimum of d */
+    double v = 0.0;
+    int idx = 0x7fffffff;
+    for (int i = lane; i < n; i += TEAM) {
+        const double d = gc[7 * i + 6];
+        if (idx == 0x7fffffff || d < v) { v = d; idx = i; }
+    }
+    wave_best(v, idx, false);
+    int s0 = idx, s1 = -1, s2 = -1;
+    v3 p0 = V(gc[7 * s0 + 3], gc[7 * s0 + 4], gc[7 * s0 + 5]), p1 = V(0, 0, 0), p2 = V(0, 0, 0);
+    for (int s = 1; s < 4; s++) {
+        /* farthest-spread: the first maximum of the squared distance to the nearest selected point */
+        double mv2 = 0.0;
+        int mi = 0x7fffffff;
+        for (int i = lane; i < n; i += TEAM) {
+            if (i == s0 || i == s1 || i == s2) continue;
+            const v3 pb = V(gc[7 * i + 3], gc[7 * i + 4], gc[7 * i + 5]);
+            double md = 1e300;
+            {
+                v3 dd = vsub(pb, p0);
+                double x = vdot(dd, dd);
+                if (x < md) md = x;
+            }
+            if (s > 1) {
+                v3 dd = vsub(pb, p1);
+                double x = vdot(dd, dd);
+                if (x < md) md = x;
+            }
+            if (s > 2) {
+                v3 dd = vsub(pb, p2);
+                double x = vdot(dd, dd);
+                if (x < md) md = x;
+            }
+            if (mi == 0x7fffffff || md > mv2) { mv2 = md; mi = i; }
+        }
+        wave_best(mv2, mi, true);
+        const v3 pm = V(gc[7 * mi + 3], gc[7 * mi + 4], gc[7 * mi + 5]);
+        if (s == 1) { s1 = mi; p1 = pm; }
+        else if (s == 2) { s2 = mi; p2 = pm; }
+        else {
+            const int si = lane == 0 ? s0 : lane == 1 ? s1 : lane == 2 ? s2 : mi;
+            if (lane < 4) sh.u.cand.c[k][lane] = gc_get(gc, si);
+        }
+    }
+    if (lane == 0) sh.u.cand.n[k] = 4;
+    __syncthreads();
+}
+/* hull (A, robot link) vs box (B), full geometry (oracle nc_hull_box) */
+__device__ __noinline__ static void team_hull_box_full(const HullArg& A, const HullArg& B, const XF& TA, const XF& TB,
+                                                       double thr, int k, unsigned short* hcert, gdouble* gc) {
+    const int lane = threadIdx.x;
+    const m3 RAB = mtm(TB.R, TA.R);
+    const v3 pAB = mtv(TB.R, vsub(TA.p, TB.p));
+    const v3 h = V(B.half[0], B.half[1], B.half[2]);
+    const double mA = A.margin;
+    int n = 0;
+    for (int v0 = 0; v0 < A.nv; v0 += TEAM) {
+        const int vi = v0 + lane;
+        int vvalid = 0;
+        Cand vc;
+        if (vi < A.nv) {
+            const double* vv = &UG_HULL_V[3 * (A.v0 + vi)];
+            v3 x = vadd(mv(RAB, V(vv[0], vv[1], vv[2])), pAB);
+            v3 d = V(ug_fabs(x.x) - h.x, ug_fabs(x.y) - h.y, ug_fabs(x.z) - h.z);
+            double dist = 0.0;
+            v3 nl = V(0, 0, 0), pl = V(0, 0, 0);
+            int ok = 1;
+            if (d.x < 0 && d.y < 0 && d.z < 0) {
+                int kk = 0;
+                double dm = d.x;
+                if (d.y > dm) { dm = d.y; kk = 1; }
+                if (d.z > dm) { dm = d.z; kk = 2; }
+                dist = dm;
+                double sg = vget(x, kk) < 0 ? -1.0 : 1.0;
+                vsetc(nl, kk, sg);
+                pl = x; vsetc(pl, kk, sg * vget(h, kk));
+            } else {
+                v3 q = V(ug_max(-h.x, ug_min(h.x, x.x)), ug_max(-h.y, ug_min(h.y, x.y)), ug_max(-h.z, ug_min(h.z, x.z)));
+                v3 df = vsub(x, q);
+                double dl = vlen(df);
+                if (dl - mA >= thr) ok = 0;
+                else { dist = dl; nl = vscale(df, 1.0 / dl); pl = q; }
+            }
+            double depth = dist - mA;
+            if (ok && depth < thr) {
+                vvalid = 1;
+                vc.n = mv(TB.R, nl);
+                vc.pB = xf_apply(TB, pl);
+                vc.d = depth;
+            }
+        }
+        const unsigned long long vb = ballot(vvalid);
+        if (vvalid) gc_put(gc, n + lane_prefix(vb), vc);
+        n += __popcll(vb);
+    }
+    /* box corners: 8 lanes per corner, faces strided over the group, group arg-max (first maximum) */
+    const int c = lane >> 3, j = lane & 7;
+    const m3 RBA = mtm(TA.R, TB.R);
+    const v3 pBA = mtv(TA.R, vsub(TB.p, TA.p));
+    const v3 cl = V((c & 1) ? h.x : -h.x, (c & 2) ? h.y : -h.y, (c & 4) ? h.z : -h.z);
+    const v3 y = vadd(mv(RBA, cl), pBA);
+    double smax = -1e300;
+    int fm = 0x7fffffff;
+    const int nf = A.nf;
+    bool certified = false;
+    {
+        int fc = hcert[c];
+        fc = fc < nf ? fc : nf - 1;
+        const double* F = &UG_HULL_F[4 * (A.f0 + fc)];
+        const double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
+        certified = ballot(j == 0 && sd - mA >= thr) == 0x0101010101010101ull;
+    }
+    if (!certified) {
+        for (int f = j; f < nf; f += 8) {
+            const double* F = &UG_HULL_F[4 * (A.f0 + f)];
+            const double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
+            if (sd > smax) { smax = sd; fm = f; }
+        }
+        double w;
+        int jj;
+        w = dpp<0xB1>(smax); jj = dppi<0xB1>(fm);
+        if (!better(smax, fm, w, jj, true)) { smax = w; fm = jj; }
+        w = dpp<0x4E>(smax); jj = dppi<0x4E>(fm);
+        if (!better(smax, fm, w, jj, true)) { smax = w; fm = jj; }
+        w = dpp<0x141>(smax); jj = dppi<0x141>(fm);
+        if (!better(smax, fm, w, jj, true)) { smax = w; fm = jj; }
+        if (j == 0 && fm != 0x7fffffff) hcert[c] = (unsigned short)fm;
+    }
+    int cvalid = 0;
+    Cand cc;
+    if (j == 0 && fm != 0x7fffffff) {
+        const double depth = smax - mA;
+        if (depth < thr) {
+            const double* F = &UG_HULL_F[4 * (A.f0 + fm)];
+            const v3 nw = mv(TA.R, V(F[0], F[1], F[2]));
+            cvalid = 1;
+            cc.n = vneg(nw);
+            cc.pB = xf_apply(TB, cl);
+            cc.d = depth;
+        }
+    }
+    const unsigned long long cb = ballot(cvalid);
+    if (cvalid) gc_put(gc, n + lane_prefix(cb), cc);
+    n += __popcll(cb);
+    gc_publish();
+    team_reduce4_g(n, k, gc);
+}
+/* hull (A, robot link) vs hull (B), full geometry (oracle nc_hull_hull, every candidate kept) */
+__device__ __noinline__ static void team_hull_hull_full(const HullArg& A, const HullArg& B, const XF& TA, const XF& TB,
+                                                        double thr, int k, gdouble* gc) {
+    const int lane = threadIdx.x;
+    const double mA = A.margin, mB = B.margin;
+    int n = 0;
+    const m3 RAB = mtm(TB.R, TA.R);
+    const v3 pAB = mtv(TB.R, vsub(TA.p, TB.p));
+    for (int v0 = 0; v0 < A.nv; v0 += TEAM) {
+        const int vi = v0 + lane;
+        int valid = 0;
+        Cand ac;
+        if (vi < A.nv) {
+            const double* vv = &UG_HULL_V[3 * (A.v0 + vi)];
+            const v3 x = vadd(mv(RAB, V(vv[0], vv[1], vv[2])), pAB);
+            double smax = -1e300;
+            int fm = -1;
+            hull_plane_max(B, x, smax, fm);
+            const double depth = smax - mA - mB;
+            if (depth < thr) {
+                const double* F = &UG_HULL_F[4 * (B.f0 + fm)];
+                const v3 nl = V(F[0], F[1], F[2]);
+                const v3 pl = vsub(x, vscale(nl, smax));
+                valid = 1;
+                ac.n = mv(TB.R, nl);
+                ac.pB = xf_apply(TB, pl);
+                ac.d = depth;
+            }
+        }
+        const unsigned long long m = ballot(valid);
+        if (valid) gc_put(gc, n + lane_prefix(m), ac);
+        n += __popcll(m);
+    }
+    const m3 RBA = mtm(TA.R, TB.R);
+    const v3 pBA = mtv(TA.R, vsub(TB.p, TA.p));
+    for (int v0 = 0; v0 < B.nv; v0 += TEAM) {
+        const int vi = v0 + lane;
+        int valid = 0;
+        Cand bc;
+        if (vi < B.nv) {
+            const double* vv = &UG_HULL_V[3 * (B.v0 + vi)];
+            const v3 yl = V(vv[0], vv[1], vv[2]);
+            const v3 y = vadd(mv(RBA, yl), pBA);
+            double smax = -1e300;
+            int fm = -1;
+            hull_plane_max(A, y, smax, fm);
+            const double depth = smax - mA - mB;
+            if (depth < thr) {
+                const double* F = &UG_HULL_F[4 * (A.f0 + fm)];
+                const v3 nw = mv(TA.R, V(F[0], F[1], F[2]));
+                valid = 1;
+                bc.n = vneg(nw);
+                bc.pB = xf_apply(TB, yl);
+                bc.d = depth;
+            }
+        }
+        const unsigned long long m = ballot(valid);
+        if (valid) gc_put(gc, n + lane_prefix(m), bc);
+        n += __popcll(m);
+    }
+    gc_publish();
+    team_reduce4_g(n, k, gc);
+}
+
 /* box (A) vs box (B) (oracle nc_box_box: ODE dBoxBox2 as btBoxBoxDetector), the whole wave per pair.  The same
  * operations on the same values as the serial routine, spread over lanes:
  *   - the 15 separating-axis tests in lanes 0..14 (any positive separation ends the pair, as the serial early
@@ -869,7 +1119,12 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         for (unsigned long long hm = ballot(hk); hm != 0ull; hm &= hm - 1ull) {
             const int k = __builtin_ctzll(hm);
             const PairInfo pi = sh.pinfo[k];
-            if (pi.kb == UG_SHAPE_BOX)
+            if (pi.A.nv > TEAM) { /* a full-geometry robot hull (UG_GEOM_FULL: every full hull has more than 64) */
+                if (pi.kb == UG_SHAPE_BOX)
+                    team_hull_box_full(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k,
+                                       (unsigned short*)(ws + WS_HC2) + 8 * sh.ov[c0 + k], (gdouble*)(ws + WS_FC));
+                else team_hull_hull_full(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k, (gdouble*)(ws + WS_FC));
+            } else if (pi.kb == UG_SHAPE_BOX)
                 team_hull_box(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k, (unsigned char*)(ws + WS_HC) + 8 * sh.ov[c0 + k]);
             else team_hull_hull(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k);
             PROF_CNT(PC_HULL, 1);
@@ -1583,8 +1838,6 @@ __device__ __forceinline__ static void build_row(const Scene* s, int pos, double
  * order is the oracle's pgs() (oracle/ug_oracle.c). */
 #define NCMAX (2 * NB + 12) /* limits (both sides) + 7 motors + 5 gears */
 #define CHUNK 8             /* rows per branch-free sweep chunk (one scalar test per chunk; 4 measured slower) */
-typedef __attribute__((address_space(1))) const double gcdouble;
-typedef __attribute__((address_space(1))) double gdouble;
 struct Lrow { /* the two rows this lane owns (slot s: position lane + 64 s) */
     double rhs[2], invD[2], rinv[2], lo[2], hi[2], imp[2];
     double dlo[2], dhi[2]; /* lo - imp, hi - imp */
