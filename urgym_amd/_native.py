@@ -99,7 +99,7 @@ class Sim:
         self.L = lib()
         self.task = task
         self.n = n_envs
-        self.flags = flags
+        self.create_flags = flags
         self.h = self.L.urgym_create_ex(task, n_envs, device, 64, seed & 0xFFFFFFFF, env_offset, flags)
         if not self.h:
             raise RuntimeError("urgym_create failed: " + self.L.urgym_last_error(None).decode())
