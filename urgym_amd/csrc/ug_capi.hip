@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(TEAM, 1) k_reset(const Scene* sc, double* S, u
     io.autoreset = 0;
     io.trunc = 0;
     PROF_T0(t_tot);
-    int ns = team_run(sc, ws + (size_t)i * WS_DOUBLES, G_RESET, io);
+    int ns = team_run(sc, ws + (size_t)i * WS_STRIDE(sc->full), G_RESET, io);
     PROF_ADD(PF_TOTAL, t_tot);
     team_store(Si, stats + (size_t)i * UG_NSTAT, flags + i);
     team_prof_flush();
@@ -298,7 +298,7 @@ __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, ui
     io.trunc = (max_steps > 0 && el >= max_steps) ? 1 : 0;
     io.reset_done = 0;
     PROF_T0(t_tot);
-    int ns = team_run(sc, ws + (size_t)i * WS_DOUBLES, G_STEP, io);
+    int ns = team_run(sc, ws + (size_t)i * WS_STRIDE(sc->full), G_STEP, io);
     PROF_ADD(PF_TOTAL, t_tot);
     team_store(Si, stats + (size_t)i * UG_NSTAT, flags + i);
     team_prof_flush();
@@ -357,7 +357,7 @@ __global__ void __launch_bounds__(TEAM, 1) k_substep(const Scene* sc, double* S,
     if (i >= n) return;
     double* Si = S + (size_t)i * UG_STATE_DIM;
     team_load(Si, stats + (size_t)i * UG_NSTAT);
-    team_substep(sc, ws + (size_t)i * WS_DOUBLES);
+    team_substep(sc, ws + (size_t)i * WS_STRIDE(sc->full));
     team_store(Si, stats + (size_t)i * UG_NSTAT, nullptr);
 }
 
@@ -539,7 +539,7 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     size_t N = (size_t)n;
     HIPCHK(h, hipMalloc(&h->d_state, sizeof(double) * UG_STATE_DIM * N));
     HIPCHK(h, hipMalloc(&h->d_mt, sizeof(uint32_t) * UG_MT_WORDS * N));
-    HIPCHK(h, hipMalloc(&h->d_ws, sizeof(double) * WS_DOUBLES * N));
+    HIPCHK(h, hipMalloc(&h->d_ws, sizeof(double) * WS_STRIDE(flags & UG_GEOM_FULL) * N));
     HIPCHK(h, hipMalloc(&h->d_elapsed, sizeof(int) * N));
     HIPCHK(h, hipMalloc(&h->d_act, sizeof(float) * 9 * N));
     HIPCHK(h, hipMalloc(&h->d_obs, sizeof(double) * 17 * N));
@@ -849,12 +849,12 @@ int urgym_debug_prof(urgym_handle* h, unsigned long long* out16, int reset) {
 
 // Development aid: copy env's per-env workspace (count doubles from its start) to the host.
 int urgym_debug_workspace(urgym_handle* h, int env, double* out, int count) {
-    if (!h || !out || env < 0 || env >= h->n || count < 0 || count > (int)WS_DOUBLES) return -1;
+    if (!h || !out || env < 0 || env >= h->n || count < 0 || count > (int)WS_STRIDE(h->flags & UG_GEOM_FULL)) return -1;
     HIPCHK(h, hipSetDevice(h->dev));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    HIPCHK(h, hipMemcpy(out, h->d_ws + (size_t)env * WS_DOUBLES, sizeof(double) * count, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy(out, h->d_ws + (size_t)env * WS_STRIDE(h->flags & UG_GEOM_FULL), sizeof(double) * count, hipMemcpyDeviceToHost));
     return 0;
 }
-int urgym_debug_ws_doubles(void) { return (int)WS_DOUBLES; }
+int urgym_debug_ws_doubles(void) { return (int)WS_STRIDE(0); } /* the LOD stride (the full geometry adds 7,488 doubles) */
 
 }  // extern "C"

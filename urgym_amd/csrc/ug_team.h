@@ -56,11 +56,17 @@ static_assert(NV <= NVP, "dof slots exceed the padded row");
 static_assert(UG_FULL_HULL_MAXV + 64 + 8 <= FC_MAX, "a full hull pair's candidates must fit the workspace list");
 #define WS_FC (WS_HC + MAXPAIR)
 #define WS_HC2 (WS_FC + 7 * FC_MAX)
+/* per-env workspace stride: the LOD geometry ends at WS_FC, the full geometry adds its candidate list and 16-bit
+ * certificates (a handle allocates only what its mode uses) */
+#define WS_LOD_DOUBLES WS_FC
+#define WS_FULL_DOUBLES (WS_HC2 + 2 * MAXPAIR)
 #ifdef UG_DEBUG_DUMP /* development aid: team_pgs dumps A, w and impulses after the workspace proper */
-#define WS_DBG (WS_HC2 + 2 * MAXPAIR)
+#define WS_DBG WS_FULL_DOUBLES
 #define WS_DOUBLES (WS_DBG + MAXROWS * MAXROWS + 8 * MAXROWS)
+#define WS_STRIDE(full) ((size_t)WS_DOUBLES)
 #else
-#define WS_DOUBLES (WS_HC2 + 2 * MAXPAIR)
+#define WS_DOUBLES WS_FULL_DOUBLES
+#define WS_STRIDE(full) ((size_t)((full) ? WS_FULL_DOUBLES : WS_LOD_DOUBLES))
 #endif
 
 #define MAXOV 26 /* pairs per lane-per-pair pass: their working manifolds share LDS with the rows (Shared::pm) */
@@ -574,6 +580,7 @@ __device__ __noinline__ static void team_hull_box_full(const HullArg& A, const H
     const v3 h = V(B.half[0], B.half[1], B.half[2]);
     const double mA = A.margin;
     int n = 0;
+    PROF_T0(t_hv);
     for (int v0 = 0; v0 < A.nv; v0 += TEAM) {
         const int vi = v0 + lane;
         int vvalid = 0;
@@ -613,6 +620,8 @@ __device__ __noinline__ static void team_hull_box_full(const HullArg& A, const H
         if (vvalid) gc_put(gc, n + lane_prefix(vb), vc);
         n += __popcll(vb);
     }
+    PROF_ADD(PF_HB_VERT, t_hv);
+    PROF_T0(t_hc);
     /* box corners: 8 lanes per corner, faces strided over the group, group arg-max (first maximum) */
     const int c = lane >> 3, j = lane & 7;
     const m3 RBA = mtm(TA.R, TB.R);
@@ -663,7 +672,10 @@ __device__ __noinline__ static void team_hull_box_full(const HullArg& A, const H
     if (cvalid) gc_put(gc, n + lane_prefix(cb), cc);
     n += __popcll(cb);
     gc_publish();
+    PROF_ADD(PF_HB_CORNER, t_hc);
+    PROF_T0(t_hr);
     team_reduce4_g(n, k, gc);
+    PROF_ADD(PF_HB_REDUCE, t_hr);
 }
 /* hull (A, robot link) vs hull (B), full geometry (oracle nc_hull_hull, every candidate kept) */
 __device__ __noinline__ static void team_hull_hull_full(const HullArg& A, const HullArg& B, const XF& TA, const XF& TB,
@@ -1050,6 +1062,9 @@ __device__ __forceinline__ static void team_box_box(const XF& TA, const double (
 }
 
 /* performDiscreteCollisionDetection (oracle collide()), team version.  ws: this env's global workspace. */
+/* FULL: the full-geometry instantiation (UG_GEOM_FULL); the LOD one has no calls into the full-hull functions, so
+ * its register allocation is that of the LOD path alone */
+template <bool FULL>
 __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
@@ -1119,7 +1134,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         for (unsigned long long hm = ballot(hk); hm != 0ull; hm &= hm - 1ull) {
             const int k = __builtin_ctzll(hm);
             const PairInfo pi = sh.pinfo[k];
-            if (pi.A.nv > TEAM) { /* a full-geometry robot hull (UG_GEOM_FULL: every full hull has more than 64) */
+            if (FULL && pi.A.nv > TEAM) { /* a full-geometry robot hull (every full hull has more than 64 vertices) */
                 if (pi.kb == UG_SHAPE_BOX)
                     team_hull_box_full(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k,
                                        (unsigned short*)(ws + WS_HC2) + 8 * sh.ov[c0 + k], (gdouble*)(ws + WS_FC));
@@ -2994,7 +3009,8 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     __syncthreads();
     PROF_ADD(PF_FK, t_col);
     const double ov0 = e.overflow;
-    team_collide(s, ws);
+    if (s->full) team_collide<true>(s, ws);
+    else team_collide<false>(s, ws);
     const double ov1 = e.overflow;
     if (lane == 0) {
         sh.stats[UG_STAT_SUBSTEPS]++;
