@@ -125,6 +125,25 @@ def hull_planes(h):
     return np.array([[p[0], p[1], p[2], -p[3]] for p in planes])
 
 
+def spatial_chunks(verts, size=64):
+    """vertex order for the full hulls: spatially coherent groups of <= size (recursive split of the group count
+    along the longest extent), each group contiguous, so a 64-lane chunk has a tight bounding sphere (the kernel's
+    exact chunk cull, team_hull_box_full).  Deterministic; returns the permutation."""
+    def split(idx, k):
+        if k == 1:
+            return [idx]
+        p = verts[idx]
+        ax = int(np.argmax(p.max(0) - p.min(0)))
+        o = idx[np.argsort(p[:, ax], kind="stable")]
+        kl = k // 2
+        nl = int(round(len(idx) * kl / k))
+        return split(o[:nl], kl) + split(o[nl:], k - kl)
+    n = len(verts)
+    groups = split(np.arange(n), max(1, -(-n // size)))
+    assert all(len(g) <= size for g in groups), [len(g) for g in groups]
+    return np.concatenate([np.sort(g) for g in groups]), [len(g) for g in groups]
+
+
 def hull_of(points):
     """(LOD vertices, LOD planes, full hull vertices, full hull planes): the collision LOD of the product's default
     geometry, and the convex hull of all mesh vertices that PyBullet builds (optimizeConvexHull) for the full mode"""
@@ -140,7 +159,8 @@ def hull_of(points):
     hf = ConvexHull(full)
     fverts = full[hf.vertices]
     fplanes = planes if len(fverts) == len(verts) and np.array_equal(fverts, verts) else hull_planes(hf)
-    return verts, planes, fverts, fplanes
+    perm, sizes = spatial_chunks(fverts)
+    return verts, planes, fverts[perm], fplanes, sizes
 
 
 def face_loops(verts, planes):
@@ -214,9 +234,9 @@ def main():
                 scale = np.array([float(v) for v in m.get("scale", "1 1 1").split()])
                 pts = read_stl(fn) if fn.endswith(".stl") else read_dae(fn)
                 pts = pts * scale
-                verts, planes, full, fplanes = hull_of(pts)
+                verts, planes, full, fplanes, csizes = hull_of(pts)
                 shapes.append(dict(kind="hull", T=Tc, verts=verts, planes=planes, full=full, fplanes=fplanes,
-                                   file=os.path.basename(fn)))
+                                   csizes=csizes, file=os.path.basename(fn)))
         # compound AABB in inertial frame (child AABB includes margin; compound margin 0)
         Tinv = np.linalg.inv(Ti)
         lo = np.full(3, np.inf)
@@ -405,13 +425,20 @@ def main():
         FV0.append(len(FV)); FVN.append(nseg); FV.extend(cyl_v0 + k for k in reversed(range(nseg)))
     # the full hulls (every vertex of PyBullet's convex hull of the mesh, every merged face) after the LOD data and
     # the prism, for the full-geometry mode (URGYM_FLAG_FULL_GEOMETRY): per-shape offsets into the same arrays
-    shp_fv0, shp_fnv, shp_ff0, shp_fnf = [], [], [], []
+    shp_fv0, shp_fnv, shp_ff0, shp_fnf, shp_fc0 = [], [], [], [], []
+    CS = []  # per 64-vertex chunk of a full hull: bounding sphere (centre in the shape frame, radius)
     for i in range(19):
         for sh in L[i]["shapes"]:
             if sh["kind"] == "box":
-                shp_fv0.append(0); shp_fnv.append(0); shp_ff0.append(0); shp_fnf.append(0)
+                shp_fv0.append(0); shp_fnv.append(0); shp_ff0.append(0); shp_fnf.append(0); shp_fc0.append(0)
             else:
                 shp_fv0.append(len(V)); shp_fnv.append(len(sh["full"])); shp_ff0.append(len(F)); shp_fnf.append(len(sh["fplanes"]))
+                shp_fc0.append(len(CS) // 4)
+                for a in range(0, len(sh["full"]), 64):
+                    cv = sh["full"][a:a + 64]
+                    c = (cv.min(0) + cv.max(0)) / 2
+                    r = float(np.linalg.norm(cv - c, axis=1).max())
+                    CS.extend([c[0], c[1], c[2], r * (1 + 1e-12) + 1e-12])  # rounded up: an upper bound
                 if HULL_POLYS:
                     for lp in face_loops(sh["full"], sh["fplanes"]):
                         FV0.append(len(FV)); FVN.append(len(lp)); FV.extend(len(V) + k for k in lp)
@@ -444,6 +471,9 @@ def main():
     arr("UG_SHAPE_FNV", shp_fnv, "int")
     arr("UG_SHAPE_FF0", shp_ff0, "int")
     arr("UG_SHAPE_FNF", shp_fnf, "int")
+    arr("UG_SHAPE_FC0", shp_fc0, "int")
+    w("/* full hulls: bounding sphere (centre x y z, radius) of each 64-vertex chunk, vertices grouped spatially */")
+    arr("UG_HULL_CS", CS)
     arr("UG_HULL_V", V)
     arr("UG_HULL_F", F)
     if HULL_POLYS:

@@ -1,0 +1,10 @@
+#!/bin/bash
+# full-geometry parity after the chunk cull, phase cycles of both modes (BallBalance), benches of both modes
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/r3d
+timeout -k 10 600 python -u -m pytest tests/test_gpu_fullgeom.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r3d/full.log 2>&1; rc=$?; echo "full rc=$rc"; tail -2 gpurun_out/r3d/full.log; [ $rc -eq 0 ] || exit $rc
+for g in lod full; do
+  timeout -k 10 200 python tools/phase_prof.py --steps 5 --geometry $g > gpurun_out/r3d/phase_bb_$g.txt 2>&1 || exit 1
+  timeout -k 10 300 python bench.py --no-cpu-baseline --geometry $g > gpurun_out/r3d/bench_bb_$g.json 2> gpurun_out/r3d/bench_bb_$g.err || exit 1
+  cut -c1-150 gpurun_out/r3d/bench_bb_$g.json
+done

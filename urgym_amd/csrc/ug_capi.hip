@@ -29,7 +29,7 @@ __device__ static void box_collider(Collider* c, double hx, double hy, double hz
     c->kind = UG_SHAPE_BOX;
     c->half[0] = hx; c->half[1] = hy; c->half[2] = hz;
     c->margin = margin;
-    c->v0 = c->nv = c->f0 = c->nf = 0;
+    c->v0 = c->nv = c->f0 = c->nf = c->c0 = 0;
     c->R = mident(); c->P = V(0, 0, 0);
     c->aR = mident(); c->aP = V(0, 0, 0);
     c->ac = V(0, 0, 0); c->ah = V(hx, hy, hz);
@@ -82,8 +82,10 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
         c->half[0] = UG_SHAPE_HALF[3 * si]; c->half[1] = UG_SHAPE_HALF[3 * si + 1]; c->half[2] = UG_SHAPE_HALF[3 * si + 2];
         c->margin = UG_URDF_MARGIN;
         c->v0 = UG_SHAPE_V0[si]; c->nv = UG_SHAPE_NV[si]; c->f0 = UG_SHAPE_F0[si]; c->nf = UG_SHAPE_NF[si];
+        c->c0 = 0;
         if (s->full) { /* PyBullet's hull of all mesh vertices instead of the collision LOD (oracle build_scene) */
             c->v0 = UG_SHAPE_FV0[si]; c->nv = UG_SHAPE_FNV[si]; c->f0 = UG_SHAPE_FF0[si]; c->nf = UG_SHAPE_FNF[si];
+            c->c0 = UG_SHAPE_FC0[si];
         }
         c->R = mload(&UG_SHAPE_R[9 * si]);
         c->P = V(UG_SHAPE_P[3 * si], UG_SHAPE_P[3 * si + 1], UG_SHAPE_P[3 * si + 2]);

@@ -214,6 +214,7 @@ struct Collider {
     double half[3];
     double margin;
     int v0, nv, f0, nf;
+    int c0; /* full hulls: first chunk bounding sphere (UG_HULL_CS) */
     m3 R; v3 P;
     m3 aR; v3 aP;
     v3 ac, ah;

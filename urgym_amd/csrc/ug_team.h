@@ -88,11 +88,11 @@ static_assert(sizeof(Manifold) * MAXOV <= 88 * MAXROWS, "working manifolds must 
 
 /* the collider fields the wave narrowphases read, and a pair's shape transforms: formed lane-per-pair once
  * per collision pass (team_collide), read back uniformly by the hull pair loop */
-struct HullArg { int nv, v0, nf, f0; double margin; double half[3]; };
+struct HullArg { int nv, v0, nf, f0, c0; double margin; double half[3]; };
 struct PairInfo { XF TA, TB; HullArg A, B; double thr; int a, b, ka, kb; };
 __device__ __forceinline__ static HullArg hull_arg(const Collider& c) {
     HullArg h;
-    h.nv = c.nv; h.v0 = c.v0; h.nf = c.nf; h.f0 = c.f0; h.margin = c.margin;
+    h.nv = c.nv; h.v0 = c.v0; h.nf = c.nf; h.f0 = c.f0; h.c0 = c.c0; h.margin = c.margin;
     h.half[0] = c.half[0]; h.half[1] = c.half[1]; h.half[2] = c.half[2];
     return h;
 }
@@ -581,7 +581,16 @@ __device__ __noinline__ static void team_hull_box_full(const HullArg& A, const H
     const double mA = A.margin;
     int n = 0;
     PROF_T0(t_hv);
-    for (int v0 = 0; v0 < A.nv; v0 += TEAM) {
+    for (int v0 = 0, ch = A.c0; v0 < A.nv; v0 += TEAM, ch++) {
+        /* exact chunk cull: every vertex of the chunk lies in its bounding sphere (UG_HULL_CS); when the sphere is
+         * farther than thr + margin from the box (with 1e-9 for rounding), no vertex is inside the box or within
+         * the threshold, so the chunk adds no candidate -- the skipped work would have produced none */
+        {
+            const double* S = &UG_HULL_CS[4 * ch];
+            const v3 cc = vadd(mv(RAB, V(S[0], S[1], S[2])), pAB);
+            const v3 q = V(ug_max(-h.x, ug_min(h.x, cc.x)), ug_max(-h.y, ug_min(h.y, cc.y)), ug_max(-h.z, ug_min(h.z, cc.z)));
+            if (vlen(vsub(cc, q)) - S[3] >= thr + mA + 1e-9) continue;
+        }
         const int vi = v0 + lane;
         int vvalid = 0;
         Cand vc;
@@ -640,10 +649,26 @@ __device__ __noinline__ static void team_hull_box_full(const HullArg& A, const H
         certified = ballot(j == 0 && sd - mA >= thr) == 0x0101010101010101ull;
     }
     if (!certified) {
-        for (int f = j; f < nf; f += 8) {
-            const double* F = &UG_HULL_F[4 * (A.f0 + f)];
-            const double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
-            if (sd > smax) { smax = sd; fm = f; }
+        /* faces strided over the 8-lane group, HB_FACE_UNROLL planes per lane per batch with their loads issued
+         * together (clamped index, predicated update), as team_hull_box */
+        for (int fb = 0; fb < nf; fb += 8 * HB_FACE_UNROLL) {
+            double F[HB_FACE_UNROLL][4];
+#pragma unroll
+            for (int i = 0; i < HB_FACE_UNROLL; i++) {
+                const int f = fb + j + 8 * i;
+#pragma unroll
+                for (int cc = 0; cc < 4; cc++) F[i][cc] = UG_HULL_F[4 * (A.f0 + (f < nf ? f : 0)) + cc];
+            }
+#pragma unroll
+            for (int i = 0; i < HB_FACE_UNROLL; i++)
+#pragma unroll
+                for (int cc = 0; cc < 4; cc++) asm volatile("" : "+v"(F[i][cc]));
+#pragma unroll
+            for (int i = 0; i < HB_FACE_UNROLL; i++) {
+                const int f = fb + j + 8 * i;
+                const double sd = F[i][0] * y.x + F[i][1] * y.y + F[i][2] * y.z - F[i][3];
+                if (f < nf && sd > smax) { smax = sd; fm = f; }
+            }
         }
         double w;
         int jj;
