@@ -572,7 +572,7 @@ __device__ __noinline__ static void team_reduce4_g(int n, int k, gdouble* gc) {
     __syncthreads();
 }
 /* hull (A, robot link) vs box (B), full geometry (oracle nc_hull_box) */
-__device__ __noinline__ static void team_hull_box_full(const HullArg& A, const HullArg& B, const XF& TA, const XF& TB,
+__device__ __forceinline__ static void team_hull_box_full(const HullArg& A, const HullArg& B, const XF& TA, const XF& TB,
                                                        double thr, int k, unsigned short* hcert, gdouble* gc) {
     const int lane = threadIdx.x;
     const m3 RAB = mtm(TB.R, TA.R);
@@ -703,7 +703,7 @@ __device__ __noinline__ static void team_hull_box_full(const HullArg& A, const H
     PROF_ADD(PF_HB_REDUCE, t_hr);
 }
 /* hull (A, robot link) vs hull (B), full geometry (oracle nc_hull_hull, every candidate kept) */
-__device__ __noinline__ static void team_hull_hull_full(const HullArg& A, const HullArg& B, const XF& TA, const XF& TB,
+__device__ __forceinline__ static void team_hull_hull_full(const HullArg& A, const HullArg& B, const XF& TA, const XF& TB,
                                                         double thr, int k, gdouble* gc) {
     const int lane = threadIdx.x;
     const double mA = A.margin, mB = B.margin;
