@@ -441,6 +441,10 @@ static void build_scene(scene* s, int variant, int flags) {
         box_collider(c, r, r, hh, UG_CYL_MARGIN, UG_DEFAULT_FRICTION);
         c->kind = UG_SHAPE_HULL;
         c->margin = UG_CYL_MARGIN;
+        if (s->full) { /* GEOM_CYLINDER (env_golf_v0.py:305) as a cylinder, not the 16-gon prism */
+            c->kind = UG_SHAPE_CYL;
+            c->margin = 0.0;
+        }
         c->v0 = UG_CYL_V0; c->nv = UG_CYL_NV; c->f0 = UG_CYL_F0; c->nf = UG_CYL_NF;
         c->P = V(0.0, 0.0, d2); c->aP = c->P;
         c->owner = -2; c->ent = 1;
@@ -1180,6 +1184,134 @@ static void nc_hull_sphere(const xf* TA, const collider* A, const xf* TB, const 
 #include "ug_fidelity.h"
 #endif
 
+/* ---- full geometry: the club disc as a true cylinder (UG_SHAPE_CYL) ----
+ * btCylinderShapeZ [ext] (env_golf_v0.py:305: GEOM_CYLINDER radius 0.04, height 0.01) collides through GJK/EPA on its
+ * analytic support map.  Restated here in the framework of the other convex pairs: exact point-to-cylinder distances
+ * for the other shape's vertices (box corners / hull vertices / sphere centre), and the cylinder's support points
+ * along the other shape's inward face normals tested against that shape's planes (as a box corner is against a
+ * hull), deepest + farthest-spread 4.  The cylinder is its outer surface (radius r, half height hh, the safe margin
+ * included); a support direction along the axis (a flat cap against a face) gives the cap's 4 rim points on the
+ * shape frame's x / y axes.  Used only with UG_GEOM_FULL; the LOD geometry keeps the 16-gon prism. */
+/* signed distance from x (cylinder frame) to the solid cylinder; nl: outward unit normal at the nearest surface point
+ * pl (inside: the nearer of the side and the cap) */
+static double cyl_point(double r, double hh, v3 x, v3* nl, v3* pl) {
+    const double rho = ug_sqrt(x.x * x.x + x.y * x.y);
+    const double dr = rho - r, dz = ug_fabs(x.z) - hh;
+    const double sz = x.z < 0 ? -1.0 : 1.0;
+    if (dr <= 0 && dz <= 0) {
+        if (dr > dz && rho > 0) {
+            *nl = V(x.x / rho, x.y / rho, 0.0);
+            *pl = V(nl->x * r, nl->y * r, x.z);
+            return dr;
+        }
+        *nl = V(0.0, 0.0, sz);
+        *pl = V(x.x, x.y, sz * hh);
+        return dz;
+    }
+    const double k = rho > r ? r / rho : 1.0;
+    const v3 q = V(x.x * k, x.y * k, ug_max(-hh, ug_min(hh, x.z)));
+    const v3 d = vsub(x, q);
+    const double len = vlen(d);
+    *nl = vscale(d, 1.0 / len);
+    *pl = q;
+    return len;
+}
+/* support points of the cylinder along u (cylinder frame): one rim point, or the cap's 4 rim points when u lies along
+ * the axis */
+static int cyl_support(double r, double hh, v3 u, v3* out) {
+    const double sz = u.z < 0 ? -1.0 : 1.0;
+    const double ur = ug_sqrt(u.x * u.x + u.y * u.y);
+    if (ur > 1e-9) {
+        out[0] = V(r * (u.x / ur), r * (u.y / ur), sz * hh);
+        return 1;
+    }
+    out[0] = V(r, 0.0, sz * hh);
+    out[1] = V(-r, 0.0, sz * hh);
+    out[2] = V(0.0, r, sz * hh);
+    out[3] = V(0.0, -r, sz * hh);
+    return 4;
+}
+/* sphere (A) vs cylinder (B) */
+static void nc_sphere_cyl(const xf* TA, const collider* A, const xf* TB, const collider* B, double thr, candlist* out) {
+    const v3 x = xf_inv_apply(TB, TA->p);
+    v3 nl, pl;
+    const double d = cyl_point(B->half[0], B->half[2], x, &nl, &pl);
+    const double depth = d - A->half[0];
+    if (depth < thr) cand_add(out, mv(&TB->R, nl), xf_apply(TB, pl), depth);
+}
+/* face f of the polytope A (a box's 6 faces -x +x -y +y -z +z, or a hull's planes) as n.x <= off in A's frame */
+static void poly_face(const collider* A, int f, v3* n, double* off) {
+    if (A->kind == UG_SHAPE_BOX) {
+        const int ax = f >> 1;
+        const double sg = (f & 1) ? 1.0 : -1.0;
+        *n = V(ax == 0 ? sg : 0.0, ax == 1 ? sg : 0.0, ax == 2 ? sg : 0.0);
+        *off = A->half[ax];
+        return;
+    }
+    const double* F = &UG_HULL_F[4 * (A->f0 + f)];
+    *n = V(F[0], F[1], F[2]);
+    *off = F[3];
+}
+/* polytope (A: robot hull or box) vs cylinder (B): A's vertices against the cylinder, then the cylinder's support
+ * points along -n_f for every face f of A that has the cylinder's centre in front of it, each tested against all of
+ * A's planes (the first maximum; the scan stops at a plane that already clears the threshold, as the corner test) */
+static void nc_poly_cyl(const xf* TA, const collider* A, const xf* TB, const collider* B, double thr, candlist* out) {
+    const double r = B->half[0], hh = B->half[2];
+    const int hull = A->kind == UG_SHAPE_HULL;
+    const double mA = hull ? A->margin : 0.0;
+    const int nv = hull ? A->nv : 8, nf = hull ? A->nf : 6;
+    static _Thread_local candlist L;
+    cand_init(&L, A->full ? MAXCAND : LOD_MAXCAND);
+    const m3 RAB = mtm(&TB->R, &TA->R);
+    const v3 pAB = mtv(&TB->R, vsub(TA->p, TB->p));
+    for (int i = 0; i < nv; i++) {
+        v3 xa;
+        if (hull) {
+            const double* vv = &UG_HULL_V[3 * (A->v0 + i)];
+            xa = V(vv[0], vv[1], vv[2]);
+        } else {
+            xa = V((i & 1) ? A->half[0] : -A->half[0], (i & 2) ? A->half[1] : -A->half[1], (i & 4) ? A->half[2] : -A->half[2]);
+        }
+        const v3 x = vadd(mv(&RAB, xa), pAB);
+        v3 nl, pl;
+        const double depth = cyl_point(r, hh, x, &nl, &pl) - mA;
+        if (depth < thr) cand_add(&L, mv(&TB->R, nl), xf_apply(TB, pl), depth);
+    }
+    const m3 RBA = mtm(&TA->R, &TB->R);
+    const v3 pBA = mtv(&TA->R, vsub(TB->p, TA->p));
+    for (int f = 0; f < nf; f++) {
+        v3 n;
+        double off;
+        poly_face(A, f, &n, &off);
+        if (vdot(n, pBA) - off <= 0) continue; /* the cylinder's centre is not in front of face f */
+        v3 sp[4];
+        const int k = cyl_support(r, hh, mtv(&RBA, vneg(n)), sp);
+        for (int j = 0; j < k; j++) {
+            const v3 y = vadd(mv(&RBA, sp[j]), pBA);
+            if (vdot(n, y) - off - mA >= thr) continue;
+            double smax = -1e300;
+            int fm = -1;
+            for (int g = 0; g < nf; g++) {
+                v3 ng;
+                double og;
+                poly_face(A, g, &ng, &og);
+                const double sd = ng.x * y.x + ng.y * y.y + ng.z * y.z - og;
+                if (sd > smax) { smax = sd; fm = g; }
+                if (sd - mA >= thr) break;
+            }
+            const double depth = smax - mA;
+            if (depth < thr) {
+                v3 nm;
+                double om;
+                poly_face(A, fm, &nm, &om);
+                cand_add(&L, vneg(mv(&TA->R, nm)), xf_apply(TB, sp[j]), depth);
+            }
+        }
+    }
+    reduce4(&L);
+    for (int i = 0; i < L.n; i++) cand_add(out, L.c[i].n, L.c[i].pB, L.c[i].d);
+}
+
 /* btPersistentManifold [ext]: getCacheEntry / replaceContactPoint / addManifoldPoint / sortCachedPoints */
 static int sort_cached(const manifold* M, const cpoint* pt) {
     int maxi = -1;
@@ -1295,6 +1427,17 @@ static void collide(ugo_env* e, const kin* k) {
         else if (A->kind == UG_SHAPE_HULL && B->kind == UG_SHAPE_BOX) nc_hull_box(&TA, A, &TB, B, P->thr, &L);
         else if (A->kind == UG_SHAPE_HULL && B->kind == UG_SHAPE_SPHERE) nc_hull_sphere(&TA, A, &TB, B, P->thr, &L);
         else if (A->kind == UG_SHAPE_HULL && B->kind == UG_SHAPE_HULL) nc_hull_hull(&TA, A, &TB, B, P->thr, &L);
+        else if (A->kind == UG_SHAPE_SPHERE && B->kind == UG_SHAPE_CYL) nc_sphere_cyl(&TA, A, &TB, B, P->thr, &L);
+        else if ((A->kind == UG_SHAPE_HULL || A->kind == UG_SHAPE_BOX) && B->kind == UG_SHAPE_CYL)
+            nc_poly_cyl(&TA, A, &TB, B, P->thr, &L);
+        else if (A->kind == UG_SHAPE_CYL && B->kind == UG_SHAPE_BOX) {
+            /* cylinder-box with swapped roles: flip the normal, move the point onto the box */
+            candlist L2;
+            cand_init(&L2, LOD_MAXCAND);
+            nc_poly_cyl(&TB, B, &TA, A, P->thr, &L2);
+            for (int i = 0; i < L2.n; i++)
+                cand_add(&L, vneg(L2.c[i].n), vadd(L2.c[i].pB, vscale(L2.c[i].n, L2.c[i].d)), L2.c[i].d);
+        }
         else if (A->kind == UG_SHAPE_SPHERE && B->kind == UG_SHAPE_HULL) {
             /* hull-sphere with swapped roles: flip normal, move the point onto the sphere */
             candlist L2;

@@ -8,3 +8,9 @@ for g in lod full; do
   timeout -k 10 300 python bench.py --no-cpu-baseline --geometry $g > gpurun_out/r3d/bench_bb_$g.json 2> gpurun_out/r3d/bench_bb_$g.err || exit 1
   cut -c1-150 gpurun_out/r3d/bench_bb_$g.json
 done
+timeout -k 10 300 python tools/phase_prof.py --steps 3 --task 3 --envs 2048 --geometry full > gpurun_out/r3d/phase_golf_full.txt 2>&1 || exit 1
+for t in 1 2 3; do
+  e=4096; [ $t -ge 2 ] && e=8192
+  timeout -k 10 300 python bench.py --no-cpu-baseline --geometry full --task $t --envs $e --steps 10 --warmup 2 --reps 3 > gpurun_out/r3d/bench_t${t}_full.json 2> gpurun_out/r3d/bench_t${t}_full.err || exit 1
+  cut -c1-150 gpurun_out/r3d/bench_t${t}_full.json
+done

@@ -67,6 +67,8 @@ UG_CONST double UG_GEAR_RATIO[5] = {1.0, -1.0, -1.0, 1.0, -1.0};
 #define UG_SHAPE_BOX 0
 #define UG_SHAPE_HULL 1
 #define UG_SHAPE_SPHERE 2
+#define UG_SHAPE_CYL 3 /* full geometry: the Golf club's disc as a true cylinder (radius half[0], half height half[2],
+                        * axis z of the shape frame; its outer surface, the safe margin included) */
 
 /* statics: plane.urdf = 30x30x10 box, top at the load height, lateral friction 1 [ext];
  * table = box 1 x 2 x 0.5 centred at (0,0,-0.25) (env_ball_balance_v0.py:69-71, 216-247);

@@ -181,6 +181,10 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
         c->kind = UG_SHAPE_HULL;
         c->margin = UG_CYL_MARGIN;
         c->v0 = UG_CYL_V0; c->nv = UG_CYL_NV; c->f0 = UG_CYL_F0; c->nf = UG_CYL_NF;
+        if (s->full) { /* GEOM_CYLINDER as a cylinder (oracle build_scene) */
+            c->kind = UG_SHAPE_CYL;
+            c->margin = 0.0;
+        }
         c->P = V(0.0, 0.0, d2); c->aP = c->P;
         c->owner = -2; c->ent = 1;
         s->oncol[0] = 3;

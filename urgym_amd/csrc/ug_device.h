@@ -784,6 +784,46 @@ DFI void hull_plane_max(const C& A, v3 y, double& smax, int& fm) {
         }
     }
 }
+/* ---- full geometry: the club disc as a true cylinder (UG_SHAPE_CYL), oracle cyl_point / cyl_support / nc_sphere_cyl
+ * (the polytope pairs run on the whole wave: ug_team.h team_poly_cyl) ---- */
+DFI double cyl_point(double r, double hh, v3 x, v3& nl, v3& pl) {
+    const double rho = ug_sqrt(x.x * x.x + x.y * x.y);
+    const double dr = rho - r, dz = ug_fabs(x.z) - hh;
+    const double sz = x.z < 0 ? -1.0 : 1.0;
+    if (dr <= 0 && dz <= 0) {
+        if (dr > dz && rho > 0) {
+            nl = V(x.x / rho, x.y / rho, 0.0);
+            pl = V(nl.x * r, nl.y * r, x.z);
+            return dr;
+        }
+        nl = V(0.0, 0.0, sz);
+        pl = V(x.x, x.y, sz * hh);
+        return dz;
+    }
+    const double k = rho > r ? r / rho : 1.0;
+    const v3 q = V(x.x * k, x.y * k, ug_max(-hh, ug_min(hh, x.z)));
+    const v3 d = vsub(x, q);
+    const double len = vlen(d);
+    nl = vscale(d, 1.0 / len);
+    pl = q;
+    return len;
+}
+/* support points along u (cylinder frame): returns their count (1, or the cap's 4 rim points when u is axial);
+ * point j of 4 is (+-r, 0) / (0, +-r) in order */
+DFI int cyl_support_n(v3 u) { return ug_sqrt(u.x * u.x + u.y * u.y) > 1e-9 ? 1 : 4; }
+DFI v3 cyl_support_pt(double r, double hh, v3 u, int j) {
+    const double sz = u.z < 0 ? -1.0 : 1.0;
+    const double ur = ug_sqrt(u.x * u.x + u.y * u.y);
+    if (ur > 1e-9) return V(r * (u.x / ur), r * (u.y / ur), sz * hh);
+    return j == 0 ? V(r, 0.0, sz * hh) : j == 1 ? V(-r, 0.0, sz * hh) : j == 2 ? V(0.0, r, sz * hh) : V(0.0, -r, sz * hh);
+}
+DF void nc_sphere_cyl(const XF& TA, const Collider& A, const XF& TB, const Collider& B, double thr, CandList& out) {
+    const v3 x = xf_inv_apply(TB, TA.p);
+    v3 nl, pl;
+    const double d = cyl_point(B.half[0], B.half[2], x, nl, pl);
+    const double depth = d - A.half[0];
+    if (depth < thr) cand_add(out, mv(TB.R, nl), xf_apply(TB, pl), depth);
+}
 /* hull (robot link) vs box: cooperative, one wavefront per pair -- ug_team.h team_hull_box */
 DF void nc_hull_sphere(const XF& TA, const Collider& A, const XF& TB, const Collider& B, double thr, CandList& out) {
     v3 y = mtv(TA.R, vsub(TB.p, TA.p));

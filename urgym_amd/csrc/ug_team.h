@@ -766,6 +766,136 @@ __device__ __forceinline__ static void team_hull_hull_full(const HullArg& A, con
     team_reduce4_g(n, k, gc);
 }
 
+/* polytope (A: full robot hull or box) vs the disc cylinder (B), full geometry (oracle nc_poly_cyl): A's vertices
+ * (chunks of 64 lanes, chunk spheres culled exactly) against the cylinder, then lane per face f of A: the cylinder's
+ * support points along -n_f when its centre is in front of f, each scanned against all of A's planes (lane-serial,
+ * the oracle's loop with its early exit), candidates face-major in the workspace list, reduce4.  swapped: the pair is
+ * (cylinder, box) -- the 4 results get the oracle's role swap (normal flipped, point moved onto the box). */
+__device__ __forceinline__ void poly_face(const HullArg& A, bool hull, int f, v3& n, double& off) {
+    if (!hull) {
+        const int ax = f >> 1;
+        const double sg = (f & 1) ? 1.0 : -1.0;
+        n = V(ax == 0 ? sg : 0.0, ax == 1 ? sg : 0.0, ax == 2 ? sg : 0.0);
+        off = ax == 0 ? A.half[0] : ax == 1 ? A.half[1] : A.half[2];
+        return;
+    }
+    const double* F = &UG_HULL_F[4 * (A.f0 + f)];
+    n = V(F[0], F[1], F[2]);
+    off = F[3];
+}
+__device__ __forceinline__ static void team_poly_cyl(int k, bool swapped, gdouble* gc) {
+    Shared& sh = g_sh;
+    const int lane = threadIdx.x;
+    /* the pair's record straight from LDS, sides picked there: a run-time pick between two private copies is the
+     * pattern this compiler miscompiles (tools/scc_audit.py, tests/test_isa_audit.py) */
+    const PairInfo& P = sh.pinfo[k];
+    const HullArg A = swapped ? P.B : P.A, B = swapped ? P.A : P.B;
+    const XF TA = swapped ? P.TB : P.TA, TB = swapped ? P.TA : P.TB;
+    const int akind = swapped ? P.kb : P.ka;
+    const double thr = P.thr;
+    const double r = B.half[0], hh = B.half[2];
+    const bool hull = akind == UG_SHAPE_HULL;
+    const double mA = hull ? A.margin : 0.0;
+    const int nv = hull ? A.nv : 8, nf = hull ? A.nf : 6;
+    const m3 RAB = mtm(TB.R, TA.R);
+    const v3 pAB = mtv(TB.R, vsub(TA.p, TB.p));
+    int n = 0;
+    for (int v0 = 0, ch = A.c0; v0 < nv; v0 += TEAM, ch++) {
+        if (hull) { /* exact chunk cull (the cylinder distance is 1-Lipschitz): no vertex of the chunk qualifies */
+            const double* S = &UG_HULL_CS[4 * ch];
+            const v3 cc = vadd(mv(RAB, V(S[0], S[1], S[2])), pAB);
+            v3 t0, t1;
+            if (cyl_point(r, hh, cc, t0, t1) - S[3] >= thr + mA + 1e-9) continue;
+        }
+        const int vi = v0 + lane;
+        int valid = 0;
+        Cand c;
+        if (vi < nv) {
+            v3 xa;
+            if (hull) {
+                const double* vv = &UG_HULL_V[3 * (A.v0 + vi)];
+                xa = V(vv[0], vv[1], vv[2]);
+            } else {
+                xa = V((vi & 1) ? A.half[0] : -A.half[0], (vi & 2) ? A.half[1] : -A.half[1], (vi & 4) ? A.half[2] : -A.half[2]);
+            }
+            const v3 x = vadd(mv(RAB, xa), pAB);
+            v3 nl, pl;
+            const double depth = cyl_point(r, hh, x, nl, pl) - mA;
+            if (depth < thr) {
+                valid = 1;
+                c.n = mv(TB.R, nl);
+                c.pB = xf_apply(TB, pl);
+                c.d = depth;
+            }
+        }
+        const unsigned long long m = ballot(valid);
+        if (valid) gc_put(gc, n + lane_prefix(m), c);
+        n += __popcll(m);
+    }
+    const m3 RBA = mtm(TA.R, TB.R);
+    const v3 pBA = mtv(TA.R, vsub(TB.p, TA.p));
+    for (int f0 = 0; f0 < nf; f0 += TEAM) {
+        const int f = f0 + lane;
+        Cand cs[4];
+        bool vb[4] = {false, false, false, false};
+        if (f < nf) {
+            v3 nf_;
+            double off;
+            poly_face(A, hull, f, nf_, off);
+            if (vdot(nf_, pBA) - off > 0) {
+                const v3 u = mtv(RBA, vneg(nf_));
+                const int ks = cyl_support_n(u);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (j >= ks) break;
+                    const v3 sp = cyl_support_pt(r, hh, u, j);
+                    const v3 y = vadd(mv(RBA, sp), pBA);
+                    if (vdot(nf_, y) - off - mA >= thr) continue;
+                    double smax = -1e300;
+                    int fm = -1;
+                    for (int g = 0; g < nf; g++) {
+                        v3 ng;
+                        double og;
+                        poly_face(A, hull, g, ng, og);
+                        const double sd = ng.x * y.x + ng.y * y.y + ng.z * y.z - og;
+                        if (sd > smax) { smax = sd; fm = g; }
+                        if (sd - mA >= thr) break;
+                    }
+                    const double depth = smax - mA;
+                    if (depth < thr) {
+                        v3 nm;
+                        double om;
+                        poly_face(A, hull, fm, nm, om);
+                        vb[j] = true;
+                        cs[j].n = vneg(mv(TA.R, nm));
+                        cs[j].pB = xf_apply(TB, sp);
+                        cs[j].d = depth;
+                    }
+                }
+            }
+        }
+        const int cnt = (int)vb[0] + (int)vb[1] + (int)vb[2] + (int)vb[3];
+        const unsigned long long b0 = ballot(cnt & 1), b1 = ballot(cnt & 2), b2 = ballot(cnt & 4);
+        int pos = n + lane_prefix(b0) + 2 * lane_prefix(b1) + 4 * lane_prefix(b2);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (vb[j]) gc_put(gc, pos++, cs[j]);
+        n += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+    }
+    gc_publish();
+    team_reduce4_g(n, k, gc);
+    if (swapped) { /* cylinder-box: the oracle's role swap on the kept points */
+        if (lane < sh.u.cand.n[k]) {
+            Cand c = sh.u.cand.c[k][lane];
+            const v3 n0 = c.n;
+            c.n = vneg(n0);
+            c.pB = vadd(c.pB, vscale(n0, c.d));
+            sh.u.cand.c[k][lane] = c;
+        }
+        __syncthreads();
+    }
+}
+
 /* box (A) vs box (B) (oracle nc_box_box: ODE dBoxBox2 as btBoxBoxDetector), the whole wave per pair.  The same
  * operations on the same values as the serial routine, spread over lanes:
  *   - the 15 separating-axis tests in lanes 0..14 (any positive separation ends the pair, as the serial early
@@ -1153,13 +1283,18 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
             pi.a = P.a; pi.b = P.b; pi.ka = A.kind; pi.kb = B.kind;
             sh.pinfo[lane] = pi;
             hk = A.kind == UG_SHAPE_HULL && (B.kind == UG_SHAPE_BOX || B.kind == UG_SHAPE_HULL);
+            if (FULL) /* the disc cylinder against a polytope, either side */
+                hk = hk || (B.kind == UG_SHAPE_CYL && (A.kind == UG_SHAPE_HULL || A.kind == UG_SHAPE_BOX)) ||
+                     (A.kind == UG_SHAPE_CYL && B.kind == UG_SHAPE_BOX);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         for (unsigned long long hm = ballot(hk); hm != 0ull; hm &= hm - 1ull) {
             const int k = __builtin_ctzll(hm);
             const PairInfo pi = sh.pinfo[k];
-            if (FULL && pi.A.nv > TEAM) { /* a full-geometry robot hull (every full hull has more than 64 vertices) */
+            if (FULL && (pi.kb == UG_SHAPE_CYL || pi.ka == UG_SHAPE_CYL))
+                team_poly_cyl(k, pi.ka == UG_SHAPE_CYL, (gdouble*)(ws + WS_FC));
+            else if (FULL && pi.A.nv > TEAM) { /* a full-geometry robot hull (every full hull has more than 64 vertices) */
                 if (pi.kb == UG_SHAPE_BOX)
                     team_hull_box_full(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k,
                                        (unsigned short*)(ws + WS_HC2) + 8 * sh.ov[c0 + k], (gdouble*)(ws + WS_FC));
@@ -1209,8 +1344,11 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
             L.n = 0;
             L.c = (LCand*)&sh.u.cand.c[lane][0];
             isbb = A.kind == UG_SHAPE_BOX && B.kind == UG_SHAPE_BOX;
-            if (A.kind == UG_SHAPE_HULL && (B.kind == UG_SHAPE_BOX || B.kind == UG_SHAPE_HULL)) {
-                L.n = sh.u.cand.n[lane]; /* team_hull_box / team_hull_hull wrote them */
+            if ((A.kind == UG_SHAPE_HULL && (B.kind == UG_SHAPE_BOX || B.kind == UG_SHAPE_HULL)) ||
+                (FULL && ((B.kind == UG_SHAPE_CYL && A.kind != UG_SHAPE_SPHERE) || A.kind == UG_SHAPE_CYL))) {
+                L.n = sh.u.cand.n[lane]; /* team_hull_box / team_hull_hull / team_poly_cyl wrote them */
+            } else if (FULL && A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_CYL) {
+                nc_sphere_cyl(TA, A, TB, B, P.thr, L);
             } else if (A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_HULL) {
                 nc_hull_sphere(TB, B, TA, A, P.thr, L);
                 for (int i = 0; i < L.n; i++) { /* swapped roles: flip the normal, move the point onto the sphere */
