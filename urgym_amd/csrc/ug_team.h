@@ -493,6 +493,16 @@ __device__ __forceinline__ static void team_reduce4(int n, int k) {
     __syncthreads();
 }
 
+__device__ __noinline__ static void team_reduce4_g(int n, int k, gdouble* gc);
+__device__ __forceinline__ void fc_reduce(int n, int k, gdouble* gc) {
+    if (n <= 64) { /* the LDS copy is complete: the LOD path's reduce4 (same selection, same arithmetic) */
+        __syncthreads();
+        team_reduce4(n, k);
+    } else {
+        gc_publish();
+        team_reduce4_g(n, k, gc);
+    }
+}
 /* ---- full-geometry mode (UG_GEOM_FULL): hulls with more vertices than lanes (up to UG_FULL_HULL_MAXV) and more
  * candidates than the LDS list holds.  Same arithmetic as the LOD functions above and as the oracle's nc_hull_box /
  * nc_hull_hull with every candidate kept (collider.full): vertices in chunks of 64 lanes, candidates in canonical
@@ -514,6 +524,14 @@ __device__ __forceinline__ void gc_publish() { /* the wave's workspace stores, v
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
 }
+/* candidate i to the workspace list, and to the LDS list (g_sh.hc) while it fits: a pair that ends with at most 64
+ * candidates is reduced from LDS (team_reduce4), a larger one from the workspace (team_reduce4_g) */
+__device__ __forceinline__ void fc_put(gdouble* gc, int i, const Cand& c) {
+    gc_put(gc, i, c);
+    if (i < 64) g_sh.hc[i] = c;
+}
+__device__ __forceinline__ static void team_reduce4(int n, int k);
+__device__ __forceinline__ void fc_reduce(int n, int k, gdouble* gc);
 /* candidates gc[0..n) -> at most 4 in sh.u.cand.c[k] (oracle reduce4) */
 __device__ __noinline__ static void team_reduce4_g(int n, int k, gdouble* gc) {
     Shared& sh = g_sh;
@@ -626,7 +644,7 @@ __device__ __forceinline__ static void team_hull_box_full(const HullArg& A, cons
             }
         }
         const unsigned long long vb = ballot(vvalid);
-        if (vvalid) gc_put(gc, n + lane_prefix(vb), vc);
+        if (vvalid) fc_put(gc, n + lane_prefix(vb), vc);
         n += __popcll(vb);
     }
     PROF_ADD(PF_HB_VERT, t_hv);
@@ -694,12 +712,11 @@ __device__ __forceinline__ static void team_hull_box_full(const HullArg& A, cons
         }
     }
     const unsigned long long cb = ballot(cvalid);
-    if (cvalid) gc_put(gc, n + lane_prefix(cb), cc);
+    if (cvalid) fc_put(gc, n + lane_prefix(cb), cc);
     n += __popcll(cb);
-    gc_publish();
     PROF_ADD(PF_HB_CORNER, t_hc);
     PROF_T0(t_hr);
-    team_reduce4_g(n, k, gc);
+    fc_reduce(n, k, gc);
     PROF_ADD(PF_HB_REDUCE, t_hr);
 }
 /* hull (A, robot link) vs hull (B), full geometry (oracle nc_hull_hull, every candidate kept) */
@@ -732,7 +749,7 @@ __device__ __forceinline__ static void team_hull_hull_full(const HullArg& A, con
             }
         }
         const unsigned long long m = ballot(valid);
-        if (valid) gc_put(gc, n + lane_prefix(m), ac);
+        if (valid) fc_put(gc, n + lane_prefix(m), ac);
         n += __popcll(m);
     }
     const m3 RBA = mtm(TA.R, TB.R);
@@ -759,11 +776,10 @@ __device__ __forceinline__ static void team_hull_hull_full(const HullArg& A, con
             }
         }
         const unsigned long long m = ballot(valid);
-        if (valid) gc_put(gc, n + lane_prefix(m), bc);
+        if (valid) fc_put(gc, n + lane_prefix(m), bc);
         n += __popcll(m);
     }
-    gc_publish();
-    team_reduce4_g(n, k, gc);
+    fc_reduce(n, k, gc);
 }
 
 /* polytope (A: full robot hull or box) vs the disc cylinder (B), full geometry (oracle nc_poly_cyl): A's vertices
@@ -829,7 +845,7 @@ __device__ __forceinline__ static void team_poly_cyl(int k, bool swapped, gdoubl
             }
         }
         const unsigned long long m = ballot(valid);
-        if (valid) gc_put(gc, n + lane_prefix(m), c);
+        if (valid) fc_put(gc, n + lane_prefix(m), c);
         n += __popcll(m);
     }
     const m3 RBA = mtm(TA.R, TB.R);
@@ -879,11 +895,10 @@ __device__ __forceinline__ static void team_poly_cyl(int k, bool swapped, gdoubl
         int pos = n + lane_prefix(b0) + 2 * lane_prefix(b1) + 4 * lane_prefix(b2);
 #pragma unroll
         for (int j = 0; j < 4; j++)
-            if (vb[j]) gc_put(gc, pos++, cs[j]);
+            if (vb[j]) fc_put(gc, pos++, cs[j]);
         n += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
     }
-    gc_publish();
-    team_reduce4_g(n, k, gc);
+    fc_reduce(n, k, gc);
     if (swapped) { /* cylinder-box: the oracle's role swap on the kept points */
         if (lane < sh.u.cand.n[k]) {
             Cand c = sh.u.cand.c[k][lane];
