@@ -493,16 +493,6 @@ __device__ __forceinline__ static void team_reduce4(int n, int k) {
     __syncthreads();
 }
 
-__device__ __noinline__ static void team_reduce4_g(int n, int k, gdouble* gc);
-__device__ __forceinline__ void fc_reduce(int n, int k, gdouble* gc) {
-    if (n <= 64) { /* the LDS copy is complete: the LOD path's reduce4 (same selection, same arithmetic) */
-        __syncthreads();
-        team_reduce4(n, k);
-    } else {
-        gc_publish();
-        team_reduce4_g(n, k, gc);
-    }
-}
 /* ---- full-geometry mode (UG_GEOM_FULL): hulls with more vertices than lanes (up to UG_FULL_HULL_MAXV) and more
  * candidates than the LDS list holds.  Same arithmetic as the LOD functions above and as the oracle's nc_hull_box /
  * nc_hull_hull with every candidate kept (collider.full): vertices in chunks of 64 lanes, candidates in canonical
@@ -588,6 +578,15 @@ __device__ __noinline__ static void team_reduce4_g(int n, int k, gdouble* gc) {
     }
     if (lane == 0) sh.u.cand.n[k] = 4;
     __syncthreads();
+}
+__device__ __forceinline__ void fc_reduce(int n, int k, gdouble* gc) {
+    if (n <= 64) { /* the LDS copy is complete: the LOD path's reduce4 (same selection, same arithmetic) */
+        __syncthreads();
+        team_reduce4(n, k);
+    } else {
+        gc_publish();
+        team_reduce4_g(n, k, gc);
+    }
 }
 /* hull (A, robot link) vs box (B), full geometry (oracle nc_hull_box) */
 __device__ __forceinline__ static void team_hull_box_full(const HullArg& A, const HullArg& B, const XF& TA, const XF& TB,
