@@ -849,53 +849,66 @@ __device__ __forceinline__ static void team_poly_cyl(int k, bool swapped, gdoubl
     }
     const m3 RBA = mtm(TA.R, TB.R);
     const v3 pBA = mtv(TA.R, vsub(TB.p, TA.p));
+    /* lane per face f: the filter, the support points and their own-plane test; then each surviving point in
+     * (face, point) order gets the plane scan on the whole wave -- rejected as soon as a batch of 64 planes holds one
+     * that clears the threshold (the oracle's early exit rejects exactly those), else the first maximum over all */
     for (int f0 = 0; f0 < nf; f0 += TEAM) {
         const int f = f0 + lane;
-        Cand cs[4];
-        bool vb[4] = {false, false, false, false};
+        bool sv[4] = {false, false, false, false};
+        v3 u = V(0, 0, 0);
         if (f < nf) {
             v3 nf_;
             double off;
             poly_face(A, hull, f, nf_, off);
             if (vdot(nf_, pBA) - off > 0) {
-                const v3 u = mtv(RBA, vneg(nf_));
+                u = mtv(RBA, vneg(nf_));
                 const int ks = cyl_support_n(u);
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     if (j >= ks) break;
-                    const v3 sp = cyl_support_pt(r, hh, u, j);
-                    const v3 y = vadd(mv(RBA, sp), pBA);
-                    if (vdot(nf_, y) - off - mA >= thr) continue;
-                    double smax = -1e300;
-                    int fm = -1;
-                    for (int g = 0; g < nf; g++) {
+                    const v3 y = vadd(mv(RBA, cyl_support_pt(r, hh, u, j)), pBA);
+                    sv[j] = !(vdot(nf_, y) - off - mA >= thr);
+                }
+            }
+        }
+        const unsigned long long m0 = ballot(sv[0]), m1 = ballot(sv[1]), m2 = ballot(sv[2]), m3 = ballot(sv[3]);
+        for (unsigned long long any = m0 | m1 | m2 | m3; any != 0ull; any &= any - 1ull) {
+            const int L = __builtin_ctzll(any);
+            const v3 uL = V(readlane_d(u.x, L), readlane_d(u.y, L), readlane_d(u.z, L));
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const unsigned long long mj = j == 0 ? m0 : j == 1 ? m1 : j == 2 ? m2 : m3;
+                if (!((mj >> L) & 1ull)) continue;
+                const v3 sp = cyl_support_pt(r, hh, uL, j);
+                const v3 y = vadd(mv(RBA, sp), pBA);
+                double smax = -1e300;
+                int fm = 0x7fffffff;
+                bool rej = false;
+                for (int g0 = 0; g0 < nf; g0 += TEAM) {
+                    const int g = g0 + lane;
+                    if (g < nf) {
                         v3 ng;
                         double og;
                         poly_face(A, hull, g, ng, og);
                         const double sd = ng.x * y.x + ng.y * y.y + ng.z * y.z - og;
                         if (sd > smax) { smax = sd; fm = g; }
-                        if (sd - mA >= thr) break;
+                        rej = rej || sd - mA >= thr;
                     }
-                    const double depth = smax - mA;
-                    if (depth < thr) {
-                        v3 nm;
-                        double om;
-                        poly_face(A, hull, fm, nm, om);
-                        vb[j] = true;
-                        cs[j].n = vneg(mv(TA.R, nm));
-                        cs[j].pB = xf_apply(TB, sp);
-                        cs[j].d = depth;
-                    }
+                    if (ballot(rej)) break;
                 }
+                if (ballot(rej)) continue;
+                wave_best(smax, fm, true);
+                v3 nm;
+                double om;
+                poly_face(A, hull, fm, nm, om);
+                Cand c;
+                c.n = vneg(mv(TA.R, nm));
+                c.pB = xf_apply(TB, sp);
+                c.d = smax - mA;
+                if (lane == 0) fc_put(gc, n, c);
+                n++;
             }
         }
-        const int cnt = (int)vb[0] + (int)vb[1] + (int)vb[2] + (int)vb[3];
-        const unsigned long long b0 = ballot(cnt & 1), b1 = ballot(cnt & 2), b2 = ballot(cnt & 4);
-        int pos = n + lane_prefix(b0) + 2 * lane_prefix(b1) + 4 * lane_prefix(b2);
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-            if (vb[j]) fc_put(gc, pos++, cs[j]);
-        n += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
     }
     fc_reduce(n, k, gc);
     if (swapped) { /* cylinder-box: the oracle's role swap on the kept points */
