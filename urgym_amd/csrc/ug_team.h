@@ -598,16 +598,23 @@ __device__ __forceinline__ static void team_hull_box_full(const HullArg& A, cons
     const double mA = A.margin;
     int n = 0;
     PROF_T0(t_hv);
-    for (int v0 = 0, ch = A.c0; v0 < A.nv; v0 += TEAM, ch++) {
-        /* exact chunk cull: every vertex of the chunk lies in its bounding sphere (UG_HULL_CS); when the sphere is
-         * farther than thr + margin from the box (with 1e-9 for rounding), no vertex is inside the box or within
-         * the threshold, so the chunk adds no candidate -- the skipped work would have produced none */
-        {
-            const double* S = &UG_HULL_CS[4 * ch];
+    /* exact chunk cull, every chunk at once (lane c tests chunk c): every vertex of a chunk lies in its bounding
+     * sphere (UG_HULL_CS); when the sphere is farther than thr + margin from the box (with 1e-9 for rounding), no
+     * vertex is inside the box or within the threshold, so the chunk adds no candidate -- the skipped work would
+     * have produced none */
+    unsigned long long live;
+    {
+        bool keep = false;
+        if (lane < (A.nv + TEAM - 1) / TEAM) {
+            const double* S = &UG_HULL_CS[4 * (A.c0 + lane)];
             const v3 cc = vadd(mv(RAB, V(S[0], S[1], S[2])), pAB);
             const v3 q = V(ug_max(-h.x, ug_min(h.x, cc.x)), ug_max(-h.y, ug_min(h.y, cc.y)), ug_max(-h.z, ug_min(h.z, cc.z)));
-            if (vlen(vsub(cc, q)) - S[3] >= thr + mA + 1e-9) continue;
+            keep = !(vlen(vsub(cc, q)) - S[3] >= thr + mA + 1e-9);
         }
+        live = ballot(keep);
+    }
+    for (; live != 0ull; live &= live - 1ull) {
+        const int v0 = TEAM * __builtin_ctzll(live);
         const int vi = v0 + lane;
         int vvalid = 0;
         Cand vc;
@@ -815,13 +822,19 @@ __device__ __forceinline__ static void team_poly_cyl(int k, bool swapped, gdoubl
     const m3 RAB = mtm(TB.R, TA.R);
     const v3 pAB = mtv(TB.R, vsub(TA.p, TB.p));
     int n = 0;
-    for (int v0 = 0, ch = A.c0; v0 < nv; v0 += TEAM, ch++) {
-        if (hull) { /* exact chunk cull (the cylinder distance is 1-Lipschitz): no vertex of the chunk qualifies */
-            const double* S = &UG_HULL_CS[4 * ch];
+    unsigned long long live = 1ull; /* a box: its 8 corners, one chunk */
+    if (hull) { /* exact chunk cull, all chunks at once (the cylinder distance is 1-Lipschitz) */
+        bool keep = false;
+        if (lane < (nv + TEAM - 1) / TEAM) {
+            const double* S = &UG_HULL_CS[4 * (A.c0 + lane)];
             const v3 cc = vadd(mv(RAB, V(S[0], S[1], S[2])), pAB);
             v3 t0, t1;
-            if (cyl_point(r, hh, cc, t0, t1) - S[3] >= thr + mA + 1e-9) continue;
+            keep = !(cyl_point(r, hh, cc, t0, t1) - S[3] >= thr + mA + 1e-9);
         }
+        live = ballot(keep);
+    }
+    for (; live != 0ull; live &= live - 1ull) {
+        const int v0 = TEAM * __builtin_ctzll(live);
         const int vi = v0 + lane;
         int valid = 0;
         Cand c;
