@@ -54,7 +54,10 @@ static_assert(NV <= NVP, "dof slots exceed the padded row");
  * certificates as 16-bit face indices (the full hulls have up to UG_FULL_HULL_MAXF faces) */
 #define FC_MAX 1024
 static_assert(UG_FULL_HULL_MAXV + 64 + 8 <= FC_MAX, "a full hull pair's candidates must fit the workspace list");
-#define WS_FC (WS_HC + MAXPAIR)
+/* hull-hull pairs (LOD): per pair and per B vertex, the A face that last maximised its plane distance (a hint, as
+ * the corner certificates) */
+#define WS_HH (WS_HC + MAXPAIR)
+#define WS_FC (WS_HH + 8 * MAXPAIR)
 #define WS_HC2 (WS_FC + 7 * FC_MAX)
 /* per-env workspace stride: the LOD geometry ends at WS_FC, the full geometry adds its candidate list and 16-bit
  * certificates (a handle allocates only what its mode uses) */
@@ -401,7 +404,7 @@ __device__ __forceinline__ static void team_hull_box(const HullArg& A, const Hul
 /* hull (A) vs hull (B) (oracle nc_hull_hull): lane per A vertex against B's planes, lane per B vertex against
  * A's planes; candidates in canonical order (A vertices, then B vertices; at most 64 kept), then reduce4 */
 __device__ __forceinline__ static void team_hull_hull(const HullArg& A, const HullArg& B, const XF& TA, const XF& TB,
-                                                   double thr, int k) {
+                                                   double thr, int k, unsigned char* hcert) {
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
     double mA = A.margin, mB = B.margin;
@@ -434,7 +437,18 @@ __device__ __forceinline__ static void team_hull_hull(const HullArg& A, const Hu
         v3 y = vadd(mv(RBA, yl), pBA);
         double smax = -1e300;
         int fm = -1;
-        hull_plane_max(A, y, smax, fm);
+        /* certificate: the face that last maximised this vertex's plane distance; when its plane (the scan's own
+         * expression) already clears thr + margins, the scan's maximum does too -- no candidate, scan skipped */
+        int fc = lane < 64 ? hcert[lane] : 0;
+        fc = fc < A.nf ? fc : A.nf - 1;
+        const double* Fc = &UG_HULL_F[4 * (A.f0 + fc)];
+        const double sdc = Fc[0] * y.x + Fc[1] * y.y + Fc[2] * y.z - Fc[3];
+        if (sdc - mA - mB < thr) {
+            hull_plane_max(A, y, smax, fm);
+            hcert[lane] = (unsigned char)fm;
+        } else {
+            smax = sdc; /* rejected below */
+        }
         double depth = smax - mA - mB;
         if (depth < thr) {
             const double* F = &UG_HULL_F[4 * (A.f0 + fm)];
@@ -1341,7 +1355,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
                 else team_hull_hull_full(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k, (gdouble*)(ws + WS_FC));
             } else if (pi.kb == UG_SHAPE_BOX)
                 team_hull_box(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k, (unsigned char*)(ws + WS_HC) + 8 * sh.ov[c0 + k]);
-            else team_hull_hull(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k);
+            else team_hull_hull(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k, (unsigned char*)(ws + WS_HH) + 64 * sh.ov[c0 + k]);
             PROF_CNT(PC_HULL, 1);
         }
         PROF_ADD(PF_HULL, t_hull);
