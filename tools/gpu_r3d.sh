@@ -14,3 +14,7 @@ for t in 1 2 3; do
   timeout -k 10 300 python bench.py --no-cpu-baseline --geometry full --task $t --envs $e --steps 10 --warmup 2 --reps 3 > gpurun_out/r3d/bench_t${t}_full.json 2> gpurun_out/r3d/bench_t${t}_full.err || exit 1
   cut -c1-150 gpurun_out/r3d/bench_t${t}_full.json
 done
+timeout -k 10 300 python tools/phase_prof.py --steps 3 --task 3 --envs 2048 --geometry lod > gpurun_out/r3d/phase_golf_lod.txt 2>&1 || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_features.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "golf or Golf or 3 or sharded" > gpurun_out/r3d/golf_parity.log 2>&1; rc=$?; echo "golf parity rc=$rc"; tail -1 gpurun_out/r3d/golf_parity.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --no-cpu-baseline --task 3 --envs 8192 --steps 10 --warmup 2 --reps 3 > gpurun_out/r3d/bench_t3_lod.json 2> gpurun_out/r3d/bench_t3_lod.err || exit 1
+cut -c1-150 gpurun_out/r3d/bench_t3_lod.json

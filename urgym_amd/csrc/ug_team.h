@@ -62,7 +62,8 @@ static_assert(UG_FULL_HULL_MAXV + 64 + 8 <= FC_MAX, "a full hull pair's candidat
 /* per-env workspace stride: the LOD geometry ends at WS_FC, the full geometry adds its candidate list and 16-bit
  * certificates (a handle allocates only what its mode uses) */
 #define WS_LOD_DOUBLES WS_FC
-#define WS_FULL_DOUBLES (WS_HC2 + 2 * MAXPAIR)
+#define WS_SV (WS_HC2 + 2 * MAXPAIR) /* the cylinder pass's surviving support points (4 x UG_FULL_HULL_MAXF ints) */
+#define WS_FULL_DOUBLES (WS_SV + 2 * UG_FULL_HULL_MAXF)
 #ifdef UG_DEBUG_DUMP /* development aid: team_pgs dumps A, w and impulses after the workspace proper */
 #define WS_DBG WS_FULL_DOUBLES
 #define WS_DOUBLES (WS_DBG + MAXROWS * MAXROWS + 8 * MAXROWS)
@@ -876,66 +877,75 @@ __device__ __forceinline__ static void team_poly_cyl(int k, bool swapped, gdoubl
     }
     const m3 RBA = mtm(TA.R, TB.R);
     const v3 pBA = mtv(TA.R, vsub(TB.p, TA.p));
-    /* lane per face f: the filter, the support points and their own-plane test; then each surviving point in
-     * (face, point) order gets the plane scan on the whole wave -- rejected as soon as a batch of 64 planes holds one
-     * that clears the threshold (the oracle's early exit rejects exactly those), else the first maximum over all */
+    /* pass 1, lane per face f: the filter and the support points' own-plane test; the surviving (face, point) codes
+     * 4 f + j go to a list in the workspace in (face, point) order.  Pass 2, lane per survivor: the plane scan
+     * (lane-serial, the oracle's loop with its early exit), candidates appended in survivor order */
+    typedef __attribute__((address_space(1))) int gint;
+    gint* sv = (gint*)(gc + (WS_SV - WS_FC));
+    int ns = 0;
     for (int f0 = 0; f0 < nf; f0 += TEAM) {
         const int f = f0 + lane;
-        bool sv[4] = {false, false, false, false};
-        v3 u = V(0, 0, 0);
+        bool ok[4] = {false, false, false, false};
         if (f < nf) {
             v3 nf_;
             double off;
             poly_face(A, hull, f, nf_, off);
             if (vdot(nf_, pBA) - off > 0) {
-                u = mtv(RBA, vneg(nf_));
+                const v3 u = mtv(RBA, vneg(nf_));
                 const int ks = cyl_support_n(u);
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     if (j >= ks) break;
                     const v3 y = vadd(mv(RBA, cyl_support_pt(r, hh, u, j)), pBA);
-                    sv[j] = !(vdot(nf_, y) - off - mA >= thr);
+                    ok[j] = !(vdot(nf_, y) - off - mA >= thr);
                 }
             }
         }
-        const unsigned long long m0 = ballot(sv[0]), m1 = ballot(sv[1]), m2 = ballot(sv[2]), m3 = ballot(sv[3]);
-        for (unsigned long long any = m0 | m1 | m2 | m3; any != 0ull; any &= any - 1ull) {
-            const int L = __builtin_ctzll(any);
-            const v3 uL = V(readlane_d(u.x, L), readlane_d(u.y, L), readlane_d(u.z, L));
+        const int cnt = (int)ok[0] + (int)ok[1] + (int)ok[2] + (int)ok[3];
+        const unsigned long long b0 = ballot(cnt & 1), b1 = ballot(cnt & 2), b2 = ballot(cnt & 4);
+        int pos = ns + lane_prefix(b0) + 2 * lane_prefix(b1) + 4 * lane_prefix(b2);
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const unsigned long long mj = j == 0 ? m0 : j == 1 ? m1 : j == 2 ? m2 : m3;
-                if (!((mj >> L) & 1ull)) continue;
-                const v3 sp = cyl_support_pt(r, hh, uL, j);
-                const v3 y = vadd(mv(RBA, sp), pBA);
-                double smax = -1e300;
-                int fm = 0x7fffffff;
-                bool rej = false;
-                for (int g0 = 0; g0 < nf; g0 += TEAM) {
-                    const int g = g0 + lane;
-                    if (g < nf) {
-                        v3 ng;
-                        double og;
-                        poly_face(A, hull, g, ng, og);
-                        const double sd = ng.x * y.x + ng.y * y.y + ng.z * y.z - og;
-                        if (sd > smax) { smax = sd; fm = g; }
-                        rej = rej || sd - mA >= thr;
-                    }
-                    if (ballot(rej)) break;
-                }
-                if (ballot(rej)) continue;
-                wave_best(smax, fm, true);
+        for (int j = 0; j < 4; j++)
+            if (ok[j]) sv[pos++] = 4 * f + j;
+        ns += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    for (int s0 = 0; s0 < ns; s0 += TEAM) {
+        const int si = s0 + lane;
+        int valid = 0;
+        Cand c;
+        if (si < ns) {
+            const int code = sv[si], f = code >> 2, j = code & 3;
+            v3 nf_;
+            double off;
+            poly_face(A, hull, f, nf_, off);
+            const v3 sp = cyl_support_pt(r, hh, mtv(RBA, vneg(nf_)), j);
+            const v3 y = vadd(mv(RBA, sp), pBA);
+            double smax = -1e300;
+            int fm = -1;
+            for (int g = 0; g < nf; g++) {
+                v3 ng;
+                double og;
+                poly_face(A, hull, g, ng, og);
+                const double sd = ng.x * y.x + ng.y * y.y + ng.z * y.z - og;
+                if (sd > smax) { smax = sd; fm = g; }
+                if (sd - mA >= thr) break;
+            }
+            const double depth = smax - mA;
+            if (depth < thr) {
                 v3 nm;
                 double om;
                 poly_face(A, hull, fm, nm, om);
-                Cand c;
+                valid = 1;
                 c.n = vneg(mv(TA.R, nm));
                 c.pB = xf_apply(TB, sp);
-                c.d = smax - mA;
-                if (lane == 0) fc_put(gc, n, c);
-                n++;
+                c.d = depth;
             }
         }
+        const unsigned long long m = ballot(valid);
+        if (valid) fc_put(gc, n + lane_prefix(m), c);
+        n += __popcll(m);
     }
     fc_reduce(n, k, gc);
     if (swapped) { /* cylinder-box: the oracle's role swap on the kept points */
