@@ -136,9 +136,9 @@ def main(argv=None):
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--task", type=int, default=0)
-    ap.add_argument("--geometry", choices=("lod", "full"), default="lod",
-                    help="robot collision hulls: lod (<= 48 vertices, default) or full (every vertex of PyBullet's mesh hull, "
-                         "URGYM_FLAG_FULL_GEOMETRY)")
+    ap.add_argument("--geometry", choices=("full", "lod"), default="full",
+                    help="collision geometry: full (default: every vertex of PyBullet's mesh hulls, a true cylinder disc) "
+                         "or lod (<= 48-vertex hulls, a 16-gon disc prism: URGYM_FLAG_LOD_GEOMETRY)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL over xGMI); gloo only to rehearse several ranks "
@@ -162,9 +162,9 @@ def main(argv=None):
         world = dist.get_world_size()
     dev = torch.device("cuda", gpu)
 
-    from urgym_amd._native import GEOM_FULL, Sim
+    from urgym_amd._native import GEOM_LOD, Sim
     n = args.envs
-    geom_flags = GEOM_FULL if args.geometry == "full" else 0
+    geom_flags = GEOM_LOD if args.geometry == "lod" else 0
     sim = Sim(args.task, n, device=gpu, seed=20241220, env_offset=rank * n, flags=geom_flags)
     sim.set_autoreset(True, MAX_STEPS[args.task])
     sim.reset()

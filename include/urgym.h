@@ -41,11 +41,14 @@ typedef struct urgym_handle urgym_handle;
 urgym_handle* urgym_create(int task_id, int n_envs, int device_ordinal, int precision, uint32_t seed,
                            int env_offset);
 
-/* urgym_create with creation flags (0 = urgym_create).  URGYM_FLAG_FULL_GEOMETRY: the robot's mesh colliders are
- * PyBullet's convex hulls of all mesh vertices (URDF2Bullet: btConvexHullShape + optimizeConvexHull, up to 865
- * vertices / 1306 faces per link) instead of the default <= 48-vertex collision LOD; same contact algorithm.
- * Slower (more vertices and faces per hull pair); parity: bit-identical to the CPU restatement's same mode. */
+/* urgym_create with creation flags (0 = urgym_create).  The default geometry (0 or URGYM_FLAG_FULL_GEOMETRY) is the
+ * reference's: the robot's mesh colliders are PyBullet's convex hulls of all mesh vertices (URDF2Bullet:
+ * btConvexHullShape + optimizeConvexHull, up to 865 vertices / 1306 faces per link) and the Golf club's disc
+ * (GEOM_CYLINDER, env_golf_v0.py:305) a true cylinder.  URGYM_FLAG_LOD_GEOMETRY selects the collision LOD instead
+ * (<= 48-vertex hulls, a 16-gon disc prism; same contact algorithm): faster, knowingly off the reference's geometry.
+ * Both are bit-identical to the CPU restatement's same mode; both flags together are an error. */
 #define URGYM_FLAG_FULL_GEOMETRY 1 /* == UG_GEOM_FULL (urgym_amd/csrc/ug_layout.h) */
+#define URGYM_FLAG_LOD_GEOMETRY 2  /* == UG_GEOM_LOD */
 urgym_handle* urgym_create_ex(int task_id, int n_envs, int device_ordinal, int precision, uint32_t seed,
                               int env_offset, int flags);
 

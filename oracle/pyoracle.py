@@ -96,7 +96,7 @@ class OracleEnv:
     """One environment of the CPU restatement."""
 
     def __init__(self, task, seed, lib_path=None, flags=0):
-        """flags: 1 = full geometry (UG_GEOM_FULL / URGYM_FLAG_FULL_GEOMETRY)"""
+        """flags: 0 / 1 = full geometry (the default), 2 = the collision LOD (UG_GEOM_LOD)"""
         self.L = lib(lib_path)
         self.task = task
         self.h = self.L.ugo_create_ex(task, seed, flags)

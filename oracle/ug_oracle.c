@@ -325,7 +325,7 @@ static void add_pair(scene* s, int a, int b) {
 static void build_scene(scene* s, int variant, int flags) {
     memset(s, 0, sizeof(*s));
     const int task = UG_BASE_TASK(variant);
-    s->full = (flags & UG_GEOM_FULL) != 0;
+    s->full = UG_GEOM_IS_FULL(flags);
     s->task = task;
     s->variant = variant;
     s->gravity = task == UG_TASK_CUBESGRASP ? -10.0 : -9.8; /* env_cubes_grasp_v0.py:43 vs :59 */
@@ -1191,7 +1191,7 @@ static void nc_hull_sphere(const xf* TA, const collider* A, const xf* TB, const 
  * along the other shape's inward face normals tested against that shape's planes (as a box corner is against a
  * hull), deepest + farthest-spread 4.  The cylinder is its outer surface (radius r, half height hh, the safe margin
  * included); a support direction along the axis (a flat cap against a face) gives the cap's 4 rim points on the
- * shape frame's x / y axes.  Used only with UG_GEOM_FULL; the LOD geometry keeps the 16-gon prism. */
+ * shape frame's x / y axes.  Used with the full geometry (the default); UG_GEOM_LOD keeps the 16-gon prism. */
 /* signed distance from x (cylinder frame) to the solid cylinder; nl: outward unit normal at the nearest surface point
  * pl (inside: the nearer of the side and the cap) */
 static double cyl_point(double r, double hh, v3 x, v3* nl, v3* pl) {
@@ -2572,7 +2572,8 @@ static int gf_step(ugo_env* e, const float* a, double* obs, double* rew, uint8_t
 /* public API                                                                */
 /* ======================================================================== */
 ugo_env* ugo_create(int task, uint32_t seed) { return ugo_create_ex(task, seed, 0); }
-/* flags: UG_GEOM_FULL (urgym_create_ex's URGYM_FLAG_FULL_GEOMETRY) -- the full-geometry mode */
+/* flags: UG_GEOM_LOD selects the collision LOD (urgym_create_ex's URGYM_FLAG_LOD_GEOMETRY); the default (0 or
+ * UG_GEOM_FULL) is the full geometry */
 ugo_env* ugo_create_ex(int task, uint32_t seed, int flags) {
     ugo_env* e = (ugo_env*)calloc(1, sizeof(ugo_env));
     build_scene(&e->sc, task, flags);

@@ -27,7 +27,7 @@ typedef struct ugo_env ugo_env;
 
 /* task: 0 BallBalance, 1 CubesPush, 2 CubesGrasp, 3 Golf, 4 CubesPushDiff, 5 GolfJoints, 6 TwoBallsBalance */
 ugo_env* ugo_create(int task, uint32_t seed);
-/* flags: UG_GEOM_FULL (ug_layout.h) -- robot hulls with every vertex and face of the meshes' convex hulls */
+/* flags: UG_GEOM_LOD (ug_layout.h) -- the collision LOD instead of the default full geometry */
 ugo_env* ugo_create_ex(int task, uint32_t seed, int flags);
 void ugo_destroy(ugo_env* e);
 int ugo_obs_dim(int task);

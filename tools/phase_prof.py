@@ -33,10 +33,10 @@ def main():
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--task", type=int, default=0)
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--geometry", choices=("lod", "full"), default="lod")
+    ap.add_argument("--geometry", choices=("lod", "full"), default="full")
     a = ap.parse_args()
-    from urgym_amd._native import GEOM_FULL, Sim
-    sim = Sim(a.task, a.envs, seed=20241220, flags=GEOM_FULL if a.geometry == "full" else 0)
+    from urgym_amd._native import GEOM_LOD, Sim
+    sim = Sim(a.task, a.envs, seed=20241220, flags=GEOM_LOD if a.geometry == "lod" else 0)
     from urgym_amd.envs import spaces_for
     _, asp = spaces_for(a.task)
     sim.set_autoreset(True, 500)

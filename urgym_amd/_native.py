@@ -23,7 +23,7 @@ SYMBOLS = [
 
 # UG_FLAG_* / UG_STAT_* (urgym_amd/csrc/ug_layout.h)
 FLAG_UNSTABLE, FLAG_NONFINITE, FLAG_DROPPED = 1, 2, 4
-GEOM_FULL = 1  # urgym_create_ex flag URGYM_FLAG_FULL_GEOMETRY
+GEOM_FULL, GEOM_LOD = 1, 2  # urgym_create_ex flags: the full geometry (the default) / the collision LOD
 STAT_NAMES = ["unstable_waits", "split_substeps", "row_capacity_substeps", "manifold_capacity_substeps",
               "nonfinite_terminations", "substeps", "reserved6", "reserved7"]
 CONTACT_FIELDS = 24  # pybullet getContactPoints tuple, flattened
@@ -95,7 +95,7 @@ class Sim:
     """One handle = n_envs environments of one task on one GPU."""
 
     def __init__(self, task, n_envs, device=0, seed=0, env_offset=0, flags=0):
-        """flags: GEOM_FULL = full geometry (robot hulls with every mesh-hull vertex / face)"""
+        """flags: 0 or GEOM_FULL = the full geometry (default), GEOM_LOD = the collision LOD"""
         self.L = lib()
         self.task = task
         self.n = n_envs

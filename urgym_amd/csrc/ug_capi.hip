@@ -66,7 +66,7 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
     const int task = UG_BASE_TASK(variant);
     s->task = task;
     s->variant = variant;
-    s->full = (flags & UG_GEOM_FULL) != 0;
+    s->full = UG_GEOM_IS_FULL(flags);
     s->gravity = task == UG_TASK_CUBESGRASP ? -10.0 : -9.8;
     s->nobj = 0;
     s->ncol = 0;
@@ -545,7 +545,7 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     size_t N = (size_t)n;
     HIPCHK(h, hipMalloc(&h->d_state, sizeof(double) * UG_STATE_DIM * N));
     HIPCHK(h, hipMalloc(&h->d_mt, sizeof(uint32_t) * UG_MT_WORDS * N));
-    HIPCHK(h, hipMalloc(&h->d_ws, sizeof(double) * WS_STRIDE(flags & UG_GEOM_FULL) * N));
+    HIPCHK(h, hipMalloc(&h->d_ws, sizeof(double) * WS_STRIDE(UG_GEOM_IS_FULL(flags)) * N));
     HIPCHK(h, hipMalloc(&h->d_elapsed, sizeof(int) * N));
     HIPCHK(h, hipMalloc(&h->d_act, sizeof(float) * 9 * N));
     HIPCHK(h, hipMalloc(&h->d_obs, sizeof(double) * 17 * N));
@@ -583,8 +583,9 @@ urgym_handle* urgym_create(int task, int n, int dev, int precision, uint32_t see
 }
 
 urgym_handle* urgym_create_ex(int task, int n, int dev, int precision, uint32_t seed, int env_offset, int flags) {
-    if (flags & ~URGYM_FLAG_FULL_GEOMETRY) {
-        fail(nullptr, "urgym_create_ex: unknown flags " + std::to_string(flags));
+    if ((flags & ~(URGYM_FLAG_FULL_GEOMETRY | URGYM_FLAG_LOD_GEOMETRY)) ||
+        (flags & URGYM_FLAG_FULL_GEOMETRY && flags & URGYM_FLAG_LOD_GEOMETRY)) {
+        fail(nullptr, "urgym_create_ex: invalid flags " + std::to_string(flags));
         return nullptr;
     }
     if (task < URGYM_TASK_BALLBALANCE || task > URGYM_TASK_TWOBALLSBALANCE) {
@@ -855,10 +856,10 @@ int urgym_debug_prof(urgym_handle* h, unsigned long long* out16, int reset) {
 
 // Development aid: copy env's per-env workspace (count doubles from its start) to the host.
 int urgym_debug_workspace(urgym_handle* h, int env, double* out, int count) {
-    if (!h || !out || env < 0 || env >= h->n || count < 0 || count > (int)WS_STRIDE(h->flags & UG_GEOM_FULL)) return -1;
+    if (!h || !out || env < 0 || env >= h->n || count < 0 || count > (int)WS_STRIDE(UG_GEOM_IS_FULL(h->flags))) return -1;
     HIPCHK(h, hipSetDevice(h->dev));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    HIPCHK(h, hipMemcpy(out, h->d_ws + (size_t)env * WS_STRIDE(h->flags & UG_GEOM_FULL), sizeof(double) * count, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy(out, h->d_ws + (size_t)env * WS_STRIDE(UG_GEOM_IS_FULL(h->flags)), sizeof(double) * count, hipMemcpyDeviceToHost));
     return 0;
 }
 int urgym_debug_ws_doubles(void) { return (int)WS_STRIDE(0); } /* the LOD stride (the full geometry adds 7,488 doubles) */

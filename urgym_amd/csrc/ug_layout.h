@@ -42,9 +42,13 @@
 #define UG_FLAG_NONFINITE 2  /* the state became non-finite: the env was terminated (and reset by autoreset) */
 #define UG_FLAG_DROPPED 4    /* contacts were dropped at a capacity limit */
 
-/* creation flags (urgym_create_ex / ugo_create_ex) */
-#define UG_GEOM_FULL 1       /* full geometry: robot hulls with every vertex / face of the mesh's convex hull (PyBullet's
-                              * optimizeConvexHull of all mesh vertices) instead of the <= 48-vertex collision LOD */
+/* creation flags (urgym_create_ex / ugo_create_ex).  The default geometry is the full one: the robot's mesh colliders
+ * are PyBullet's convex hulls of all mesh vertices (optimizeConvexHull) and the Golf club's disc a true cylinder.
+ * UG_GEOM_LOD selects the collision LOD instead (<= 48-vertex hulls, a 16-gon disc prism): faster, knowingly off the
+ * reference's geometry. */
+#define UG_GEOM_FULL 1       /* the full geometry, explicitly (the default) */
+#define UG_GEOM_LOD 2        /* the collision LOD */
+#define UG_GEOM_IS_FULL(flags) (((flags) & UG_GEOM_LOD) == 0)
 
 #define UG_MT_WORDS 625      /* MT19937 state (624) + index, uint32, contiguous per env */
 
