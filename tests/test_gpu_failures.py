@@ -4,8 +4,8 @@ env_ball_balance_v0.py:102-103), and trigger the split-impulse pass (penetration
 one env-step on the GPU and in the CPU restatement from the same crafted state: every output, the flags, the event
 counters and the final state are bit-identical, and the counter the case targets is > 0.
 
-The states were found with the restatement (arm folded into the table; a CubesGrasp joint move across the whole
-pan range against the joint's current motion; a cube 3 cm inside the table)."""
+The states were found with the restatement in the default (full) geometry (arm folded into the table; a CubesGrasp
+joint move across the whole pan range against the joint's current motion; a cube 3 cm inside the table)."""
 import numpy as np
 import pytest
 
@@ -67,7 +67,10 @@ def _fold(q1, q2):
     return edit
 
 
-POSES = [(-0.5, 1.5), (0.0, 1.5), (0.5, 0.0), (1.0, 1.5), (0.5, 2.5)]
+# (shoulder lift, elbow) folds that stay finite with the default (full) geometry and overflow both capacities;
+# the last of each task also runs its wait_until_stable into the 480 cap
+POSES = {0: [(0.5, 0.0), (0.5, 2.5), (0.8, 2.5), (1.0, 2.0), (0.3, 1.5)],
+         1: [(-0.5, 1.5), (-0.3, 1.5), (0.3, 0.0), (0.0, 2.5), (0.3, 1.5)]}
 
 
 @pytest.mark.parametrize("task", [0, 1])
@@ -76,7 +79,7 @@ def test_manifold_and_row_capacity_overflow(mods, task):
     counters and the DROPPED flag fire (and, for the deepest poses, the 480 cap and the split pass too), equal to
     the restatement's."""
     Sim, OracleEnv = mods
-    out, fl, d = crafted_step(Sim, OracleEnv, task, [_fold(*p) for p in POSES], np.zeros(3))
+    out, fl, d = crafted_step(Sim, OracleEnv, task, [_fold(*p) for p in POSES[task]], np.zeros(3))
     assert (d[:, MANCAP] > 0).sum() >= 3 and (d[:, ROWCAP] > 0).sum() >= 4, d.tolist()
     assert np.all((fl & FLAG_DROPPED) != 0), fl.tolist()
     assert (d[:, SPLIT] > 0).all() and (d[:, UNSTABLE] > 0).any(), d.tolist()
