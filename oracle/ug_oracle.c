@@ -34,7 +34,9 @@
 #ifndef MAXCAND
 #define MAXCAND 1024 /* candidate storage: a full hull's vertices + the box corners (UG_FULL_HULL_MAXV + 8) */
 #endif
+#ifndef LOD_MAXCAND
 #define LOD_MAXCAND 64 /* candidates a hull pair keeps with the LOD hulls (the kernels' LDS list) */
+#endif
 #define PT_DOUBLES UG_PT_DOUBLES
 #define MAN_DOUBLES UG_MAN_DOUBLES
 #define STATE_DIM UG_STATE_DIM

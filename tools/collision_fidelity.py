@@ -1,29 +1,27 @@
 #!/usr/bin/env python3
-"""Collision-LOD / contact-generation divergence table ("quantify the collision substitutes").
+"""Geometry / contact-generation divergence table ("quantify the collision substitutes"; r2: the
+reference-faithful geometry on the product path).
 
-The product path (kernels and the parity oracle) uses collision substitutes: robot hulls decimated to <= 48
-vertices, hull-box / hull-hull contacts from vertex-in-hull tests with the face planes (no edge-edge contacts,
-deepest + farthest-spread 4 points), hull-sphere from the deepest face plane, and the club's disc cylinder as a
-16-sided prism.  This tool builds two more variants of the CPU restatement (test /
-measurement infrastructure; never shipped, never measured as the product):
+The product path (kernels and the parity oracle) defaults to the reference's geometry: robot hulls with every
+vertex and face of PyBullet's mesh hulls and the club's disc as a true cylinder, with contacts from vertex-in-hull
+tests against the face planes (no edge-edge contacts, deepest + farthest-spread 4 points), hull-sphere from the
+deepest face plane.  This tool runs the same seeded random-action rollouts from the same initial states through
 
-  full   full hulls (every hull vertex and face of the meshes) and a 128-sided disc prism, product algorithm
-  bullet full hulls + 128-gon + Bullet's polyhedral path restated (oracle/ug_fidelity.h: separating axis over
-         face normals and edge-edge cross products, incident-face clipping, edge-edge contact, exact hull-sphere)
-
-and runs the same seeded random-action rollouts from the same initial states through
-
-  product   the restatement the kernels match bit for bit
+  product   the default restatement (flags 0), the one the kernels match bit for bit
   floor     product with Bullet's own PGS arithmetic form (oracle pgs_bullet, ~1e-11 per substep): the growth of a
             rounding-level difference, i.e. the chaos floor of each task
-  full, bullet
+  lod       the shipped collision LOD (URGYM_FLAG_LOD_GEOMETRY: <= 48-vertex hulls, 16-gon disc prism), also
+            matched bit for bit by the kernels in that mode
+  bullet    full hulls + a 128-gon disc prism + Bullet's polyhedral path restated (oracle/ug_fidelity.h: separating
+            axis over face normals and edge-edge cross products, incident-face clipping, edge-edge contact, exact
+            hull-sphere); a separate build (oracle/_fid/, test / measurement infrastructure, never shipped)
 
 reporting, after 1, 10 and 100 env-steps, the divergence of each variant from `product`: max |dq| over the
 12 robot dofs (rad), max object position difference (m), and the fraction of envs whose episode ended at a
 different step.  Output: profiles/collision_fidelity.json and a markdown table on stdout.
 
 usage: python tools/collision_fidelity.py [--envs 6] [--steps 100] [--tasks 0,1,2,3,4,5,6] [--jobs 8]
-(CPU only, this container: it needs /root/reference for the full meshes)
+(CPU only, this container: the bullet build needs /root/reference for the full meshes)
 """
 import argparse
 import json
@@ -38,7 +36,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 FID = os.path.join(ROOT, "oracle", "_fid")
 HDR = os.path.join(FID, "model_data.h")
-LIBS = {"full": os.path.join(FID, "libugoracle_full.so"), "bullet": os.path.join(FID, "libugoracle_fid.so")}
+LIBS = {"bullet": os.path.join(FID, "libugoracle_fid.so")}
+# creation flags per variant: the bullet build's LOD slot holds the full hulls + 128-gon (URGYM_HULL_MAXV above)
+FLAGS = {"lod": 2, "bullet": 2}
 CFLAGS = ["-O2", "-std=gnu99", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-mfma", "-Wall",
           "-Wno-unused-function", "-Wno-unknown-pragmas", "-shared"]
 CHECK = (1, 10, 100)
@@ -52,8 +52,7 @@ def build():
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "build_model.py")], env=env, check=True,
                    stdout=subprocess.DEVNULL)
     src = os.path.join(ROOT, "oracle", "ug_oracle.c")
-    common = CFLAGS + ["-DMAXCAND=4096", '-DUG_MODEL_DATA="_fid/model_data.h"']
-    subprocess.run(["gcc"] + common + ["-o", LIBS["full"], src, "-lm"], check=True, cwd=os.path.join(ROOT, "oracle"))
+    common = CFLAGS + ["-DMAXCAND=4096", "-DLOD_MAXCAND=4096", '-DUG_MODEL_DATA="_fid/model_data.h"']
     subprocess.run(["gcc"] + common + ["-DUG_FIDELITY", "-o", LIBS["bullet"], src, "-lm"], check=True,
                    cwd=os.path.join(ROOT, "oracle"))
 
@@ -71,7 +70,7 @@ def rollout(job):
     task, env_i, variant, steps, s0 = job
     from oracle.pyoracle import OracleEnv
     from urgym_amd import layout as LY
-    e = OracleEnv(task, 1000 + env_i, lib_path=LIBS.get(variant))
+    e = OracleEnv(task, 1000 + env_i, lib_path=LIBS.get(variant), flags=FLAGS.get(variant, 0))
     if variant == "floor":
         e.set_pgs_bullet(True)
     e.set_state(s0)
@@ -107,7 +106,7 @@ def main():
         build()
     from urgym_amd import layout as LY
     tasks = [int(t) for t in a.tasks.split(",")]
-    variants = ["product", "floor", "full", "bullet"]
+    variants = ["product", "floor", "lod", "bullet"]
     jobs = []
     for t in tasks:
         for i in range(a.envs):
@@ -141,9 +140,9 @@ def main():
                                "median_dpos_m": float(np.median(dp)) if dp else None,
                                "episode_end_differs": ended_diff}
             table[NAMES[t]][v] = row
-    out = {"what": __doc__.split("\n\n")[0],
+    out = {"what": __doc__.split("\n\n")[0], "product": "full hulls + true cylinder disc (the default geometry)",
            "variants": {"floor": "product restatement with Bullet's PGS arithmetic form (rounding-level seed)",
-                        "full": "full hulls + 128-gon disc prism, product contact algorithm",
+                        "lod": "the collision LOD (<= 48-vertex hulls, 16-gon disc prism), product contact algorithm",
                         "bullet": "full hulls + 128-gon + Bullet polyhedral clipping / edge-edge / exact hull-sphere "
                                   "(oracle/ug_fidelity.h)"},
            "envs_per_task": a.envs, "steps": a.steps, "checkpoints": list(CHECK),
