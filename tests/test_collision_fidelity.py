@@ -76,8 +76,8 @@ def test_variants_step_finite(fid, task):
     e0.reset()
     s0 = e0.get_state()
     acts = fid.actions(task, 2, 3)
-    for v in ("full", "bullet"):
-        e = OracleEnv(task, 1000, lib_path=fid.LIBS[v])
+    for v in ("lod", "bullet"):
+        e = OracleEnv(task, 1000, lib_path=fid.LIBS.get(v), flags=fid.FLAGS.get(v, 0))
         e.set_state(s0)
         for a in acts:
             e.step(a)
