@@ -88,25 +88,28 @@ def cpu_baseline(task, seconds=10.0, seconds_1core=5.0, flags=0):
                          "sample": f"1 env, {s1} env-steps ({sub1} substeps) in {dt1:.1f}s, 1 thread"}}
 
 
-def pmc_traffic(task, n):
+def pmc_traffic(task, n, geometry):
     """HBM bytes per k_step launch from the committed PMC summary of this workload (profiles/traffic_k_step.json,
-    tools/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), keyed on (task, envs)."""
+    tools/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), keyed on (task, envs,
+    geometry); a record without a geometry key is a round-2 LOD measurement."""
     path = os.path.join(ROOT, "profiles", "traffic_k_step.json")
     try:
         t = json.load(open(path))
     except (OSError, ValueError):
         return None, None
     for rec in (t if isinstance(t, list) else [t]):
-        if (rec.get("task"), rec.get("envs")) == (task, n):
+        if (rec.get("task"), rec.get("envs"), rec.get("geometry", "lod")) == (task, n, geometry):
             return float(rec["hbm_bytes_per_launch"]), \
                 f"profiles/traffic_k_step.json ({rec.get('source', 'rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE')})"
     return None, None
 
 
-def work_model(task):
-    """FP64 FLOPs per substep / per env-step outside substeps (profiles/work_model.json, tools/opcount.py)"""
+def work_model(task, geometry):
+    """FP64 FLOPs per substep / per env-step outside substeps (profiles/work_model.json, tools/opcount.py), counted
+    on the restatement in the same geometry mode"""
     try:
-        m = json.load(open(os.path.join(ROOT, "profiles", "work_model.json")))["tasks"][str(task)]
+        key = "tasks_full" if geometry == "full" else "tasks"
+        m = json.load(open(os.path.join(ROOT, "profiles", "work_model.json")))[key][str(task)]
         return float(m["F_sub"]), float(m["F_nonsub_per_env_step"])
     except (OSError, ValueError, KeyError):
         return None, None
@@ -248,7 +251,7 @@ def main(argv=None):
     value = env_steps / dt
     # roofline of the dominant kernel (k_step): FP64 VALU, algorithmic FLOPs per launch from the op-counted
     # restatement (profiles/work_model.json) with this run's substep count, over the HIP-event launch time
-    F_sub, F_non = work_model(args.task)
+    F_sub, F_non = work_model(args.task, args.geometry)
     flops_per_launch = None
     if F_sub is not None:
         flops_per_launch = (F_sub * substeps + F_non * env_steps) / (K * world)
@@ -256,7 +259,7 @@ def main(argv=None):
     S = state_bytes()
     bytes_per_env = 2 * S + 4 * A + 8 * O * 2 + 8 + 3 + 4
     achieved_gbs = bytes_per_env * n / (avg_kernel_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args.task, n)
+    traffic, traffic_src = pmc_traffic(args.task, n, args.geometry)
     if flops_per_launch is not None:
         tf = flops_per_launch / (avg_kernel_ms * 1e-3) / 1e12
         roof = {"bound": "fp64-valu", "achieved": tf, "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",

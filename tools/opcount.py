@@ -148,12 +148,12 @@ def build(tmp):
     return so
 
 
-def count_task(L, pyoracle, spaces_for, task, n_envs, steps):
+def count_task(L, pyoracle, spaces_for, task, n_envs, steps, flags=0):
     """per-phase FP64 op counts of a canonical trajectory of one task"""
     tab = np.zeros(64, np.int64)
     L.ugo_opcount_reset()
     max_steps = {0: 500, 1: 50, 2: 20, 3: 100, 4: 50, 5: 100, 6: 500}[task]
-    envs = [pyoracle.OracleEnv(task, 20241220 + i) for i in range(n_envs)]
+    envs = [pyoracle.OracleEnv(task, 20241220 + i, flags=flags) for i in range(n_envs)]
     for e in envs:
         e.reset()
     L.ugo_opcount_read(tab.ctypes.data_as(ctypes.c_void_p))
@@ -208,17 +208,24 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tasks", default="0,1,2,3,4,5,6")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "work_model.json"))
+    ap.add_argument("--geometry", choices=("full", "lod"), default="full",
+                    help="collision geometry of the counted trajectories: the counts land in tasks_full / tasks (lod)")
     args = ap.parse_args()
+    key = "tasks_full" if args.geometry == "full" else "tasks"
+    flags = 0 if args.geometry == "full" else 2  # UG_GEOM_LOD
     sys.path.insert(0, ROOT)
     from oracle import pyoracle
     from urgym_amd.envs import spaces_for
     model = {"what": "FP64 FLOPs of the CPU restatement (oracle/ug_oracle.c) on canonical seeded trajectories "
                      "(random actions in the action space, seeds 20241220 + env, autoreset at max_episode_steps); "
                      "FLOPs = add + sub + mul + div + sqrt + 2*fma, counted by tools/opcount.py (LLVM-IR op counters). "
-                     "bench.py: achieved = F_sub * substeps + F_nonsub_per_env_step * env_steps per launch.",
-             "tasks": {}}
+                     "bench.py: achieved = F_sub * substeps + F_nonsub_per_env_step * env_steps per launch. "
+                     "tasks: the collision LOD (URGYM_FLAG_LOD_GEOMETRY); tasks_full: the default full geometry.",
+             "tasks": {}, "tasks_full": {}}
     if os.path.exists(args.out):
-        model["tasks"] = json.load(open(args.out)).get("tasks", {})
+        old = json.load(open(args.out))
+        model["tasks"] = old.get("tasks", {})
+        model["tasks_full"] = old.get("tasks_full", {})
     with tempfile.TemporaryDirectory() as tmp:
         so = build(tmp)
         pyoracle.LIB_PATH = so
@@ -227,8 +234,8 @@ def main():
         L.ugo_opcount_read.argtypes = [ctypes.c_void_p]
         for t in [int(x) for x in args.tasks.split(",")]:
             n, k = CANON[t]
-            m = count_task(L, pyoracle, spaces_for, t, n, k)
-            model["tasks"][str(t)] = m
+            m = count_task(L, pyoracle, spaces_for, t, n, k, flags)
+            model[key][str(t)] = m
             print(t, json.dumps({k2: m[k2] for k2 in ("env_steps", "substeps", "resets", "mean_substeps_per_env_step",
                                                       "F_sub", "F_nonsub_per_env_step", "F_IK_per_env_step")}), flush=True)
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
