@@ -49,6 +49,9 @@ def lib(path=None):
         L.ugo_g_cg_opening.argtypes = [D]
         L.ugo_g_cg_opening.restype = D
         L.ugo_g_cg_reward.argtypes = [P, D, D, I, D, P]
+        L.ugo_g_box_reward.argtypes = [P, D, I, P]
+        L.ugo_g_box_press.argtypes = [D, I, I, I]
+        L.ugo_g_box_target.argtypes = [P, P, P]
         L.ugo_g_union_center.argtypes = [P, P]
         L.ugo_g_gf_ball_xy.argtypes = [D, D, P]
         L.ugo_g_gf_reward.argtypes = [P, P, P, I, I, I, I, P, P]
@@ -57,6 +60,7 @@ def lib(path=None):
         L.ugo_flags.argtypes = [P]
         L.ugo_get_stats.argtypes = [P, P]
         L.ugo_set_reward_type.argtypes = [P, I]
+        L.ugo_set_button_mode.argtypes = [P, I]
         L.ugo_get_rng.argtypes = [P, P]
         L.ugo_set_rng.argtypes = [P, P]
         L.ugo_contact_points.argtypes = [P, I, I, I, I, P, I]
@@ -100,6 +104,8 @@ class OracleEnv:
         self.L = lib(lib_path)
         self.task = task
         self.h = self.L.ugo_create_ex(task, seed, flags)
+        if not self.h:
+            raise ValueError(f"ugo_create_ex refused task {task} with flags {flags}")
         self.obs_dim = self.L.ugo_obs_dim(task)
         self.act_dim = self.L.ugo_act_dim(task)
         self.state_dim = self.L.ugo_state_dim()
@@ -156,6 +162,10 @@ class OracleEnv:
 
     def set_reward_type(self, reward_type):
         self.L.ugo_set_reward_type(self.h, int(reward_type == "sparse"))
+
+    def set_button_mode(self, mode):
+        """Box-v0 button_touch_mode: 'any', 'robot' or 'fingers' (env_box_v0.py:20)"""
+        self.L.ugo_set_button_mode(self.h, {"any": 0, "robot": 1, "fingers": 2}[mode])
 
     def set_pgs_bullet(self, on):
         """solve with Bullet's velocity-space PGS form (tests only)"""

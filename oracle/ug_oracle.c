@@ -22,6 +22,7 @@
 #include "../urgym_amd/csrc/scene_data.h"
 #include "../urgym_amd/csrc/ug_detmath.h"
 #include "../urgym_amd/csrc/ug_glue.h"
+#include "../urgym_amd/csrc/ug_joint.h"
 #include "../urgym_amd/csrc/ug_layout.h"
 
 #define NB UG_NB
@@ -30,7 +31,7 @@
 #define MAXMAN UG_MAXMAN
 #define MAXROWS 128
 #define MAXCOL 28
-#define MAXPAIR 160
+#define MAXPAIR 192
 #ifndef MAXCAND
 #define MAXCAND 1024 /* candidate storage: a full hull's vertices + the box corners (UG_FULL_HULL_MAXV + 8) */
 #endif
@@ -260,6 +261,8 @@ typedef struct {
     collider col[MAXCOL];
     int ocol[MAXOBJ]; /* first collider of each object */
     int oncol[MAXOBJ]; /* colliders of each object (consecutive) */
+    UgJoint ojoint[MAXOBJ]; /* one-dof links on a fixed base (Box: door, button; ug_joint.h); kind UGJ_FREE otherwise */
+    int njoint, jorder[MAXOBJ]; /* the jointed objects in the multibody's joint order (Box: button = joint 0, door = 1) */
     int npair;
     pairdef pair[MAXPAIR];
 } scene;
@@ -279,6 +282,9 @@ struct ugo_env {
     int nman;
     manifold man[MAXMAN];
     int goal_approached, goal_grasped;
+    int goal_closed;       /* Box: box_closed (env_box_v0.py:90); goal_approached / goal_grasped = box_opened / button_pressed */
+    int button_mode;       /* Box: button_touch_mode (UG_BX_TOUCH_*, env_box_v0.py:20) */
+    double jM[MAXOBJ];     /* effective inertia of the jointed objects in the current substep (not state) */
     int overflow;
     mt19937 rng;
     int sparse;            /* reward_type != 'dense' (ctor kwarg of every env, env_cubes_push_v0.py:42) */
@@ -360,7 +366,7 @@ static void build_scene(scene* s, int variant, int flags) {
         c->full = s->full;
     }
     int nrobot = s->ncol;
-    int statics[4], nstat = 0;
+    int statics[8], nstat = 0;
     if (task == UG_TASK_BALLBALANCE) {
         /* paddle (env_ball_balance_v0.py:175-184), ball (:186-205); TwoBallsBalance: two balls of radius 0.003
          * (env_two_balls_balance_v0.py:187, 212-235) */
@@ -490,9 +496,93 @@ static void build_scene(scene* s, int variant, int flags) {
         c->owner = -100; c->ent = 12;
         statics[nstat++] = s->ncol++;
     }
+    if (task == UG_TASK_BOX) {
+        /* skew-box-button.urdf (env_box_v0.py:80-85), fixed base at the world origin = (0, -UG_BX_ROBOT_Y, 0) here:
+         * object 0 = the door link (revolute, the handles merged in: a box and three cylinders), object 1 = the
+         * button (prismatic cylinder), the merged base's four walls static (entity 13), plane.urdf at z = 0 (11).
+         * Each link is one collision object whose compound shape sets the breaking threshold (its angular motion
+         * disc); URDF primitives keep their URDF extents as the outer surface, default lateral friction (the
+         * <contact_coefficients> tag of h3 is not read by PyBullet's URDF parser [ext]). */
+        const double by = -UG_BX_ROBOT_Y;
+        s->nobj = 2;
+        ugj_box_links(&s->ojoint[0], &s->ojoint[1]);
+        s->njoint = 2;
+        s->jorder[0] = 1; /* joint 0: the button (env_box_v0.py:173-175, :193) */
+        s->jorder[1] = 0; /* joint 1: the door (:144, :155, :174-176) */
+        /* door compound AABB in its inertial frame (COM origin) -> disc */
+        const double* B = UG_BX_DOOR_BOX;
+        const UgJoint* D = &s->ojoint[0];
+        double lo[3] = {B[0] - B[3], B[1] - B[4], B[2] - B[5]}, hi[3] = {B[0] + B[3], B[1] + B[4], B[2] + B[5]};
+        for (int i = 0; i < 3; i++) {
+            const double* H = &UG_BX_HANDLE[4 * i];
+            double e3[3] = {H[3], i == 2 ? UG_BX_HANDLE_HH[i] : H[3], i == 2 ? H[3] : UG_BX_HANDLE_HH[i]};
+            for (int k = 0; k < 3; k++) {
+                double l = H[k] - e3[k], u = H[k] + e3[k];
+                lo[k] = l < lo[k] ? l : lo[k];
+                hi[k] = u > hi[k] ? u : hi[k];
+            }
+        }
+        for (int k = 0; k < 3; k++) { lo[k] = lo[k] - D->com[k]; hi[k] = hi[k] - D->com[k]; }
+        double ddisc = ugj_disc(lo, hi);
+        collider* c = &s->col[s->ncol];
+        box_collider(c, B[3], B[4], B[5], UG_URDF_MARGIN, UG_DEFAULT_FRICTION);
+        c->P = V(B[0], B[1], B[2]); c->aP = c->P;
+        c->disc = ddisc;
+        c->owner = -2; c->ent = 1;
+        s->ocol[0] = s->ncol++;
+        for (int i = 0; i < 3; i++) {
+            const double* H = &UG_BX_HANDLE[4 * i];
+            c = &s->col[s->ncol++];
+            box_collider(c, H[3], H[3], UG_BX_HANDLE_HH[i], 0.0, UG_DEFAULT_FRICTION);
+            c->kind = UG_SHAPE_CYL;
+            c->P = V(H[0], H[1], H[2]); c->aP = c->P;
+            if (i == 2) { q4 qh; ugj_box_h3_quat(&qh.x); c->R = qmat(qh); c->aR = c->R; }
+            c->disc = ddisc;
+            c->owner = -2; c->ent = 1;
+        }
+        s->oncol[0] = 4;
+        c = &s->col[s->ncol];
+        box_collider(c, UG_BX_BUTTON_R, UG_BX_BUTTON_R, UG_BX_BUTTON_HH, 0.0, UG_DEFAULT_FRICTION);
+        c->kind = UG_SHAPE_CYL;
+        {
+            double blo[3] = {-UG_BX_BUTTON_R, -UG_BX_BUTTON_R, -UG_BX_BUTTON_HH}, bhi[3] = {UG_BX_BUTTON_R, UG_BX_BUTTON_R, UG_BX_BUTTON_HH};
+            c->disc = ugj_disc(blo, bhi);
+        }
+        c->owner = -3; c->ent = 2;
+        s->ocol[1] = s->ncol++;
+        s->oncol[1] = 1;
+        /* walls: the fixed base's compound (box1..box4) */
+        double wlo[3] = {1e30, 1e30, 1e30}, whi[3] = {-1e30, -1e30, -1e30};
+        for (int w = 0; w < 4; w++)
+            for (int k = 0; k < 3; k++) {
+                double l = UG_BX_WALL_POS[3 * w + k] - UG_BX_WALL_HALF[3 * w + k], u = UG_BX_WALL_POS[3 * w + k] + UG_BX_WALL_HALF[3 * w + k];
+                wlo[k] = l < wlo[k] ? l : wlo[k];
+                whi[k] = u > whi[k] ? u : whi[k];
+            }
+        double wdisc = ugj_disc(wlo, whi);
+        for (int w = 0; w < 4; w++) {
+            c = &s->col[s->ncol];
+            box_collider(c, UG_BX_WALL_HALF[3 * w], UG_BX_WALL_HALF[3 * w + 1], UG_BX_WALL_HALF[3 * w + 2], UG_URDF_MARGIN,
+                         UG_DEFAULT_FRICTION);
+            c->P = V(UG_BX_WALL_POS[3 * w], UG_BX_WALL_POS[3 * w + 1] + by, UG_BX_WALL_POS[3 * w + 2]); c->aP = c->P;
+            c->disc = wdisc;
+            c->owner = -100; c->ent = 13;
+            statics[nstat++] = s->ncol++;
+        }
+        c = &s->col[s->ncol];
+        box_collider(c, UG_PLANE_HALF_XY, UG_PLANE_HALF_XY, UG_PLANE_HALF_Z, UG_URDF_MARGIN, UG_PLANE_FRICTION);
+        c->P = V(0.0, by, -UG_PLANE_HALF_Z); c->aP = c->P;
+        c->disc = ug_sqrt(15.0 * 15.0 * 2.0 + 25.0) + 5.0;
+        c->owner = -100; c->ent = 11;
+        statics[nstat++] = s->ncol++;
+    }
     for (int o = 0; o < s->nobj; o++)
         if (s->oncol[o] == 0) s->oncol[o] = 1;
-    /* pairs: robot x objects, robot x statics, object x object, object x static (objects: each collider) */
+    /* pairs: robot x objects, robot x statics, object x object, object x static (objects: each collider).  Box:
+     * the door's box against the button (URDF_USE_SELF_COLLISION: siblings collide, a link and its parent -- the
+     * walls -- do not); the handle cylinders never reach the button (they sit on the door's top face, which
+     * rotates away from it over the joint range [0, 2]) and carry no pair; of the statics only the plane can meet
+     * the button (fully pressed its bottom reaches z = -0.005), the door cannot reach the plane. */
     for (int o = 0; o < s->nobj; o++)
         for (int c = s->ocol[o]; c < s->ocol[o] + s->oncol[o]; c++)
             for (int l = 0; l < nrobot; l++) add_pair(s, l, c);
@@ -503,13 +593,17 @@ static void build_scene(scene* s, int variant, int flags) {
             for (int ca = s->ocol[o]; ca < s->ocol[o] + s->oncol[o]; ca++)
                 for (int cb = s->ocol[p]; cb < s->ocol[p] + s->oncol[p]; cb++) {
                     int a = ca, b = cb;
+                    if (task == UG_TASK_BOX && s->col[a].kind == UG_SHAPE_CYL) continue;
                     /* canonical order for the narrowphase: sphere first */
                     if (s->col[b].kind == UG_SHAPE_SPHERE && s->col[a].kind != UG_SHAPE_SPHERE) { int t = a; a = b; b = t; }
                     add_pair(s, a, b);
                 }
     for (int o = 0; o < s->nobj; o++)
         for (int c = s->ocol[o]; c < s->ocol[o] + s->oncol[o]; c++)
-            for (int t = 0; t < nstat; t++) add_pair(s, c, statics[t]);
+            for (int t = 0; t < nstat; t++) {
+                if (task == UG_TASK_BOX && !(o == 1 && s->col[statics[t]].ent == 11)) continue;
+                add_pair(s, c, statics[t]);
+            }
 }
 
 /* ======================================================================== */
@@ -1524,6 +1618,14 @@ static void point_jac(const ugo_env* e, const kin* k, int ent, int body, v3 p, v
         ldlt_solve(LDL, NB, MiJ);
     } else {
         int o = ent - 1;
+        const UgJoint* Jt = &e->sc.ojoint[o];
+        if (Jt->kind != UGJ_FREE) { /* one-dof link (ug_joint.h): its slot 0 */
+            double pp[3] = {p.x, p.y, p.z}, dd[3] = {d.x, d.y, d.z};
+            double j = ugj_point_jac(Jt, pp, dd);
+            J[0] = j; J[1] = 0.0; J[2] = 0.0; J[3] = 0.0; J[4] = 0.0; J[5] = 0.0;
+            MiJ[0] = j / e->jM[o]; MiJ[1] = 0.0; MiJ[2] = 0.0; MiJ[3] = 0.0; MiJ[4] = 0.0; MiJ[5] = 0.0;
+            return;
+        }
         v3 r = vsub(p, e->opos[o]);
         v3 rn = vcross(r, d);
         J[0] = d.x; J[1] = d.y; J[2] = d.z; J[3] = rn.x; J[4] = rn.y; J[5] = rn.z;
@@ -1546,6 +1648,14 @@ static void ang_jac(const ugo_env* e, const kin* k, int ent, int body, v3 u, dou
         ldlt_solve(LDL, NB, MiJ);
     } else {
         int o = ent - 1;
+        const UgJoint* Jt = &e->sc.ojoint[o];
+        if (Jt->kind != UGJ_FREE) {
+            double uu[3] = {u.x, u.y, u.z};
+            double j = ugj_ang_jac(Jt, uu);
+            J[0] = j; J[1] = 0.0; J[2] = 0.0; J[3] = 0.0; J[4] = 0.0; J[5] = 0.0;
+            MiJ[0] = j / e->jM[o]; MiJ[1] = 0.0; MiJ[2] = 0.0; MiJ[3] = 0.0; MiJ[4] = 0.0; MiJ[5] = 0.0;
+            return;
+        }
         J[0] = 0.0; J[1] = 0.0; J[2] = 0.0; J[3] = u.x; J[4] = u.y; J[5] = u.z;
         m3 R = qmat(e->oquat[o]);
         v3 ir = mtv(&R, u);
@@ -1588,6 +1698,15 @@ static double contact_row(const ugo_env* e, const kin* k, const double* LDL, con
     double den = dA + dB;
     r->invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
     return relv;
+}
+/* single-dof row of a jointed object's slot (its limits and motor) */
+static double jdof_row(const ugo_env* e, const double* v0, row* r, int o, double sgn) {
+    int off = NB + 6 * o;
+    r->J[off] = sgn;
+    r->MiJ[off] = sgn / e->jM[o];
+    double den = sgn * r->MiJ[off];
+    r->invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
+    return sgn * v0[off];
 }
 /* single-dof row (limit / motor): J = sgn * e_d */
 static double dof_row(const double* LDL, const double* v0, row* r, int d, double sgn) {
@@ -1676,8 +1795,49 @@ static void build_rows(ugo_env* e, const kin* k, const double* LDL, const double
         r->kind = 0;
         rs->idx_nc[rs->nnc++] = rs->n++;
     }
-    /* contacts, manifold order: normal row + two friction rows per point */
+    /* the box's joint limits (btMultiBodyJointLimitConstraint, created at its load after the robot's constraints,
+     * joint order) and the button's position motor (reset_box, env_box_v0.py:175: force 1, target 0, default
+     * gains, no maxVelocity -> no clamp [ext]; the door's motor has force 0 (:176) and carries no row) */
     const scene* s = &e->sc;
+    for (int jj = 0; jj < s->njoint; jj++) {
+        int o = s->jorder[jj];
+        if (!e->oactive[o]) continue;
+        const UgJoint* Jt = &s->ojoint[o];
+        double qj = e->ow[o].x;
+        for (int side = 0; side < 2; side++) {
+            double pen = side == 0 ? qj - Jt->lower : Jt->upper - qj;
+            if (pen > 0) continue;
+            if (rs->n >= MAXROWS) { e->overflow++; continue; }
+            row* r = &rs->r[rs->n];
+            row_clear(r);
+            double relv = jdof_row(e, v0, r, o, side == 0 ? 1.0 : -1.0);
+            double erp = (pen > UG_SPLIT_PEN_THR) ? UG_ERP : UG_ERP2;
+            double perr = -pen * erp / dt, verr = -relv;
+            double pimp = perr * r->invD, vimp = verr * r->invD;
+            r->rhs = (pen > UG_SPLIT_PEN_THR) ? pimp + vimp : vimp;
+            r->lo = 0.0; r->hi = UG_LIMIT_MAXIMP;
+            r->kind = 0;
+            rs->idx_nc[rs->nnc++] = rs->n++;
+        }
+    }
+    if (s->task == UG_TASK_BOX && e->oactive[1]) {
+        if (rs->n >= MAXROWS) e->overflow++;
+        else {
+            row* r = &rs->r[rs->n];
+            row_clear(r);
+            double relv = jdof_row(e, v0, r, 1, 1.0);
+            double qd = v0[NB + 6];
+            double pst = 1.0 * (0.0 - e->ow[1].x) / dt;
+            double verr = 0.0 - qd;
+            double des = UG_MOTOR_KP * pst + qd + UG_MOTOR_KD * verr;
+            double maxImp = UG_BX_BUTTON_FORCE * dt;
+            r->rhs = 0.0 * r->invD + (des - relv) * r->invD;
+            r->lo = -maxImp; r->hi = maxImp;
+            r->kind = 0;
+            rs->idx_nc[rs->nnc++] = rs->n++;
+        }
+    }
+    /* contacts, manifold order: normal row + two friction rows per point */
     for (int m = 0; m < e->nman; m++) {
         const manifold* M = &e->man[m];
         const pairdef* P = &s->pair[M->pair];
@@ -1986,6 +2146,16 @@ static void substep(ugo_env* e) {
     /* free objects: gravity + default damping + gyroscopic (btMultiBody floating base, 0 links) */
     for (int o = 0; o < s->nobj; o++) {
         if (!e->oactive[o]) continue;
+        if (s->ojoint[o].kind != UGJ_FREE) {
+            /* one-dof link on a fixed base (ug_joint.h): joint velocity in ov.x, joint position in ow.x */
+            double Mj, Cj;
+            ugj_dynamics(&s->ojoint[o], &e->oquat[o].x, e->ov[o].x, s->gravity, &Mj, &Cj);
+            e->jM[o] = Mj;
+            double qdd = -Cj / Mj;
+            e->ov[o].x = e->ov[o].x + qdd * dt;
+            v0[NB + 6 * o] = e->ov[o].x;
+            continue;
+        }
         v3 v = e->ov[o];
         double vn = vlen(v);
         v3 a = vsub(V(0, 0, s->gravity), vscale(v, UG_LIN_DAMP + UG_LIN_DAMP * vn));
@@ -2029,6 +2199,13 @@ static void substep(ugo_env* e) {
     for (int o = 0; o < s->nobj; o++) {
         if (!e->oactive[o]) continue;
         int off = NB + 6 * o;
+        if (s->ojoint[o].kind != UGJ_FREE) {
+            e->ov[o].x = e->ov[o].x + dv[off];
+            double vi = split ? e->ov[o].x + dvs[off] : e->ov[o].x;
+            e->ow[o].x = e->ow[o].x + vi * dt;
+            ugj_frame(&s->ojoint[o], e->ow[o].x, &e->oquat[o].x, &e->opos[o].x);
+            continue;
+        }
         e->ov[o] = vadd(e->ov[o], V(dv[off], dv[off + 1], dv[off + 2]));
         e->ow[o] = vadd(e->ow[o], V(dv[off + 3], dv[off + 4], dv[off + 5]));
         v3 vl = e->ov[o], wa = e->ow[o];
@@ -2570,6 +2747,73 @@ static int gf_step(ugo_env* e, const float* a, double* obs, double* rew, uint8_t
     return n;
 }
 
+/* ---- Box (env_box_v0.py) ---- */
+/* reset_box (:172-177): both joints to 0 at rest (resetJointState), the links' frames follow; the button's motor
+ * (force 1, target 0) is always on in this scene and the door's has force 0 (build_rows) */
+static void bx_place(ugo_env* e) {
+    for (int o = 0; o < 2; o++) {
+        e->oactive[o] = 1;
+        e->ov[o] = V(0, 0, 0);
+        e->ow[o] = V(0, 0, 0);
+        ugj_frame(&e->sc.ojoint[o], 0.0, &e->oquat[o].x, &e->opos[o].x);
+    }
+}
+/* get_ee_pose() in world coordinates (robot.py:142-145): the robot base stands at (0, UG_BX_ROBOT_Y, 0) with the
+ * identity orientation, so the world pose is the base-frame pose shifted along y */
+static void bx_ee_world(const ugo_env* e, double* w7) {
+    v3 pe;
+    q4 oe;
+    link_state(e, UG_EE_LINK, &pe, &oe);
+    w7[0] = pe.x; w7[1] = pe.y + UG_BX_ROBOT_Y; w7[2] = pe.z;
+    w7[3] = oe.x; w7[4] = oe.y; w7[5] = oe.z; w7[6] = oe.w;
+}
+/* move_ee(world pose, 'end'): calculateInverseKinematics takes the target into the base frame
+ * (PhysicsServerCommandProcessor: base transform inverse * btTransform(target) [ext]) -- the position shifted
+ * back along y, the orientation through btMatrix3x3::setRotation / getRotation (unit norm) */
+static void bx_move_ee(ugo_env* e, const double* w7) {
+    q4 t = Q(w7[3], w7[4], w7[5], w7[6]);
+    m3 R = qmat(t);
+    move_ee_end(e, V(w7[0], w7[1] - UG_BX_ROBOT_Y, w7[2]), mquat(&R));
+}
+static void bx_obs(const ugo_env* e, double* obs) { bx_ee_world(e, obs); } /* :161-170 np.array(ee_pos) */
+static int bx_reset(ugo_env* e, double* obs) {
+    /* :179-186 robot.reset(), move_ee(get_ee_pose(), 'end'), reset_box() */
+    int n = robot_reset(e);
+    double w7[7];
+    bx_ee_world(e, w7);
+    bx_move_ee(e, w7);
+    bx_place(e);
+    e->goal_approached = e->goal_grasped = e->goal_closed = 0;
+    bx_obs(e, obs);
+    return n;
+}
+static int bx_step(ugo_env* e, const float* a, double* obs, double* rew, uint8_t* term, uint8_t* succ) {
+    /* :118-139 */
+    double w7[7], t7[7];
+    bx_ee_world(e, w7);
+    ugg_box_target(w7, a, t7);
+    bx_move_ee(e, t7);
+    e->mtarget[6] = ugo_gripper_angle((double)a[7]); /* move_gripper(action[-1]) (robot.py:213-218) */
+    e->mon[6] = 1;
+    int n = 0;
+    while (n < UG_BX_STEPS) { /* :128-129 a fixed 120 substeps */
+        substep(e);
+        n++;
+        if (!state_finite(e)) break;
+    }
+    int bc = e->sc.ocol[1];
+    int press = ugg_box_press(e->ow[1].x, e->button_mode, robot_contact(e, bc, 0, UG_NL - 1), robot_contact(e, bc, 9, 18));
+    int op = e->goal_approached, pr = e->goal_grasped, cl = e->goal_closed;
+    double r;
+    int closed = ugg_box_reward(&op, &pr, &cl, e->ow[0].x, press, &r);
+    e->goal_approached = op; e->goal_grasped = pr; e->goal_closed = cl;
+    *rew = r;
+    *term = (uint8_t)closed;
+    *succ = (uint8_t)closed;
+    bx_obs(e, obs);
+    return n;
+}
+
 /* ======================================================================== */
 /* public API                                                                */
 /* ======================================================================== */
@@ -2577,6 +2821,9 @@ ugo_env* ugo_create(int task, uint32_t seed) { return ugo_create_ex(task, seed, 
 /* flags: UG_GEOM_LOD selects the collision LOD (urgym_create_ex's URGYM_FLAG_LOD_GEOMETRY); the default (0 or
  * UG_GEOM_FULL) is the full geometry */
 ugo_env* ugo_create_ex(int task, uint32_t seed, int flags) {
+    if (task < 0 || task >= UG_NTASK) return NULL;
+    /* Box-v0 has cylinders on the robot's path (door handles, button): full geometry only */
+    if (task == UG_TASK_BOX && !UG_GEOM_IS_FULL(flags)) return NULL;
     ugo_env* e = (ugo_env*)calloc(1, sizeof(ugo_env));
     build_scene(&e->sc, task, flags);
     mt_seed(&e->rng, seed);
@@ -2613,7 +2860,7 @@ static void sanitize(ugo_env* e) {
 }
 static int reset_impl(ugo_env* e, const double* draws, double* obs) {
     sanitize(e);
-    e->goal_approached = e->goal_grasped = 0;
+    e->goal_approached = e->goal_grasped = e->goal_closed = 0;
     int n = -1;
     if (e->sc.variant == UG_TASK_TWOBALLS) n = tb_reset(e, draws, obs);
     else switch (e->sc.task) {
@@ -2621,6 +2868,7 @@ static int reset_impl(ugo_env* e, const double* draws, double* obs) {
         case UG_TASK_CUBESPUSH: n = cp_reset(e, draws, obs); break;
         case UG_TASK_CUBESGRASP: n = cg_reset(e, draws, obs); break;
         case UG_TASK_GOLF: n = gf_reset(e, draws, obs); break;
+        case UG_TASK_BOX: n = bx_reset(e, obs); break;
     }
     /* a reset whose settling went non-finite is surfaced like a step's (flag + counter); its observation is
      * returned as computed */
@@ -2644,6 +2892,7 @@ int ugo_step(ugo_env* e, const float* action, double* obs, double* reward, uint8
         case UG_TASK_CUBESPUSH: n = cp_step(e, action, obs, reward, terminated, success); break;
         case UG_TASK_CUBESGRASP: n = cg_step(e, action, obs, reward, terminated, success); break;
         case UG_TASK_GOLF: n = gf_step(e, action, obs, reward, terminated, success); break;
+        case UG_TASK_BOX: n = bx_step(e, action, obs, reward, terminated, success); break;
     }
     if (!state_finite(e)) { /* terminate the episode, zero reward; the autoreset restarts from a clean state */
         *terminated = 1;
@@ -2670,6 +2919,7 @@ int ugo_step(ugo_env* e, const float* action, double* obs, double* reward, uint8
 static int link_of_collider(const scene* s, int ci) {
     const collider* c = &s->col[ci];
     if (c->ent == 0) return c->link;
+    if (s->task == UG_TASK_BOX && (c->ent == 1 || c->ent == 2)) return c->ent == 1 ? 1 : 0; /* door = joint 1, button = 0 */
     if (c->ent >= 1 && c->ent <= MAXOBJ) return ci - s->ocol[c->ent - 1] - 1;
     return -1;
 }
@@ -2742,6 +2992,14 @@ void ugo_dynamics(const double* q, const double* qd, double g, double* M, double
 int ugo_flags(const ugo_env* e) { return e->flags; }
 void ugo_get_stats(const ugo_env* e, int32_t* out) { memcpy(out, e->stats, sizeof(e->stats)); }
 void ugo_set_reward_type(ugo_env* e, int sparse) { e->sparse = sparse != 0; }
+void ugo_set_button_mode(ugo_env* e, int mode) { e->button_mode = mode; }
+int ugo_g_box_reward(int* flags3, double door, int press, double* r) {
+    return ugg_box_reward(&flags3[0], &flags3[1], &flags3[2], door, press, r);
+}
+void ugo_g_box_target(const double* ee7, const float* a, double* t7) { ugg_box_target(ee7, a, t7); }
+int ugo_g_box_press(double button, int mode, int robot_touch, int finger_touch) {
+    return ugg_box_press(button, mode, robot_touch, finger_touch);
+}
 void ugo_set_pgs_bullet(ugo_env* e, int on) { e->pgs_bullet = on != 0; }
 /* checkpoint of the env's Python-random stream (624 words + index) */
 void ugo_get_rng(const ugo_env* e, uint32_t* mt625) {
@@ -2782,7 +3040,7 @@ void ugo_get_state(const ugo_env* e, double* s) {
     s[i++] = e->goal_approached;
     s[i++] = e->goal_grasped;
     s[i++] = e->overflow;
-    s[i++] = 0.0;
+    s[i++] = e->goal_closed;
 }
 void ugo_set_state(ugo_env* e, const double* s) {
     int i = 0;
@@ -2813,6 +3071,7 @@ void ugo_set_state(ugo_env* e, const double* s) {
     e->goal_approached = (int)s[i++];
     e->goal_grasped = (int)s[i++];
     e->overflow = (int)s[i++];
+    e->goal_closed = (int)s[i++];
 }
 void ugo_rng_seed(ugo_env* e, uint32_t seed) { mt_seed(&e->rng, seed); }
 double ugo_rng_random(ugo_env* e) { return mt_random(&e->rng); }

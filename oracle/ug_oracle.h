@@ -46,6 +46,8 @@ int ugo_flags(const ugo_env* e);
 void ugo_get_stats(const ugo_env* e, int32_t* out);
 /* reward_type: 0 'dense', 1 'sparse' (ctor kwarg of every reference env) */
 void ugo_set_reward_type(ugo_env* e, int sparse);
+/* Box-v0 button_touch_mode: 0 'any', 1 'robot', 2 'fingers' (env_box_v0.py:20, :191-216) */
+void ugo_set_button_mode(ugo_env* e, int mode);
 /* tests only: 1 = solve with Bullet's velocity-space PGS form (clamp-and-assign) instead of the row-space
  * restatement the kernels reproduce; bounds the restatement's rounding against Bullet's arithmetic */
 void ugo_set_pgs_bullet(ugo_env* e, int on);

@@ -18,7 +18,8 @@ def fid():
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import collision_fidelity as cf
-    if not all(os.path.exists(p) for p in cf.LIBS.values()):
+    src = os.path.join(ROOT, "oracle", "ug_oracle.c")
+    if not all(os.path.exists(p) and os.path.getmtime(p) >= os.path.getmtime(src) for p in cf.LIBS.values()):
         cf.build()
     return cf
 

@@ -544,8 +544,100 @@ def gen_variants(p):
     json.dump(out, open(os.path.join(OUT, "variants_glue.json"), "w"), indent=1)
 
 
+def gen_box(p):
+    """Box-v0 glue (env_box_v0.py:118-216) with scripted physics: the step head (ee pose + action, the gripper
+    command from the last action component), the fixed 120 substeps, the opened -> pressed -> closed reward state
+    machine with the step penalty, termination / is_success, the observation, valid_button_press in the three
+    button_touch_modes over scripted getContactPoints() lists, and reset's call order (robot.reset, move_ee of the
+    current pose, reset_box)."""
+    from urgym.base.robot import UR5Robotiq85
+    from urgym.envs.env_box_v0 import BoxManipulation
+    out = {"box_step": [], "box_press": [], "box_reset": None}
+    rng = np.random.default_rng(7)
+    grip = UR5Robotiq85.__new__(UR5Robotiq85)
+    grip.id, grip.mimic_parent_id = 1, 9
+    grip.joints = {9: types.SimpleNamespace(maxForce=1000.0, maxVelocity=2.0)}
+    robot_id, box_id = 1, 2
+    for mode in ["any", "robot", "fingers"]:
+        env = BoxManipulation.__new__(BoxManipulation)
+        env.button_touch_mode, env.camera, env.control_method, env.vis = mode, None, "end", False
+        env.boxID = box_id
+        env.box_opened = env.button_pressed = env.box_closed = False
+        env.episode_steps = 0
+        ee = [tuple(float(x) for x in np.r_[rng.uniform(-0.3, 0.3, 3), rng.normal(size=4)]) for _ in range(8)]
+        cur = {"ee": ee[0]}
+        moves, grips, nsub = [], [], [0]
+
+        def move_gripper(L):
+            p.reset_mock()
+            UR5Robotiq85.move_gripper(grip, L)
+            grips.append(float(p.setJointMotorControl2.call_args.kwargs["targetPosition"]))
+
+        env.robot = types.SimpleNamespace(id=robot_id, get_ee_pose=lambda: cur["ee"],
+                                          move_ee=lambda pose, m: moves.append(([float(x) for x in pose], m)),
+                                          move_gripper=move_gripper,
+                                          get_joint_obs=lambda: dict(positions=[], velocities=[], ee_pos=cur["ee"]))
+        env.step_simulation = lambda: nsub.__setitem__(0, nsub[0] + 1)
+        # (door angle, button position, contact list) per step: walks the state machine with misses in between
+        script = [(0.5, 0.0, []), (1.95, 0.0, []), (1.95, -0.01, [contact(12, 0)]), (1.9, -0.03, []),
+                  (1.0, -0.03, [(0, box_id, robot_id, 0, 12)]), (1.0, -0.03, [(0, robot_id, box_id, 3, 0)]),
+                  (0.2, -0.03, [(0, robot_id, box_id, 12, 0)]), (0.05, 0.0, [])]
+        for k, (door, button, contacts) in enumerate(script):
+            moves.clear(); grips.clear(); nsub[0] = 0
+            cur["ee"] = ee[k]
+            a = np.r_[rng.uniform(-0.05, 0.05, 3), rng.uniform(-np.pi / 10, np.pi / 10, 4),
+                      rng.uniform(0.0, 0.085)].astype(np.float32)
+            p.getJointState.side_effect = lambda bid, j, d=door, b=button: ((b if j == 0 else d), 0.0, (0,) * 6, 0.0)
+            p.getContactPoints.side_effect = lambda *aa, c=contacts, **kw: list(c)
+            move_gripper_calls = grips
+            # numpy 1.26 (setup.py:8) promotes np.float32 - float to float64 in move_gripper; this container's
+            # numpy 2 keeps float32 (NEP 50): drive the step with the float32 values held in float64 (the same
+            # values, evaluated as the pinned numpy does)
+            obs, rew, term, trunc, info = env.step(a.astype(np.float64))
+            out["box_step"].append({"mode": mode, "ee_pose": list(ee[k]), "action": a.tolist(), "door": door,
+                                    "button": button, "contacts": [list(c) for c in contacts],
+                                    "move_target": moves[0][0], "control": moves[0][1],
+                                    "gripper_target": move_gripper_calls[0], "substeps": nsub[0],
+                                    "reward": float(rew), "terminated": bool(term), "is_success": bool(info["is_success"]),
+                                    "obs": [float(x) for x in obs],
+                                    "flags": [env.box_opened, env.button_pressed, env.box_closed]})
+        for button, contacts in [(-0.021, []), (-0.019, [(0, box_id, robot_id, 0, 5)]), (-0.05, [(0, box_id, robot_id, 0, 5)]),
+                                 (-0.05, [(0, box_id, robot_id, 1, 12)]), (-0.05, [(0, robot_id, box_id, 9, 0)]),
+                                 (-0.05, [(0, robot_id, box_id, 8, 0)]), (-0.05, [(0, robot_id, 7, 9, 0)])]:
+            p.getJointState.side_effect = lambda bid, j, b=button: ((b if j == 0 else 0.0), 0.0, (0,) * 6, 0.0)
+            p.getContactPoints.side_effect = lambda *aa, c=contacts, **kw: list(c)
+            out["box_press"].append({"mode": mode, "button": button, "contacts": [list(c) for c in contacts],
+                                     "valid": bool(env.valid_button_press())})
+    # reset (:179-186): the calls in order
+    env = BoxManipulation.__new__(BoxManipulation)
+    env.boxID, env.control_method, env.camera = box_id, "end", None
+    calls = []
+    pose = (0.1, 0.02, 0.5, 0.5, 0.5, -0.5, 0.5)
+    env.robot = types.SimpleNamespace(reset=lambda: calls.append(["robot.reset"]), get_ee_pose=lambda: pose,
+                                      move_ee=lambda ps, m: calls.append(["move_ee", [float(x) for x in ps], m]),
+                                      get_joint_obs=lambda: dict(ee_pos=pose))
+    p.reset_mock()
+
+    def plain(x):  # pybullet constants are mock attributes here: keep their names
+        return x._mock_name if isinstance(x, mock.MagicMock) else x
+
+    p.resetJointState.side_effect = lambda *aa, **kw: calls.append(["resetJointState", [plain(x) for x in aa],
+                                                                     {k: plain(v) for k, v in kw.items()}])
+    p.setJointMotorControl2.side_effect = lambda *aa, **kw: calls.append(["setJointMotorControl2", [plain(x) for x in aa],
+                                                                           {k: plain(v) for k, v in kw.items()}])
+    obs, info = env.reset()
+    out["box_reset"] = {"calls": calls, "obs": [float(x) for x in obs],
+                        "flags": [env.box_opened, env.button_pressed, env.box_closed], "episode_steps": env.episode_steps}
+    p.resetJointState.side_effect = None
+    p.setJointMotorControl2.side_effect = None
+    json.dump(out, open(os.path.join(OUT, "box_glue.json"), "w"), indent=1)
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "variants":  # only the variant fixtures
+    if len(sys.argv) > 1 and sys.argv[1] == "box":
+        os.makedirs(OUT, exist_ok=True)
+        gen_box(install_stubs())
+    elif len(sys.argv) > 1 and sys.argv[1] == "variants":  # only the variant fixtures
         os.makedirs(OUT, exist_ok=True)
         gen_variants(install_stubs())
     elif len(sys.argv) > 1 and sys.argv[1] == "twoballs":

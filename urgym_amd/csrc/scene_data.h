@@ -8,6 +8,44 @@
 #define URGYM_SCENE_DATA_H
 #ifndef UG_CONST
 #define UG_CONST static const
+/* Box (env_box_v0.py, skew-box-button.urdf loaded with URDF_MERGE_FIXED_LINKS | URDF_USE_SELF_COLLISION, fixed base
+ * at the origin, :80-85).  The robot stands at (0, 0.5, 0) (:55); the restatement keeps the robot base at its own
+ * origin, so every world position of this task is stored shifted by -UG_BX_ROBOT_Y (observations and IK targets
+ * convert, as PyBullet's base transform does).  Gravity -10 (:60), plane.urdf at z = 0 (:65), no table. */
+#define UG_BX_ROBOT_Y 0.5
+#define UG_BX_STEPS 120                /* :128 for _ in range(120): step_simulation() */
+#define UG_BX_OPENED 1.9               /* :144 door joint > 1.9 */
+#define UG_BX_CLOSED 0.1               /* :155 door joint < 0.1 */
+#define UG_BX_PRESSED (-0.02)          /* :193 button joint < -0.02 */
+#define UG_BX_BUTTON_FORCE 1.0         /* :175 setJointMotorControl2(box, 0, POSITION_CONTROL, force=1), target 0 */
+/* merged base_link: walls box1..box4 (URDF :14-118), box half extents / centres in the box base frame */
+UG_CONST double UG_BX_WALL_HALF[12] = {0.005, 0.1, 0.045, 0.005, 0.1, 0.045, 0.075, 0.005, 0.045, 0.075, 0.005, 0.045};
+UG_CONST double UG_BX_WALL_POS[12] = {0.075, 0.0, 0.045, -0.075, 0.0, 0.045, 0.0, 0.1, 0.045, 0.0, -0.1, 0.045};
+/* door link (revolute about y at (0.075, 0, 0.1), limits [0, 2], URDF :120-147) merged with its fixed handles
+ * h1, h2 (cylinders r 0.005, length 0.05) and h3 (r 0.01, length 0.1, rpy (pi/2, 0, 0) on h2) (:149-223) */
+#define UG_BX_DOOR_X 0.075
+#define UG_BX_DOOR_Z 0.1
+#define UG_BX_DOOR_LO 0.0
+#define UG_BX_DOOR_HI 2.0
+UG_CONST double UG_BX_DOOR_BOX[6] = {-0.076, 0.0, 0.0, 0.08, 0.1, 0.005}; /* centre, half extents */
+/* handles: centre (door frame), radius, half length, axis (0 = z, 1 = the h3 rotation: z -> -y) */
+UG_CONST double UG_BX_HANDLE[12] = {-0.13, 0.05, 0.025, 0.005, -0.13, -0.05, 0.025, 0.005, -0.13, 0.0, 0.05, 0.01};
+UG_CONST double UG_BX_HANDLE_HH[3] = {0.025, 0.025, 0.05};
+/* link masses (URDF :122, :151, :176, :202): door 0.1, h1 0.05, h2 0.05, h3 0.1 */
+UG_CONST double UG_BX_DOOR_MASSES[4] = {0.1, 0.05, 0.05, 0.1};
+/* button link (prismatic along z at (0, 0, 0.07), limits [-0.05, 0], mass 0.01; collision cylinder r 0.02,
+ * length 0.05, URDF :225-252) */
+#define UG_BX_BUTTON_Z 0.07
+#define UG_BX_BUTTON_LO (-0.05)
+#define UG_BX_BUTTON_HI 0.0
+#define UG_BX_BUTTON_MASS 0.01
+#define UG_BX_BUTTON_R 0.02
+#define UG_BX_BUTTON_HH 0.025
+/* button_touch_mode (ctor kwarg, :20, :191-216; registered default 'any', envs/__init__.py:3-8) */
+#define UG_BX_TOUCH_ANY 0
+#define UG_BX_TOUCH_ROBOT 1
+#define UG_BX_TOUCH_FINGERS 2
+
 #endif
 
 /* ---- world / solver (PyBullet defaults, none overridden by the reference) ---- */
@@ -56,12 +94,13 @@ UG_CONST double UG_GEAR_RATIO[5] = {1.0, -1.0, -1.0, 1.0, -1.0};
 #define UG_TASK_CUBESPUSHDIFF 4 /* env_cubes_push_diff_v0.py: obs = ee, cube - ee (x2) */
 #define UG_TASK_GOLFJOINTS 5    /* env_golf_joints_v0.py: joint-space action[6], obs = joints + Golf obs */
 #define UG_TASK_TWOBALLS 6      /* env_two_balls_balance_v0.py: BallBalance robot + paddle, two balls r 0.003 */
-#define UG_NTASK 7
+#define UG_TASK_BOX 7           /* env_box_v0.py: the skew box with a door and a button */
+#define UG_NTASK 8
 #define UG_BASE_TASK(t) ((t) == UG_TASK_CUBESPUSHDIFF ? UG_TASK_CUBESPUSH : \
                          ((t) == UG_TASK_GOLFJOINTS ? UG_TASK_GOLF : ((t) == UG_TASK_TWOBALLS ? UG_TASK_BALLBALANCE : (t))))
-#define UG_OBS_DIM(t) ((t) == 0 ? 6 : ((t) == 2 ? 17 : ((t) == 5 ? 15 : 9)))
-#define UG_ACT_DIM(t) ((t) == 2 ? 9 : ((t) == 5 ? 6 : 3))
-#define UG_NDRAW(t) ((t) == 1 || (t) == 4 ? 1 : ((t) == 6 ? 4 : 2))
+#define UG_OBS_DIM(t) ((t) == 0 ? 6 : ((t) == 2 ? 17 : ((t) == 5 ? 15 : ((t) == 7 ? 7 : 9))))
+#define UG_ACT_DIM(t) ((t) == 2 ? 9 : ((t) == 5 ? 6 : ((t) == 7 ? 8 : 3)))
+#define UG_NDRAW(t) ((t) == 1 || (t) == 4 ? 1 : ((t) == 6 ? 4 : ((t) == 7 ? 0 : 2)))
 
 /* ---- shapes ---- */
 #define UG_SHAPE_BOX 0
@@ -140,5 +179,43 @@ UG_CONST double UG_GEAR_RATIO[5] = {1.0, -1.0, -1.0, 1.0, -1.0};
 #define UG_GF_PITCH_Z 0.02
 #define UG_GF_PITCH_HX 0.4
 #define UG_GF_PITCH_HZ 0.025
+
+/* Box (env_box_v0.py, skew-box-button.urdf loaded with URDF_MERGE_FIXED_LINKS | URDF_USE_SELF_COLLISION, fixed base
+ * at the origin, :80-85).  The robot stands at (0, 0.5, 0) (:55); the restatement keeps the robot base at its own
+ * origin, so every world position of this task is stored shifted by -UG_BX_ROBOT_Y (observations and IK targets
+ * convert, as PyBullet's base transform does).  Gravity -10 (:60), plane.urdf at z = 0 (:65), no table. */
+#define UG_BX_ROBOT_Y 0.5
+#define UG_BX_STEPS 120                /* :128 for _ in range(120): step_simulation() */
+#define UG_BX_OPENED 1.9               /* :144 door joint > 1.9 */
+#define UG_BX_CLOSED 0.1               /* :155 door joint < 0.1 */
+#define UG_BX_PRESSED (-0.02)          /* :193 button joint < -0.02 */
+#define UG_BX_BUTTON_FORCE 1.0         /* :175 setJointMotorControl2(box, 0, POSITION_CONTROL, force=1), target 0 */
+/* merged base_link: walls box1..box4 (URDF :14-118), box half extents / centres in the box base frame */
+UG_CONST double UG_BX_WALL_HALF[12] = {0.005, 0.1, 0.045, 0.005, 0.1, 0.045, 0.075, 0.005, 0.045, 0.075, 0.005, 0.045};
+UG_CONST double UG_BX_WALL_POS[12] = {0.075, 0.0, 0.045, -0.075, 0.0, 0.045, 0.0, 0.1, 0.045, 0.0, -0.1, 0.045};
+/* door link (revolute about y at (0.075, 0, 0.1), limits [0, 2], URDF :120-147) merged with its fixed handles
+ * h1, h2 (cylinders r 0.005, length 0.05) and h3 (r 0.01, length 0.1, rpy (pi/2, 0, 0) on h2) (:149-223) */
+#define UG_BX_DOOR_X 0.075
+#define UG_BX_DOOR_Z 0.1
+#define UG_BX_DOOR_LO 0.0
+#define UG_BX_DOOR_HI 2.0
+UG_CONST double UG_BX_DOOR_BOX[6] = {-0.076, 0.0, 0.0, 0.08, 0.1, 0.005}; /* centre, half extents */
+/* handles: centre (door frame), radius, half length, axis (0 = z, 1 = the h3 rotation: z -> -y) */
+UG_CONST double UG_BX_HANDLE[12] = {-0.13, 0.05, 0.025, 0.005, -0.13, -0.05, 0.025, 0.005, -0.13, 0.0, 0.05, 0.01};
+UG_CONST double UG_BX_HANDLE_HH[3] = {0.025, 0.025, 0.05};
+/* link masses (URDF :122, :151, :176, :202): door 0.1, h1 0.05, h2 0.05, h3 0.1 */
+UG_CONST double UG_BX_DOOR_MASSES[4] = {0.1, 0.05, 0.05, 0.1};
+/* button link (prismatic along z at (0, 0, 0.07), limits [-0.05, 0], mass 0.01; collision cylinder r 0.02,
+ * length 0.05, URDF :225-252) */
+#define UG_BX_BUTTON_Z 0.07
+#define UG_BX_BUTTON_LO (-0.05)
+#define UG_BX_BUTTON_HI 0.0
+#define UG_BX_BUTTON_MASS 0.01
+#define UG_BX_BUTTON_R 0.02
+#define UG_BX_BUTTON_HH 0.025
+/* button_touch_mode (ctor kwarg, :20, :191-216; registered default 'any', envs/__init__.py:3-8) */
+#define UG_BX_TOUCH_ANY 0
+#define UG_BX_TOUCH_ROBOT 1
+#define UG_BX_TOUCH_FINGERS 2
 
 #endif

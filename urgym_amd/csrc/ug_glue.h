@@ -173,4 +173,34 @@ UG_HD void ugg_gf_obs(const double* stick, const double* ball, const double* hol
     }
 }
 
+/* ---- Box (env_box_v0.py) ---- */
+/* step head (:125): get_ee_pose() + action[:-1] -- the 7-tuple (world pose) plus the float32 action components, a
+ * float64 array (numpy 1.26 promotion) */
+UG_HD void ugg_box_target(const double* ee7, const float* a, double* t7) {
+    for (int i = 0; i < 7; i++) t7[i] = ee7[i] + (double)a[i];
+}
+/* update_reward (:141-159) with the step penalty (:138): the state machine opened -> button pressed -> closed again;
+ * flags in/out; returns box_closed (terminated and is_success, :132, :136) */
+UG_HD int ugg_box_reward(int* opened, int* pressed, int* closed, double door, int button_press, double* reward) {
+    double r = 0.0;
+    if (!*opened) {
+        if (door > 1.9) { *opened = 1; r = 1.0; }
+    } else if (!*pressed) {
+        if (button_press) { *pressed = 1; r = 1.0; }
+    } else if (*opened && door < 0.1) {
+        *closed = 1;
+        r = 1.0;
+    }
+    r -= 0.1;
+    *reward = r;
+    return *closed;
+}
+/* valid_button_press (:191-216): the button joint below -0.02 and, unless the mode is 'any', a contact between the
+ * button and the robot ('robot') or one of its finger links 9..18 ('fingers') */
+UG_HD int ugg_box_press(double button, int mode, int robot_touch, int finger_touch) {
+    if (!(button < -0.02)) return 0;
+    if (mode == 0) return 1;
+    return mode == 1 ? robot_touch : finger_touch;
+}
+
 #endif
