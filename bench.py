@@ -25,8 +25,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 TASK_NAMES = {0: "URGym/BallBalance-v0", 1: "URGym/CubesPush-v0", 2: "URGym/CubesGrasp-v0", 3: "URGym/Golf-v0",
-              4: "URGym/CubesPushDiff-v0", 5: "URGym/GolfJoints-v0", 6: "URGym/TwoBallsBalance-v0"}
-MAX_STEPS = {0: 500, 1: 50, 2: 20, 3: 100, 4: 50, 5: 100, 6: 500}
+              4: "URGym/CubesPushDiff-v0", 5: "URGym/GolfJoints-v0", 6: "URGym/TwoBallsBalance-v0", 7: "URGym/Box-v0"}
+MAX_STEPS = {0: 500, 1: 50, 2: 20, 3: 100, 4: 50, 5: 100, 6: 500, 7: 200}
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (AMD spec; the path's bounding roofline)
 

@@ -336,7 +336,8 @@ static void build_scene(scene* s, int variant, int flags) {
     s->full = UG_GEOM_IS_FULL(flags);
     s->task = task;
     s->variant = variant;
-    s->gravity = task == UG_TASK_CUBESGRASP ? -10.0 : -9.8; /* env_cubes_grasp_v0.py:43 vs :59 */
+    s->gravity = task == UG_TASK_CUBESGRASP || task == UG_TASK_BOX ? -10.0 : -9.8; /* env_cubes_grasp_v0.py:43,
+                                                                                   * env_box_v0.py:60 vs :59 */
     /* robot links 1..18 (link 0 is welded to the fixed base: its contacts carry no dynamics and no
      * reward predicate reads them -- env_cubes_push_v0.py:180 excludes it) */
     for (int l = 1; l < UG_NL; l++) {

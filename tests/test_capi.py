@@ -52,9 +52,16 @@ def test_spaces_match_reference(built):
 
 
 def test_wrappers_refuse_what_they_do_not_implement(built):
-    from urgym_amd.envs import make
-    with pytest.raises(NotImplementedError):
-        make("URGym/Box-v0")
+    import numpy as np
+    from urgym_amd.envs import make, TASKS, spaces_for
+    assert TASKS["URGym/Box-v0"] == (7, 200)  # envs/__init__.py:3-8
+    obs, act = spaces_for(7)  # env_box_v0.py:41-43: ee pose; pose deltas + gripper opening
+    assert obs.shape == (7,) and act.shape == (8,) and act.high[7] == np.float32(0.085)
+    from urgym_amd.envs.core import _check_button
+    with pytest.raises(ValueError):
+        _check_button(7, "elbow")
+    with pytest.raises(TypeError):
+        _check_button(0, "any")  # button_touch_mode is Box-v0's kwarg only
     with pytest.raises(KeyError):
         make("URGym/NoSuchEnv-v0")
     from urgym_amd.envs.core import _check_kwargs

@@ -53,8 +53,8 @@ def test_sb3_semantics_cpu(monkeypatch):
     _, _, _, infos = bb.step(np.zeros((3, 3), np.float32))
     assert "is_success" not in infos[3 - 1]                             # BallBalance info is {} (env_ball_balance_v0.py:134)
     assert env.env_is_wrapped(object) == [False] * 4 and env.get_attr("task") == [1] * 4
-    with pytest.raises(NotImplementedError):
-        V.URGymSB3VecEnv("URGym/Box-v0", 2)
+    with pytest.raises(KeyError):
+        V.URGymSB3VecEnv("URGym/NoSuchEnv-v0", 2)
 
 
 @pytest.mark.gpu

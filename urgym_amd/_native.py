@@ -18,7 +18,7 @@ SYMBOLS = [
     "urgym_reset_device", "urgym_sync", "urgym_stream", "urgym_get_state", "urgym_set_state", "urgym_substep",
     "urgym_link_state", "urgym_ik", "urgym_last_kernel_ms", "urgym_debug_prof", "urgym_debug_workspace",
     "urgym_debug_ws_doubles", "urgym_set_reward_type", "urgym_get_flags", "urgym_flags_device", "urgym_get_stats",
-    "urgym_get_rng", "urgym_set_rng", "urgym_contact_points",
+    "urgym_get_rng", "urgym_set_rng", "urgym_contact_points", "urgym_set_button_mode",
 ]
 
 # UG_FLAG_* / UG_STAT_* (urgym_amd/csrc/ug_layout.h)
@@ -76,6 +76,7 @@ def lib():
     L.urgym_debug_workspace.argtypes = [P, I, P, I]
     L.urgym_debug_ws_doubles.argtypes = []
     L.urgym_set_reward_type.argtypes = [P, I]
+    L.urgym_set_button_mode.argtypes = [P, I]
     L.urgym_get_flags.argtypes = [P, P]
     L.urgym_flags_device.restype = P
     L.urgym_flags_device.argtypes = [P]
@@ -179,6 +180,13 @@ class Sim:
         if reward_type not in ("dense", "sparse"):
             raise ValueError(f"reward_type must be 'dense' or 'sparse', not {reward_type!r}")
         self._chk(self.L.urgym_set_reward_type(self.h, int(reward_type == "sparse")), "urgym_set_reward_type")
+
+    def set_button_mode(self, mode):
+        """Box-v0 button_touch_mode: 'any', 'robot' or 'fingers' (env_box_v0.py:20)"""
+        modes = {"any": 0, "robot": 1, "fingers": 2}
+        if mode not in modes:
+            raise ValueError(f"button_touch_mode must be one of {sorted(modes)}, not {mode!r}")
+        self._chk(self.L.urgym_set_button_mode(self.h, modes[mode]), "urgym_set_button_mode")
 
     def flags(self):
         """UG_FLAG_* bits per env of the last step / reset call"""

@@ -72,7 +72,10 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
     s->ncol = 0;
     s->npair = 0;
     s->sparse = 0;
-    for (int o = 0; o < MAXOBJ; o++) s->oncol[o] = 0;
+    s->button_mode = UG_BX_TOUCH_ANY;
+    s->njoint = 0;
+    for (int o = 0; o < MAXOBJ; o++) { s->oncol[o] = 0; s->ojoint[o].kind = UGJ_FREE; }
+    if (task == UG_TASK_BOX) s->gravity = -10.0; /* env_box_v0.py:60 */
     for (int l = 1; l < UG_NL; l++) {
         Collider* c = &s->col[s->ncol++];
         int si = -1;
@@ -102,7 +105,7 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
         c->link = l;
     }
     int nrobot = s->ncol;
-    int statics[4], nstat = 0;
+    int statics[8], nstat = 0;
     if (task == UG_TASK_BALLBALANCE) {
         /* paddle, ball (env_ball_balance_v0.py:175-205); TwoBallsBalance: two balls of radius 0.003
          * (env_two_balls_balance_v0.py:187, 212-235) */
@@ -224,8 +227,84 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
         c->owner = -100; c->ent = 12;
         statics[nstat++] = s->ncol++;
     }
+    if (task == UG_TASK_BOX) {
+        /* skew-box-button.urdf (oracle build_scene): object 0 the door (box + three handle cylinders), object 1 the
+         * button cylinder, the walls static (entity 13), plane.urdf at z = 0 (11); robot frame (box base at y -0.5) */
+        const double by = -UG_BX_ROBOT_Y;
+        s->nobj = 2;
+        ugj_box_links(&s->ojoint[0], &s->ojoint[1]);
+        s->njoint = 2;
+        s->jorder[0] = 1;
+        s->jorder[1] = 0;
+        const double* B = UG_BX_DOOR_BOX;
+        const UgJoint* D = &s->ojoint[0];
+        double lo[3] = {B[0] - B[3], B[1] - B[4], B[2] - B[5]}, hi[3] = {B[0] + B[3], B[1] + B[4], B[2] + B[5]};
+        for (int i = 0; i < 3; i++) {
+            const double* H = &UG_BX_HANDLE[4 * i];
+            double e3[3] = {H[3], i == 2 ? UG_BX_HANDLE_HH[i] : H[3], i == 2 ? H[3] : UG_BX_HANDLE_HH[i]};
+            for (int k = 0; k < 3; k++) {
+                double l = H[k] - e3[k], u = H[k] + e3[k];
+                lo[k] = l < lo[k] ? l : lo[k];
+                hi[k] = u > hi[k] ? u : hi[k];
+            }
+        }
+        for (int k = 0; k < 3; k++) { lo[k] = lo[k] - D->com[k]; hi[k] = hi[k] - D->com[k]; }
+        const double ddisc = ugj_disc(lo, hi);
+        Collider* c = &s->col[s->ncol];
+        box_collider(c, B[3], B[4], B[5], UG_URDF_MARGIN, UG_DEFAULT_FRICTION);
+        c->P = V(B[0], B[1], B[2]); c->aP = c->P;
+        c->disc = ddisc;
+        c->owner = -2; c->ent = 1;
+        s->ocol[0] = s->ncol++;
+        for (int i = 0; i < 3; i++) {
+            const double* H = &UG_BX_HANDLE[4 * i];
+            c = &s->col[s->ncol++];
+            box_collider(c, H[3], H[3], UG_BX_HANDLE_HH[i], 0.0, UG_DEFAULT_FRICTION);
+            c->kind = UG_SHAPE_CYL;
+            c->P = V(H[0], H[1], H[2]); c->aP = c->P;
+            if (i == 2) { double qh[4]; ugj_box_h3_quat(qh); c->R = qmat(Q(qh[0], qh[1], qh[2], qh[3])); c->aR = c->R; }
+            c->disc = ddisc;
+            c->owner = -2; c->ent = 1;
+        }
+        s->oncol[0] = 4;
+        c = &s->col[s->ncol];
+        box_collider(c, UG_BX_BUTTON_R, UG_BX_BUTTON_R, UG_BX_BUTTON_HH, 0.0, UG_DEFAULT_FRICTION);
+        c->kind = UG_SHAPE_CYL;
+        {
+            double blo[3] = {-UG_BX_BUTTON_R, -UG_BX_BUTTON_R, -UG_BX_BUTTON_HH}, bhi[3] = {UG_BX_BUTTON_R, UG_BX_BUTTON_R, UG_BX_BUTTON_HH};
+            c->disc = ugj_disc(blo, bhi);
+        }
+        c->owner = -3; c->ent = 2;
+        s->ocol[1] = s->ncol++;
+        s->oncol[1] = 1;
+        double wlo[3] = {1e30, 1e30, 1e30}, whi[3] = {-1e30, -1e30, -1e30};
+        for (int w = 0; w < 4; w++)
+            for (int k = 0; k < 3; k++) {
+                double l = UG_BX_WALL_POS[3 * w + k] - UG_BX_WALL_HALF[3 * w + k], u = UG_BX_WALL_POS[3 * w + k] + UG_BX_WALL_HALF[3 * w + k];
+                wlo[k] = l < wlo[k] ? l : wlo[k];
+                whi[k] = u > whi[k] ? u : whi[k];
+            }
+        const double wdisc = ugj_disc(wlo, whi);
+        for (int w = 0; w < 4; w++) {
+            c = &s->col[s->ncol];
+            box_collider(c, UG_BX_WALL_HALF[3 * w], UG_BX_WALL_HALF[3 * w + 1], UG_BX_WALL_HALF[3 * w + 2], UG_URDF_MARGIN,
+                         UG_DEFAULT_FRICTION);
+            c->P = V(UG_BX_WALL_POS[3 * w], UG_BX_WALL_POS[3 * w + 1] + by, UG_BX_WALL_POS[3 * w + 2]); c->aP = c->P;
+            c->disc = wdisc;
+            c->owner = -100; c->ent = 13;
+            statics[nstat++] = s->ncol++;
+        }
+        c = &s->col[s->ncol];
+        box_collider(c, UG_PLANE_HALF_XY, UG_PLANE_HALF_XY, UG_PLANE_HALF_Z, UG_URDF_MARGIN, UG_PLANE_FRICTION);
+        c->P = V(0.0, by, -UG_PLANE_HALF_Z); c->aP = c->P;
+        c->disc = ug_sqrt(15.0 * 15.0 * 2.0 + 25.0) + 5.0;
+        c->owner = -100; c->ent = 11;
+        statics[nstat++] = s->ncol++;
+    }
     for (int o = 0; o < s->nobj; o++)
         if (s->oncol[o] == 0) s->oncol[o] = 1;
+    /* pairs in the oracle's order; Box: door box x button only among the objects, button x plane only among the
+     * object-static pairs (oracle build_scene) */
     for (int o = 0; o < s->nobj; o++)
         for (int c = s->ocol[o]; c < s->ocol[o] + s->oncol[o]; c++)
             for (int l = 0; l < nrobot; l++) add_pair(s, l, c);
@@ -236,12 +315,16 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
             for (int ca = s->ocol[o]; ca < s->ocol[o] + s->oncol[o]; ca++)
                 for (int cb = s->ocol[p]; cb < s->ocol[p] + s->oncol[p]; cb++) {
                     int a = ca, b = cb;
+                    if (task == UG_TASK_BOX && s->col[a].kind == UG_SHAPE_CYL) continue;
                     if (s->col[b].kind == UG_SHAPE_SPHERE && s->col[a].kind != UG_SHAPE_SPHERE) { int t = a; a = b; b = t; }
                     add_pair(s, a, b);
                 }
     for (int o = 0; o < s->nobj; o++)
         for (int c = s->ocol[o]; c < s->ocol[o] + s->oncol[o]; c++)
-            for (int t = 0; t < nstat; t++) add_pair(s, c, statics[t]);
+            for (int t = 0; t < nstat; t++) {
+                if (task == UG_TASK_BOX && !(o == 1 && s->col[statics[t]].ent == 11)) continue;
+                add_pair(s, c, statics[t]);
+            }
 }
 
 // ---------------------------------------------------------------------------
@@ -400,6 +483,7 @@ __global__ void __launch_bounds__(WAVE) k_ik(const double* S, int n, const doubl
 __device__ static int link_of_collider(const Scene* s, int ci) {
     const Collider& c = s->col[ci];
     if (c.ent == 0) return c.link;
+    if (s->task == UG_TASK_BOX && (c.ent == 1 || c.ent == 2)) return c.ent == 1 ? 1 : 0; /* door = joint 1, button = 0 */
     if (c.ent >= 1 && c.ent <= MAXOBJ) return ci - s->ocol[c.ent - 1] - 1;
     return -1;
 }
@@ -588,8 +672,12 @@ urgym_handle* urgym_create_ex(int task, int n, int dev, int precision, uint32_t 
         fail(nullptr, "urgym_create_ex: invalid flags " + std::to_string(flags));
         return nullptr;
     }
-    if (task < URGYM_TASK_BALLBALANCE || task > URGYM_TASK_TWOBALLSBALANCE) {
+    if (task < URGYM_TASK_BALLBALANCE || task > URGYM_TASK_BOX) {
         fail(nullptr, "urgym_create: unknown task " + std::to_string(task));
+        return nullptr;
+    }
+    if (task == URGYM_TASK_BOX && (flags & URGYM_FLAG_LOD_GEOMETRY)) {
+        fail(nullptr, "urgym_create_ex: Box-v0 runs the full geometry only (its door handles and button are cylinders)");
         return nullptr;
     }
     if (n <= 0) { fail(nullptr, "urgym_create: n_envs must be > 0"); return nullptr; }
@@ -768,6 +856,15 @@ int urgym_set_reward_type(urgym_handle* h, int sparse) {
     const int v = sparse != 0;
     HIPCHK(h, hipSetDevice(h->dev));
     HIPCHK(h, hipMemcpyAsync((char*)h->d_scene + offsetof(Scene, sparse), &v, sizeof(int), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int urgym_set_button_mode(urgym_handle* h, int mode) {
+    if (!h) return -1;
+    if (mode < UG_BX_TOUCH_ANY || mode > UG_BX_TOUCH_FINGERS) return fail(h, "urgym_set_button_mode: unknown mode " + std::to_string(mode));
+    HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipMemcpyAsync((char*)h->d_scene + offsetof(Scene, button_mode), &mode, sizeof(int), hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
 }

@@ -18,6 +18,7 @@
 #include "model_data.h"
 #include "scene_data.h"
 #include "ug_detmath.h"
+#include "ug_joint.h"
 #include "ug_layout.h"
 
 #define NB UG_NB
@@ -26,7 +27,7 @@
 #define MAXMAN UG_MAXMAN
 #define MAXROWS 128
 #define MAXCOL 28
-#define MAXPAIR 160
+#define MAXPAIR 192
 #define MAXCAND 4   /* per-pair narrowphases emit <= 4 points (box-box culls to 4) */
 
 #define DF __device__ static
@@ -234,9 +235,12 @@ struct Scene {
     Collider col[MAXCOL];
     int ocol[MAXOBJ];  /* first collider of each object */
     int oncol[MAXOBJ]; /* colliders of each object (consecutive) */
+    UgJoint ojoint[MAXOBJ]; /* one-dof links on a fixed base (Box: door, button; ug_joint.h); kind UGJ_FREE otherwise */
+    int njoint, jorder[MAXOBJ]; /* the jointed objects in the multibody's joint order (Box: button = joint 0, door = 1) */
     int npair;
     PairDef pair[MAXPAIR];
     int sparse; /* reward_type != 'dense' (urgym_set_reward_type) */
+    int button_mode; /* Box-v0 button_touch_mode (UG_BX_TOUCH_*, urgym_set_button_mode) */
     int full;   /* full-geometry mode (UG_GEOM_FULL): robot hulls with every vertex and face */
 };
 

@@ -103,8 +103,9 @@ __device__ __forceinline__ static HullArg hull_arg(const Collider& c) {
 
 struct RowS {
     double invD, rinv, rhs, rhsPen, lo, hi, imp, impPen, fric; /* rinv = invD == 0 ? 0 : 1 / invD */
-    int kind; /* 0 limit, 1 motor, 2 gear, 3 normal, 4/5 friction dir 1/2, 6/7 rolling axis 1/2 */
-    int a, b; /* limit: dof, side | motor: m | gear: g | contact: manifold, point */
+    int kind; /* 0 limit, 1 motor, 2 gear, 3 normal, 4/5 friction dir 1/2, 6/7 rolling axis 1/2,
+               * 8 a jointed object's limit, 9 the Box button's motor */
+    int a, b; /* limit: dof, side | motor: m | gear: g | contact: manifold, point | 8: object, side | 9: object */
     int nrow; /* friction: position of its normal row */
 };
 
@@ -135,6 +136,7 @@ struct Shared {
         BoxScratch bs[NBOXSLOT];  /* lane-per-pair box-box clip buffers (after the hull pairs of the pass) */
     };
     double a12[NB];
+    double jM[MAXOBJ];    /* effective inertia of the jointed objects in this substep (serial_pre; ug_joint.h) */
     double fs[8];
     int is[8];
     int ecnt[2 * MAXMAN]; /* team_enumerate: accepted points / rolling points per manifold */
@@ -1598,6 +1600,29 @@ __device__ static void enumerate_rows(Shared& sh, const Scene* s) {
         r.kind = 2; r.a = g;
         nnc++; ncnt++;
     }
+    /* the box's joint limits in joint order, then the button's motor (oracle build_rows) */
+    for (int jj = 0; jj < s->njoint; jj++) {
+        const int o = s->jorder[jj];
+        if (e.oactive[o] == 0.0) continue;
+        const UgJoint& J = s->ojoint[o];
+        const double qj = e.obj[o].w.x;
+        for (int side = 0; side < 2; side++) {
+            double pen = side == 0 ? qj - J.lower : J.upper - qj;
+            if (pen > 0) continue;
+            if (ncnt >= MAXROWS) { e.overflow += 1.0; continue; }
+            RowS& r = sh.rs[nnc];
+            r.kind = 8; r.a = o; r.b = side;
+            nnc++; ncnt++;
+        }
+    }
+    if (s->task == UG_TASK_BOX && e.oactive[1] != 0.0) {
+        if (ncnt >= MAXROWS) e.overflow += 1.0;
+        else {
+            RowS& r = sh.rs[nnc];
+            r.kind = 9; r.a = 1;
+            nnc++; ncnt++;
+        }
+    }
     int nman = (int)e.nman;
     /* contact points kept (capacity: 3 rows each) */
     /* accepted points (capacity: 3 rows each, 5 with rolling friction), as the oracle's running count */
@@ -1679,7 +1704,34 @@ __device__ __noinline__ static void team_enumerate(const Scene* s) {
         RowS& r = sh.rs[nlim + nmot + lane];
         r.kind = 2; r.a = lane;
     }
-    const int nnc = nlim + nmot + 5;
+    /* the box's joint limits (lane 2 k + side: joint k in joint order) and the button's motor */
+    int nbx = 0;
+    if (s->njoint > 0) {
+        const int side = lane & 1;
+        int o = 0;
+        bool jl = false;
+        if (lane < 2 * s->njoint) {
+            o = s->jorder[lane >> 1];
+            const UgJoint& J = s->ojoint[o];
+            const double qj = e.obj[o].w.x;
+            const double pen = side == 0 ? qj - J.lower : J.upper - qj;
+            jl = e.oactive[o] != 0.0 && !(pen > 0);
+        }
+        const unsigned long long mj = ballot(jl);
+        nbx = __popcll(mj);
+        if (jl) {
+            RowS& r = sh.rs[nlim + nmot + 5 + lane_prefix(mj)];
+            r.kind = 8; r.a = o; r.b = side;
+        }
+        if (s->task == UG_TASK_BOX && e.oactive[1] != 0.0) {
+            if (lane == 0) {
+                RowS& r = sh.rs[nlim + nmot + 5 + nbx];
+                r.kind = 9; r.a = 1;
+            }
+            nbx++;
+        }
+    }
+    const int nnc = nlim + nmot + 5 + nbx;
     /* contact points per manifold (lane m) */
     const int nman = (int)e.nman;
     int npt = 0, nroll = 0;
@@ -1856,6 +1908,15 @@ __device__ __forceinline__ void robot_jac_sel(const Kin& k, bool ang, int body, 
 __device__ __forceinline__ void object_jac_sel(const Scene* sc, const EnvState& e, bool ang, int ent, v3 p, v3 d,
                                                double (&J)[NB], double (&MiJ)[NB]) {
     const int o = ent - 1;
+    if (sc->ojoint[o].kind != UGJ_FREE) { /* a one-dof link (ug_joint.h): its slot 0 only */
+        const double pp[3] = {p.x, p.y, p.z}, dd[3] = {d.x, d.y, d.z};
+        const double j = ang ? ugj_ang_jac(&sc->ojoint[o], dd) : ugj_point_jac(&sc->ojoint[o], pp, dd);
+#pragma unroll
+        for (int i = 0; i < NB; i++) { J[i] = 0.0; MiJ[i] = 0.0; }
+        J[0] = j;
+        MiJ[0] = j / g_sh.jM[o];
+        return;
+    }
     const m3 R = qmat(e.obj[o].quat);
     const v3 r = vsub(p, e.obj[o].pos);
     const v3 rn = vcross(r, d);
@@ -1914,6 +1975,11 @@ __device__ __forceinline__ static void build_row(const Scene* s, int pos, double
             MA[i] = sh.u.mcol[pa][i];      /* = ldlt_solve(JA) */
             MB[i] = sh.u.mcol[NB + r.a][i]; /* = ldlt_solve(JB) */
         }
+    } else if (kind >= 8) { /* a jointed object's limit / the button's motor: slot 0 of object r.a (oracle jdof_row) */
+        sgn = (kind == 8 && r.b == 1) ? -1.0 : 1.0;
+        JA[0] = sgn;
+        MA[0] = sgn / sh.jM[r.a];
+        entA = 1 + r.a;
     } else {
         const StMan& M = e.man[r.a];
         PP = &s->pair[(int)M.pair];
@@ -2012,6 +2078,29 @@ __device__ __forceinline__ static void build_row(const Scene* s, int pos, double
         rhs = perr * invD + verr * invD;
         double maxImp = UG_GEAR_MAXF * dt;
         lo = -maxImp; hi = maxImp;
+    } else if (kind >= 8) {
+        const int o = r.a;
+        double den = sgn * MA[0];
+        invD = den > 2.220446049250313e-16 ? 1.0 / den : 0.0;
+        double relv = sgn * sh.v0[NB + 6 * o];
+        if (kind == 8) {
+            const UgJoint& J = s->ojoint[o];
+            const double qj = e.obj[o].w.x;
+            double pen = r.b == 0 ? qj - J.lower : J.upper - qj;
+            double erp = (pen > UG_SPLIT_PEN_THR) ? UG_ERP : UG_ERP2;
+            double perr = -pen * erp / dt, verr = -relv;
+            double pimp = perr * invD, vimp = verr * invD;
+            rhs = (pen > UG_SPLIT_PEN_THR) ? pimp + vimp : vimp;
+            lo = 0.0; hi = UG_LIMIT_MAXIMP;
+        } else { /* reset_box: position control, force 1, target 0, no velocity clamp */
+            double qd = sh.v0[NB + 6 * o];
+            double pst = 1.0 * (0.0 - e.obj[o].w.x) / dt;
+            double verr = 0.0 - qd;
+            double des = UG_MOTOR_KP * pst + qd + UG_MOTOR_KD * verr;
+            double maxImp = UG_BX_BUTTON_FORCE * dt;
+            rhs = 0.0 * invD + (des - relv) * invD;
+            lo = -maxImp; hi = maxImp;
+        }
     } else {
         const PairDef& P = *PP;
         double dA = 0.0, dB = 0.0, relv = 0.0;
@@ -2632,7 +2721,17 @@ __device__ __noinline__ static void serial_pre(const Scene* s) {
         for (int i = 0; i < NB; i++) { e.qd[i] = e.qd[i] + qdd[i] * dt; sh.v0[i] = e.qd[i]; }
     } else if (lane <= s->nobj) { /* free bodies, one lane each (independent of the robot solve) */
         const int o = lane - 1;
-        if (e.oactive[o] != 0.0) {
+        if (e.oactive[o] != 0.0 && s->ojoint[o].kind != UGJ_FREE) {
+            /* a one-dof link on a fixed base (oracle substep, ug_joint.h): joint velocity in v.x, position in w.x */
+            StObj& ob = e.obj[o];
+            const double qt[4] = {ob.quat.x, ob.quat.y, ob.quat.z, ob.quat.w};
+            double Mj, Cj;
+            ugj_dynamics(&s->ojoint[o], qt, ob.v.x, s->gravity, &Mj, &Cj);
+            sh.jM[o] = Mj;
+            const double qdd = -Cj / Mj;
+            ob.v.x = ob.v.x + qdd * dt;
+            sh.v0[NB + 6 * o] = ob.v.x;
+        } else if (e.oactive[o] != 0.0) {
             StObj& ob = e.obj[o];
             v3 v = ob.v;
             double vn = vlen(v);
@@ -2675,6 +2774,16 @@ __device__ __noinline__ static void serial_post(const Scene* s, int split) {
             if (e.oactive[o] == 0.0) continue;
             StObj& ob = e.obj[o];
             int off = NB + 6 * o;
+            if (s->ojoint[o].kind != UGJ_FREE) {
+                ob.v.x = ob.v.x + DV[off];
+                double vi = split ? ob.v.x + DVS[off] : ob.v.x;
+                ob.w.x = ob.w.x + vi * dt;
+                double qt[4], pt[3];
+                ugj_frame(&s->ojoint[o], ob.w.x, qt, pt);
+                ob.quat = Q(qt[0], qt[1], qt[2], qt[3]);
+                ob.pos = V(pt[0], pt[1], pt[2]);
+                continue;
+            }
             ob.v = vadd(ob.v, V(DV[off], DV[off + 1], DV[off + 2]));
             ob.w = vadd(ob.w, V(DV[off + 3], DV[off + 4], DV[off + 5]));
             v3 vl = ob.v, wa = ob.w;
@@ -3512,8 +3621,36 @@ __device__ static void sanitize(const Scene* s, EnvState& e) {
     }
     e.nman = 0.0;
 }
+/* ---- Box (env_box_v0.py; oracle bx_*) ---- */
+/* get_ee_pose() in world coordinates: the robot base stands at (0, UG_BX_ROBOT_Y, 0) */
+__device__ static void bx_ee_world(const EnvState& e, double* w7) {
+    v3 pe;
+    q4 oe;
+    link_state_of(e.q, UG_EE_LINK, pe, oe);
+    w7[0] = pe.x; w7[1] = pe.y + UG_BX_ROBOT_Y; w7[2] = pe.z;
+    w7[3] = oe.x; w7[4] = oe.y; w7[5] = oe.z; w7[6] = oe.w;
+}
+/* move_ee(world pose, 'end'): the target taken into the base frame (position shifted back, orientation through
+ * btMatrix3x3 setRotation / getRotation) */
+__device__ static void bx_move_ee(EnvState& e, const double* w7) {
+    const m3 R = qmat(Q(w7[3], w7[4], w7[5], w7[6]));
+    move_ee_end(e, V(w7[0], w7[1] - UG_BX_ROBOT_Y, w7[2]), mquat(R));
+}
+/* reset_box (:172-177): both joints to 0 at rest, the link frames follow */
+__device__ static void bx_place(const Scene* s, EnvState& e) {
+    for (int o = 0; o < 2; o++) {
+        e.oactive[o] = 1.0;
+        e.obj[o].v = V(0, 0, 0);
+        e.obj[o].w = V(0, 0, 0);
+        double qt[4], pt[3];
+        ugj_frame(&s->ojoint[o], 0.0, qt, pt);
+        e.obj[o].quat = Q(qt[0], qt[1], qt[2], qt[3]);
+        e.obj[o].pos = V(pt[0], pt[1], pt[2]);
+    }
+}
 __device__ static void task_obs(const Scene* s, const EnvState& e, double* obs) {
-    if (s->variant == UG_TASK_TWOBALLS) tb_obs(e, obs);
+    if (s->task == UG_TASK_BOX) bx_ee_world(e, obs); /* :161-170 np.array(ee_pos) */
+    else if (s->variant == UG_TASK_TWOBALLS) tb_obs(e, obs);
     else if (s->variant == UG_TASK_CUBESPUSHDIFF) cpd_obs(e, obs);
     else if (s->task == UG_TASK_CUBESPUSH) cp_obs(e, obs);
     else if (s->task == UG_TASK_CUBESGRASP) cg_obs(e, obs);
@@ -3528,7 +3665,7 @@ __device__ static void task_obs(const Scene* s, const EnvState& e, double* obs) 
  * 94-103, robot.reset 89-106) is a sequence of glue actions separated by physics loops.  It runs here as
  * a small state machine around a single inlined team_substep(), so the PGS register slots exist once. */
 enum { G_STEP = 0, G_STEP_DONE, G_RESET, G_RESET_ROBOT, G_RESET_PLACE, G_RESET_DONE, G_END };
-enum { L_NONE = 0, L_FIXED10, L_WAIT };
+enum { L_NONE = 0, L_FIXED10, L_WAIT, L_FIXED120 };
 struct RunIO {
     const float* act;    /* step action (task act_dim floats) */
     double* obs;         /* obs row */
@@ -3547,6 +3684,16 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
         case G_STEP: {
             v3 pe;
             q4 oe;
+            if (task == UG_TASK_BOX) { /* env_box_v0.py:125-129: ee pose + action, the gripper, 120 substeps */
+                double w7[7], t7[7];
+                bx_ee_world(e, w7);
+                ugg_box_target(w7, io.act, t7);
+                bx_move_ee(e, t7);
+                e.mtarget[6] = gripper_angle((double)io.act[7]); /* move_gripper(action[-1]) */
+                e.mon[6] = 1.0;
+                *next = G_STEP_DONE;
+                return L_FIXED120;
+            }
             if (task == UG_TASK_CUBESGRASP) {
                 /* env_cubes_grasp_v0.py:132-158: random.choices picks joint move or gripper command */
                 int sel = ugg_cg_choose(io.act[0], io.act[1], io.dr.next());
@@ -3611,6 +3758,16 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
                 double stick[3] = {st.x, st.y, st.z}, ball[3] = {e.obj[1].pos.x, e.obj[1].pos.y, e.obj[1].pos.z};
                 double hole[3] = {UG_GF_PITCH_X, UG_GF_PITCH_Y, UG_GF_PITCH_Z};
                 io.succ = ugg_gf_reward(ball, hole, stick, in_fingers, floor, touched, s->sparse, &io.rew, &io.term);
+            } else if (task == UG_TASK_BOX) { /* env_box_v0.py:131-139, update_reward :141-159 */
+                const int bc = s->ocol[1];
+                int press = ugg_box_press(e.obj[1].w.x, s->button_mode, robot_contact(e, s, bc, 0, UG_NL - 1),
+                                          robot_contact(e, s, bc, 9, 18));
+                int op = (int)e.goal_approached, pr = (int)e.goal_grasped, cl = (int)e.spare;
+                io.term = ugg_box_reward(&op, &pr, &cl, e.obj[0].w.x, press, &io.rew);
+                e.goal_approached = (double)op;
+                e.goal_grasped = (double)pr;
+                e.spare = (double)cl;
+                io.succ = io.term;
             } else if (s->variant == UG_TASK_TWOBALLS) { /* env_two_balls_balance_v0.py:110-146 */
                 double b1[3] = {e.obj[1].pos.x, e.obj[1].pos.y, e.obj[1].pos.z};
                 double b2[3] = {e.obj[2].pos.x, e.obj[2].pos.y, e.obj[2].pos.z};
@@ -3641,11 +3798,20 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
             sanitize(s, e);
             e.goal_approached = 0.0;
             e.goal_grasped = 0.0;
+            e.spare = 0.0; /* Box: box_closed */
             for (int i = 0; i < 6; i++) { e.q[i] = UG_ARM_REST[i]; e.qd[i] = 0.0; }
             *next = G_RESET_ROBOT;
             return L_FIXED10;
         case G_RESET_ROBOT: /* reset_gripper (open 100), then the task's scene and start pose */
             open_gripper(e, 100.0);
+            if (task == UG_TASK_BOX) { /* env_box_v0.py:181-184: move_ee(get_ee_pose(), 'end'), reset_box(); no settling */
+                double w7[7];
+                bx_ee_world(e, w7);
+                bx_move_ee(e, w7);
+                bx_place(s, e);
+                *next = G_RESET_DONE;
+                return L_NONE;
+            }
             for (int o = 0; o < s->nobj; o++) remove_object(e, s, o);
             if (task == UG_TASK_CUBESPUSH) { /* env_cubes_push_v0.py:207-227, create_cubes :240-246 */
                 place_object(e, 0, V(0.0, -0.5, 0.1), Q(0, 0, 0, 1));
@@ -3711,6 +3877,7 @@ __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* 
         case G_RESET_DONE:
             e.goal_approached = 0.0;
             e.goal_grasped = 0.0;
+            e.spare = 0.0;
             if (!state_finite(s, e)) { /* a reset that settled into a non-finite state: surfaced (oracle reset_impl) */
                 g_sh.flags |= UG_FLAG_NONFINITE;
                 g_sh.stats[UG_STAT_NONFINITE]++;
@@ -3764,8 +3931,8 @@ __device__ __forceinline__ static int team_run(const Scene* s, double* ws, int p
             ns++;
             /* a non-finite state ends the loop at once (oracle wait_until_stable / robot_reset) */
             if (team_nonfinite(s)) break;
-            if (loop == L_FIXED10) {
-                if (i + 1 == 10) break;
+            if (loop == L_FIXED10 || loop == L_FIXED120) { /* robot.reset's 10 substeps / Box's 120 per step */
+                if (i + 1 == (loop == L_FIXED10 ? 10 : UG_BX_STEPS)) break;
                 continue;
             }
             double qn = lane < NB ? sh.e.q[lane] : 0.0;

@@ -26,10 +26,9 @@ TASKS = {
     "URGym/CubesPushDiff-v0": (4, 50),  # :16-20  (variant of CubesPush: relative obs)
     "URGym/GolfJoints-v0": (5, 100),    # :46-50  (variant of Golf: joint-space action, joints in obs)
     "URGym/TwoBallsBalance-v0": (6, 500),  # :34-38  (BallBalance scene with two balls)
+    "URGym/Box-v0": (7, 200),           # :3-8    (skew box with door and button; kwargs button_touch_mode='any')
 }
-UNSUPPORTED = {  # registered by the reference, not built (different scene / solver features)
-    "URGym/Box-v0": 200,
-}
+UNSUPPORTED = {}  # every id the reference registers is built
 
 
 def spaces_for(task):
@@ -43,6 +42,11 @@ def spaces_for(task):
     elif task in (1, 3, 4):  # env_cubes_push_v0.py:58-60, env_golf_v0.py:58-60, env_cubes_push_diff_v0.py:58-62
         obs = Box(low=np.array([-1.0] * 9), high=np.array([1.0] * 9), dtype=np.float64)
         act = Box(low=np.array([-0.1] * 3), high=np.array([+0.1] * 3), dtype=np.float32)
+    elif task == 7:  # env_box_v0.py:41-43
+        obs = Box(low=np.array([-1.0, -1.0, -1.0, -math.pi, -math.pi, -math.pi, -math.pi]),
+                  high=np.array([1.0, 1.0, 1.0, math.pi, math.pi, math.pi, math.pi]), dtype=np.float64)
+        act = Box(low=np.array([-0.05] * 3 + [-math.pi / 10] * 4 + [0.0]),
+                  high=np.array([+0.05] * 3 + [+math.pi / 10] * 4 + [0.085]), dtype=np.float32)
     elif task == 5:  # env_golf_joints_v0.py:59-63
         obs = Box(low=np.array([-2 * math.pi] * 6 + [-1.0] * 3 + [-1.0] * 3 + [-1.0] * 3),
                   high=np.array([2 * math.pi] * 6 + [1.0] * 3 + [1.0] * 3 + [1.0] * 3), dtype=np.float64)
@@ -63,6 +67,8 @@ def make(env_id, num_envs=None, device=0, seed=0, env_offset=0, **kwargs):
     if env_id not in TASKS:
         raise KeyError(env_id)
     task, max_steps = TASKS[env_id]
+    if task == 7:
+        kwargs.setdefault("button_touch_mode", "any")  # the registry's kwargs (envs/__init__.py:7)
     if num_envs is None:
         return URGymEnv(task, max_episode_steps=max_steps, device=device, seed=seed, **kwargs)
     return URGymVectorEnv(task, num_envs, max_episode_steps=max_steps, device=device, seed=seed,
@@ -104,5 +110,11 @@ def TwoBallsBalance(camera=None, reward_type="dense", render_mode="human", **kw)
     return URGymEnv(6, max_episode_steps=None, camera=camera, reward_type=reward_type, render_mode=render_mode, **kw)
 
 
+def BoxManipulation(button_touch_mode="any", camera=None, render_mode="human", **kw):
+    """env_box_v0.BoxManipulation(button_touch_mode, camera, render_mode) signature."""
+    return URGymEnv(7, max_episode_steps=None, camera=camera, render_mode=render_mode,
+                    button_touch_mode=button_touch_mode, **kw)
+
+
 __all__ = ["make", "TASKS", "URGymEnv", "URGymVectorEnv", "BallBalance", "CubesPush", "CubesGrasp", "Golf",
-           "CubesPushDiff", "GolfJoints", "TwoBallsBalance", "spaces_for"]
+           "CubesPushDiff", "GolfJoints", "TwoBallsBalance", "BoxManipulation", "spaces_for"]

@@ -50,6 +50,16 @@ def _check_kwargs(camera, reward_type):
         raise ValueError(f"reward_type must be 'dense' or 'sparse', not {reward_type!r}")
 
 
+def _check_button(task, mode):
+    """button_touch_mode is Box-v0's ctor kwarg (env_box_v0.py:20); the other envs have no such parameter"""
+    if mode is None:
+        return
+    if task != 7:
+        raise TypeError("button_touch_mode is a Box-v0 argument")
+    if mode not in ("any", "robot", "fingers"):
+        raise ValueError(f"button_touch_mode must be 'any', 'robot' or 'fingers', not {mode!r}")
+
+
 def _flag_info(flags):
     """failure surfacing: only the events that happened, so the usual info stays the reference's"""
     info = {}
@@ -72,15 +82,19 @@ class URGymVectorEnv(_VecBase):
     """
 
     def __init__(self, task, num_envs, max_episode_steps=None, device=0, seed=0, env_offset=0,
-                 camera=None, reward_type="dense", render_mode="rgb_array"):
+                 camera=None, reward_type="dense", render_mode="rgb_array", button_touch_mode=None):
         from . import spaces_for
         _check_kwargs(camera, reward_type)
+        _check_button(task, button_touch_mode)
         self.task = task
         self.num_envs = num_envs
         self.single_observation_space, self.single_action_space = spaces_for(task)
         _init_vector_base(self, num_envs, self.single_observation_space, self.single_action_space)
         self.sim = Sim(task, num_envs, device=device, seed=seed, env_offset=env_offset)
         self.sim.set_reward_type(reward_type)
+        if task == 7:
+            self.sim.set_button_mode(button_touch_mode or "any")
+        self.button_touch_mode = button_touch_mode
         self.reward_type = reward_type
         self.max_episode_steps = max_episode_steps or 0
         self.sim.set_autoreset(True, self.max_episode_steps)
@@ -117,15 +131,19 @@ class URGymEnv(_EnvBase):
     gymnasium TimeLimit truncation the registry adds (urgym/envs/__init__.py)."""
 
     def __init__(self, task, max_episode_steps=None, device=0, seed=0, camera=None, reward_type="dense",
-                 render_mode="human"):
+                 render_mode="human", button_touch_mode=None):
         from . import spaces_for
         _check_kwargs(camera, reward_type)
+        _check_button(task, button_touch_mode)
         if _EnvBase is not object:  # pragma: no cover - gymnasium is absent in this image
             _EnvBase.__init__(self)
         self.task = task
         self.observation_space, self.action_space = spaces_for(task)
         self.sim = Sim(task, 1, device=device, seed=seed)
         self.sim.set_reward_type(reward_type)
+        if task == 7:
+            self.sim.set_button_mode(button_touch_mode or "any")
+        self.button_touch_mode = button_touch_mode
         self.reward_type = reward_type
         self.max_episode_steps = max_episode_steps or 0
         self.sim.set_autoreset(False, 0)
