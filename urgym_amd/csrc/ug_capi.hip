@@ -647,6 +647,8 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     HIPCHK(h, hipMalloc(&h->d_stats, sizeof(int) * UG_NSTAT * N));
     HIPCHK(h, hipMalloc(&h->d_flags, N));
     HIPCHK(h, hipMemsetAsync(h->d_stats, 0, sizeof(int) * UG_NSTAT * N, h->stream));
+    /* the workspace starts zeroed: its separation certificates (WS_PC) must read "none" until written */
+    HIPCHK(h, hipMemsetAsync(h->d_ws, 0, sizeof(double) * WS_STRIDE(UG_GEOM_IS_FULL(flags)) * N, h->stream));
     HIPCHK(h, hipMemsetAsync(h->d_flags, 0, N, h->stream));
     k_iota<<<grid_of(n), WAVE, 0, h->stream>>>(h->d_order, h->d_prio, n);
     HIPCHK(h, hipGetLastError());

@@ -63,7 +63,13 @@ static_assert(UG_FULL_HULL_MAXV + 64 + 8 <= FC_MAX, "a full hull pair's candidat
  * certificates (a handle allocates only what its mode uses) */
 #define WS_LOD_DOUBLES WS_FC
 #define WS_SV (WS_HC2 + 2 * MAXPAIR) /* the cylinder pass's surviving support points (4 x UG_FULL_HULL_MAXF ints) */
-#define WS_FULL_DOUBLES (WS_SV + 2 * UG_FULL_HULL_MAXF)
+/* full-geometry hull-box pairs' separation certificates (team_hull_box_full): per pair, the slack by which the last
+ * candidate-free evaluation cleared the contact threshold, the relative pose it was taken at and the two radii that
+ * bound how far a vertex / box corner can move when the pose changes: [0] slack, [1..9] R_AB, [10..12] p_AB,
+ * [13..15] p_BA, [16] the hull's vertex radius, [17] the box's corner radius.  Zeroed at creation (slack 0: none). */
+#define PC_DOUBLES 18
+#define WS_PC (WS_SV + 2 * UG_FULL_HULL_MAXF)
+#define WS_FULL_DOUBLES (WS_PC + PC_DOUBLES * MAXPAIR)
 #ifdef UG_DEBUG_DUMP /* development aid: team_pgs dumps A, w and impulses after the workspace proper */
 #define WS_DBG WS_FULL_DOUBLES
 #define WS_DOUBLES (WS_DBG + MAXROWS * MAXROWS + 8 * MAXROWS)
@@ -211,6 +217,15 @@ __device__ __forceinline__ double half_bcast(double x, int h) {
     return h == 0 ? __hiloint2double(phi[0], plo[0]) : __hiloint2double(phi[1], plo[1]);
 }
 __device__ __forceinline__ unsigned long long ballot(int p) { return __ballot(p); }
+/* wave-wide min / max of a double (rows of 16 by DPP, then the four rows), uniform result */
+__device__ __forceinline__ double wave_min_d(double x) {
+    x = ug_min(x, dpp<0xB1>(x)); x = ug_min(x, dpp<0x4E>(x)); x = ug_min(x, dpp<0x141>(x)); x = ug_min(x, dpp<0x140>(x));
+    return ug_min(ug_min(readlane_d(x, 0), readlane_d(x, 16)), ug_min(readlane_d(x, 32), readlane_d(x, 48)));
+}
+__device__ __forceinline__ double wave_max_d(double x) {
+    x = ug_max(x, dpp<0xB1>(x)); x = ug_max(x, dpp<0x4E>(x)); x = ug_max(x, dpp<0x141>(x)); x = ug_max(x, dpp<0x140>(x));
+    return ug_max(ug_max(readlane_d(x, 0), readlane_d(x, 16)), ug_max(readlane_d(x, 32), readlane_d(x, 48)));
+}
 __device__ __forceinline__ int lane_prefix(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
 }
@@ -605,9 +620,13 @@ __device__ __forceinline__ void fc_reduce(int n, int k, gdouble* gc) {
         team_reduce4_g(n, k, gc);
     }
 }
-/* hull (A, robot link) vs box (B), full geometry (oracle nc_hull_box) */
+/* hull (A, robot link) vs box (B), full geometry (oracle nc_hull_box).  A candidate-free evaluation whose every
+ * chunk sphere and every box corner clears the threshold by a positive slack leaves a separation certificate
+ * (pcert, WS_PC): team_collide skips the pair while the relative pose has moved less than that slack from the
+ * certificate's pose (the skipped evaluation would produce no candidate; the manifold update still runs). */
 __device__ __forceinline__ static void team_hull_box_full(const HullArg& A, const HullArg& B, const XF& TA, const XF& TB,
-                                                       double thr, int k, unsigned short* hcert, gdouble* gc) {
+                                                       double thr, int k, unsigned short* hcert, gdouble* gc,
+                                                       gdouble* pcert) {
     const int lane = threadIdx.x;
     const m3 RAB = mtm(TB.R, TA.R);
     const v3 pAB = mtv(TB.R, vsub(TA.p, TB.p));
@@ -620,16 +639,21 @@ __device__ __forceinline__ static void team_hull_box_full(const HullArg& A, cons
      * vertex is inside the box or within the threshold, so the chunk adds no candidate -- the skipped work would
      * have produced none */
     unsigned long long live;
+    double cslack = 1e300, crad = 0.0; /* this lane's chunk: the margin it clears the cull by; its vertex radius */
     {
         bool keep = false;
         if (lane < (A.nv + TEAM - 1) / TEAM) {
             const double* S = &UG_HULL_CS[4 * (A.c0 + lane)];
             const v3 cc = vadd(mv(RAB, V(S[0], S[1], S[2])), pAB);
             const v3 q = V(ug_max(-h.x, ug_min(h.x, cc.x)), ug_max(-h.y, ug_min(h.y, cc.y)), ug_max(-h.z, ug_min(h.z, cc.z)));
-            keep = !(vlen(vsub(cc, q)) - S[3] >= thr + mA + 1e-9);
+            const double dd = vlen(vsub(cc, q)) - S[3];
+            keep = !(dd >= thr + mA + 1e-9);
+            cslack = dd - (thr + mA + 1e-9);
+            crad = vlen(V(S[0], S[1], S[2])) + S[3];
         }
         live = ballot(keep);
     }
+    const bool all_culled = live == 0ull;
     for (; live != 0ull; live &= live - 1ull) {
         const int v0 = TEAM * __builtin_ctzll(live);
         const int vi = v0 + lane;
@@ -682,12 +706,14 @@ __device__ __forceinline__ static void team_hull_box_full(const HullArg& A, cons
     int fm = 0x7fffffff;
     const int nf = A.nf;
     bool certified = false;
+    double csd; /* the corner's distance beyond a separating face of A (the cached one, or the scanned maximum) */
     {
         int fc = hcert[c];
         fc = fc < nf ? fc : nf - 1;
         const double* F = &UG_HULL_F[4 * (A.f0 + fc)];
         const double sd = F[0] * y.x + F[1] * y.y + F[2] * y.z - F[3];
         certified = ballot(j == 0 && sd - mA >= thr) == 0x0101010101010101ull;
+        csd = sd;
     }
     if (!certified) {
         /* faces strided over the 8-lane group, HB_FACE_UNROLL planes per lane per batch with their loads issued
@@ -720,6 +746,7 @@ __device__ __forceinline__ static void team_hull_box_full(const HullArg& A, cons
         w = dpp<0x141>(smax); jj = dppi<0x141>(fm);
         if (!better(smax, fm, w, jj, true)) { smax = w; fm = jj; }
         if (j == 0 && fm != 0x7fffffff) hcert[c] = (unsigned short)fm;
+        csd = smax;
     }
     int cvalid = 0;
     Cand cc;
@@ -737,6 +764,22 @@ __device__ __forceinline__ static void team_hull_box_full(const HullArg& A, cons
     const unsigned long long cb = ballot(cvalid);
     if (cvalid) fc_put(gc, n + lane_prefix(cb), cc);
     n += __popcll(cb);
+    if (all_culled && n == 0) { /* candidate-free: certify when every chunk and corner clears by a positive slack */
+        const double ks = j == 0 ? csd - mA - thr - 1e-9 : 1e300;
+        if (ballot(!(cslack > 0.0) || !(ks > 0.0)) == 0ull) {
+            const double slack = ug_min(wave_min_d(cslack), wave_min_d(ks));
+            const double rA = wave_max_d(crad);
+            if (lane == 0) {
+                pcert[0] = slack;
+#pragma unroll
+                for (int i = 0; i < 9; i++) pcert[1 + i] = RAB.m[i];
+                pcert[10] = pAB.x; pcert[11] = pAB.y; pcert[12] = pAB.z;
+                pcert[13] = pBA.x; pcert[14] = pBA.y; pcert[15] = pBA.z;
+                pcert[16] = rA;
+                pcert[17] = vlen(h);
+            }
+        }
+    }
     PROF_ADD(PF_HB_CORNER, t_hc);
     PROF_T0(t_hr);
     fc_reduce(n, k, gc);
@@ -1352,6 +1395,32 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
             if (FULL) /* the disc cylinder against a polytope, either side */
                 hk = hk || (B.kind == UG_SHAPE_CYL && (A.kind == UG_SHAPE_HULL || A.kind == UG_SHAPE_BOX)) ||
                      (A.kind == UG_SHAPE_CYL && B.kind == UG_SHAPE_BOX);
+            if (FULL && A.kind == UG_SHAPE_HULL && B.kind == UG_SHAPE_BOX && A.nv > TEAM) {
+                /* the pair's separation certificate (team_hull_box_full): while no vertex or box corner can have moved
+                 * by its slack since, the evaluation would find no candidate -- skip it.  Every A vertex lies within
+                 * rA of A's origin and every corner within |h| of B's, so a point moves by at most
+                 * |dp| + ||dR||_F r in the other frame. */
+                gcdouble* pc = (gcdouble*)(ws + WS_PC) + PC_DOUBLES * p;
+                double rec[PC_DOUBLES];
+#pragma unroll
+                for (int i = 0; i < PC_DOUBLES; i++) rec[i] = pc[i];
+                const m3 RAB = mtm(pi.TB.R, pi.TA.R);
+                const v3 pAB = mtv(pi.TB.R, vsub(pi.TA.p, pi.TB.p));
+                const v3 pBA = mtv(pi.TA.R, vsub(pi.TB.p, pi.TA.p));
+                double f2 = 0.0;
+#pragma unroll
+                for (int i = 0; i < 9; i++) {
+                    const double d = RAB.m[i] - rec[1 + i];
+                    f2 += d * d;
+                }
+                const double fr = ug_sqrt(f2);
+                const double dA = vlen(vsub(pAB, V(rec[10], rec[11], rec[12]))) + fr * rec[16];
+                const double dB = vlen(vsub(pBA, V(rec[13], rec[14], rec[15]))) + fr * rec[17];
+                if (rec[0] > 0.0 && dA < rec[0] && dB < rec[0]) {
+                    hk = 0;
+                    sh.u.cand.n[lane] = 0;
+                }
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
@@ -1363,7 +1432,8 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
             else if (FULL && pi.A.nv > TEAM) { /* a full-geometry robot hull (every full hull has more than 64 vertices) */
                 if (pi.kb == UG_SHAPE_BOX)
                     team_hull_box_full(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k,
-                                       (unsigned short*)(ws + WS_HC2) + 8 * sh.ov[c0 + k], (gdouble*)(ws + WS_FC));
+                                       (unsigned short*)(ws + WS_HC2) + 8 * sh.ov[c0 + k], (gdouble*)(ws + WS_FC),
+                                       (gdouble*)(ws + WS_PC) + PC_DOUBLES * sh.ov[c0 + k]);
                 else team_hull_hull_full(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k, (gdouble*)(ws + WS_FC));
             } else if (pi.kb == UG_SHAPE_BOX)
                 team_hull_box(pi.A, pi.B, pi.TA, pi.TB, pi.thr, k, (unsigned char*)(ws + WS_HC) + 8 * sh.ov[c0 + k]);
