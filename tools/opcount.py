@@ -152,7 +152,7 @@ def count_task(L, pyoracle, spaces_for, task, n_envs, steps, flags=0):
     """per-phase FP64 op counts of a canonical trajectory of one task"""
     tab = np.zeros(64, np.int64)
     L.ugo_opcount_reset()
-    max_steps = {0: 500, 1: 50, 2: 20, 3: 100, 4: 50, 5: 100, 6: 500}[task]
+    max_steps = {0: 500, 1: 50, 2: 20, 3: 100, 4: 50, 5: 100, 6: 500, 7: 200}[task]
     envs = [pyoracle.OracleEnv(task, 20241220 + i, flags=flags) for i in range(n_envs)]
     for e in envs:
         e.reset()
@@ -201,12 +201,12 @@ def count_task(L, pyoracle, spaces_for, task, n_envs, steps, flags=0):
 
 
 # canonical trajectories (envs, steps per env): long enough to include autoresets
-CANON = {0: (32, 80), 1: (16, 60), 2: (16, 30), 3: (8, 40), 4: (16, 60), 5: (8, 40), 6: (32, 80)}
+CANON = {0: (32, 80), 1: (16, 60), 2: (16, 30), 3: (8, 40), 4: (16, 60), 5: (8, 40), 6: (32, 80), 7: (8, 40)}
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--tasks", default="0,1,2,3,4,5,6")
+    ap.add_argument("--tasks", default="0,1,2,3,4,5,6,7")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "work_model.json"))
     ap.add_argument("--geometry", choices=("full", "lod"), default="full",
                     help="collision geometry of the counted trajectories: the counts land in tasks_full / tasks (lod)")

@@ -25,7 +25,8 @@ NAMES = ["collide", "dyn+enum", "rows", "pgs", "pgs_setup", "integrate", "glue",
          "pgs_warm", "sw_nc", "sw_contact", "sw_finish", "sw_fric_prep", "sw_fric", "sw_res",
          "pr_lookup", "pr_narrow", "pr_manifold", "pr_store", "chunks", "nnc", "nn", "n_le64", "n_65_80", "n_81_96",
          "free_substeps", "free_collide", "free_dyn", "free_rows", "free_pgs", "free_integrate",
-         "free_pgs_setup", "free_pgs_sweeps", "free_pgs_sweeps_plus_post", "pr_boxbox", "hull_sphere"]
+         "free_pgs_setup", "free_pgs_sweeps", "free_pgs_sweeps_plus_post", "pr_boxbox", "hull_sphere",
+         "cyl_pairs", "cyl_pass1", "cyl_pass2", "cyl_survivors", "cyl_scan_iters"]
 
 
 def main():
@@ -40,22 +41,22 @@ def main():
     from urgym_amd.envs import spaces_for
     _, asp = spaces_for(a.task)
     sim.set_autoreset(True, 500)
-    buf = np.zeros(60, np.uint64)
+    buf = np.zeros(64, np.uint64)
     sim.reset()
     sim.sync()
     rc = sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     assert rc == 0, "library not built with -DUG_PROF"
-    r = {k: float(v) for k, v in zip(NAMES, buf[:59])}
+    r = {k: float(v) for k, v in zip(NAMES, buf[:len(NAMES)])}
     print("reset (cycles per substep):", json.dumps({k: round(r[k] / max(r["substeps"], 1), 1) for k in NAMES}))
     print("reset, contact-free substeps:", json.dumps({"fraction": r["free_substeps"] / max(r["substeps"], 1),
-          **{k + "_cycles": round(r[k] / max(r["free_substeps"], 1), 1) for k in NAMES[-10:-2]}}))
+          **{k + "_cycles": round(r[k] / max(r["free_substeps"], 1), 1) for k in NAMES[-15:-7]}}))
     rng = np.random.default_rng(1)
     for _ in range(a.steps):
         sim.step(rng.uniform(asp.low, asp.high, size=(a.envs, len(asp.low))).astype(np.float32))
     sim.sync()
     sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
     es = a.envs * a.steps
-    d = {k: float(v) for k, v in zip(NAMES, buf[:59])}
+    d = {k: float(v) for k, v in zip(NAMES, buf[:len(NAMES)])}
     out = {"per_env_step_cycles": {k: d[k] / es for k in NAMES[:8]},
            "substeps_per_env_step": d["substeps"] / es,
            "rows_per_substep": d["nrows"] / max(d["substeps"], 1),
@@ -75,7 +76,8 @@ def main():
               "enumerate", "broadphase", "pair_narrowphase", "hullbox_vertices", "hullbox_corners",
               "hullbox_reduce", "fk", "lane0_ldl_objects", "unit_solves", "row_build", "rb_jacobians", "rb_solves",
               "rb_scalars", "pgs_mfma", "pgs_warm", "sw_nc", "sw_contact", "sw_finish",
-              "sw_fric_prep", "sw_fric", "sw_res", "pr_lookup", "pr_narrow", "pr_manifold", "pr_store", "integrate", "pr_boxbox", "hull_sphere"):
+              "sw_fric_prep", "sw_fric", "sw_res", "pr_lookup", "pr_narrow", "pr_manifold", "pr_store", "integrate", "pr_boxbox", "hull_sphere",
+              "cyl_pairs", "cyl_pass1", "cyl_pass2", "cyl_survivors", "cyl_scan_iters"):
         out[k + "_cycles_per_substep"] = d[k] / max(d["substeps"], 1)
     print(json.dumps(out, indent=1))
     sim.close()

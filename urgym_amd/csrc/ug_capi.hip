@@ -929,7 +929,7 @@ int urgym_contact_points(urgym_handle* h, int body_a, int body_b, int link_a, in
 }
 
 // Phase cycle counters of the team kernels (only a -DUG_PROF build records them):
-// out16 receives the UG_NPROF (60) accumulators (ug_team.h PF_* / PC_*); reset != 0 zeroes them.
+// out16 receives the UG_NPROF (64) accumulators (ug_team.h PF_* / PC_*); reset != 0 zeroes them.
 // reset == 2 instead copies the last k_step's block timeline (UG_BT_MAX x 4 words: start / end s_memrealtime,
 // env, substeps | reset << 16), tools/timeline.py.
 int urgym_debug_prof(urgym_handle* h, unsigned long long* out16, int reset) {

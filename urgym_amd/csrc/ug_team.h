@@ -35,7 +35,7 @@ namespace ugd {
 #define TEAM 64
 typedef __attribute__((address_space(1))) const double gcdouble;
 typedef __attribute__((address_space(1))) double gdouble;
-#define UG_NPROF 60 /* phase accumulators of the -DUG_PROF build */
+#define UG_NPROF 64 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* a row's J and M^-1 J^T over the NVP = 32 dof slots (robot 12, objects 3 x 6, 2 zero pads) */
@@ -184,7 +184,7 @@ enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_
        PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE, PF_FK, PF_LDL, PF_UNIT, PF_ROWB, PF_RB1, PF_RB2, PF_RB3, PF_MFMA, PF_WARM, PF_SW_NC, PF_SW_CT, PF_SW_FIN, PF_SW_FPREP, PF_SW_FR,
        PF_SW_RES, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST, PC_CHUNKS, PC_NNC, PC_NN, PC_N64, PC_N80, PC_N96,
        PC_FREE, PF_FREE_COL, PF_FREE_DYN, PF_FREE_ROWS, PF_FREE_PGS, PF_FREE_INT,
-       PF_FREE_PSETUP, PF_FREE_PSWEEP, PF_FREE_PPOST, PF_PR_BB, PF_HS };
+       PF_FREE_PSETUP, PF_FREE_PSWEEP, PF_FREE_PPOST, PF_PR_BB, PF_HS, PC_CYPAIR, PF_CY1, PF_CY2, PC_CYSV, PC_CYIT };
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -922,12 +922,17 @@ __device__ __forceinline__ static void team_poly_cyl(int k, bool swapped, gdoubl
     }
     const m3 RBA = mtm(TA.R, TB.R);
     const v3 pBA = mtv(TA.R, vsub(TB.p, TA.p));
+    PROF_CNT(PC_CYPAIR, 1);
+    PROF_T0(t_cy1);
     /* pass 1, lane per face f: the filter and the support points' own-plane test; the surviving (face, point) codes
      * 4 f + j go to a list in the workspace in (face, point) order.  Pass 2, lane per survivor: the plane scan
      * (lane-serial, the oracle's loop with its early exit), candidates appended in survivor order */
     typedef __attribute__((address_space(1))) int gint;
     gint* sv = (gint*)(gc + (WS_SV - WS_FC));
     int ns = 0;
+    /* the largest margin by which a face of A separates the whole cylinder (its support points along -n_f are the
+     * cylinder's lowest points under that plane); every vertex of A lies behind each of its face planes */
+    double sepm = -1e300;
     for (int f0 = 0; f0 < nf; f0 += TEAM) {
         const int f = f0 + lane;
         bool ok[4] = {false, false, false, false};
@@ -938,12 +943,16 @@ __device__ __forceinline__ static void team_poly_cyl(int k, bool swapped, gdoubl
             if (vdot(nf_, pBA) - off > 0) {
                 const v3 u = mtv(RBA, vneg(nf_));
                 const int ks = cyl_support_n(u);
+                double fs = 1e300;
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     if (j >= ks) break;
                     const v3 y = vadd(mv(RBA, cyl_support_pt(r, hh, u, j)), pBA);
-                    ok[j] = !(vdot(nf_, y) - off - mA >= thr);
+                    const double sj = vdot(nf_, y) - off - mA;
+                    ok[j] = !(sj >= thr);
+                    fs = ug_min(fs, sj - thr - 1e-9);
                 }
+                sepm = ug_max(sepm, fs); /* fs > 0: face f's plane separates the whole cylinder with that margin */
             }
         }
         const int cnt = (int)ok[0] + (int)ok[1] + (int)ok[2] + (int)ok[3];
@@ -956,10 +965,34 @@ __device__ __forceinline__ static void team_poly_cyl(int k, bool swapped, gdoubl
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
+    PROF_ADD(PF_CY1, t_cy1);
+    /* a separating face: every survivor is a point of the cylinder, so its plane scan would reach that face (or an
+     * earlier separating one) and reject it -- pass 2 would add nothing (and, by the same plane, the vertex pass found
+     * nothing).  The margin is the pair's separation certificate while the cylinder moves less than it in A's frame
+     * (team_collide skips the pair then). */
+    const double sep = wave_max_d(sepm);
+    if (sep > 0.0 && n == 0) {
+        ns = 0;
+        if (hull && !swapped && lane == 0) {
+            gdouble* pc = (gdouble*)(gc + (WS_PC - WS_FC)) + PC_DOUBLES * sh.ov[sh.is[3] + k];
+            pc[0] = sep;
+#pragma unroll
+            for (int i = 0; i < 9; i++) pc[1 + i] = RAB.m[i];
+            pc[10] = pAB.x; pc[11] = pAB.y; pc[12] = pAB.z;
+            pc[13] = pBA.x; pc[14] = pBA.y; pc[15] = pBA.z;
+            pc[16] = 0.0; /* the hull's vertices stay behind the face: only the cylinder's motion counts */
+            pc[17] = ug_sqrt(r * r + hh * hh);
+        }
+    }
+    PROF_T0(t_cy2);
+    PROF_CNT(PC_CYSV, ns);
     for (int s0 = 0; s0 < ns; s0 += TEAM) {
         const int si = s0 + lane;
         int valid = 0;
         Cand c;
+#ifdef UG_PROF
+        int iters = 0;
+#endif
         if (si < ns) {
             const int code = sv[si], f = code >> 2, j = code & 3;
             v3 nf_;
@@ -975,6 +1008,9 @@ __device__ __forceinline__ static void team_poly_cyl(int k, bool swapped, gdoubl
                 poly_face(A, hull, g, ng, og);
                 const double sd = ng.x * y.x + ng.y * y.y + ng.z * y.z - og;
                 if (sd > smax) { smax = sd; fm = g; }
+#ifdef UG_PROF
+                iters = g + 1;
+#endif
                 if (sd - mA >= thr) break;
             }
             const double depth = smax - mA;
@@ -991,7 +1027,11 @@ __device__ __forceinline__ static void team_poly_cyl(int k, bool swapped, gdoubl
         const unsigned long long m = ballot(valid);
         if (valid) fc_put(gc, n + lane_prefix(m), c);
         n += __popcll(m);
+#ifdef UG_PROF
+        PROF_CNT(PC_CYIT, (int)wave_max_d((double)iters));
+#endif
     }
+    PROF_ADD(PF_CY2, t_cy2);
     fc_reduce(n, k, gc);
     if (swapped) { /* cylinder-box: the oracle's role swap on the kept points */
         if (lane < sh.u.cand.n[k]) {
@@ -1395,11 +1435,11 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
             if (FULL) /* the disc cylinder against a polytope, either side */
                 hk = hk || (B.kind == UG_SHAPE_CYL && (A.kind == UG_SHAPE_HULL || A.kind == UG_SHAPE_BOX)) ||
                      (A.kind == UG_SHAPE_CYL && B.kind == UG_SHAPE_BOX);
-            if (FULL && A.kind == UG_SHAPE_HULL && B.kind == UG_SHAPE_BOX && A.nv > TEAM) {
-                /* the pair's separation certificate (team_hull_box_full): while no vertex or box corner can have moved
-                 * by its slack since, the evaluation would find no candidate -- skip it.  Every A vertex lies within
-                 * rA of A's origin and every corner within |h| of B's, so a point moves by at most
-                 * |dp| + ||dR||_F r in the other frame. */
+            if (FULL && A.kind == UG_SHAPE_HULL && (B.kind == UG_SHAPE_BOX || B.kind == UG_SHAPE_CYL) && A.nv > TEAM) {
+                /* the pair's separation certificate (team_hull_box_full / team_poly_cyl): while no point of either
+                 * shape can have moved by its slack since, the evaluation would find no candidate -- skip it.  Every
+                 * A vertex lies within rA of A's origin and every point of B within rB of B's, so a point moves by at
+                 * most |dp| + ||dR||_F r in the other frame. */
                 gcdouble* pc = (gcdouble*)(ws + WS_PC) + PC_DOUBLES * p;
                 double rec[PC_DOUBLES];
 #pragma unroll
@@ -1414,7 +1454,8 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
                     f2 += d * d;
                 }
                 const double fr = ug_sqrt(f2);
-                const double dA = vlen(vsub(pAB, V(rec[10], rec[11], rec[12]))) + fr * rec[16];
+                /* hull-box: both shapes' points; hull-cylinder (a separating face of A): the cylinder's points */
+                const double dA = B.kind == UG_SHAPE_CYL ? 0.0 : vlen(vsub(pAB, V(rec[10], rec[11], rec[12]))) + fr * rec[16];
                 const double dB = vlen(vsub(pBA, V(rec[13], rec[14], rec[15]))) + fr * rec[17];
                 if (rec[0] > 0.0 && dA < rec[0] && dB < rec[0]) {
                     hk = 0;
@@ -1424,6 +1465,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
+        if (lane == 0) sh.is[3] = c0; /* the pass's first pair (team_poly_cyl's certificate slot) */
         for (unsigned long long hm = ballot(hk); hm != 0ull; hm &= hm - 1ull) {
             const int k = __builtin_ctzll(hm);
             const PairInfo pi = sh.pinfo[k];
