@@ -52,6 +52,7 @@ def lib(path=None):
         L.ugo_g_box_reward.argtypes = [P, D, I, P]
         L.ugo_g_box_press.argtypes = [D, I, I, I]
         L.ugo_g_box_target.argtypes = [P, P, P]
+        L.ugo_box_joint.argtypes = [I, D, D, P]
         L.ugo_g_union_center.argtypes = [P, P]
         L.ugo_g_gf_ball_xy.argtypes = [D, D, P]
         L.ugo_g_gf_reward.argtypes = [P, P, P, I, I, I, I, P, P]

@@ -2998,6 +2998,17 @@ int ugo_g_box_reward(int* flags3, double door, int press, double* r) {
     return ugg_box_reward(&flags3[0], &flags3[1], &flags3[2], door, press, r);
 }
 void ugo_g_box_target(const double* ee7, const float* a, double* t7) { ugg_box_target(ee7, a, t7); }
+/* the Box scene's jointed object o at joint state (q, qd): frame (quat 4, pos 3), M, C, then the link's mass, COM (3)
+ * and principal inertia (3) -- for the known-answer tests (tests/test_box_kat.py) */
+void ugo_box_joint(int o, double q, double qd, double* out) {
+    UgJoint J[2];
+    ugj_box_links(&J[0], &J[1]);
+    const UgJoint* Jo = &J[o];
+    ugj_frame(Jo, q, out, out + 4);
+    ugj_dynamics(Jo, out, qd, -10.0, out + 7, out + 8);
+    out[9] = Jo->mass;
+    for (int i = 0; i < 3; i++) { out[10 + i] = Jo->com[i]; out[13 + i] = Jo->inertia[i]; }
+}
 int ugo_g_box_press(double button, int mode, int robot_touch, int finger_touch) {
     return ugg_box_press(button, mode, robot_touch, finger_touch);
 }
