@@ -3735,7 +3735,7 @@ __device__ static void sanitize(const Scene* s, EnvState& e) {
 }
 /* ---- Box (env_box_v0.py; oracle bx_*) ---- */
 /* get_ee_pose() in world coordinates: the robot base stands at (0, UG_BX_ROBOT_Y, 0) */
-__device__ static void bx_ee_world(const EnvState& e, double* w7) {
+__device__ __forceinline__ static void bx_ee_world(const EnvState& e, double* w7) {
     v3 pe;
     q4 oe;
     link_state_of(e.q, UG_EE_LINK, pe, oe);
