@@ -63,11 +63,13 @@ static_assert(UG_FULL_HULL_MAXV + 64 + 8 <= FC_MAX, "a full hull pair's candidat
  * certificates (a handle allocates only what its mode uses) */
 #define WS_LOD_DOUBLES WS_FC
 #define WS_SV (WS_HC2 + 2 * MAXPAIR) /* the cylinder pass's surviving support points (4 x UG_FULL_HULL_MAXF ints) */
-/* full-geometry hull-box pairs' separation certificates (team_hull_box_full): per pair, the slack by which the last
- * candidate-free evaluation cleared the contact threshold, the relative pose it was taken at and the two radii that
- * bound how far a vertex / box corner can move when the pose changes: [0] slack, [1..9] R_AB, [10..12] p_AB,
- * [13..15] p_BA, [16] the hull's vertex radius, [17] the box's corner radius.  Zeroed at creation (slack 0: none). */
-#define PC_DOUBLES 18
+/* full-geometry separation certificates of hull-box and hull-cylinder pairs (team_hull_box_full, team_poly_cyl): per
+ * pair, the relative pose of the last candidate-free evaluation and the margins by which it cleared the contact
+ * threshold: [0] the box corners' (hull-box) / the separating face's (hull-cylinder) margin, [1..9] R_AB,
+ * [10..12] p_AB, [13..15] p_BA, [16] the hull's vertex radius, [17] B's point radius (box corner / cylinder),
+ * hull-box: [18] the margin by which every hull vertex lies beyond the box face [19] (0..5 = -x, +x, -y, +y, -z, +z).
+ * Zeroed at creation (margin 0: no certificate). */
+#define PC_DOUBLES 20
 #define WS_PC (WS_SV + 2 * UG_FULL_HULL_MAXF)
 #define WS_FULL_DOUBLES (WS_PC + PC_DOUBLES * MAXPAIR)
 #ifdef UG_DEBUG_DUMP /* development aid: team_pgs dumps A, w and impulses after the workspace proper */
@@ -639,21 +641,25 @@ __device__ __forceinline__ static void team_hull_box_full(const HullArg& A, cons
      * vertex is inside the box or within the threshold, so the chunk adds no candidate -- the skipped work would
      * have produced none */
     unsigned long long live;
-    double cslack = 1e300, crad = 0.0; /* this lane's chunk: the margin it clears the cull by; its vertex radius */
+    /* certificate accumulators: this lane's lowest extent of the hull along each box face normal (culled chunks by
+     * their spheres, surviving chunks vertex by vertex), and its chunk's vertex radius */
+    double mf[6] = {1e300, 1e300, 1e300, 1e300, 1e300, 1e300};
+    double crad = 0.0;
     {
         bool keep = false;
         if (lane < (A.nv + TEAM - 1) / TEAM) {
             const double* S = &UG_HULL_CS[4 * (A.c0 + lane)];
             const v3 cc = vadd(mv(RAB, V(S[0], S[1], S[2])), pAB);
             const v3 q = V(ug_max(-h.x, ug_min(h.x, cc.x)), ug_max(-h.y, ug_min(h.y, cc.y)), ug_max(-h.z, ug_min(h.z, cc.z)));
-            const double dd = vlen(vsub(cc, q)) - S[3];
-            keep = !(dd >= thr + mA + 1e-9);
-            cslack = dd - (thr + mA + 1e-9);
+            keep = !(vlen(vsub(cc, q)) - S[3] >= thr + mA + 1e-9);
             crad = vlen(V(S[0], S[1], S[2])) + S[3];
+            if (!keep) {
+                mf[0] = -cc.x - S[3]; mf[1] = cc.x - S[3]; mf[2] = -cc.y - S[3];
+                mf[3] = cc.y - S[3]; mf[4] = -cc.z - S[3]; mf[5] = cc.z - S[3];
+            }
         }
         live = ballot(keep);
     }
-    const bool all_culled = live == 0ull;
     for (; live != 0ull; live &= live - 1ull) {
         const int v0 = TEAM * __builtin_ctzll(live);
         const int vi = v0 + lane;
@@ -662,6 +668,8 @@ __device__ __forceinline__ static void team_hull_box_full(const HullArg& A, cons
         if (vi < A.nv) {
             const double* vv = &UG_HULL_V[3 * (A.v0 + vi)];
             v3 x = vadd(mv(RAB, V(vv[0], vv[1], vv[2])), pAB);
+            mf[0] = ug_min(mf[0], -x.x); mf[1] = ug_min(mf[1], x.x); mf[2] = ug_min(mf[2], -x.y);
+            mf[3] = ug_min(mf[3], x.y); mf[4] = ug_min(mf[4], -x.z); mf[5] = ug_min(mf[5], x.z);
             v3 d = V(ug_fabs(x.x) - h.x, ug_fabs(x.y) - h.y, ug_fabs(x.z) - h.z);
             double dist = 0.0;
             v3 nl = V(0, 0, 0), pl = V(0, 0, 0);
@@ -764,19 +772,34 @@ __device__ __forceinline__ static void team_hull_box_full(const HullArg& A, cons
     const unsigned long long cb = ballot(cvalid);
     if (cvalid) fc_put(gc, n + lane_prefix(cb), cc);
     n += __popcll(cb);
-    if (all_culled && n == 0) { /* candidate-free: certify when every chunk and corner clears by a positive slack */
+    if (n == 0) {
+        /* candidate-free: certify when every box corner clears its face of A and the whole hull lies beyond one box
+         * face plane, each by a positive margin (a vertex beyond a face plane by more than thr + margin is that far
+         * from the box; the plane's margin changes only by the motion along its normal) */
         const double ks = j == 0 ? csd - mA - thr - 1e-9 : 1e300;
-        if (ballot(!(cslack > 0.0) || !(ks > 0.0)) == 0ull) {
-            const double slack = ug_min(wave_min_d(cslack), wave_min_d(ks));
-            const double rA = wave_max_d(crad);
-            if (lane == 0) {
-                pcert[0] = slack;
+        if (ballot(!(ks > 0.0)) == 0ull) {
+            double best = -1e300;
+            int bf = 0;
 #pragma unroll
-                for (int i = 0; i < 9; i++) pcert[1 + i] = RAB.m[i];
-                pcert[10] = pAB.x; pcert[11] = pAB.y; pcert[12] = pAB.z;
-                pcert[13] = pBA.x; pcert[14] = pBA.y; pcert[15] = pBA.z;
-                pcert[16] = rA;
-                pcert[17] = vlen(h);
+            for (int f = 0; f < 6; f++) {
+                const double hf = (f >> 1) == 0 ? h.x : ((f >> 1) == 1 ? h.y : h.z);
+                const double sf = wave_min_d(mf[f]) - hf - thr - mA - 1e-9;
+                if (sf > best) { best = sf; bf = f; }
+            }
+            if (best > 0.0) {
+                const double sc = wave_min_d(ks);
+                const double rA = wave_max_d(crad);
+                if (lane == 0) {
+                    pcert[0] = sc;
+#pragma unroll
+                    for (int i = 0; i < 9; i++) pcert[1 + i] = RAB.m[i];
+                    pcert[10] = pAB.x; pcert[11] = pAB.y; pcert[12] = pAB.z;
+                    pcert[13] = pBA.x; pcert[14] = pBA.y; pcert[15] = pBA.z;
+                    pcert[16] = rA;
+                    pcert[17] = vlen(h);
+                    pcert[18] = best;
+                    pcert[19] = (double)bf;
+                }
             }
         }
     }
@@ -1454,10 +1477,21 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
                     f2 += d * d;
                 }
                 const double fr = ug_sqrt(f2);
-                /* hull-box: both shapes' points; hull-cylinder (a separating face of A): the cylinder's points */
-                const double dA = B.kind == UG_SHAPE_CYL ? 0.0 : vlen(vsub(pAB, V(rec[10], rec[11], rec[12]))) + fr * rec[16];
+                /* B's points (box corners / the cylinder) move by at most dB in A's frame; hull-box: the hull's
+                 * extent along the certified box face normal n changes by at most |n . dp_AB| + |dR_AB^T n| rA */
                 const double dB = vlen(vsub(pBA, V(rec[13], rec[14], rec[15]))) + fr * rec[17];
-                if (rec[0] > 0.0 && dA < rec[0] && dB < rec[0]) {
+                bool ok = rec[0] > 0.0 && dB < rec[0];
+                if (B.kind == UG_SHAPE_BOX) {
+                    const int f = (int)rec[19], ax = f >> 1;
+                    const double sg = (f & 1) ? 1.0 : -1.0;
+                    const double dpa = ax == 0 ? pAB.x - rec[10] : (ax == 1 ? pAB.y - rec[11] : pAB.z - rec[12]);
+                    const double r0 = ax == 0 ? RAB.m[0] - rec[1] : (ax == 1 ? RAB.m[3] - rec[4] : RAB.m[6] - rec[7]);
+                    const double r1 = ax == 0 ? RAB.m[1] - rec[2] : (ax == 1 ? RAB.m[4] - rec[5] : RAB.m[7] - rec[8]);
+                    const double r2 = ax == 0 ? RAB.m[2] - rec[3] : (ax == 1 ? RAB.m[5] - rec[6] : RAB.m[8] - rec[9]);
+                    const double dV = ug_fabs(sg * dpa) + ug_sqrt(r0 * r0 + r1 * r1 + r2 * r2) * rec[16];
+                    ok = ok && rec[18] > 0.0 && dV < rec[18];
+                }
+                if (ok) {
                     hk = 0;
                     sh.u.cand.n[lane] = 0;
                 }
