@@ -5,7 +5,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 OUT=${1:-gpurun_out/r6_tasks}
 mkdir -p "$OUT"
-for te in "1 4096" "2 8192" "3 8192" "4 4096" "5 8192" "6 4096"; do
+for te in "1 4096" "2 8192" "3 8192" "4 4096" "5 8192" "6 4096" "7 4096"; do
   set -- $te
   timeout -k 10 240 python bench.py --task $1 --envs $2 --steps 50 --warmup 5 --reps 3 > "$OUT/task$1.json" 2> "$OUT/task$1.err" || { echo "TASK $1 FAILED"; exit 1; }
   echo "task $1 done"
