@@ -148,6 +148,23 @@ int urgym_set_rng(urgym_handle* h, const uint32_t* mt, const int32_t* elapsed);
 int urgym_contact_points(urgym_handle* h, int body_a, int body_b, int link_a, int link_b, int max_pts, double* out,
                          int32_t* count);
 
+/* Replaces: Camera.shot() -> p.getCameraImage(width, height, viewMatrix, projectionMatrix) (utilities.py:84-89;
+ * env_box_v0.py:163-164) for envs [env0, env0 + count) of the handle, one image each, rendered on the GPU.
+ * view16 / proj16: the 16 floats p.computeViewMatrix / p.computeProjectionMatrixFOV return (column-major;
+ * urgym_amd/camera.py restates them).  Outputs (each may be NULL): rgba count x height x width x 4 (u8), depth
+ * count x height x width (f32, OpenGL depth-buffer value, 1 = nothing hit), seg count x height x width (i32: body
+ * code as in urgym_contact_points, plus ((link + 1) << 24) when flags & 1 -- pybullet's
+ * ER_SEGMENTATION_MASK_OBJECT_AND_LINKINDEX -- and -1 = nothing hit).  Pixel (i, j) casts the ray of the
+ * reference's rgbd_2_world inverse, NDC ((2i - W) / W, -(2j - H) / H) (urgym_amd/csrc/ug_render.h).
+ * Deviations (unpinned: pybullet is absent): the collision shapes are drawn, not the visual meshes (the same for the
+ * tasks' primitives; the robot's hulls cover its concave visual meshes); a flat colour per shape with a headlight
+ * replaces TinyRenderer's lighting and textures; body codes, not pybullet's body unique ids.
+ * urgym_camera_shot_device: device output pointers, asynchronous on urgym_stream(h). */
+int urgym_camera_shot(urgym_handle* h, int env0, int count, const float* view16, const float* proj16, int width,
+                      int height, int flags, uint8_t* rgba, float* depth, int32_t* seg);
+int urgym_camera_shot_device(urgym_handle* h, int env0, int count, const float* view16, const float* proj16, int width,
+                             int height, int flags, uint8_t* d_rgba, float* d_depth, int32_t* d_seg);
+
 /* Replaces: one p.stepSimulation() for every env (fine-grained parity tests). */
 int urgym_substep(urgym_handle* h);
 /* Replaces: p.getLinkState(robot, link)[0:2] -> n_envs x 7 (pos, quat xyzw). */

@@ -65,6 +65,7 @@ def lib(path=None):
         L.ugo_get_rng.argtypes = [P, P]
         L.ugo_set_rng.argtypes = [P, P]
         L.ugo_contact_points.argtypes = [P, I, I, I, I, P, I]
+        L.ugo_camera.argtypes = [P, P, P, I, I, I, P, P, P]
         L.ugo_dynamics.argtypes = [P, P, D, P, P, P]
         L.ugo_set_pgs_bullet.argtypes = [P, I]
         L.ugo_step.argtypes = [P, P, P, P, P, P]
@@ -184,6 +185,17 @@ class OracleEnv:
         out = np.zeros((max_pts, 24))
         n = self.L.ugo_contact_points(self.h, body_a, body_b, link_a, link_b, _p(out), max_pts)
         return out[:min(n, max_pts)]
+
+    def camera(self, view16, proj16, width, height, link_index=False):
+        """ugo_camera: the restated Camera.shot() of this env -> rgb (H, W, 4) u8, depth (H, W) f32, seg (H, W) i32"""
+        v = np.ascontiguousarray(view16, dtype=np.float32)
+        p = np.ascontiguousarray(proj16, dtype=np.float32)
+        rgb = np.zeros((height, width, 4), np.uint8)
+        depth = np.zeros((height, width), np.float32)
+        seg = np.zeros((height, width), np.int32)
+        rc = self.L.ugo_camera(self.h, _p(v), _p(p), width, height, 1 if link_index else 0, _p(rgb), _p(depth), _p(seg))
+        assert rc == 0, "singular projection * view"
+        return rgb, depth, seg
 
     def get_state(self):
         s = np.zeros(self.state_dim)

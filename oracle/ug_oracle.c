@@ -24,6 +24,7 @@
 #include "../urgym_amd/csrc/ug_glue.h"
 #include "../urgym_amd/csrc/ug_joint.h"
 #include "../urgym_amd/csrc/ug_layout.h"
+#include "../urgym_amd/csrc/ug_render.h"
 
 #define NB UG_NB
 #define MAXOBJ UG_MAXOBJ
@@ -2980,6 +2981,50 @@ int ugo_contact_points(const ugo_env* e, int bodyA, int bodyB, int linkA, int li
         }
     }
     return cnt;
+}
+/* Camera.shot() -> p.getCameraImage (utilities.py:84-89) restated as ray casting of the env's collision shapes
+ * (ug_render.h, shared with the kernel): every pixel against every active collider in collider order, first
+ * nearest hit kept.  rgba H x W x 4, depth H x W, seg H x W (each may be NULL).  Returns -1 for a singular P V. */
+int ugo_camera(const ugo_env* e, const float* view16, const float* proj16, int W, int H, int flags, uint8_t* rgba,
+               float* depth, int32_t* seg) {
+    const scene* s = &e->sc;
+    UgrCam cam;
+    if (ugr_setup(view16, proj16, &cam) != 0) return -1;
+    kin k;
+    fk(e->q, &k);
+    double R[MAXCOL][9], P[MAXCOL][3], rad[MAXCOL];
+    int on[MAXCOL];
+    for (int ci = 0; ci < s->ncol; ci++) {
+        const collider* c = &s->col[ci];
+        const xf O = owner_xf(e, &k, c->owner);
+        const xf T = shape_xf(&O, c);
+        for (int m = 0; m < 9; m++) R[ci][m] = T.R.m[m];
+        P[ci][0] = T.p.x; P[ci][1] = T.p.y; P[ci][2] = T.p.z;
+        rad[ci] = ugr_radius(c->kind, c->half, UG_HULL_V + 3 * c->v0, c->nv);
+        on[ci] = collider_active(e, c) != 0;
+    }
+    for (int pix = 0; pix < W * H; pix++) {
+        double o[3], d[3], nb[3] = {0.0, 0.0, 0.0};
+        ugr_ray(&cam, pix % W, pix / W, W, H, o, d);
+        double best = UGR_MISS;
+        int bc = -1;
+        for (int ci = 0; ci < s->ncol; ci++) {
+            if (!on[ci]) continue;
+            const collider* c = &s->col[ci];
+            double nw[3];
+            const double t = ugr_shape(R[ci], P[ci], rad[ci], c->kind, c->half, UG_HULL_F + 4 * c->f0, c->nf, o, d, nw);
+            if (t < best) { best = t; bc = ci; nb[0] = nw[0]; nb[1] = nw[1]; nb[2] = nw[2]; }
+        }
+        const int ent = bc >= 0 ? s->col[bc].ent : -1, link = bc >= 0 ? link_of_collider(s, bc) : -1;
+        unsigned char px[4];
+        float dp;
+        int sg;
+        ugr_shade(&cam, s->variant, best, nb, ent, link, flags, o, d, px, &dp, &sg);
+        if (rgba) { rgba[4 * pix] = px[0]; rgba[4 * pix + 1] = px[1]; rgba[4 * pix + 2] = px[2]; rgba[4 * pix + 3] = px[3]; }
+        if (depth) depth[pix] = dp;
+        if (seg) seg[pix] = sg;
+    }
+    return 0;
 }
 /* the robot's equations of motion at (q, qd) for the dynamics known-answer tests: mass matrix M (NB x NB,
  * CRBA), bias C (RNEA with qdd = 0: gravity g along z, Coriolis / gyroscopic, btMultiBody link damping) and

@@ -58,6 +58,8 @@ void ugo_set_rng(ugo_env* e, const uint32_t* mt625);
 void ugo_dynamics(const double* q, const double* qd, double g, double* M, double* C, double* com);
 /* p.getContactPoints over the manifold cache: 24 doubles per point (see ug_oracle.c); returns the count */
 int ugo_contact_points(const ugo_env* e, int bodyA, int bodyB, int linkA, int linkB, double* out, int max_pts);
+int ugo_camera(const ugo_env* e, const float* view16, const float* proj16, int W, int H, int flags, uint8_t* rgba,
+               float* depth, int32_t* seg);
 void ugo_set_state(ugo_env* e, const double* s);
 /* one physics substep (p.stepSimulation) -- for fine-grained parity tests */
 void ugo_substep(ugo_env* e);

@@ -67,8 +67,10 @@ def test_wrappers_refuse_what_they_do_not_implement(built):
     from urgym_amd.envs.core import _check_kwargs
     with pytest.raises(ValueError):
         _check_kwargs(None, "shaped")
-    with pytest.raises(NotImplementedError):
-        _check_kwargs(object(), "dense")
+    with pytest.raises(TypeError):
+        _check_kwargs(object(), "dense")  # a camera must be urgym_amd.camera.Camera (utilities.py:62)
+    from urgym_amd.camera import Camera
+    _check_kwargs(Camera((1, 1, 1), (0, 0, 0), (0, 0, 1), 0.1, 5, (32, 32), 40), "dense")
     _check_kwargs(None, "sparse")
 
 

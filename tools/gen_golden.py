@@ -633,8 +633,40 @@ def gen_box(p):
     json.dump(out, open(os.path.join(OUT, "box_glue.json"), "w"), indent=1)
 
 
+def gen_camera(p):
+    """Camera (utilities.py:62-107): the reference's own class, its pybullet matrix calls answered by this repo's
+    restatement (urgym_amd/camera.py, [ext]), so the fixture pins the class's back projection (tran_pix_world,
+    rgbd_2_world, rgbd_2_world_batch) on those matrices."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from urgym_amd.camera import compute_projection_matrix_fov, compute_view_matrix
+    from urgym.base.utilities import Camera
+    p.computeViewMatrix.side_effect = compute_view_matrix
+    p.computeProjectionMatrixFOV.side_effect = compute_projection_matrix_fov
+    rng = np.random.default_rng(11)
+    out = []
+    for args in [((1, 1, 1), (0, 0, 0), (0, 0, 1), 0.1, 5, (320, 320), 40),  # env_box_v0.py:49-52
+                 ((0.6, -0.6, 0.9), (0.0, -0.6, 0.5), (0, 0, 1), 0.05, 3.0, (8, 6), 50),
+                 ((-0.4, 0.3, 1.2), (0.1, -0.2, 0.0), (0, 1, 0), 0.2, 4.0, (7, 5), 70)]:
+        cam = Camera(*args)
+        pts = [[int(rng.integers(0, cam.width)), int(rng.integers(0, cam.height)), float(rng.uniform(0.5, 1.0))]
+               for _ in range(6)]
+        rec = {"args": [list(args[0]), list(args[1]), list(args[2]), args[3], args[4], list(args[5]), args[6]],
+               "view": list(cam.view_matrix), "proj": list(cam.projection_matrix),
+               "tran_pix_world": cam.tran_pix_world.tolist(),
+               "points": [[w, h, d, cam.rgbd_2_world(w, h, d).tolist()] for w, h, d in pts]}
+        if cam.width * cam.height <= 64:
+            depth = rng.uniform(0.6, 1.0, size=(cam.height, cam.width))
+            rec["depth"] = depth.tolist()
+            rec["world"] = cam.rgbd_2_world_batch(depth).tolist()
+        out.append(rec)
+    json.dump(out, open(os.path.join(OUT, "camera.json"), "w"), indent=1)
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "box":
+    if len(sys.argv) > 1 and sys.argv[1] == "camera":
+        os.makedirs(OUT, exist_ok=True)
+        gen_camera(install_stubs())
+    elif len(sys.argv) > 1 and sys.argv[1] == "box":
         os.makedirs(OUT, exist_ok=True)
         gen_box(install_stubs())
     elif len(sys.argv) > 1 and sys.argv[1] == "variants":  # only the variant fixtures

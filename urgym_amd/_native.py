@@ -19,6 +19,7 @@ SYMBOLS = [
     "urgym_link_state", "urgym_ik", "urgym_last_kernel_ms", "urgym_debug_prof", "urgym_debug_workspace",
     "urgym_debug_ws_doubles", "urgym_set_reward_type", "urgym_get_flags", "urgym_flags_device", "urgym_get_stats",
     "urgym_get_rng", "urgym_set_rng", "urgym_contact_points", "urgym_set_button_mode",
+    "urgym_camera_shot", "urgym_camera_shot_device",
 ]
 
 # UG_FLAG_* / UG_STAT_* (urgym_amd/csrc/ug_layout.h)
@@ -84,6 +85,8 @@ def lib():
     L.urgym_get_rng.argtypes = [P, P, P]
     L.urgym_set_rng.argtypes = [P, P, P]
     L.urgym_contact_points.argtypes = [P, I, I, I, I, I, P, P]
+    L.urgym_camera_shot.argtypes = [P, I, I, P, P, I, I, I, P, P, P]
+    L.urgym_camera_shot_device.argtypes = [P, I, I, P, P, I, I, I, P, P, P]
     _lib = L
     return L
 

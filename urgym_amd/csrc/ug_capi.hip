@@ -17,6 +17,7 @@
 
 #include "../../include/urgym.h"
 #include "ug_team.h"
+#include "ug_render.h"
 
 using namespace ugd;
 
@@ -547,6 +548,52 @@ __global__ void __launch_bounds__(WAVE) k_contacts(const Scene* sc, const double
     count[i] = cnt;
 }
 
+// Camera.shot() for a range of envs (ug_render.h): block (tile of 64 pixels, env).  The block's lanes first pose
+// one collider each (fk + owner / shape frame, the same functions the physics uses) into LDS, then every lane
+// casts its pixel's ray against the env's active colliders in collider order (first nearest hit wins).
+__global__ void __launch_bounds__(WAVE) k_camera(const Scene* sc, const double* S, int env0, UgrCam cam, int W, int H,
+                                                 int flags, uint8_t* rgba, float* depth, int32_t* seg) {
+    __shared__ double sR[MAXCOL][9], sP[MAXCOL][3], sRad[MAXCOL];
+    __shared__ int sOn[MAXCOL];
+    const int lane = threadIdx.x;
+    const size_t img = blockIdx.y;
+    const EnvState& e = *(const EnvState*)(S + (size_t)(env0 + (int)img) * UG_STATE_DIM);
+    const int nc = sc->ncol;
+    if (lane < nc) {
+        Kin k;
+        fk(e.q, k);
+        const Collider& c = sc->col[lane];
+        const XF T = shape_xf(owner_xf(e, k, c.owner), c);
+        for (int m = 0; m < 9; m++) sR[lane][m] = T.R.m[m];
+        sP[lane][0] = T.p.x; sP[lane][1] = T.p.y; sP[lane][2] = T.p.z;
+        sRad[lane] = ugr_radius(c.kind, c.half, UG_HULL_V + 3 * c.v0, c.nv);
+        sOn[lane] = collider_active(e, c);
+    }
+    __syncthreads();
+    const int pix = blockIdx.x * WAVE + lane;
+    if (pix >= W * H) return;
+    double o[3], d[3], nb[3] = {0.0, 0.0, 0.0};
+    ugr_ray(&cam, pix % W, pix / W, W, H, o, d);
+    double best = UGR_MISS;
+    int bc = -1;
+    for (int ci = 0; ci < nc; ci++) {
+        if (!sOn[ci]) continue;
+        const Collider& c = sc->col[ci];
+        double nw[3];
+        const double t = ugr_shape(sR[ci], sP[ci], sRad[ci], c.kind, c.half, UG_HULL_F + 4 * c.f0, c.nf, o, d, nw);
+        if (t < best) { best = t; bc = ci; nb[0] = nw[0]; nb[1] = nw[1]; nb[2] = nw[2]; }
+    }
+    const int ent = bc >= 0 ? sc->col[bc].ent : -1, link = bc >= 0 ? link_of_collider(sc, bc) : -1;
+    unsigned char px[4];
+    float dp;
+    int sg;
+    ugr_shade(&cam, sc->variant, best, nb, ent, link, flags, o, d, px, &dp, &sg);
+    const size_t at = img * (size_t)(W * H) + (size_t)pix;
+    if (rgba) { rgba[4 * at] = px[0]; rgba[4 * at + 1] = px[1]; rgba[4 * at + 2] = px[2]; rgba[4 * at + 3] = px[3]; }
+    if (depth) depth[at] = dp;
+    if (seg) seg[at] = sg;
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -925,6 +972,60 @@ int urgym_contact_points(urgym_handle* h, int body_a, int body_b, int link_a, in
     hipFree(d_out);
     hipFree(d_cnt);
     if (e != hipSuccess) return fail(h, std::string("urgym_contact_points: ") + hipGetErrorString(e));
+    return 0;
+}
+
+static int camera_args(urgym_handle* h, int env0, int count, const float* view16, const float* proj16, int width,
+                       int height, UgrCam* cam) {
+    if (!h) return -1;
+    if (!view16 || !proj16) return fail(h, "urgym_camera_shot: view / projection matrix missing");
+    if (env0 < 0 || count < 1 || count > 65535 || env0 + count > h->n)
+        return fail(h, "urgym_camera_shot: env range [env0, env0 + count) outside the handle's envs (or count > 65535)");
+    if (width < 1 || height < 1 || width > 4096 || height > 4096)
+        return fail(h, "urgym_camera_shot: image size must be 1..4096 x 1..4096");
+    if (ugr_setup(view16, proj16, cam) != 0) return fail(h, "urgym_camera_shot: projection * view is singular");
+    return 0;
+}
+
+int urgym_camera_shot_device(urgym_handle* h, int env0, int count, const float* view16, const float* proj16, int width,
+                             int height, int flags, uint8_t* d_rgba, float* d_depth, int32_t* d_seg) {
+    UgrCam cam;
+    if (camera_args(h, env0, count, view16, proj16, width, height, &cam) != 0) return -1;
+    HIPCHK(h, hipSetDevice(h->dev));
+    dim3 grid((unsigned)((width * height + WAVE - 1) / WAVE), (unsigned)count);
+    k_camera<<<grid, WAVE, 0, h->stream>>>(h->d_scene, h->d_state, env0, cam, width, height, flags, d_rgba, d_depth,
+                                           d_seg);
+    HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
+int urgym_camera_shot(urgym_handle* h, int env0, int count, const float* view16, const float* proj16, int width,
+                      int height, int flags, uint8_t* rgba, float* depth, int32_t* seg) {
+    UgrCam cam;
+    if (camera_args(h, env0, count, view16, proj16, width, height, &cam) != 0) return -1;
+    HIPCHK(h, hipSetDevice(h->dev));
+    const size_t np = (size_t)width * (size_t)height * (size_t)count;
+    uint8_t* d_rgba = nullptr;
+    float* d_depth = nullptr;
+    int32_t* d_seg = nullptr;
+    hipError_t e = hipSuccess;
+    if (rgba) e = hipMalloc(&d_rgba, 4 * np);
+    if (e == hipSuccess && depth) e = hipMalloc(&d_depth, sizeof(float) * np);
+    if (e == hipSuccess && seg) e = hipMalloc(&d_seg, sizeof(int32_t) * np);
+    if (e == hipSuccess) {
+        dim3 grid((unsigned)((width * height + WAVE - 1) / WAVE), (unsigned)count);
+        k_camera<<<grid, WAVE, 0, h->stream>>>(h->d_scene, h->d_state, env0, cam, width, height, flags, d_rgba,
+                                               d_depth, d_seg);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess && rgba) e = hipMemcpyAsync(rgba, d_rgba, 4 * np, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && depth) e = hipMemcpyAsync(depth, d_depth, sizeof(float) * np, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && seg) e = hipMemcpyAsync(seg, d_seg, sizeof(int32_t) * np, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    hipFree(d_rgba);
+    hipFree(d_depth);
+    hipFree(d_seg);
+    if (e != hipSuccess) return fail(h, std::string("urgym_camera_shot: ") + hipGetErrorString(e));
     return 0;
 }
 

@@ -44,8 +44,9 @@ def _init_vector_base(env, num_envs, obs_space, act_space):
 
 
 def _check_kwargs(camera, reward_type):
-    if camera is not None:
-        raise NotImplementedError("camera rendering is outside the hot-path scope (SURVEY.md 8(f)4)")
+    from ..camera import Camera
+    if camera is not None and not isinstance(camera, Camera):
+        raise TypeError("camera must be None or a urgym_amd.camera.Camera")
     if reward_type not in ("dense", "sparse"):
         raise ValueError(f"reward_type must be 'dense' or 'sparse', not {reward_type!r}")
 
@@ -70,6 +71,11 @@ def _flag_info(flags):
     if flags & FLAG_DROPPED:
         info["contacts_dropped"] = True  # a contact capacity limit was hit
     return info
+
+
+# the envs whose get_observation() shoots the camera (env_cubes_grasp_v0.py:259-263, env_box_v0.py:163-167); the
+# reference builds dict(rgb, depth, seg) there and returns only the vector observation: kept here as camera_obs
+_CAMERA_TASKS = (2, 7)
 
 
 class URGymVectorEnv(_VecBase):
@@ -99,9 +105,16 @@ class URGymVectorEnv(_VecBase):
         self.max_episode_steps = max_episode_steps or 0
         self.sim.set_autoreset(True, self.max_episode_steps)
         self.render_mode = render_mode  # accepted; there is no GUI ('human' opens no window: documented deviation)
+        self.camera, self.camera_obs = camera, None
+
+    def _shoot(self):
+        if self.camera is not None and self.task in _CAMERA_TASKS:  # every env's image, one launch
+            rgb, depth, seg = self.camera.shot_batch(self.sim)
+            self.camera_obs = dict(rgb=rgb, depth=depth, seg=seg)
 
     def reset(self, *, seed=None, options=None):
         obs = self.sim.reset()
+        self._shoot()
         return obs, {}
 
     def step(self, actions):
@@ -119,6 +132,7 @@ class URGymVectorEnv(_VecBase):
                 fo[i] = out["final_obs"][i].copy()
             infos["final_observation"] = fo
             infos["_final_observation"] = done
+        self._shoot()
         return out["obs"], out["reward"], term, trunc, infos
 
     def close(self):
@@ -149,10 +163,20 @@ class URGymEnv(_EnvBase):
         self.sim.set_autoreset(False, 0)
         self._elapsed = 0
         self.render_mode = render_mode  # accepted; 'human' opens no GUI window (documented deviation)
+        self.camera, self.camera_obs = camera, None
+        if camera is not None:
+            camera.attach(self.sim, 0)
+
+    def _shoot(self):
+        if self.camera is not None and self.task in _CAMERA_TASKS:
+            rgb, depth, seg = self.camera.shot()
+            self.camera_obs = dict(rgb=rgb, depth=depth, seg=seg)
 
     def reset(self, *, seed=None, options=None):
         self._elapsed = 0
-        return self.sim.reset()[0].copy(), {}
+        obs = self.sim.reset()[0].copy()
+        self._shoot()
+        return obs, {}
 
     def step(self, action):
         out = self.sim.step(np.asarray(action, dtype=np.float32).reshape(1, -1))
@@ -161,6 +185,7 @@ class URGymEnv(_EnvBase):
         # BallBalance / TwoBallsBalance return {} (env_ball_balance_v0.py:134); the others {'is_success': ...}
         info = {} if self.task in (0, 6) else {"is_success": bool(out["success"][0])}
         info.update(_flag_info(int(self.sim.flags()[0])))
+        self._shoot()
         return out["obs"][0].copy(), float(out["reward"][0]), bool(out["terminated"][0]), trunc, info
 
     def close(self):
