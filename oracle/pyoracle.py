@@ -11,6 +11,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_build", "libugoracle.so")
+LIB_PATH_R140 = os.path.join(_HERE, "_build", "libugoracle_r140.so")  # the UR5Robotiq140 restatement
 
 _libs = {}
 

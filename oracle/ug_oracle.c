@@ -16,6 +16,8 @@
 
 #ifdef UG_MODEL_DATA /* collision-fidelity builds (tools/collision_fidelity.py) swap in their model header */
 #include UG_MODEL_DATA
+#elif defined(UG_ROBOT_R140) /* the UR5Robotiq140 restatement (libugoracle_r140.so, robot.py:221-240) */
+#include "../urgym_amd/csrc/model_data_r140.h"
 #else
 #include "../urgym_amd/csrc/model_data.h"
 #endif

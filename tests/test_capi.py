@@ -19,11 +19,24 @@ def test_header_and_binding_agree(built):
     assert sorted(SYMBOLS) == header_symbols()
 
 
-def test_library_exports_every_declared_symbol(built):
-    from urgym_amd._native import LIB_PATH
-    L = ctypes.CDLL(LIB_PATH)
+@pytest.mark.parametrize("robot", ["ur5_robotiq_85", "ur5_robotiq_140"])
+def test_library_exports_every_declared_symbol(built, robot):
+    from urgym_amd._native import ROBOT_LIBS
+    L = ctypes.CDLL(ROBOT_LIBS[robot])  # both robots' builds carry the whole C-ABI
     for s in header_symbols():
         assert hasattr(L, s), s
+
+
+def test_robot_builds_differ_only_in_the_robot():
+    """UR5Robotiq140's restatement (robot.py:221-240): the same tree, its own limits / finger axis / mimic signs;
+    the same task shapes and state layout as the Robotiq-85 build"""
+    from oracle.pyoracle import LIB_PATH_R140, lib as olib
+    a, b = olib(), olib(LIB_PATH_R140)
+    assert a.ugo_state_dim() == b.ugo_state_dim()
+    assert [a.ugo_obs_dim(t) for t in range(8)] == [b.ugo_obs_dim(t) for t in range(8)]
+    from urgym_amd._native import lib
+    with pytest.raises(ValueError):
+        lib("panda")  # robot.py:150-175, not built (DESIGN.md 9)
 
 
 def test_static_shapes(built):

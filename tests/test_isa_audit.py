@@ -17,10 +17,10 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math", 
          "-S"]
 
 
-def _isa(src, out):
+def _isa(src, out, defs=()):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
-    subprocess.run([HIPCC] + FLAGS + ["-o", str(out), src], check=True, cwd=ROOT)
+    subprocess.run([HIPCC] + FLAGS + list(defs) + ["-o", str(out), src], check=True, cwd=ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import scc_audit
     return scc_audit.audit(str(out))
@@ -31,6 +31,7 @@ def test_audit_flags_the_reproducer(tmp_path):
     assert len(hits) >= 1 and all("s_cselect" in h[4] for h in hits), hits
 
 
-def test_shipped_library_has_no_scc_clobbered_pick(tmp_path):
-    hits = _isa(os.path.join(ROOT, "urgym_amd", "csrc", "ug_capi.hip"), tmp_path / "ug.s")
+@pytest.mark.parametrize("defs", [(), ("-DUG_ROBOT_R140",)], ids=["ur5_robotiq_85", "ur5_robotiq_140"])
+def test_shipped_library_has_no_scc_clobbered_pick(tmp_path, defs):
+    hits = _isa(os.path.join(ROOT, "urgym_amd", "csrc", "ug_capi.hip"), tmp_path / "ug.s", defs)
     assert hits == [], hits

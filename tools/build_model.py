@@ -39,7 +39,10 @@ import numpy as np
 from scipy.spatial import ConvexHull
 
 REF = os.environ.get("URGYM_REFERENCE", "/root/reference")
-URDF = os.path.join(REF, "urgym/urdf/ur5_robotiq_85.urdf")
+# the robot: UR5Robotiq85 (robot.py:179-186, every registered env) or UR5Robotiq140 (robot.py:221-229) via
+# URGYM_MODEL_URDF=urgym/urdf/ur5_robotiq_140.urdf (same tree shape and DFS order, its own meshes and limits)
+URDF_REL = os.environ.get("URGYM_MODEL_URDF", "urgym/urdf/ur5_robotiq_85.urdf")
+URDF = os.path.join(REF, URDF_REL)
 OUT = os.environ.get("URGYM_MODEL_OUT",
                      os.path.join(os.path.dirname(__file__), "..", "urgym_amd", "csrc", "model_data.h"))
 # collision-fidelity builds (tools/collision_fidelity.py; never the product): full hulls (URGYM_HULL_MAXV),
@@ -336,7 +339,7 @@ def main():
         s = math.sqrt(1.0 + R[2, 2] - R[0, 0] - R[1, 1]) * 2
         return [(R[0, 2] + R[2, 0]) / s, (R[1, 2] + R[2, 1]) / s, 0.25 * s, (R[1, 0] - R[0, 1]) / s]
 
-    w("/* GENERATED by tools/build_model.py from %s and its collision meshes. Do not edit. */" % "urgym/urdf/ur5_robotiq_85.urdf")
+    w("/* GENERATED by tools/build_model.py from %s and its collision meshes. Do not edit. */" % URDF_REL)
     w("/* Data, not code: shared as input by oracle/ (CPU restatement) and urgym_amd/csrc (HIP). */")
     w("#ifndef URGYM_MODEL_DATA_H")
     w("#define URGYM_MODEL_DATA_H")

@@ -23,8 +23,10 @@ from scipy.spatial import ConvexHull
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = os.environ.get("URGYM_REFERENCE", "/root/reference")
-URDF = os.path.join(REF, "urgym/urdf/ur5_robotiq_85.urdf")
-OUT = os.path.join(ROOT, "tests", "golden", "urdf_model.json")
+# URGYM_MODEL_URDF=urgym/urdf/ur5_robotiq_140.urdf writes the UR5Robotiq140 fixture (urdf_model_r140.json)
+URDF_REL = os.environ.get("URGYM_MODEL_URDF", "urgym/urdf/ur5_robotiq_85.urdf")
+URDF = os.path.join(REF, URDF_REL)
+OUT = os.path.join(ROOT, "tests", "golden", "urdf_model_r140.json" if "140" in URDF_REL else "urdf_model.json")
 
 
 def fib_dirs(n=64):

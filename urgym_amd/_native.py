@@ -29,15 +29,21 @@ STAT_NAMES = ["unstable_waits", "split_substeps", "row_capacity_substeps", "mani
               "nonfinite_terminations", "substeps", "reserved6", "reserved7"]
 CONTACT_FIELDS = 24  # pybullet getContactPoints tuple, flattened
 
-_lib = None
+# robot.py's arm + gripper classes -> their build of the library (same sources, the robot's model header):
+# UR5Robotiq85 (every registered env) and UR5Robotiq140 (robot.py:221-240, liburgym_r140.so)
+ROBOT_LIBS = {"ur5_robotiq_85": LIB_PATH, "ur5_robotiq_140": os.path.join(_HERE, "_lib", "liburgym_r140.so")}
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError(f"liburgym.so not built ({LIB_PATH}); run __graft_entry__.build() -- no CPU fallback exists")
+def lib(robot="ur5_robotiq_85"):
+    if robot not in ROBOT_LIBS:
+        raise ValueError(f"robot must be one of {sorted(ROBOT_LIBS)}, not {robot!r}")
+    path = ROBOT_LIBS[robot]
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
+        raise RuntimeError(f"{os.path.basename(path)} not built ({path}); run __graft_entry__.build() -- "
+                           "no CPU fallback exists")
     # torch, when installed, is loaded first: it bundles its own HIP runtime, and importing it after this library
     # has initialised the /opt/rocm runtime leaves torch.cuda unavailable in the process (measured on MI355X,
     # tools/gpu_diag.sh); the other order works, and the device tensors / streams of vec.py need torch's side
@@ -45,7 +51,7 @@ def lib():
         import torch  # noqa: F401
     except Exception:  # pragma: no cover - torch is part of this image
         pass
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     P, I, D, U32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_uint32
     L.urgym_create.restype = P
     L.urgym_create.argtypes = [I, I, I, I, U32, I]
@@ -87,7 +93,7 @@ def lib():
     L.urgym_contact_points.argtypes = [P, I, I, I, I, I, P, P]
     L.urgym_camera_shot.argtypes = [P, I, I, P, P, I, I, I, P, P, P]
     L.urgym_camera_shot_device.argtypes = [P, I, I, P, P, I, I, I, P, P, P]
-    _lib = L
+    _libs[path] = L
     return L
 
 
@@ -98,9 +104,11 @@ def ptr(a):
 class Sim:
     """One handle = n_envs environments of one task on one GPU."""
 
-    def __init__(self, task, n_envs, device=0, seed=0, env_offset=0, flags=0):
-        """flags: 0 or GEOM_FULL = the full geometry (default), GEOM_LOD = the collision LOD"""
-        self.L = lib()
+    def __init__(self, task, n_envs, device=0, seed=0, env_offset=0, flags=0, robot="ur5_robotiq_85"):
+        """flags: 0 or GEOM_FULL = the full geometry (default), GEOM_LOD = the collision LOD; robot: the arm +
+        gripper (robot.py's UR5Robotiq85, every registered env's, or UR5Robotiq140)"""
+        self.L = lib(robot)
+        self.robot = robot
         self.task = task
         self.n = n_envs
         self.create_flags = flags

@@ -83,7 +83,11 @@ UG_CONST double UG_BX_DOOR_MASSES[4] = {0.1, 0.05, 0.05, 0.1};
 /* constraints are created in joint-id order (robot.py:202 iterates self.joints): links 11,13,14,16,18
  * = dofs 7,8,9,10,11; gearRatio = -multiplier (robot.py:196-200, 211) */
 UG_CONST int UG_GEAR_CHILD[5] = {7, 8, 9, 10, 11};
+#ifdef UG_ROBOT_R140 /* UR5Robotiq140.__post_load__ (robot.py:231-240): every multiplier's sign flipped */
+UG_CONST double UG_GEAR_RATIO[5] = {-1.0, 1.0, 1.0, -1.0, 1.0};
+#else
 UG_CONST double UG_GEAR_RATIO[5] = {1.0, -1.0, -1.0, 1.0, -1.0};
+#endif
 
 /* ---- task ids (urgym/envs/__init__.py) ---- */
 #define UG_TASK_BALLBALANCE 0

@@ -15,7 +15,11 @@
 #include <stdint.h>
 
 #define UG_CONST static __constant__ const
+#ifdef UG_ROBOT_R140 /* the UR5Robotiq140 build (liburgym_r140.so, robot.py:221-240) */
+#include "model_data_r140.h"
+#else
 #include "model_data.h"
+#endif
 #include "scene_data.h"
 #include "ug_detmath.h"
 #include "ug_joint.h"

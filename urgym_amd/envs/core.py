@@ -88,7 +88,8 @@ class URGymVectorEnv(_VecBase):
     """
 
     def __init__(self, task, num_envs, max_episode_steps=None, device=0, seed=0, env_offset=0,
-                 camera=None, reward_type="dense", render_mode="rgb_array", button_touch_mode=None):
+                 camera=None, reward_type="dense", render_mode="rgb_array", button_touch_mode=None,
+                 robot="ur5_robotiq_85"):
         from . import spaces_for
         _check_kwargs(camera, reward_type)
         _check_button(task, button_touch_mode)
@@ -96,7 +97,8 @@ class URGymVectorEnv(_VecBase):
         self.num_envs = num_envs
         self.single_observation_space, self.single_action_space = spaces_for(task)
         _init_vector_base(self, num_envs, self.single_observation_space, self.single_action_space)
-        self.sim = Sim(task, num_envs, device=device, seed=seed, env_offset=env_offset)
+        # robot: an extension (the reference's envs hard-code UR5Robotiq85); 'ur5_robotiq_140' = robot.py:221-240
+        self.sim = Sim(task, num_envs, device=device, seed=seed, env_offset=env_offset, robot=robot)
         self.sim.set_reward_type(reward_type)
         if task == 7:
             self.sim.set_button_mode(button_touch_mode or "any")
@@ -145,7 +147,7 @@ class URGymEnv(_EnvBase):
     gymnasium TimeLimit truncation the registry adds (urgym/envs/__init__.py)."""
 
     def __init__(self, task, max_episode_steps=None, device=0, seed=0, camera=None, reward_type="dense",
-                 render_mode="human", button_touch_mode=None):
+                 render_mode="human", button_touch_mode=None, robot="ur5_robotiq_85"):
         from . import spaces_for
         _check_kwargs(camera, reward_type)
         _check_button(task, button_touch_mode)
@@ -153,7 +155,7 @@ class URGymEnv(_EnvBase):
             _EnvBase.__init__(self)
         self.task = task
         self.observation_space, self.action_space = spaces_for(task)
-        self.sim = Sim(task, 1, device=device, seed=seed)
+        self.sim = Sim(task, 1, device=device, seed=seed, robot=robot)
         self.sim.set_reward_type(reward_type)
         if task == 7:
             self.sim.set_button_mode(button_touch_mode or "any")
