@@ -46,11 +46,13 @@ def cpu_model():
     return "unknown"
 
 
-def _oracle_sample(task, n, threads, seconds, flags=0):
+def _oracle_sample(task, n, threads, seconds, flags=0, robot="ur5_robotiq_85"):
     import ctypes
-    from oracle.pyoracle import OracleEnv, lib as olib
+    from oracle.pyoracle import LIB_PATH, LIB_PATH_R140, OracleEnv, lib
     from urgym_amd.envs import spaces_for
-    envs = [OracleEnv(task, 20241220 + i, flags=flags) for i in range(n)]
+    lib_path = LIB_PATH_R140 if robot == "ur5_robotiq_140" else LIB_PATH
+    olib = lambda: lib(lib_path)  # noqa: E731
+    envs = [OracleEnv(task, 20241220 + i, lib_path=lib_path, flags=flags) for i in range(n)]
     for e in envs:
         e.reset()
     arr = (ctypes.c_void_p * n)(*[e.h for e in envs])
@@ -71,15 +73,15 @@ def _oracle_sample(task, n, threads, seconds, flags=0):
     return steps, substeps, time.perf_counter() - t0
 
 
-def cpu_baseline(task, seconds=10.0, seconds_1core=5.0, flags=0):
+def cpu_baseline(task, seconds=10.0, seconds_1core=5.0, flags=0, robot="ur5_robotiq_85"):
     """CPU restatement (oracle/, test infrastructure) timed on this host's cores: bounded samples of the same
     workload (same task, random actions, autoreset) -- all cores with OpenMP (one env per thread at a time,
     4 envs per thread) and the 1-env / 1-core analogue of config A."""
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     os.environ["OMP_NUM_THREADS"] = str(threads)
     n = 4 * threads
-    steps, substeps, dt = _oracle_sample(task, n, threads, seconds, flags)
-    s1, sub1, dt1 = _oracle_sample(task, 1, 1, seconds_1core, flags)
+    steps, substeps, dt = _oracle_sample(task, n, threads, seconds, flags, robot)
+    s1, sub1, dt1 = _oracle_sample(task, 1, 1, seconds_1core, flags, robot)
     return {"value": steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(),
             "sample": f"{TASK_NAMES[task]} x {n} envs, {steps} env-steps incl. autoresets ({substeps} substeps) in "
@@ -142,6 +144,8 @@ def main(argv=None):
     ap.add_argument("--geometry", choices=("full", "lod"), default="full",
                     help="collision geometry: full (default: every vertex of PyBullet's mesh hulls, a true cylinder disc) "
                          "or lod (<= 48-vertex hulls, a 16-gon disc prism: URGYM_FLAG_LOD_GEOMETRY)")
+    ap.add_argument("--robot", choices=("ur5_robotiq_85", "ur5_robotiq_140"), default="ur5_robotiq_85",
+                    help="arm + gripper (robot.py): UR5Robotiq85 (every registered env; default) or UR5Robotiq140")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL over xGMI); gloo only to rehearse several ranks "
@@ -168,7 +172,7 @@ def main(argv=None):
     from urgym_amd._native import GEOM_LOD, Sim
     n = args.envs
     geom_flags = GEOM_LOD if args.geometry == "lod" else 0
-    sim = Sim(args.task, n, device=gpu, seed=20241220, env_offset=rank * n, flags=geom_flags)
+    sim = Sim(args.task, n, device=gpu, seed=20241220, env_offset=rank * n, flags=geom_flags, robot=args.robot)
     sim.set_autoreset(True, MAX_STEPS[args.task])
     sim.reset()
     A, O = sim.act_dim, sim.obs_dim
@@ -260,6 +264,8 @@ def main(argv=None):
     bytes_per_env = 2 * S + 4 * A + 8 * O * 2 + 8 + 3 + 4
     achieved_gbs = bytes_per_env * n / (avg_kernel_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args.task, n, args.geometry)
+    if args.robot != "ur5_robotiq_85":  # the PMC record and the work model were measured on the Robotiq-85 build
+        traffic, traffic_src = None, None
     if flops_per_launch is not None:
         tf = flops_per_launch / (avg_kernel_ms * 1e-3) / 1e12
         roof = {"bound": "fp64-valu", "achieved": tf, "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -292,14 +298,14 @@ def main(argv=None):
         "config": {"workload": f"{TASK_NAMES[args.task]} x {n} envs per GPU, autoreset, max_episode_steps "
                                f"{MAX_STEPS[args.task]}", "envs_per_gpu": n, "total_envs": n * world,
                    "parallelism": f"env-dp{world}", "world_size": world, "geometry": args.geometry,
-                   "backend": args.backend if world > 1 else None},
+                   "backend": args.backend if world > 1 else None, "robot": args.robot},
         "rep_values": [env_steps / x[0] for x in reps],
         "substeps_per_env_step": substeps / env_steps,
         "resets": int(resets),
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.task, args.cpu_seconds, flags=geom_flags)
+        line["cpu_baseline"] = cpu_baseline(args.task, args.cpu_seconds, flags=geom_flags, robot=args.robot)
     if rank == 0:
         print(json.dumps(line), flush=True)
     sim.close()
