@@ -2985,8 +2985,9 @@ int ugo_contact_points(const ugo_env* e, int bodyA, int bodyB, int linkA, int li
     return cnt;
 }
 /* Camera.shot() -> p.getCameraImage (utilities.py:84-89) restated as ray casting of the env's collision shapes
- * (ug_render.h, shared with the kernel): every pixel against every active collider in collider order, first
- * nearest hit kept.  rgba H x W x 4, depth H x W, seg H x W (each may be NULL).  Returns -1 for a singular P V. */
+ * (ug_render.h, shared with the kernel): every pixel against every active collider, the last collider first (statics
+ * and objects before the robot's hulls), nearest hit kept, ties to the lower collider index.  rgba H x W x 4,
+ * depth H x W, seg H x W (each may be NULL).  Returns -1 for a singular P V. */
 int ugo_camera(const ugo_env* e, const float* view16, const float* proj16, int W, int H, int flags, uint8_t* rgba,
                float* depth, int32_t* seg) {
     const scene* s = &e->sc;
@@ -2994,7 +2995,7 @@ int ugo_camera(const ugo_env* e, const float* view16, const float* proj16, int W
     if (ugr_setup(view16, proj16, &cam) != 0) return -1;
     kin k;
     fk(e->q, &k);
-    double R[MAXCOL][9], P[MAXCOL][3], rad[MAXCOL];
+    double R[MAXCOL][9], P[MAXCOL][3], rad[MAXCOL], box[MAXCOL][6];
     int on[MAXCOL];
     for (int ci = 0; ci < s->ncol; ci++) {
         const collider* c = &s->col[ci];
@@ -3003,6 +3004,7 @@ int ugo_camera(const ugo_env* e, const float* view16, const float* proj16, int W
         for (int m = 0; m < 9; m++) R[ci][m] = T.R.m[m];
         P[ci][0] = T.p.x; P[ci][1] = T.p.y; P[ci][2] = T.p.z;
         rad[ci] = ugr_radius(c->kind, c->half, UG_HULL_V + 3 * c->v0, c->nv);
+        ugr_hull_box(UG_HULL_V + 3 * c->v0, c->kind == UG_SHAPE_HULL ? c->nv : 0, box[ci]);
         on[ci] = collider_active(e, c) != 0;
     }
     for (int pix = 0; pix < W * H; pix++) {
@@ -3010,12 +3012,13 @@ int ugo_camera(const ugo_env* e, const float* view16, const float* proj16, int W
         ugr_ray(&cam, pix % W, pix / W, W, H, o, d);
         double best = UGR_MISS;
         int bc = -1;
-        for (int ci = 0; ci < s->ncol; ci++) {
+        for (int ci = s->ncol - 1; ci >= 0; ci--) {
             if (!on[ci]) continue;
             const collider* c = &s->col[ci];
             double nw[3];
-            const double t = ugr_shape(R[ci], P[ci], rad[ci], c->kind, c->half, UG_HULL_F + 4 * c->f0, c->nf, o, d, nw);
-            if (t < best) { best = t; bc = ci; nb[0] = nw[0]; nb[1] = nw[1]; nb[2] = nw[2]; }
+            const double t = ugr_shape(R[ci], P[ci], rad[ci], c->kind, c->half, UG_HULL_F + 4 * c->f0, c->nf, box[ci],
+                                       best, o, d, nw);
+            if (t < best || (t == best && t != UGR_MISS)) { best = t; bc = ci; nb[0] = nw[0]; nb[1] = nw[1]; nb[2] = nw[2]; }
         }
         const int ent = bc >= 0 ? s->col[bc].ent : -1, link = bc >= 0 ? link_of_collider(s, bc) : -1;
         unsigned char px[4];

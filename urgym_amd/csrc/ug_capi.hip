@@ -548,48 +548,59 @@ __global__ void __launch_bounds__(WAVE) k_contacts(const Scene* sc, const double
     count[i] = cnt;
 }
 
-// Camera.shot() for a range of envs (ug_render.h): block (tile of 64 pixels, env).  The block's lanes first pose
-// one collider each (fk + owner / shape frame, the same functions the physics uses) into LDS, then every lane
-// casts its pixel's ray against the env's active colliders in collider order (first nearest hit wins).
-__global__ void __launch_bounds__(WAVE) k_camera(const Scene* sc, const double* S, int env0, UgrCam cam, int W, int H,
+// Camera.shot() for a range of envs (ug_render.h), two launches.  k_camera_pose: block per env, lane per collider:
+// its world pose (fk + owner / shape frame, the same functions the physics uses), culling bounds and active flag
+// into a per-env record (CAM_REC doubles per collider).  k_camera: block = (8 x 8 pixel tile, env): the env's records
+// into LDS, then every lane casts its pixel's ray against the active colliders, statics and objects first (their
+// hits prune the robot's hulls behind them), keeping the nearest hit, ties to the lower collider index.
+#define CAM_REC 20 /* R 9, p 3, bounding radius, vertex box 6, active */
+__global__ void __launch_bounds__(WAVE) k_camera_pose(const Scene* sc, const double* S, int env0, double* rec) {
+    __shared__ Kin k; /* the env's frames, once (lane 0), read by every collider's lane */
+    const int lane = threadIdx.x;
+    const EnvState& e = *(const EnvState*)(S + (size_t)(env0 + (int)blockIdx.x) * UG_STATE_DIM);
+    if (lane == 0) fk(e.q, k);
+    __syncthreads();
+    if (lane >= sc->ncol) return;
+    const Collider& c = sc->col[lane];
+    const XF T = shape_xf(owner_xf(e, k, c.owner), c);
+    double* r = rec + ((size_t)blockIdx.x * MAXCOL + lane) * CAM_REC;
+    for (int m = 0; m < 9; m++) r[m] = T.R.m[m];
+    r[9] = T.p.x; r[10] = T.p.y; r[11] = T.p.z;
+    r[12] = ugr_radius(c.kind, c.half, UG_HULL_V + 3 * c.v0, c.nv);
+    ugr_hull_box(UG_HULL_V + 3 * c.v0, c.kind == UG_SHAPE_HULL ? c.nv : 0, r + 13);
+    r[19] = collider_active(e, c) ? 1.0 : 0.0;
+}
+__global__ void __launch_bounds__(WAVE) k_camera(const Scene* sc, const double* rec, UgrCam cam, int W, int H,
                                                  int flags, uint8_t* rgba, float* depth, int32_t* seg) {
-    __shared__ double sR[MAXCOL][9], sP[MAXCOL][3], sRad[MAXCOL];
-    __shared__ int sOn[MAXCOL];
+    __shared__ double sr[MAXCOL * CAM_REC];
     const int lane = threadIdx.x;
     const size_t img = blockIdx.y;
-    const EnvState& e = *(const EnvState*)(S + (size_t)(env0 + (int)img) * UG_STATE_DIM);
     const int nc = sc->ncol;
-    if (lane < nc) {
-        Kin k;
-        fk(e.q, k);
-        const Collider& c = sc->col[lane];
-        const XF T = shape_xf(owner_xf(e, k, c.owner), c);
-        for (int m = 0; m < 9; m++) sR[lane][m] = T.R.m[m];
-        sP[lane][0] = T.p.x; sP[lane][1] = T.p.y; sP[lane][2] = T.p.z;
-        sRad[lane] = ugr_radius(c.kind, c.half, UG_HULL_V + 3 * c.v0, c.nv);
-        sOn[lane] = collider_active(e, c);
-    }
+    const double* src = rec + img * MAXCOL * CAM_REC;
+    for (int i = lane; i < nc * CAM_REC; i += WAVE) sr[i] = src[i];
     __syncthreads();
-    const int pix = blockIdx.x * WAVE + lane;
-    if (pix >= W * H) return;
+    const int tw = (W + 7) / 8;
+    const int px = (blockIdx.x % tw) * 8 + (lane & 7), py = (blockIdx.x / tw) * 8 + (lane >> 3);
+    if (px >= W || py >= H) return;
     double o[3], d[3], nb[3] = {0.0, 0.0, 0.0};
-    ugr_ray(&cam, pix % W, pix / W, W, H, o, d);
+    ugr_ray(&cam, px, py, W, H, o, d);
     double best = UGR_MISS;
     int bc = -1;
-    for (int ci = 0; ci < nc; ci++) {
-        if (!sOn[ci]) continue;
+    for (int ci = nc - 1; ci >= 0; ci--) {
+        const double* r = sr + ci * CAM_REC;
+        if (r[19] == 0.0) continue;
         const Collider& c = sc->col[ci];
         double nw[3];
-        const double t = ugr_shape(sR[ci], sP[ci], sRad[ci], c.kind, c.half, UG_HULL_F + 4 * c.f0, c.nf, o, d, nw);
-        if (t < best) { best = t; bc = ci; nb[0] = nw[0]; nb[1] = nw[1]; nb[2] = nw[2]; }
+        const double t = ugr_shape(r, r + 9, r[12], c.kind, c.half, UG_HULL_F + 4 * c.f0, c.nf, r + 13, best, o, d, nw);
+        if (t < best || (t == best && t != UGR_MISS)) { best = t; bc = ci; nb[0] = nw[0]; nb[1] = nw[1]; nb[2] = nw[2]; }
     }
     const int ent = bc >= 0 ? sc->col[bc].ent : -1, link = bc >= 0 ? link_of_collider(sc, bc) : -1;
-    unsigned char px[4];
+    unsigned char pxl[4];
     float dp;
     int sg;
-    ugr_shade(&cam, sc->variant, best, nb, ent, link, flags, o, d, px, &dp, &sg);
-    const size_t at = img * (size_t)(W * H) + (size_t)pix;
-    if (rgba) { rgba[4 * at] = px[0]; rgba[4 * at + 1] = px[1]; rgba[4 * at + 2] = px[2]; rgba[4 * at + 3] = px[3]; }
+    ugr_shade(&cam, sc->variant, best, nb, ent, link, flags, o, d, pxl, &dp, &sg);
+    const size_t at = img * (size_t)(W * H) + (size_t)(py * W + px);
+    if (rgba) { rgba[4 * at] = pxl[0]; rgba[4 * at + 1] = pxl[1]; rgba[4 * at + 2] = pxl[2]; rgba[4 * at + 3] = pxl[3]; }
     if (depth) depth[at] = dp;
     if (seg) seg[at] = sg;
 }
@@ -619,6 +630,8 @@ struct urgym_handle {
     int autoreset = 0, max_steps = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
+    double* d_campose = nullptr; // k_camera_pose records (count x MAXCOL x CAM_REC), grown on demand
+    size_t campose_envs = 0;
     std::string err;
 };
 
@@ -747,7 +760,7 @@ void urgym_destroy(urgym_handle* h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     void* ptrs[] = {h->d_scene, h->d_state, h->d_ws, h->d_mt, h->d_elapsed, h->d_act, h->d_obs, h->d_final, h->d_rew,
                     h->d_draws, h->d_aux, h->d_term, h->d_trunc, h->d_succ, h->d_mask, h->d_sub, h->d_order, h->d_prio,
-                    h->d_stats, h->d_flags};
+                    h->d_stats, h->d_flags, h->d_campose};
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -987,15 +1000,32 @@ static int camera_args(urgym_handle* h, int env0, int count, const float* view16
     return 0;
 }
 
+static hipError_t camera_launch(urgym_handle* h, int env0, int count, const UgrCam& cam, int width, int height, int flags,
+                                uint8_t* d_rgba, float* d_depth, int32_t* d_seg) {
+    if ((size_t)count > h->campose_envs) {
+        if (h->d_campose) {
+            hipError_t e = hipStreamSynchronize(h->stream);
+            if (e == hipSuccess) e = hipFree(h->d_campose);
+            h->d_campose = nullptr;
+            h->campose_envs = 0;
+            if (e != hipSuccess) return e;
+        }
+        hipError_t e = hipMalloc(&h->d_campose, sizeof(double) * (size_t)count * MAXCOL * CAM_REC);
+        if (e != hipSuccess) return e;
+        h->campose_envs = (size_t)count;
+    }
+    k_camera_pose<<<count, WAVE, 0, h->stream>>>(h->d_scene, h->d_state, env0, h->d_campose);
+    dim3 grid((unsigned)(((width + 7) / 8) * ((height + 7) / 8)), (unsigned)count);
+    k_camera<<<grid, WAVE, 0, h->stream>>>(h->d_scene, h->d_campose, cam, width, height, flags, d_rgba, d_depth, d_seg);
+    return hipGetLastError();
+}
+
 int urgym_camera_shot_device(urgym_handle* h, int env0, int count, const float* view16, const float* proj16, int width,
                              int height, int flags, uint8_t* d_rgba, float* d_depth, int32_t* d_seg) {
     UgrCam cam;
     if (camera_args(h, env0, count, view16, proj16, width, height, &cam) != 0) return -1;
     HIPCHK(h, hipSetDevice(h->dev));
-    dim3 grid((unsigned)((width * height + WAVE - 1) / WAVE), (unsigned)count);
-    k_camera<<<grid, WAVE, 0, h->stream>>>(h->d_scene, h->d_state, env0, cam, width, height, flags, d_rgba, d_depth,
-                                           d_seg);
-    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, camera_launch(h, env0, count, cam, width, height, flags, d_rgba, d_depth, d_seg));
     return 0;
 }
 
@@ -1012,12 +1042,7 @@ int urgym_camera_shot(urgym_handle* h, int env0, int count, const float* view16,
     if (rgba) e = hipMalloc(&d_rgba, 4 * np);
     if (e == hipSuccess && depth) e = hipMalloc(&d_depth, sizeof(float) * np);
     if (e == hipSuccess && seg) e = hipMalloc(&d_seg, sizeof(int32_t) * np);
-    if (e == hipSuccess) {
-        dim3 grid((unsigned)((width * height + WAVE - 1) / WAVE), (unsigned)count);
-        k_camera<<<grid, WAVE, 0, h->stream>>>(h->d_scene, h->d_state, env0, cam, width, height, flags, d_rgba,
-                                               d_depth, d_seg);
-        e = hipGetLastError();
-    }
+    if (e == hipSuccess) e = camera_launch(h, env0, count, cam, width, height, flags, d_rgba, d_depth, d_seg);
     if (e == hipSuccess && rgba) e = hipMemcpyAsync(rgba, d_rgba, 4 * np, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess && depth) e = hipMemcpyAsync(depth, d_depth, sizeof(float) * np, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess && seg) e = hipMemcpyAsync(seg, d_seg, sizeof(int32_t) * np, hipMemcpyDeviceToHost, h->stream);

@@ -198,15 +198,37 @@ UG_HD unsigned char ugr_u8(double v) {
     return (unsigned char)(int)(c * 255.0 + 0.5);
 }
 
-/* one shape in world pose (R row-major, p): transforms the ray into the shape frame, bounding-sphere cull (radius
- * rad about the shape origin), the entry test; returns t or UGR_MISS, the normal in world axes */
+/* a ray's slab interval against an axis-aligned box lo..hi (shape frame): 0 when it misses it or the box lies
+ * entirely outside t in [0, tmax] */
+UG_HD int ugr_slab(const double o[3], const double d[3], const double* lo, const double* hi, double tmax) {
+    double t0 = 0.0, t1 = tmax;
+    for (int k = 0; k < 3; k++) {
+        if (d[k] == 0.0) {
+            if (o[k] < lo[k] || o[k] > hi[k]) return 0;
+            continue;
+        }
+        double a = (lo[k] - o[k]) / d[k], b = (hi[k] - o[k]) / d[k];
+        if (a > b) { const double t = a; a = b; b = t; }
+        if (a > t0) t0 = a;
+        if (b < t1) t1 = b;
+        if (t0 > t1) return 0;
+    }
+    return 1;
+}
+/* one shape in world pose (R row-major, p): transforms the ray into the shape frame; culls by the bounding sphere
+ * (radius rad about the shape origin) -- also when the sphere's entry lies beyond `best`, the nearest hit so far,
+ * which no point of the shape can then beat -- and, for a hull, by its vertices' box (box6: lo xyz, hi xyz);
+ * then the entry test.  Returns t or UGR_MISS, the normal in world axes. */
 UG_HD double ugr_shape(const double R[9], const double p[3], double rad, int kind, const double half[3],
-                       const double* F, int nf, const double o[3], const double d[3], double nw[3]) {
+                       const double* F, int nf, const double* box6, double best, const double o[3], const double d[3],
+                       double nw[3]) {
     const double q[3] = {o[0] - p[0], o[1] - p[1], o[2] - p[2]};
     const double dd = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
-    const double tc = ((q[0] * d[0] + q[1] * d[1]) + q[2] * d[2]) / dd;
-    const double e[3] = {q[0] - tc * d[0], q[1] - tc * d[1], q[2] - tc * d[2]};
-    if ((e[0] * e[0] + e[1] * e[1]) + e[2] * e[2] > rad * rad) return UGR_MISS;
+    const double tc = -((q[0] * d[0] + q[1] * d[1]) + q[2] * d[2]) / dd;
+    const double e[3] = {q[0] + tc * d[0], q[1] + tc * d[1], q[2] + tc * d[2]};
+    const double e2 = (e[0] * e[0] + e[1] * e[1]) + e[2] * e[2];
+    if (e2 > rad * rad) return UGR_MISS;
+    if (tc - ug_sqrt((rad * rad - e2) / dd) > best) return UGR_MISS;
     double os[3], ds[3], n[3];
     for (int k = 0; k < 3; k++) {
         os[k] = (R[k] * q[0] + R[3 + k] * q[1]) + R[6 + k] * q[2];
@@ -214,12 +236,22 @@ UG_HD double ugr_shape(const double R[9], const double p[3], double rad, int kin
     }
     double t;
     if (kind == 0) t = ugr_box(os, ds, half, n);
-    else if (kind == 1) t = ugr_hull(os, ds, F, nf, n);
+    else if (kind == 1) t = ugr_slab(os, ds, box6, box6 + 3, best < 1.0 ? best : 1.0) ? ugr_hull(os, ds, F, nf, n) : UGR_MISS;
     else if (kind == 2) t = ugr_sphere(os, ds, half[0], n);
     else t = ugr_cyl(os, ds, half[0], half[2], n);
     if (t == UGR_MISS || t > 1.0) return UGR_MISS;
     for (int k = 0; k < 3; k++) nw[k] = (R[3 * k] * n[0] + R[3 * k + 1] * n[1]) + R[3 * k + 2] * n[2];
     return t;
+}
+/* a hull's vertex box in its shape frame (box6: lo xyz, hi xyz) */
+UG_HD void ugr_hull_box(const double* V, int nv, double box6[6]) {
+    for (int k = 0; k < 3; k++) { box6[k] = UGR_MISS; box6[3 + k] = -UGR_MISS; }
+    for (int v = 0; v < nv; v++)
+        for (int k = 0; k < 3; k++) {
+            const double x = V[3 * v + k];
+            if (x < box6[k]) box6[k] = x;
+            if (x > box6[3 + k]) box6[3 + k] = x;
+        }
 }
 /* bounding radius of a shape about its origin (hull: its farthest vertex) */
 UG_HD double ugr_radius(int kind, const double half[3], const double* V, int nv) {
