@@ -132,3 +132,18 @@ def test_env_camera_hook(mods):
     env.step(acts(7, np.random.default_rng(0), 1)[0])
     assert env.camera_obs["depth"].shape == (cam.height, cam.width)
     env.close()
+
+
+def test_vector_env_camera_hook(mods):
+    """URGymVectorEnv with a camera: every env's images in one launch after reset and after each step
+    (CubesGrasp, env_cubes_grasp_v0.py:259-263), equal to the batched shot of the env's handle"""
+    Sim, Camera, OracleEnv = mods
+    from urgym_amd.envs import URGymVectorEnv
+    cam = cams(Camera)[2]
+    venv = URGymVectorEnv(2, 4, max_episode_steps=20, seed=9, camera=cam)
+    venv.reset()
+    assert venv.camera_obs["rgb"].shape == (4, cam.height, cam.width, 4)
+    venv.step(acts(2, np.random.default_rng(1), 4))
+    r, d, s = cam.shot_batch(venv.sim)
+    assert np.array_equal(venv.camera_obs["depth"], d) and np.array_equal(venv.camera_obs["seg"], s)
+    venv.close()
