@@ -41,7 +41,7 @@ def main():
     from urgym_amd.envs import spaces_for
     _, asp = spaces_for(a.task)
     sim.set_autoreset(True, 500)
-    buf = np.zeros(64, np.uint64)
+    buf = np.zeros(80, np.uint64)
     sim.reset()
     sim.sync()
     rc = sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
@@ -50,6 +50,11 @@ def main():
     print("reset (cycles per substep):", json.dumps({k: round(r[k] / max(r["substeps"], 1), 1) for k in NAMES}))
     print("reset, contact-free substeps:", json.dumps({"fraction": r["free_substeps"] / max(r["substeps"], 1),
           **{k + "_cycles": round(r[k] / max(r["free_substeps"], 1), 1) for k in NAMES[-15:-7]}}))
+    free_split = ["fk", "broadphase", "hull_narrowphase", "pr_lookup", "pr_narrow", "pr_manifold", "pr_store",
+                  "pairs", "overlap_pairs", "hull_pairs", "robot_dynamics", "lane0_ldl_objects", "enumerate",
+                  "unit_solves"]
+    print("reset, contact-free substeps' sub-phases (cycles or counts per substep):",
+          json.dumps({k: round(float(buf[64 + i]) / max(r["free_substeps"], 1), 1) for i, k in enumerate(free_split)}))
     rng = np.random.default_rng(1)
     for _ in range(a.steps):
         sim.step(rng.uniform(asp.low, asp.high, size=(a.envs, len(asp.low))).astype(np.float32))

@@ -1055,7 +1055,7 @@ int urgym_camera_shot(urgym_handle* h, int env0, int count, const float* view16,
 }
 
 // Phase cycle counters of the team kernels (only a -DUG_PROF build records them):
-// out16 receives the UG_NPROF (64) accumulators (ug_team.h PF_* / PC_*); reset != 0 zeroes them.
+// out16 receives the UG_NPROF (80) accumulators (ug_team.h PF_* / PC_*); reset != 0 zeroes them.
 // reset == 2 instead copies the last k_step's block timeline (UG_BT_MAX x 4 words: start / end s_memrealtime,
 // env, substeps | reset << 16), tools/timeline.py.
 int urgym_debug_prof(urgym_handle* h, unsigned long long* out16, int reset) {

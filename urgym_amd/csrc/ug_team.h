@@ -35,7 +35,7 @@ namespace ugd {
 #define TEAM 64
 typedef __attribute__((address_space(1))) const double gcdouble;
 typedef __attribute__((address_space(1))) double gdouble;
-#define UG_NPROF 64 /* phase accumulators of the -DUG_PROF build */
+#define UG_NPROF 80 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* a row's J and M^-1 J^T over the NVP = 32 dof slots (robot 12, objects 3 x 6, 2 zero pads) */
@@ -186,7 +186,14 @@ enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_
        PF_RDYN, PF_ENUM, PF_BROAD, PF_PAIRS, PF_HB_VERT, PF_HB_CORNER, PF_HB_REDUCE, PF_FK, PF_LDL, PF_UNIT, PF_ROWB, PF_RB1, PF_RB2, PF_RB3, PF_MFMA, PF_WARM, PF_SW_NC, PF_SW_CT, PF_SW_FIN, PF_SW_FPREP, PF_SW_FR,
        PF_SW_RES, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST, PC_CHUNKS, PC_NNC, PC_NN, PC_N64, PC_N80, PC_N96,
        PC_FREE, PF_FREE_COL, PF_FREE_DYN, PF_FREE_ROWS, PF_FREE_PGS, PF_FREE_INT,
-       PF_FREE_PSETUP, PF_FREE_PSWEEP, PF_FREE_PPOST, PF_PR_BB, PF_HS, PC_CYPAIR, PF_CY1, PF_CY2, PC_CYSV, PC_CYIT };
+       PF_FREE_PSETUP, PF_FREE_PSWEEP, PF_FREE_PPOST, PF_PR_BB, PF_HS, PC_CYPAIR, PF_CY1, PF_CY2, PC_CYSV, PC_CYIT,
+       /* the contact-free substeps' share of these sub-phase counters (UG_FREE_SPLIT below) */
+       PF_FREE_SUB0 = 64 };
+#define UG_FREE_SPLIT_N 14
+#ifdef UG_PROF
+__device__ static const int kFreeSplit[UG_FREE_SPLIT_N] = {PF_FK, PF_BROAD, PF_HULL, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST,
+                                                           PF_PAIRS, PC_OVL, PC_HULL, PF_RDYN, PF_LDL, PF_ENUM, PF_UNIT};
+#endif
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -1441,6 +1448,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         /* every pair's transforms and collider fields at once (lane per pair: one load latency for the pass),
          * then the hull pairs in pair order, each reading its record uniformly from LDS */
         int hk = 0;
+        bool certd = false; /* this lane's pair skipped by its separation certificate */
         if (lane < cn) {
             const int p = sh.ov[c0 + lane];
             const PairDef& P = s->pair[p];
@@ -1493,6 +1501,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
                 }
                 if (ok) {
                     hk = 0;
+                    certd = true;
                     sh.u.cand.n[lane] = 0;
                 }
             }
@@ -1517,6 +1526,12 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
             PROF_CNT(PC_HULL, 1);
         }
         PROF_ADD(PF_HULL, t_hull);
+        if (nold == 0 && ballot(lane < cn && !certd) == 0ull) {
+            /* every pair of the chunk certified separated and no manifold from the last substep: the stages below
+             * would find no candidate and no old point, and store nothing (the contact-free substeps of a reset) */
+            __builtin_amdgcn_wave_barrier();
+            continue;
+        }
         PROF_T0(t_pairs);
         /* lane per pair: remaining narrowphases, manifold update.  The working manifold (g_sh.pm[lane]) and the
          * candidate list (g_sh.u.cand.c[lane], where the hull pairs' candidates already are) live in LDS. */
@@ -3486,6 +3501,9 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
     EnvState& e = sh.e;
+#ifdef UG_PROF
+    unsigned long long fsnap = lane < UG_FREE_SPLIT_N ? sh.prof[kFreeSplit[lane]] : 0ull; /* lane i: counter i */
+#endif
     PROF_T0(t_col);
     serial_fk();
     __syncthreads();
@@ -3560,6 +3578,9 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
         PROF_CNT(PF_FREE_PGS, t_int - t_pgs);
         PROF_ADD(PF_FREE_INT, t_int);
     }
+    __syncthreads();
+    if (n == 12 && nnc == 12 && lane < UG_FREE_SPLIT_N) sh.prof[PF_FREE_SUB0 + lane] += sh.prof[kFreeSplit[lane]] - fsnap;
+    __syncthreads();
 #endif
 }
 
@@ -4112,7 +4133,7 @@ __device__ static void team_load(const double* S, const int* stats) {
         sh.bdepth[threadIdx.x] = body_depth(threadIdx.x);
     }
 #ifdef UG_PROF
-    if (threadIdx.x < UG_NPROF) sh.prof[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < UG_NPROF; i += TEAM) sh.prof[i] = 0;
 #endif
     __syncthreads();
 }
@@ -4120,7 +4141,7 @@ __device__ static void team_prof_flush() {
     Shared& sh = g_sh;
 #ifdef UG_PROF
     __syncthreads();
-    if (threadIdx.x < UG_NPROF) atomicAdd(&g_prof[threadIdx.x], sh.prof[threadIdx.x]);
+    for (int i = threadIdx.x; i < UG_NPROF; i += TEAM) atomicAdd(&g_prof[i], sh.prof[i]);
 #endif
 }
 /* BallBalance / TwoBalls reset predictor (scheduling only): ball i in the paddle frame -> the logit of "this
