@@ -248,6 +248,14 @@ typedef struct {
     int ent;          /* 0 robot, 1+i object i, 10+s static s */
     int link;         /* pybullet link index for robot colliders, -1 otherwise */
     int full;         /* full-geometry mode (URGYM_FLAG_FULL_GEOMETRY): hull pairs keep every candidate */
+    /* the convex-convex path (UG_CONTACT_GJK, ug_gjk_ref.h): Bullet's shape as GJK sees it */
+    v3 gimp;          /* box / cylinder implicit dimensions (outer minus margin) */
+    double gmargin;   /* getMargin(): box / hull / cylinder collision margin, sphere radius */
+    int gjkbox;       /* a convex mesh PyBullet holds as btConvexHullShape, kept here as its box (the Golf pitch): its
+                       * pairs take the convex-convex path whatever the other shape */
+    int compound;     /* the collision object's shape is a btCompoundShape (a URDF link whose collision frame is not its
+                       * inertial frame, a multi-shape body): btCompoundCollisionAlgorithm refreshes the child manifold
+                       * before the child narrowphase */
 } collider;
 
 typedef struct { int a, b; double thr, friction, restitution, rolling; } pairdef;
@@ -256,6 +264,7 @@ typedef struct {
     int task;    /* base task: scene and physics */
     int variant; /* the env id's task (a variant shares its base task's scene) */
     int full;    /* full-geometry mode: robot hulls with every vertex and face of the mesh's convex hull */
+    int gjk;     /* contact generation: 1 Bullet's convex-convex GJK / EPA (the default), 0 vertex-in-hull (UG_CONTACT_VIH) */
     double gravity;
     int nobj;
     double omass[MAXOBJ];
@@ -316,6 +325,23 @@ static double safe_margin(double hx, double hy, double hz) {
     return m < 0.04 ? m : 0.04;
 }
 
+/* Bullet's shape parameters for GJK: a box / cylinder keeps its implicit dimensions inside the margin
+ * (btBoxShape / btCylinderShape ctor + setMargin keep the outer extents); a sphere's margin is its radius.  The
+ * full-geometry cylinder (createCollisionShape(GEOM_CYLINDER) -> btCylinderShapeZ) carries the safe margin of its
+ * constructor, min(0.04, 0.1 min(r, h/2)) [ext]. */
+static void gjk_params(collider* c) {
+    c->gimp = V(0, 0, 0);
+    c->gmargin = c->margin;
+    if (c->kind == UG_SHAPE_SPHERE) c->gmargin = c->half[0];
+    else if (c->kind == UG_SHAPE_BOX) c->gimp = V(c->half[0] - c->margin, c->half[1] - c->margin, c->half[2] - c->margin);
+    else if (c->kind == UG_SHAPE_CYL) {
+        const double r = c->half[0], hh = c->half[2];
+        double m = 0.1 * (r < hh ? r : hh);
+        if (m > 0.04) m = 0.04;
+        c->gmargin = m;
+        c->gimp = V(r - m, r - m, hh - m);
+    }
+}
 static void add_pair(scene* s, int a, int b) {
     pairdef* p = &s->pair[s->npair++];
     p->a = a; p->b = b;
@@ -368,6 +394,10 @@ static void build_scene(scene* s, int variant, int flags) {
         c->ent = 0;
         c->link = l;
         c->full = s->full;
+        /* URDF2Bullet keeps a link's single collision shape bare only when its frame is the link's inertial frame
+         * (child transform identity); otherwise the link collides through a btCompoundShape [ext] */
+        c->compound = memcmp(c->R.m, c->aR.m, sizeof(c->R.m)) != 0 || c->P.x != c->aP.x || c->P.y != c->aP.y ||
+                      c->P.z != c->aP.z;
     }
     int nrobot = s->ncol;
     int statics[8], nstat = 0;
@@ -420,6 +450,7 @@ static void build_scene(scene* s, int variant, int flags) {
         c->P = V(0.0, 0.0, -UG_PLANE_HALF_Z); c->aP = c->P;
         c->disc = ug_sqrt(15.0 * 15.0 * 2.0 + 25.0) + 5.0;
         c->owner = -100; c->ent = 11;
+        c->compound = 1;
         statics[nstat++] = s->ncol++;
     }
     if (task == UG_TASK_GOLF) {
@@ -489,6 +520,7 @@ static void build_scene(scene* s, int variant, int flags) {
         c->P = V(0.0, 0.0, -0.5 - UG_PLANE_HALF_Z); c->aP = c->P;
         c->disc = ug_sqrt(15.0 * 15.0 * 2.0 + 25.0) + 5.0;
         c->owner = -100; c->ent = 11;
+        c->compound = 1;
         statics[nstat++] = s->ncol++;
     }
     if (task == UG_TASK_GOLF) {
@@ -498,6 +530,7 @@ static void build_scene(scene* s, int variant, int flags) {
                      UG_GF_PITCH_HZ + UG_URDF_MARGIN, UG_URDF_MARGIN, UG_DEFAULT_FRICTION);
         c->P = V(UG_GF_PITCH_X, UG_GF_PITCH_Y, UG_GF_PITCH_Z); c->aP = c->P;
         c->owner = -100; c->ent = 12;
+        c->gjkbox = 1; /* createCollisionShape(GEOM_MESH): a btConvexHullShape, so every pair is convex-convex */
         statics[nstat++] = s->ncol++;
     }
     if (task == UG_TASK_BOX) {
@@ -533,6 +566,7 @@ static void build_scene(scene* s, int variant, int flags) {
         c->P = V(B[0], B[1], B[2]); c->aP = c->P;
         c->disc = ddisc;
         c->owner = -2; c->ent = 1;
+        c->compound = 1; /* URDF_MERGE_FIXED_LINKS: door + h1 h2 h3 */
         s->ocol[0] = s->ncol++;
         for (int i = 0; i < 3; i++) {
             const double* H = &UG_BX_HANDLE[4 * i];
@@ -543,6 +577,7 @@ static void build_scene(scene* s, int variant, int flags) {
             if (i == 2) { q4 qh; ugj_box_h3_quat(&qh.x); c->R = qmat(qh); c->aR = c->R; }
             c->disc = ddisc;
             c->owner = -2; c->ent = 1;
+            c->compound = 1;
         }
         s->oncol[0] = 4;
         c = &s->col[s->ncol];
@@ -571,6 +606,7 @@ static void build_scene(scene* s, int variant, int flags) {
             c->P = V(UG_BX_WALL_POS[3 * w], UG_BX_WALL_POS[3 * w + 1] + by, UG_BX_WALL_POS[3 * w + 2]); c->aP = c->P;
             c->disc = wdisc;
             c->owner = -100; c->ent = 13;
+            c->compound = 1; /* the merged base: box1..box4 */
             statics[nstat++] = s->ncol++;
         }
         c = &s->col[s->ncol];
@@ -578,6 +614,7 @@ static void build_scene(scene* s, int variant, int flags) {
         c->P = V(0.0, by, -UG_PLANE_HALF_Z); c->aP = c->P;
         c->disc = ug_sqrt(15.0 * 15.0 * 2.0 + 25.0) + 5.0;
         c->owner = -100; c->ent = 11;
+        c->compound = 1;
         statics[nstat++] = s->ncol++;
     }
     for (int o = 0; o < s->nobj; o++)
@@ -608,6 +645,9 @@ static void build_scene(scene* s, int variant, int flags) {
                 if (task == UG_TASK_BOX && !(o == 1 && s->col[statics[t]].ent == 11)) continue;
                 add_pair(s, c, statics[t]);
             }
+    /* contact generation and each collider as the convex-convex path sees it (ug_gjk_ref.h) */
+    s->gjk = UG_CONTACT_IS_GJK(flags);
+    for (int i = 0; i < s->ncol; i++) gjk_params(&s->col[i]);
 }
 
 /* ======================================================================== */
@@ -819,6 +859,53 @@ static void cand_init(candlist* L, int cap) {
 }
 static void cand_add(candlist* L, v3 n, v3 pB, double d) {
     if (L->n < L->cap) { L->c[L->n].n = n; L->c[L->n].pB = pB; L->c[L->n].d = d; L->n++; }
+}
+
+#include "ug_gjk_ref.h"
+/* the convex-convex path (scene gjk): Bullet's GJK / EPA pair detector, one point per pair and call */
+static void gshape_of(const collider* c, gshape* g) {
+    g->kind = c->kind;
+    g->v = c->kind == UG_SHAPE_HULL ? &UG_HULL_V[3 * c->v0] : NULL;
+    g->nv = c->kind == UG_SHAPE_HULL ? c->nv : 0;
+    g->imp = c->gimp;
+    g->margin = c->gmargin;
+}
+/* pairs with a dedicated Bullet algorithm keep it: sphere-sphere, sphere-box (btSphereBoxCollisionAlgorithm),
+ * box-box (btBoxBoxCollisionAlgorithm); everything else is btConvexConvexAlgorithm */
+static int pair_is_gjk(const collider* A, const collider* B) {
+    if (A->gjkbox || B->gjkbox) return 1;
+    const int pa = A->kind == UG_SHAPE_SPHERE || A->kind == UG_SHAPE_BOX;
+    const int pb = B->kind == UG_SHAPE_SPHERE || B->kind == UG_SHAPE_BOX;
+    return !(pa && pb);
+}
+/* test hook: one convex-convex query on explicit shapes and poses (tests/test_gjk.py) */
+int ugo_gjk_pair(int kA, int v0A, int nvA, const double* impA, double mA, const double* RA, const double* pA, int kB, int v0B,
+                 int nvB, const double* impB, double mB, const double* RB, const double* pB, double thr, double* out) {
+    gshape A = {kA, kA == UG_SHAPE_HULL ? &UG_HULL_V[3 * v0A] : NULL, nvA, V(impA[0], impA[1], impA[2]), mA};
+    gshape B = {kB, kB == UG_SHAPE_HULL ? &UG_HULL_V[3 * v0B] : NULL, nvB, V(impB[0], impB[1], impB[2]), mB};
+    xf TA, TB;
+    TA.R = mload(RA); TA.p = V(pA[0], pA[1], pA[2]);
+    TB.R = mload(RB); TB.p = V(pB[0], pB[1], pB[2]);
+    v3 n, p;
+    double d;
+    if (!gjk_pair(&A, &TA, &B, &TB, thr, &n, &p, &d)) return 0;
+    out[0] = n.x; out[1] = n.y; out[2] = n.z;
+    out[3] = p.x; out[4] = p.y; out[5] = p.z;
+    out[6] = d;
+    return 1;
+}
+static void nc_gjk(const xf* TA, const collider* A, const xf* TB, const collider* B, double thr, candlist* out) {
+    gshape ga, gb;
+    gshape_of(A, &ga);
+    gshape_of(B, &gb);
+    v3 n, p;
+    double d;
+    if (A->kind == UG_SHAPE_SPHERE && B->kind != UG_SHAPE_SPHERE) {
+        /* the sphere-first pair order of this restatement: B is GJK's shape A, the result turned into (A, B) */
+        if (gjk_pair(&gb, TB, &ga, TA, thr, &n, &p, &d)) cand_add(out, vneg(n), vadd(p, vscale(n, d)), d);
+        return;
+    }
+    if (gjk_pair(&ga, TA, &gb, TB, thr, &n, &p, &d)) cand_add(out, n, p, d);
 }
 
 /* btSphereBoxCollisionAlgorithm::getSphereDistance [ext]: sphere A, box B */
@@ -1521,7 +1608,8 @@ static void collide(ugo_env* e, const kin* k) {
         xf TA = shape_xf(&O[a], A), TB = shape_xf(&O[b], B);
         candlist L;
         cand_init(&L, LOD_MAXCAND);
-        if (A->kind == UG_SHAPE_SPHERE && B->kind == UG_SHAPE_BOX) nc_sphere_box(&TA, A, &TB, B, P->thr, &L);
+        if (s->gjk && pair_is_gjk(A, B)) nc_gjk(&TA, A, &TB, B, P->thr, &L);
+        else if (A->kind == UG_SHAPE_SPHERE && B->kind == UG_SHAPE_BOX) nc_sphere_box(&TA, A, &TB, B, P->thr, &L);
         else if (A->kind == UG_SHAPE_SPHERE && B->kind == UG_SHAPE_SPHERE) nc_sphere_sphere(&TA, A, &TB, B, P->thr, &L);
         else if (A->kind == UG_SHAPE_BOX && B->kind == UG_SHAPE_BOX) nc_box_box(&TA, A, &TB, B, P->thr, &L);
         else if (A->kind == UG_SHAPE_HULL && B->kind == UG_SHAPE_BOX) nc_hull_box(&TA, A, &TB, B, P->thr, &L);
@@ -1562,7 +1650,10 @@ static void collide(ugo_env* e, const kin* k) {
             dprintf(2, "PAIR %d %d %d %d %d %d %.6f\n", p, a, b, A->kind, B->kind, L.n, dm);
         }
 #endif
-        /* manifold frames = owner frames */
+        /* manifold frames = owner frames.  A compound collision object refreshes its child manifolds before the
+         * child narrowphases (btCompoundCollisionAlgorithm::processCollision), then the child's own algorithm
+         * refreshes after its points (the convex-convex path; the vertex-in-hull mode keeps rounds 1-3's order) */
+        if (s->gjk && (A->compound || B->compound) && M.npts) manifold_refresh(&M, &O[a], &O[b], P->thr);
         for (int i = 0; i < L.n; i++) manifold_add(&M, &O[a], &O[b], &L.c[i], P->thr);
         if (M.npts) manifold_refresh(&M, &O[a], &O[b], P->thr);
         if (M.npts == 0) continue;

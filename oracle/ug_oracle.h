@@ -100,6 +100,11 @@ int ugo_g_gf_reward(const double* ball, const double* hole, const double* stick,
                     int touched, int sparse, double* r, int* term);
 void ugo_g_tb_balls(const double* paddle, const double* u4, double* b1, double* b2);
 int ugo_g_tb_reward(const float* a, const double* b1, const double* b2, double paddle_z, double* r);
+/* one convex-convex (GJK / EPA) query, Bullet's btGjkPairDetector (oracle/ug_gjk_ref.h): shapes kind (UG_SHAPE_*),
+ * hull vertex range, implicit dimensions, margin; poses R (row-major) + p; out = normal on B, point on B, distance.
+ * Returns 1 when a point is reported. */
+int ugo_gjk_pair(int kA, int v0A, int nvA, const double* impA, double mA, const double* RA, const double* pA, int kB, int v0B,
+                 int nvB, const double* impB, double mB, const double* RB, const double* pB, double thr, double* out);
 /* batched CPU baseline: n envs, OpenMP over envs; returns total substeps */
 long ugo_batch_step(ugo_env** envs, int n, const float* actions, double* obs, double* reward,
                     uint8_t* terminated, uint8_t* success, int32_t* substeps, int autoreset,

@@ -1,0 +1,48 @@
+/* gjk_host.cpp -- the kernels' convex-convex narrowphase (urgym_amd/csrc/ug_gjk.h) built for the host.
+ *
+ * TEST INFRASTRUCTURE: tests/test_gjk.py runs this build and the oracle's independent restatement
+ * (oracle/ug_gjk_ref.h) on the same shapes and poses and asserts bit-identical results, so arithmetic-order slips in
+ * the kernel header show up on the CPU before a GPU run.  The only piece that differs from the kernels is the hull
+ * support query: serial here (btVector3::maxDot's first maximum), a wave-parallel arg-max with the same tie rule there.
+ * Built by oracle/Makefile into oracle/_build/libgjk_host.so; never linked into the product.
+ */
+#define UGK_FN static inline
+#ifdef UG_ROBOT_R140
+#include "../urgym_amd/csrc/model_data_r140.h"
+#else
+#include "../urgym_amd/csrc/model_data.h"
+#endif
+#include "../urgym_amd/csrc/ug_gjk.h"
+
+UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
+    double best = -__builtin_inf();
+    int bi = 0;
+    for (int i = 0; i < nv; i++) {
+        const double* p = &UG_HULL_V[3 * (v0 + i)];
+        const double dd = p[0] * d.x + p[1] * d.y + p[2] * d.z;
+        if (dd > best) { best = dd; bi = i; }
+    }
+    const double* p = &UG_HULL_V[3 * (v0 + bi)];
+    return ugk::V3(p[0], p[1], p[2]);
+}
+
+static ugk::EpaMem g_epa;
+
+/* shape: kind, v0, nv, imp[3], margin; pose: R (row-major 9), p (3).  out: n[3], pB[3], d.  Returns 1 with a point. */
+extern "C" int ugk_host_pair(int kA, int v0A, int nvA, const double* impA, double mA, const double* RA, const double* pA,
+                             int kB, int v0B, int nvB, const double* impB, double mB, const double* RB, const double* pB,
+                             double thr, double* out) {
+    ugk::GShape A{kA, v0A, nvA, ugk::V3(impA[0], impA[1], impA[2]), mA};
+    ugk::GShape B{kB, v0B, nvB, ugk::V3(impB[0], impB[1], impB[2]), mB};
+    ugk::gx TA, TB;
+    for (int i = 0; i < 9; i++) { TA.R.m[i] = RA[i]; TB.R.m[i] = RB[i]; }
+    TA.p = ugk::V3(pA[0], pA[1], pA[2]);
+    TB.p = ugk::V3(pB[0], pB[1], pB[2]);
+    ugk::gv n, p;
+    double d;
+    if (!ugk::gjk_pair(&g_epa, A, TA, B, TB, thr, n, p, d)) return 0;
+    out[0] = n.x; out[1] = n.y; out[2] = n.z;
+    out[3] = p.x; out[4] = p.y; out[5] = p.z;
+    out[6] = d;
+    return 1;
+}

@@ -1,0 +1,1189 @@
+/* ug_gjk.h -- Bullet3's default convex-convex narrowphase as the kernels run it (one wavefront per pair).
+ *
+ * What it restates [ext, Bullet3; the CPU statement of the same algorithm is
+ * oracle/ug_gjk_ref.h, a separate implementation that the kernels match bit for bit]:
+ *   btGjkPairDetector::getClosestPointsNonVirtual (BT_USE_DOUBLE_PRECISION): a libccd-style intersection test of the
+ *   core shapes, the classic margin GJK over btVoronoiSimplexSolver, btGjkEpaPenetrationDepthSolver (btGjkEpa2's GJK +
+ *   EPA, 9 guess directions, ::Distance as fallback) when the cores intersect or the GJK degenerates, the
+ *   normal-direction fix, and the one point btConvexConvexAlgorithm hands to btManifoldResult::addContactPoint.
+ *
+ * How it runs on CDNA4: every lane of the env's wavefront executes the same (uniform) scalar chain, so the wave is
+ * one pair's solver; the only wave-parallel step is the hull support query (max-dot over up to 865 vertices), which
+ * the includer supplies as ugk_hull_support(v0, nv, d) (ug_team.h: lane-strided dot products + a DPP arg-max with
+ * the lowest index winning ties, as btVector3::maxDot's first maximum).  The common path (intersection test, Voronoi
+ * GJK, normal fix) keeps its small state in registers: every run-time index into the simplex arrays is an explicit
+ * select, so no private array is dynamically indexed.  The penetration path (btGjkEpa2 GJK + EPA:
+ * 132 support vertices, 256 faces, their lists) lives in the env's global workspace (EpaMem, L2-resident); EPA's
+ * recursive horizon walk (expand) runs on an explicit stack.
+ *
+ * The includer defines UGK_FN (the function qualifier: `__device__ static inline` in the kernels, `static inline` in
+ * tools/gjk_host.cpp, the host build that checks this file against the oracle on the CPU) and, after including it,
+ * ugk_hull_support (declared below).
+ */
+#ifndef UG_GJK_H
+#define UG_GJK_H
+
+#include "scene_data.h"
+#include "ug_detmath.h"
+
+namespace ugk {
+
+struct gv { double x, y, z; };
+struct gm { double m[9]; }; /* row-major */
+struct gx { gm R; gv p; };  /* rigid transform: x -> R x + p */
+
+UGK_FN gv V3(double x, double y, double z) { gv r; r.x = x; r.y = y; r.z = z; return r; }
+UGK_FN gv add(gv a, gv b) { return V3(a.x + b.x, a.y + b.y, a.z + b.z); }
+UGK_FN gv sub(gv a, gv b) { return V3(a.x - b.x, a.y - b.y, a.z - b.z); }
+UGK_FN gv scl(gv a, double s) { return V3(a.x * s, a.y * s, a.z * s); }
+UGK_FN gv neg(gv a) { return V3(-a.x, -a.y, -a.z); }
+UGK_FN double dot(gv a, gv b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+UGK_FN gv cross(gv a, gv b) { return V3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+UGK_FN double len(gv a) { return ug_sqrt(dot(a, a)); }
+UGK_FN gv mulinv(gv a, double l) { const double inv = 1.0 / l; return V3(a.x * inv, a.y * inv, a.z * inv); }
+UGK_FN gv mv(const gm& M, gv v) {
+    const double* m = M.m;
+    return V3(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[3] * v.x + m[4] * v.y + m[5] * v.z, m[6] * v.x + m[7] * v.y + m[8] * v.z);
+}
+UGK_FN gv mtv(const gm& M, gv v) {
+    const double* m = M.m;
+    return V3(m[0] * v.x + m[3] * v.y + m[6] * v.z, m[1] * v.x + m[4] * v.y + m[7] * v.z, m[2] * v.x + m[5] * v.y + m[8] * v.z);
+}
+UGK_FN gm mtm(const gm& A, const gm& B) {
+    gm C;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) C.m[3 * i + j] = A.m[i] * B.m[j] + A.m[3 + i] * B.m[3 + j] + A.m[6 + i] * B.m[6 + j];
+    return C;
+}
+UGK_FN gv xfa(const gx& T, gv x) { return add(mv(T.R, x), T.p); }
+UGK_FN bool veq(gv a, gv b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
+UGK_FN gv vsel(bool c, gv a, gv b) { return V3(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
+
+/* a convex shape as GJK sees it (kind: UG_SHAPE_*; imp: box / cylinder implicit dimensions; margin: getMargin) */
+struct GShape { int kind, v0, nv; gv imp; double margin; };
+
+} /* namespace ugk */
+
+/* the includer's hull support: the vertex of hull [v0, v0 + nv) with the first maximal dot product with d */
+UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d);
+
+namespace ugk {
+
+constexpr double kEps = 2.220446049250313e-16; /* SIMD_EPSILON */
+constexpr double kLarge = 1e30;                /* BT_LARGE_FLOAT */
+constexpr double kRelError2 = 1.0e-12;
+constexpr double kPenTol = 1.0e-12;
+constexpr double kEqVertex = (double)1e-12f;
+constexpr int kMaxIter = 1000;
+constexpr double kGjkMinDist = 1e-12, kGjkDupEps = 1e-12, kGjkAccuracy = 1e-12;
+constexpr int kGjkMaxIterations = 128;
+constexpr double kEpaAccuracy = 1e-12, kEpaPlaneEps = 0.00001;
+constexpr int kEpaMaxVertices = 128, kEpaMaxFaces = 256, kEpaMaxIterations = 255;
+
+/* localGetSupportVertexWithoutMarginNonVirtual */
+UGK_FN gv support0(const GShape& s, gv d) {
+    if (s.kind == UG_SHAPE_SPHERE) return V3(0.0, 0.0, 0.0);
+    if (s.kind == UG_SHAPE_BOX)
+        return V3(d.x >= 0.0 ? s.imp.x : -s.imp.x, d.y >= 0.0 ? s.imp.y : -s.imp.y, d.z >= 0.0 ? s.imp.z : -s.imp.z);
+    if (s.kind == UG_SHAPE_CYL) {
+        const double q = ug_sqrt(d.x * d.x + d.y * d.y);
+        const double z = d.z < 0.0 ? -s.imp.z : s.imp.z;
+        if (q != 0.0) {
+            const double k = s.imp.x / q;
+            return V3(d.x * k, d.y * k, z);
+        }
+        return V3(s.imp.x, 0.0, z);
+    }
+    return ugk_hull_support(s.v0, s.nv, d);
+}
+/* localGetSupportVertexNonVirtual */
+UGK_FN gv support(const GShape& s, gv d) {
+    gv n = d;
+    if (dot(n, n) < kEps * kEps) n = V3(-1.0, -1.0, -1.0);
+    n = mulinv(n, ug_sqrt(dot(n, n)));
+    const gv p = support0(s, n);
+    const double m = s.margin;
+    return V3(p.x + m * n.x, p.y + m * n.y, p.z + m * n.z);
+}
+
+/* ---------------- btVoronoiSimplexSolver (registers; run-time indices are explicit selects) ---------------- */
+enum { UA = 1, UB = 2, UC = 4, UD = 8 };
+struct Sub { gv closest; int used; double bc[4]; int degenerate; };
+UGK_FN void sub_reset(Sub& r) { r.degenerate = 0; r.bc[0] = r.bc[1] = r.bc[2] = r.bc[3] = 0.0; r.used = 0; }
+UGK_FN void sub_set(Sub& r, double a, double b, double c, double d) { r.bc[0] = a; r.bc[1] = b; r.bc[2] = c; r.bc[3] = d; }
+UGK_FN bool sub_valid(const Sub& r) { return r.bc[0] >= 0.0 && r.bc[1] >= 0.0 && r.bc[2] >= 0.0 && r.bc[3] >= 0.0; }
+
+struct Voronoi {
+    int n;
+    gv W[4], P[4], Q[4];
+    gv cP1, cP2, cV, lastW;
+    bool needsUpdate, validClosest;
+    Sub bc;
+};
+UGK_FN void vs_reset(Voronoi& s) {
+    s.validClosest = false;
+    s.n = 0;
+    s.needsUpdate = true;
+    s.lastW = V3(kLarge, kLarge, kLarge);
+    sub_reset(s.bc);
+}
+UGK_FN void vs_add(Voronoi& s, gv w, gv p, gv q) {
+    s.lastW = w;
+    s.needsUpdate = true;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const bool h = i == s.n;
+        s.W[i] = vsel(h, w, s.W[i]);
+        s.P[i] = vsel(h, p, s.P[i]);
+        s.Q[i] = vsel(h, q, s.Q[i]);
+    }
+    s.n++;
+}
+/* removeVertex(I): n--, slot I <- slot n (I a compile-time index, n a run-time one) */
+template <int I>
+UGK_FN void vs_remove(Voronoi& s) {
+    s.n--;
+    gv w = s.W[I], p = s.P[I], q = s.Q[I];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const bool h = j == s.n;
+        w = vsel(h, s.W[j], w);
+        p = vsel(h, s.P[j], p);
+        q = vsel(h, s.Q[j], q);
+    }
+    s.W[I] = w; s.P[I] = p; s.Q[I] = q;
+}
+UGK_FN void vs_reduce(Voronoi& s, int used) {
+    if (s.n >= 4 && !(used & UD)) vs_remove<3>(s);
+    if (s.n >= 3 && !(used & UC)) vs_remove<2>(s);
+    if (s.n >= 2 && !(used & UB)) vs_remove<1>(s);
+    if (s.n >= 1 && !(used & UA)) vs_remove<0>(s);
+}
+/* closestPtPointTriangle, p = the origin */
+UGK_FN void vs_tri(gv p, gv a, gv b, gv c, Sub& r) {
+    r.used = 0;
+    const gv ab = sub(b, a), ac = sub(c, a), ap = sub(p, a);
+    const double d1 = dot(ab, ap), d2 = dot(ac, ap);
+    if (d1 <= 0.0 && d2 <= 0.0) { r.closest = a; r.used = UA; sub_set(r, 1, 0, 0, 0); return; }
+    const gv bp = sub(p, b);
+    const double d3 = dot(ab, bp), d4 = dot(ac, bp);
+    if (d3 >= 0.0 && d4 <= d3) { r.closest = b; r.used = UB; sub_set(r, 0, 1, 0, 0); return; }
+    const double vc = d1 * d4 - d3 * d2;
+    if (vc <= 0.0 && d1 >= 0.0 && d3 <= 0.0) {
+        const double v = d1 / (d1 - d3);
+        r.closest = add(a, scl(ab, v));
+        r.used = UA | UB;
+        sub_set(r, 1 - v, v, 0, 0);
+        return;
+    }
+    const gv cp = sub(p, c);
+    const double d5 = dot(ab, cp), d6 = dot(ac, cp);
+    if (d6 >= 0.0 && d5 <= d6) { r.closest = c; r.used = UC; sub_set(r, 0, 0, 1, 0); return; }
+    const double vb = d5 * d2 - d1 * d6;
+    if (vb <= 0.0 && d2 >= 0.0 && d6 <= 0.0) {
+        const double w = d2 / (d2 - d6);
+        r.closest = add(a, scl(ac, w));
+        r.used = UA | UC;
+        sub_set(r, 1 - w, 0, w, 0);
+        return;
+    }
+    const double va = d3 * d6 - d5 * d4;
+    if (va <= 0.0 && (d4 - d3) >= 0.0 && (d5 - d6) >= 0.0) {
+        const double w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+        r.closest = add(b, scl(sub(c, b), w));
+        r.used = UB | UC;
+        sub_set(r, 0, 1 - w, w, 0);
+        return;
+    }
+    const double denom = 1.0 / (va + vb + vc);
+    const double v = vb * denom, w = vc * denom;
+    r.closest = add(add(a, scl(ab, v)), scl(ac, w));
+    r.used = UA | UB | UC;
+    sub_set(r, 1 - v - w, v, w, 0);
+}
+UGK_FN int vs_outside(gv p, gv a, gv b, gv c, gv d) {
+    const gv normal = cross(sub(b, a), sub(c, a));
+    const double signp = dot(sub(p, a), normal);
+    const double signd = dot(sub(d, a), normal);
+    if (signd * signd < (1e-8 * 1e-8)) return -1;
+    return signp * signd < 0.0;
+}
+/* closestPtPointTetrahedron: the candidate faces in Bullet's order, each relabelled into the tetrahedron's slots */
+UGK_FN bool vs_tet(gv p, gv a, gv b, gv c, gv d, Sub& fr) {
+    fr.closest = p;
+    fr.used = UA | UB | UC | UD;
+    const int oABC = vs_outside(p, a, b, c, d);
+    const int oACD = vs_outside(p, a, c, d, b);
+    const int oADB = vs_outside(p, a, d, b, c);
+    const int oBDC = vs_outside(p, b, d, c, a);
+    if (oABC < 0 || oACD < 0 || oADB < 0 || oBDC < 0) { fr.degenerate = 1; return false; }
+    if (!oABC && !oACD && !oADB && !oBDC) return false;
+    double best = 3.4028234663852886e+38; /* FLT_MAX */
+    Sub t;
+    if (oABC) {
+        vs_tri(p, a, b, c, t);
+        const double sq = dot(sub(t.closest, p), sub(t.closest, p));
+        if (sq < best) {
+            best = sq;
+            fr.closest = t.closest;
+            fr.used = t.used & (UA | UB | UC);
+            sub_set(fr, t.bc[0], t.bc[1], t.bc[2], 0);
+        }
+    }
+    if (oACD) {
+        vs_tri(p, a, c, d, t);
+        const double sq = dot(sub(t.closest, p), sub(t.closest, p));
+        if (sq < best) {
+            best = sq;
+            fr.closest = t.closest;
+            fr.used = ((t.used & UA) ? UA : 0) | ((t.used & UB) ? UC : 0) | ((t.used & UC) ? UD : 0);
+            sub_set(fr, t.bc[0], 0, t.bc[1], t.bc[2]);
+        }
+    }
+    if (oADB) {
+        vs_tri(p, a, d, b, t);
+        const double sq = dot(sub(t.closest, p), sub(t.closest, p));
+        if (sq < best) {
+            best = sq;
+            fr.closest = t.closest;
+            fr.used = ((t.used & UA) ? UA : 0) | ((t.used & UC) ? UB : 0) | ((t.used & UB) ? UD : 0);
+            sub_set(fr, t.bc[0], t.bc[2], 0, t.bc[1]);
+        }
+    }
+    if (oBDC) {
+        vs_tri(p, b, d, c, t);
+        const double sq = dot(sub(t.closest, p), sub(t.closest, p));
+        if (sq < best) {
+            best = sq;
+            fr.closest = t.closest;
+            fr.used = ((t.used & UA) ? UB : 0) | ((t.used & UC) ? UC : 0) | ((t.used & UB) ? UD : 0);
+            sub_set(fr, 0, t.bc[0], t.bc[2], t.bc[1]);
+        }
+    }
+    return true;
+}
+/* updateClosestVectorAndPoints */
+UGK_FN bool vs_update(Voronoi& s) {
+    if (!s.needsUpdate) return s.validClosest;
+    sub_reset(s.bc);
+    s.needsUpdate = false;
+    const gv O = V3(0.0, 0.0, 0.0);
+    if (s.n == 0) {
+        s.validClosest = false;
+    } else if (s.n == 1) {
+        s.cP1 = s.P[0];
+        s.cP2 = s.Q[0];
+        s.cV = sub(s.cP1, s.cP2);
+        sub_reset(s.bc);
+        sub_set(s.bc, 1.0, 0.0, 0.0, 0.0);
+        s.validClosest = sub_valid(s.bc);
+    } else if (s.n == 2) {
+        const gv from = s.W[0], to = s.W[1];
+        const gv diff = sub(O, from);
+        const gv v = sub(to, from);
+        double t = dot(v, diff);
+        if (t > 0) {
+            const double dotVV = dot(v, v);
+            if (t < dotVV) {
+                t /= dotVV;
+                s.bc.used |= UA | UB;
+            } else {
+                t = 1;
+                s.bc.used |= UB;
+            }
+        } else {
+            t = 0;
+            s.bc.used |= UA;
+        }
+        sub_set(s.bc, 1 - t, t, 0, 0);
+        s.cP1 = add(s.P[0], scl(sub(s.P[1], s.P[0]), t));
+        s.cP2 = add(s.Q[0], scl(sub(s.Q[1], s.Q[0]), t));
+        s.cV = sub(s.cP1, s.cP2);
+        vs_reduce(s, s.bc.used);
+        s.validClosest = sub_valid(s.bc);
+    } else if (s.n == 3) {
+        vs_tri(O, s.W[0], s.W[1], s.W[2], s.bc);
+        const double* b = s.bc.bc;
+        s.cP1 = add(add(scl(s.P[0], b[0]), scl(s.P[1], b[1])), scl(s.P[2], b[2]));
+        s.cP2 = add(add(scl(s.Q[0], b[0]), scl(s.Q[1], b[1])), scl(s.Q[2], b[2]));
+        s.cV = sub(s.cP1, s.cP2);
+        vs_reduce(s, s.bc.used);
+        s.validClosest = sub_valid(s.bc);
+    } else if (s.n == 4) {
+        if (vs_tet(O, s.W[0], s.W[1], s.W[2], s.W[3], s.bc)) {
+            const double* b = s.bc.bc;
+            s.cP1 = add(add(add(scl(s.P[0], b[0]), scl(s.P[1], b[1])), scl(s.P[2], b[2])), scl(s.P[3], b[3]));
+            s.cP2 = add(add(add(scl(s.Q[0], b[0]), scl(s.Q[1], b[1])), scl(s.Q[2], b[2])), scl(s.Q[3], b[3]));
+            s.cV = sub(s.cP1, s.cP2);
+            vs_reduce(s, s.bc.used);
+            s.validClosest = sub_valid(s.bc);
+        } else if (s.bc.degenerate) {
+            s.validClosest = false;
+        } else {
+            s.validClosest = true;
+            s.cV = V3(0.0, 0.0, 0.0);
+        }
+    } else {
+        s.validClosest = false;
+    }
+    return s.validClosest;
+}
+UGK_FN bool vs_in(const Voronoi& s, gv w) {
+    bool found = false;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const gv d = sub(w, s.W[i]);
+        found = found || (i < s.n && dot(d, d) <= kEqVertex);
+    }
+    return veq(w, s.lastW) || found;
+}
+
+/* ---------------- btGjkEpa2: GJK + EPA in the global workspace ---------------- */
+struct ESv { gv d, w; };
+struct EFace { gv n; double d; int c[3], f[3], l[2], e[3], pass; };
+struct EpaMem {
+    ESv sv[4 + kEpaMaxVertices]; /* [0, 4) the GJK's store, then the EPA's */
+    EFace fc[kEpaMaxFaces];
+    int sc[2][4];                /* the GJK's two simplices: vertex indices, weights, ranks */
+    double sp[2][4];
+    int srank[2];
+    int freev[4];
+    int stk[3 * kEpaMaxFaces];   /* expand()'s frames: face, edge, stage */
+};
+struct Mink { GShape s0, s1; gm toshape1; gx toshape0; bool margins; };
+UGK_FN gv mk_ls(const Mink& M, int i, gv d) {
+    const GShape& s = i ? M.s1 : M.s0;
+    return M.margins ? support(s, d) : support0(s, d);
+}
+UGK_FN gv mk_support0(const Mink& M, gv d) { return mk_ls(M, 0, d); }
+UGK_FN gv mk_support1(const Mink& M, gv d) { return xfa(M.toshape0, mk_ls(M, 1, mv(M.toshape1, d))); }
+UGK_FN gv mk_support(const Mink& M, gv d) { return sub(mk_support0(M, d), mk_support1(M, neg(d))); }
+UGK_FN void mk_init(Mink& M, const GShape& s0, const gx& w0, const GShape& s1, const gx& w1, bool margins) {
+    M.s0 = s0;
+    M.s1 = s1;
+    M.toshape1 = mtm(w1.R, w0.R);
+    M.toshape0.R = mtm(w0.R, w1.R);
+    M.toshape0.p = mtv(w0.R, sub(w1.p, w0.p));
+    M.margins = margins;
+}
+
+struct Gjk2 { /* btGjkEpa2's GJK: the scalar fields (the stores are in EpaMem) */
+    gv ray;
+    double distance;
+    int nfree, current, simplex, status;
+};
+enum { GJK_VALID = 0, GJK_INSIDE, GJK_FAILED };
+enum { EPA_VALID = 0, EPA_TOUCHING, EPA_DEGENERATED, EPA_NONCONVEX, EPA_INVALIDHULL, EPA_OUTOFFACES, EPA_OUTOFVERTICES,
+       EPA_ACCURACYREACHED, EPA_FALLBACK, EPA_FAILED };
+
+UGK_FN void g2_getsupport(EpaMem* E, const Mink& M, gv d, int sv) {
+    const gv dd = mulinv(d, len(d));
+    E->sv[sv].d = dd;
+    E->sv[sv].w = mk_support(M, dd);
+}
+UGK_FN void g2_remove(EpaMem* E, Gjk2& g, int s) { E->freev[g.nfree++] = E->sc[s][--E->srank[s]]; }
+UGK_FN void g2_append(EpaMem* E, Gjk2& g, const Mink& M, int s, gv v) {
+    const int r = E->srank[s];
+    E->sp[s][r] = 0;
+    E->sc[s][r] = E->freev[--g.nfree];
+    E->srank[s] = r + 1;
+    g2_getsupport(E, M, v, E->sc[s][r]);
+}
+UGK_FN double g2_det(gv a, gv b, gv c) {
+    return a.y * b.z * c.x + a.z * b.x * c.y - a.x * b.z * c.y - a.y * b.x * c.z + a.x * b.y * c.z - a.z * b.y * c.x;
+}
+UGK_FN double g2_proj2(gv a, gv b, double* w, int& m) {
+    const gv d = sub(b, a);
+    const double l = dot(d, d);
+    if (l > 0.0) {
+        const double t = l > 0 ? -dot(a, d) / l : 0;
+        if (t >= 1) { w[0] = 0; w[1] = 1; m = 2; return dot(b, b); }
+        if (t <= 0) { w[0] = 1; w[1] = 0; m = 1; return dot(a, a); }
+        w[1] = t;
+        w[0] = 1 - t;
+        m = 3;
+        const gv q = add(a, scl(d, t));
+        return dot(q, q);
+    }
+    return -1;
+}
+UGK_FN double g2_proj3(gv a, gv b, gv c, double* w, int& m) {
+    const gv vt[3] = {a, b, c};
+    const gv dl[3] = {sub(a, b), sub(b, c), sub(c, a)};
+    const gv n = cross(dl[0], dl[1]);
+    const double l = dot(n, n);
+    if (l > 0.0) {
+        double mindist = -1;
+        double subw[2] = {0.0, 0.0};
+        int subm = 0;
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            if (dot(vt[i], cross(dl[i], n)) > 0) {
+                const int j = i == 2 ? 0 : i + 1;
+                const double subd = g2_proj2(vt[i], vt[j], subw, subm);
+                if (mindist < 0 || subd < mindist) {
+                    mindist = subd;
+                    m = ((subm & 1) ? 1 << i : 0) + ((subm & 2) ? 1 << j : 0);
+                    w[i] = subw[0];
+                    w[j] = subw[1];
+                    w[j == 2 ? 0 : j + 1] = 0;
+                }
+            }
+        }
+        if (mindist < 0) {
+            const double d = dot(a, n);
+            const double s = ug_sqrt(l);
+            const gv p = scl(n, d / l);
+            mindist = dot(p, p);
+            m = 7;
+            w[0] = len(cross(dl[1], sub(b, p))) / s;
+            w[1] = len(cross(dl[2], sub(c, p))) / s;
+            w[2] = 1 - (w[0] + w[1]);
+        }
+        return mindist;
+    }
+    return -1;
+}
+UGK_FN double g2_proj4(gv a, gv b, gv c, gv d, double* w, int& m) {
+    const gv vt[4] = {a, b, c, d};
+    const gv dl[3] = {sub(a, d), sub(b, d), sub(c, d)};
+    const double vl = g2_det(dl[0], dl[1], dl[2]);
+    const bool ng = (vl * dot(a, cross(sub(b, c), sub(a, b)))) <= 0;
+    if (ng && ug_fabs(vl) > 0.0) {
+        double mindist = -1;
+        double subw[3] = {0.0, 0.0, 0.0};
+        int subm = 0;
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const int j = i == 2 ? 0 : i + 1;
+            const double s = vl * dot(d, cross(dl[i], dl[j]));
+            if (s > 0) {
+                const double subd = g2_proj3(vt[i], vt[j], d, subw, subm);
+                if (mindist < 0 || subd < mindist) {
+                    mindist = subd;
+                    m = ((subm & 1) ? 1 << i : 0) + ((subm & 2) ? 1 << j : 0) + ((subm & 4) ? 8 : 0);
+                    w[i] = subw[0];
+                    w[j] = subw[1];
+                    w[j == 2 ? 0 : j + 1] = 0;
+                    w[3] = subw[2];
+                }
+            }
+        }
+        if (mindist < 0) {
+            mindist = 0;
+            m = 15;
+            w[0] = g2_det(c, b, d) / vl;
+            w[1] = g2_det(a, c, d) / vl;
+            w[2] = g2_det(b, a, d) / vl;
+            w[3] = 1 - (w[0] + w[1] + w[2]);
+        }
+        return mindist;
+    }
+    return -1;
+}
+/* GJK::Evaluate */
+UGK_FN int g2_evaluate(EpaMem* E, Gjk2& g, const Mink& M, gv guess) {
+    int iterations = 0;
+    double sqdist = 0, alpha = 0;
+    gv lastw[4];
+    int clastw = 0;
+    for (int i = 0; i < 4; i++) E->freev[i] = i;
+    g.nfree = 4;
+    g.current = 0;
+    g.status = GJK_VALID;
+    g.distance = 0;
+    E->srank[0] = 0;
+    g.ray = guess;
+    const double sqrl = dot(g.ray, g.ray);
+    g2_append(E, g, M, 0, sqrl > 0 ? neg(g.ray) : V3(1, 0, 0));
+    E->sp[0][0] = 1;
+    g.ray = E->sv[E->sc[0][0]].w;
+    sqdist = sqrl;
+    lastw[0] = lastw[1] = lastw[2] = lastw[3] = g.ray;
+    do {
+        const int cs = g.current, ns = 1 - g.current;
+        const double rl = len(g.ray);
+        if (rl < kGjkMinDist) { g.status = GJK_INSIDE; break; }
+        g2_append(E, g, M, cs, neg(g.ray));
+        const gv w = E->sv[E->sc[cs][E->srank[cs] - 1]].w;
+        bool found = false;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const gv dd = sub(w, lastw[i]);
+            found = found || dot(dd, dd) < kGjkDupEps;
+        }
+        if (found) { g2_remove(E, g, cs); break; }
+        clastw = (clastw + 1) & 3;
+#pragma unroll
+        for (int i = 0; i < 4; i++) lastw[i] = vsel(i == clastw, w, lastw[i]);
+        const double omega = dot(g.ray, w) / rl;
+        alpha = omega > alpha ? omega : alpha;
+        if (((rl - alpha) - (kGjkAccuracy * rl)) <= 0) { g2_remove(E, g, cs); break; }
+        double weights[4];
+        int mask = 0;
+        const int rank = E->srank[cs];
+        const gv w0 = E->sv[E->sc[cs][0]].w, w1 = E->sv[E->sc[cs][1]].w;
+        if (rank == 2) sqdist = g2_proj2(w0, w1, weights, mask);
+        else if (rank == 3) sqdist = g2_proj3(w0, w1, E->sv[E->sc[cs][2]].w, weights, mask);
+        else if (rank == 4) sqdist = g2_proj4(w0, w1, E->sv[E->sc[cs][2]].w, E->sv[E->sc[cs][3]].w, weights, mask);
+        if (sqdist >= 0) {
+            E->srank[ns] = 0;
+            g.ray = V3(0, 0, 0);
+            g.current = ns;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                if (i >= rank) continue;
+                if (mask & (1 << i)) {
+                    const int r = E->srank[ns]++;
+                    E->sc[ns][r] = E->sc[cs][i];
+                    E->sp[ns][r] = weights[i];
+                    g.ray = add(g.ray, scl(E->sv[E->sc[cs][i]].w, weights[i]));
+                } else {
+                    E->freev[g.nfree++] = E->sc[cs][i];
+                }
+            }
+            if (mask == 15) g.status = GJK_INSIDE;
+        } else {
+            g2_remove(E, g, cs);
+            break;
+        }
+        g.status = (++iterations) < kGjkMaxIterations ? g.status : GJK_FAILED;
+    } while (g.status == GJK_VALID);
+    g.simplex = g.current;
+    if (g.status == GJK_VALID) g.distance = len(g.ray);
+    else if (g.status == GJK_INSIDE) g.distance = 0;
+    return g.status;
+}
+/* GJK::EncloseOrigin, its recursion unrolled by rank (rank r tries the simplices of rank r + 1) */
+UGK_FN gv g2_axis(int i) { return V3(i == 0 ? 1.0 : 0.0, i == 1 ? 1.0 : 0.0, i == 2 ? 1.0 : 0.0); }
+UGK_FN bool g2_enc4(EpaMem* E, const Gjk2& g) {
+    const int s = g.simplex;
+    const gv w3 = E->sv[E->sc[s][3]].w;
+    return ug_fabs(g2_det(sub(E->sv[E->sc[s][0]].w, w3), sub(E->sv[E->sc[s][1]].w, w3), sub(E->sv[E->sc[s][2]].w, w3))) > 0;
+}
+UGK_FN bool g2_enc3(EpaMem* E, Gjk2& g, const Mink& M) {
+    const int s = g.simplex;
+    const gv w0 = E->sv[E->sc[s][0]].w;
+    const gv n = cross(sub(E->sv[E->sc[s][1]].w, w0), sub(E->sv[E->sc[s][2]].w, w0));
+    if (dot(n, n) > 0) {
+        g2_append(E, g, M, s, n);
+        if (g2_enc4(E, g)) return true;
+        g2_remove(E, g, s);
+        g2_append(E, g, M, s, neg(n));
+        if (g2_enc4(E, g)) return true;
+        g2_remove(E, g, s);
+    }
+    return false;
+}
+UGK_FN bool g2_enc2(EpaMem* E, Gjk2& g, const Mink& M) {
+    const int s = g.simplex;
+    const gv d = sub(E->sv[E->sc[s][1]].w, E->sv[E->sc[s][0]].w);
+    for (int i = 0; i < 3; i++) {
+        const gv p = cross(d, g2_axis(i));
+        if (dot(p, p) > 0) {
+            g2_append(E, g, M, s, p);
+            if (g2_enc3(E, g, M)) return true;
+            g2_remove(E, g, s);
+            g2_append(E, g, M, s, neg(p));
+            if (g2_enc3(E, g, M)) return true;
+            g2_remove(E, g, s);
+        }
+    }
+    return false;
+}
+UGK_FN bool g2_enc1(EpaMem* E, Gjk2& g, const Mink& M) {
+    const int s = g.simplex;
+    for (int i = 0; i < 3; i++) {
+        const gv axis = g2_axis(i);
+        g2_append(E, g, M, s, axis);
+        if (g2_enc2(E, g, M)) return true;
+        g2_remove(E, g, s);
+        g2_append(E, g, M, s, neg(axis));
+        if (g2_enc2(E, g, M)) return true;
+        g2_remove(E, g, s);
+    }
+    return false;
+}
+UGK_FN bool g2_enclose(EpaMem* E, Gjk2& g, const Mink& M) {
+    const int r = E->srank[g.simplex];
+    if (r == 1) return g2_enc1(E, g, M);
+    if (r == 2) return g2_enc2(E, g, M);
+    if (r == 3) return g2_enc3(E, g, M);
+    if (r == 4) return g2_enc4(E, g);
+    return false;
+}
+
+struct Epa { int status, nextsv, hroot, hcount, sroot, scount; gv normal; double depth; int rc[3]; double rp[3]; int rrank; };
+UGK_FN void e_bind(EpaMem* E, int fa, int ea, int fb, int eb) {
+    E->fc[fa].e[ea] = eb; E->fc[fa].f[ea] = fb;
+    E->fc[fb].e[eb] = ea; E->fc[fb].f[eb] = fa;
+}
+UGK_FN void e_append(EpaMem* E, int& root, int& count, int f) {
+    E->fc[f].l[0] = -1;
+    E->fc[f].l[1] = root;
+    if (root >= 0) E->fc[root].l[0] = f;
+    root = f;
+    count++;
+}
+UGK_FN void e_remove(EpaMem* E, int& root, int& count, int f) {
+    const int l0 = E->fc[f].l[0], l1 = E->fc[f].l[1];
+    if (l1 >= 0) E->fc[l1].l[0] = l0;
+    if (l0 >= 0) E->fc[l0].l[1] = l1;
+    if (f == root) root = l1;
+    count--;
+}
+UGK_FN bool e_edgedist(EpaMem* E, gv fn, int a, int b, double& dist) {
+    const gv aw = E->sv[a].w, bw = E->sv[b].w;
+    const gv ba = sub(bw, aw);
+    const gv n_ab = cross(ba, fn);
+    if (dot(aw, n_ab) < 0) {
+        const double ba_l2 = dot(ba, ba);
+        const double a_dot_ba = dot(aw, ba);
+        const double b_dot_ba = dot(bw, ba);
+        if (a_dot_ba > 0) dist = len(aw);
+        else if (b_dot_ba < 0) dist = len(bw);
+        else {
+            const double a_dot_b = dot(aw, bw);
+            const double x = (dot(aw, aw) * dot(bw, bw) - a_dot_b * a_dot_b) / ba_l2;
+            dist = ug_sqrt(x > 0 ? x : 0);
+        }
+        return true;
+    }
+    return false;
+}
+UGK_FN int e_newface(EpaMem* E, Epa& P, int a, int b, int c, bool forced) {
+    if (P.sroot >= 0) {
+        const int f = P.sroot;
+        e_remove(E, P.sroot, P.scount, f);
+        e_append(E, P.hroot, P.hcount, f);
+        EFace& F = E->fc[f];
+        F.pass = 0;
+        F.c[0] = a; F.c[1] = b; F.c[2] = c;
+        const gv n = cross(sub(E->sv[b].w, E->sv[a].w), sub(E->sv[c].w, E->sv[a].w));
+        const double l = len(n);
+        if (l > kEpaAccuracy) {
+            double d;
+            if (!(e_edgedist(E, n, a, b, d) || e_edgedist(E, n, b, c, d) || e_edgedist(E, n, c, a, d)))
+                d = dot(E->sv[a].w, n) / l;
+            F.d = d;
+            F.n = mulinv(n, l);
+            if (forced || d >= -kEpaPlaneEps) return f;
+            P.status = EPA_NONCONVEX;
+        } else {
+            F.n = n;
+            P.status = EPA_DEGENERATED;
+        }
+        e_remove(E, P.hroot, P.hcount, f);
+        e_append(E, P.sroot, P.scount, f);
+        return -1;
+    }
+    P.status = P.sroot >= 0 ? EPA_OUTOFVERTICES : EPA_OUTOFFACES;
+    return -1;
+}
+UGK_FN int e_findbest(EpaMem* E, const Epa& P) {
+    int minf = P.hroot;
+    double mind = E->fc[minf].d * E->fc[minf].d;
+    for (int f = E->fc[minf].l[1]; f >= 0; f = E->fc[f].l[1]) {
+        const double sqd = E->fc[f].d * E->fc[f].d;
+        if (sqd < mind) { minf = f; mind = sqd; }
+    }
+    return minf;
+}
+/* EPA::expand as an explicit depth-first walk: frame (face, edge, stage); stage 0 = entry, 1 = the first neighbour's
+ * answer is in r, 2 = the second's.  The same visits, face allocations and list operations as the recursion. */
+UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, int f0, int e0, int& hcf, int& hff, int& hnf) {
+    int sp = 0;
+    bool r = false;
+    E->stk[0] = f0; E->stk[1] = e0; E->stk[2] = 0;
+    sp = 1;
+    while (sp > 0) {
+        int* fr = &E->stk[3 * (sp - 1)];
+        const int f = fr[0], e = fr[1], stage = fr[2];
+        const int e1 = e == 2 ? 0 : e + 1, e2 = e == 0 ? 2 : e - 1;
+        if (stage == 0) {
+            if (E->fc[f].pass == pass) { r = false; sp--; continue; }
+            if ((dot(E->fc[f].n, E->sv[w].w) - E->fc[f].d) < -kEpaPlaneEps) {
+                const int nf = e_newface(E, P, E->fc[f].c[e1], E->fc[f].c[e], w, false);
+                r = false;
+                if (nf >= 0) {
+                    e_bind(E, nf, 0, f, e);
+                    if (hcf >= 0) e_bind(E, hcf, 1, nf, 2);
+                    else hff = nf;
+                    hcf = nf;
+                    hnf++;
+                    r = true;
+                }
+                sp--;
+                continue;
+            }
+            E->fc[f].pass = pass;
+            fr[2] = 1;
+            int* ch = &E->stk[3 * sp];
+            ch[0] = E->fc[f].f[e1]; ch[1] = E->fc[f].e[e1]; ch[2] = 0;
+            sp++;
+            continue;
+        }
+        if (stage == 1) {
+            if (!r) { sp--; continue; }
+            fr[2] = 2;
+            int* ch = &E->stk[3 * sp];
+            ch[0] = E->fc[f].f[e2]; ch[1] = E->fc[f].e[e2]; ch[2] = 0;
+            sp++;
+            continue;
+        }
+        if (r) {
+            e_remove(E, P.hroot, P.hcount, f);
+            e_append(E, P.sroot, P.scount, f);
+        }
+        sp--;
+    }
+    return r;
+}
+/* EPA::Evaluate */
+UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
+    const int s = g.simplex;
+    if (E->srank[s] > 1 && g2_enclose(E, g, M)) {
+        while (P.hroot >= 0) {
+            const int f = P.hroot;
+            e_remove(E, P.hroot, P.hcount, f);
+            e_append(E, P.sroot, P.scount, f);
+        }
+        P.status = EPA_VALID;
+        P.nextsv = 0;
+        int* c = E->sc[s];
+        {
+            const gv w3 = E->sv[c[3]].w;
+            if (g2_det(sub(E->sv[c[0]].w, w3), sub(E->sv[c[1]].w, w3), sub(E->sv[c[2]].w, w3)) < 0) {
+                const int t = c[0]; c[0] = c[1]; c[1] = t;
+                const double tp = E->sp[s][0]; E->sp[s][0] = E->sp[s][1]; E->sp[s][1] = tp;
+            }
+        }
+        int tetra[4];
+        tetra[0] = e_newface(E, P, c[0], c[1], c[2], true);
+        tetra[1] = e_newface(E, P, c[1], c[0], c[3], true);
+        tetra[2] = e_newface(E, P, c[2], c[1], c[3], true);
+        tetra[3] = e_newface(E, P, c[0], c[2], c[3], true);
+        if (P.hcount == 4) {
+            int best = e_findbest(E, P);
+            EFace outer = E->fc[best];
+            int pass = 0;
+            e_bind(E, tetra[0], 0, tetra[1], 0);
+            e_bind(E, tetra[0], 1, tetra[2], 0);
+            e_bind(E, tetra[0], 2, tetra[3], 0);
+            e_bind(E, tetra[1], 1, tetra[3], 2);
+            e_bind(E, tetra[1], 2, tetra[2], 1);
+            e_bind(E, tetra[2], 2, tetra[3], 1);
+            P.status = EPA_VALID;
+            for (int it = 0; it < kEpaMaxIterations; it++) {
+                if (P.nextsv >= kEpaMaxVertices) { P.status = EPA_OUTOFVERTICES; break; }
+                int hcf = -1, hff = -1, hnf = 0;
+                const int w = 4 + P.nextsv++;
+                bool valid = true;
+                E->fc[best].pass = ++pass;
+                g2_getsupport(E, M, E->fc[best].n, w);
+                const double wdist = dot(E->fc[best].n, E->sv[w].w) - E->fc[best].d;
+                if (!(wdist > kEpaAccuracy)) { P.status = EPA_ACCURACYREACHED; break; }
+                for (int j = 0; j < 3 && valid; j++)
+                    valid = e_expand(E, P, pass, w, E->fc[best].f[j], E->fc[best].e[j], hcf, hff, hnf) && valid;
+                if (!(valid && hnf >= 3)) { P.status = EPA_INVALIDHULL; break; }
+                e_bind(E, hcf, 1, hff, 2);
+                e_remove(E, P.hroot, P.hcount, best);
+                e_append(E, P.sroot, P.scount, best);
+                best = e_findbest(E, P);
+                outer = E->fc[best];
+            }
+            const gv projection = scl(outer.n, outer.d);
+            P.normal = outer.n;
+            P.depth = outer.d;
+            P.rrank = 3;
+            P.rc[0] = outer.c[0]; P.rc[1] = outer.c[1]; P.rc[2] = outer.c[2];
+            const gv a = sub(E->sv[outer.c[0]].w, projection), b = sub(E->sv[outer.c[1]].w, projection),
+                     cc = sub(E->sv[outer.c[2]].w, projection);
+            P.rp[0] = len(cross(b, cc));
+            P.rp[1] = len(cross(cc, a));
+            P.rp[2] = len(cross(a, b));
+            const double sum = P.rp[0] + P.rp[1] + P.rp[2];
+            P.rp[0] /= sum;
+            P.rp[1] /= sum;
+            P.rp[2] /= sum;
+            return P.status;
+        }
+    }
+    P.status = EPA_FALLBACK;
+    P.normal = neg(guess);
+    const double nl = len(P.normal);
+    P.normal = nl > 0 ? mulinv(P.normal, nl) : V3(1, 0, 0);
+    P.depth = 0;
+    P.rrank = 1;
+    P.rc[0] = E->sc[s][0];
+    P.rp[0] = 1;
+    return P.status;
+}
+UGK_FN void e_init(EpaMem* E, Epa& P) {
+    P.status = EPA_FAILED;
+    P.normal = V3(0, 0, 0);
+    P.depth = 0;
+    P.nextsv = 0;
+    P.hroot = P.sroot = -1;
+    P.hcount = P.scount = 0;
+    for (int i = 0; i < kEpaMaxFaces; i++) e_append(E, P.sroot, P.scount, kEpaMaxFaces - i - 1);
+}
+struct Res { gv w0, w1, normal; double distance; };
+UGK_FN bool g2_penetration(EpaMem* E, const GShape& s0, const gx& w0, const GShape& s1, const gx& w1, gv guess, Res& r) {
+    Mink M;
+    mk_init(M, s0, w0, s1, w1, true);
+    Gjk2 g;
+    if (g2_evaluate(E, g, M, neg(guess)) == GJK_INSIDE) {
+        Epa P;
+        e_init(E, P);
+        if (e_evaluate(E, P, g, M, neg(guess)) != EPA_FAILED) {
+            gv a = V3(0, 0, 0);
+            for (int i = 0; i < P.rrank; i++) a = add(a, scl(mk_support0(M, E->sv[P.rc[i]].d), P.rp[i]));
+            r.w0 = xfa(w0, a);
+            r.w1 = xfa(w0, sub(a, scl(P.normal, P.depth)));
+            r.normal = neg(P.normal);
+            r.distance = -P.depth;
+            return true;
+        }
+    }
+    return false;
+}
+UGK_FN bool g2_distance(EpaMem* E, const GShape& s0, const gx& w0, const GShape& s1, const gx& w1, gv guess, Res& r) {
+    Mink M;
+    mk_init(M, s0, w0, s1, w1, false);
+    Gjk2 g;
+    if (g2_evaluate(E, g, M, guess) == GJK_VALID) {
+        gv a = V3(0, 0, 0), b = V3(0, 0, 0);
+        const int s = g.simplex;
+        for (int i = 0; i < E->srank[s]; i++) {
+            const double p = E->sp[s][i];
+            const gv d = E->sv[E->sc[s][i]].d;
+            a = add(a, scl(mk_support0(M, d), p));
+            b = add(b, scl(mk_support1(M, neg(d)), p));
+        }
+        r.w0 = xfa(w0, a);
+        r.w1 = xfa(w0, b);
+        r.normal = sub(a, b);
+        r.distance = len(r.normal);
+        r.normal = mulinv(r.normal, r.distance > kGjkMinDist ? r.distance : 1);
+        return true;
+    }
+    return false;
+}
+UGK_FN gv safe_normalize(gv d) {
+    const double l2 = dot(d, d);
+    return l2 >= kEps * kEps ? mulinv(d, ug_sqrt(l2)) : V3(1, 0, 0);
+}
+/* btGjkEpaPenetrationDepthSolver::calcPenDepth */
+UGK_FN bool calc_pen_depth(EpaMem* E, const GShape& A, const GShape& B, const gx& TA, const gx& TB, gv& v, gv& wA, gv& wB) {
+    for (int i = 0; i < 9; i++) {
+        gv guess;
+        if (i == 0) guess = safe_normalize(sub(TB.p, TA.p));
+        else if (i == 1) guess = safe_normalize(sub(TA.p, TB.p));
+        else if (i == 2) guess = V3(0, 0, 1);
+        else if (i == 3) guess = V3(0, 1, 0);
+        else if (i == 4) guess = V3(1, 0, 0);
+        else if (i == 5) guess = V3(1, 1, 0);
+        else if (i == 6) guess = V3(1, 1, 1);
+        else if (i == 7) guess = V3(0, 1, 1);
+        else guess = V3(1, 0, 1);
+        Res r;
+        if (g2_penetration(E, A, TA, B, TB, guess, r)) { wA = r.w0; wB = r.w1; v = r.normal; return true; }
+        if (g2_distance(E, A, TA, B, TB, guess, r)) { wA = r.w0; wB = r.w1; v = r.normal; return false; }
+    }
+    wA = wB = v = V3(0, 0, 0);
+    return false;
+}
+
+/* ---------------- btGjkPairDetector: the libccd intersection test ---------------- */
+UGK_FN bool fuzzy0(double x) { return ug_fabs(x) < kEps; }
+UGK_FN bool ccd_eq(double a_, double b_) {
+    const double ab = a_ - b_;
+    if (ug_fabs(ab) < kEps) return true;
+    const double a = ug_fabs(a_), b = ug_fabs(b_);
+    return b > a ? ug_fabs(ab) < kEps * b : ug_fabs(ab) < kEps * a;
+}
+UGK_FN int ccd_sign(double v) { return fuzzy0(v) ? 0 : (v < 0.0 ? -1 : 1); }
+UGK_FN bool ccd_veq(gv a, gv b) { return ccd_eq(a.x, b.x) && ccd_eq(a.y, b.y) && ccd_eq(a.z, b.z); }
+UGK_FN gv neg1(gv a) { return V3(a.x * -1.0, a.y * -1.0, a.z * -1.0); }
+UGK_FN gv triple(gv a, gv b, gv c) { return cross(cross(a, b), c); }
+UGK_FN double seg_dist2(gv P, gv x0, gv b, bool witness) {
+    const gv d = sub(b, x0);
+    const gv a = sub(x0, P);
+    double t = -1.0 * dot(a, d);
+    t /= dot(d, d);
+    if (t < 0.0 || fuzzy0(t)) { const gv q = sub(x0, P); return dot(q, q); }
+    if (t > 1.0 || ccd_eq(t, 1.0)) { const gv q = sub(b, P); return dot(q, q); }
+    if (witness) {
+        gv wv = V3(d.x * t, d.y * t, d.z * t);
+        wv = V3(wv.x + x0.x, wv.y + x0.y, wv.z + x0.z);
+        const gv q = sub(wv, P);
+        return dot(q, q);
+    }
+    gv dd = V3(d.x * t, d.y * t, d.z * t);
+    dd = V3(dd.x + a.x, dd.y + a.y, dd.z + a.z);
+    return dot(dd, dd);
+}
+UGK_FN double tri_dist2(gv P, gv x0, gv B, gv C) {
+    const gv d1 = sub(B, x0), d2 = sub(C, x0), a = sub(x0, P);
+    const double u = dot(a, a), v = dot(d1, d1), w = dot(d2, d2);
+    const double p = dot(a, d1), q = dot(a, d2), r = dot(d1, d2);
+    const double s = (q * r - w * p) / (w * v - r * r);
+    const double t = (-s * r - q) / w;
+    if ((fuzzy0(s) || s > 0.0) && (ccd_eq(s, 1.0) || s < 1.0) && (fuzzy0(t) || t > 0.0) && (ccd_eq(t, 1.0) || t < 1.0) &&
+        (ccd_eq(t + s, 1.0) || t + s < 1.0)) {
+        double dist = s * s * v;
+        dist += t * t * w;
+        dist += 2.0 * s * t * r;
+        dist += 2.0 * s * p;
+        dist += 2.0 * t * q;
+        dist += u;
+        return dist;
+    }
+    double dist = seg_dist2(P, x0, B, false);
+    double dist2 = seg_dist2(P, x0, C, true);
+    if (dist2 < dist) dist = dist2;
+    dist2 = seg_dist2(P, B, C, true);
+    if (dist2 < dist) dist = dist2;
+    return dist;
+}
+/* libccd's simplex: the points ps0..ps3 (registers), n = size; every update below names its slots explicitly */
+struct Ccd { gv p0, p1, p2, p3; int n; };
+UGK_FN int ccd_do3(Ccd& s, gv A, gv& dir) { /* size 3: A = p2, B = p1, C = p0 */
+    const gv B = s.p1, C = s.p0;
+    if (fuzzy0(tri_dist2(V3(0.0, 0.0, 0.0), A, B, C))) return 1;
+    if (ccd_veq(A, B) || ccd_veq(A, C)) return -1;
+    const gv AO = neg1(A);
+    const gv AB = sub(B, A), AC = sub(C, A);
+    const gv ABC = cross(AB, AC);
+    double d = dot(cross(ABC, AC), AO);
+    if (fuzzy0(d) || d > 0.0) {
+        d = dot(AC, AO);
+        if (fuzzy0(d) || d > 0.0) {
+            s.p1 = A; s.n = 2;
+            dir = triple(AC, AO, AC);
+        } else {
+            d = dot(AB, AO);
+            if (fuzzy0(d) || d > 0.0) {
+                s.p0 = B; s.p1 = A; s.n = 2;
+                dir = triple(AB, AO, AB);
+            } else {
+                s.p0 = A; s.n = 1;
+                dir = AO;
+            }
+        }
+    } else {
+        d = dot(cross(AB, ABC), AO);
+        if (fuzzy0(d) || d > 0.0) {
+            d = dot(AB, AO);
+            if (fuzzy0(d) || d > 0.0) {
+                s.p0 = B; s.p1 = A; s.n = 2;
+                dir = triple(AB, AO, AB);
+            } else {
+                s.p0 = A; s.n = 1;
+                dir = AO;
+            }
+        } else {
+            d = dot(ABC, AO);
+            if (fuzzy0(d) || d > 0.0) {
+                dir = ABC;
+            } else {
+                s.p0 = B; s.p1 = C;
+                dir = neg1(ABC);
+            }
+        }
+    }
+    return 0;
+}
+UGK_FN int ccd_do(Ccd& s, gv& dir) {
+    if (s.n == 2) { /* A = p1, B = p0 */
+        const gv A = s.p1, B = s.p0;
+        const gv AB = sub(B, A);
+        const gv AO = neg1(A);
+        const double d = dot(AB, AO);
+        const gv tmp = cross(AB, AO);
+        if (fuzzy0(dot(tmp, tmp)) && d > 0.0) return 1;
+        if (fuzzy0(d) || d < 0.0) {
+            s.p0 = A; s.n = 1;
+            dir = AO;
+        } else {
+            dir = triple(AB, AO, AB);
+        }
+        return 0;
+    }
+    if (s.n == 3) return ccd_do3(s, s.p2, dir);
+    /* size 4: A = p3, B = p2, C = p1, D = p0 */
+    const gv A = s.p3, B = s.p2, C = s.p1, D = s.p0;
+    if (fuzzy0(tri_dist2(A, B, C, D))) return -1;
+    const gv O = V3(0.0, 0.0, 0.0);
+    if (fuzzy0(tri_dist2(O, A, B, C))) return 1;
+    if (fuzzy0(tri_dist2(O, A, C, D))) return 1;
+    if (fuzzy0(tri_dist2(O, A, B, D))) return 1;
+    if (fuzzy0(tri_dist2(O, B, C, D))) return 1;
+    const gv AO = neg1(A);
+    const gv AB = sub(B, A), AC = sub(C, A), AD = sub(D, A);
+    const gv ABC = cross(AB, AC), ACD = cross(AC, AD), ADB = cross(AD, AB);
+    const int B_on_ACD = ccd_sign(dot(ACD, AB));
+    const int C_on_ADB = ccd_sign(dot(ADB, AC));
+    const int D_on_ABC = ccd_sign(dot(ABC, AD));
+    const bool AB_O = ccd_sign(dot(ACD, AO)) == B_on_ACD;
+    const bool AC_O = ccd_sign(dot(ADB, AO)) == C_on_ADB;
+    const bool AD_O = ccd_sign(dot(ABC, AO)) == D_on_ABC;
+    if (AB_O && AC_O && AD_O) return 1;
+    if (!AB_O) { s.p2 = A; }
+    else if (!AC_O) { s.p1 = D; s.p0 = B; s.p2 = A; }
+    else { s.p0 = C; s.p1 = B; s.p2 = A; }
+    s.n = 3;
+    return ccd_do3(s, s.p2, dir);
+}
+
+/* support of A - B in world: A along dir, B along -dir (cores) */
+UGK_FN gv support_ab(const GShape& A, const gx& TA, const GShape& B, const gx& TB, gv dir) {
+    const gv pA = support0(A, mtv(TA.R, dir));
+    const gv qB = support0(B, mtv(TB.R, neg(dir)));
+    return sub(xfa(TA, pA), xfa(TB, qB));
+}
+
+/* btGjkPairDetector::getClosestPointsNonVirtual: one point (normal on B, point on B, distance) or none */
+UGK_FN bool gjk_pair(EpaMem* E, const GShape& A, const gx& TA0, const GShape& B, const gx& TB0, double thr, gv& nOut,
+                           gv& pOut, double& dOut) {
+    const double marginA = A.margin, marginB = B.margin;
+    double maxd2 = marginA + marginB + thr;
+    maxd2 *= maxd2;
+    gx TA = TA0, TB = TB0;
+    const gv off = scl(add(TA.p, TB.p), 0.5);
+    TA.p = sub(TA.p, off);
+    TB.p = sub(TB.p, off);
+    double distance = 0.0;
+    gv normalInB = V3(0.0, 0.0, 0.0), pointOnB = V3(0, 0, 0);
+    gv axis = V3(0.0, 1.0, 0.0);
+    bool isValid = false, checkSimplex = false;
+    int degenerate = 0, status = -2;
+    gv orgNormalInB = V3(0, 0, 0);
+    const double margin = marginA + marginB;
+    {
+        Ccd s;
+        gv dir = V3(1, 0, 0);
+        gv sup = support_ab(A, TA, B, TB, dir);
+        s.p0 = sup;
+        s.p1 = s.p2 = s.p3 = sup;
+        s.n = 1;
+        dir = neg(sup);
+        for (int it = 0; it < kMaxIter; it++) {
+            sup = support_ab(A, TA, B, TB, dir);
+            if (dot(sup, dir) < 0) { status = -1; break; }
+            if (s.n == 1) s.p1 = sup;
+            else if (s.n == 2) s.p2 = sup;
+            else s.p3 = sup;
+            s.n++;
+            const int res = ccd_do(s, dir);
+            if (res == 1) { status = 0; break; }
+            if (res == -1) { status = -1; break; }
+            if (fuzzy0(dot(dir, dir))) status = -1;
+            if (dot(dir, dir) < kEps) { status = -1; break; }
+            if (dot(dir, dir) < kEps * kEps) { status = -1; break; }
+        }
+    }
+    Voronoi vs;
+    vs_reset(vs);
+    {
+        double squaredDistance = kLarge, delta = 0.0;
+        int curIter = 0;
+        for (;;) {
+            const gv pW = xfa(TA, support0(A, mtv(TA.R, neg(axis))));
+            const gv qW = xfa(TB, support0(B, mtv(TB.R, axis)));
+            const gv w = sub(pW, qW);
+            delta = dot(axis, w);
+            if (delta > 0.0 && delta * delta > squaredDistance * maxd2) { degenerate = 10; checkSimplex = true; break; }
+            if (vs_in(vs, w)) { degenerate = 1; checkSimplex = true; break; }
+            const double f0 = squaredDistance - delta, f1 = squaredDistance * kRelError2;
+            if (f0 <= f1) { degenerate = f0 <= 0.0 ? 2 : 11; checkSimplex = true; break; }
+            vs_add(vs, w, pW, qW);
+            const bool ok = vs_update(vs);
+            const gv nax = vs.cV;
+            if (!ok) { degenerate = 3; checkSimplex = true; break; }
+            if (dot(nax, nax) < kRelError2) { axis = nax; degenerate = 6; checkSimplex = true; break; }
+            const double prev = squaredDistance;
+            squaredDistance = dot(nax, nax);
+            if (prev - squaredDistance <= kEps * prev) { checkSimplex = true; degenerate = 12; break; }
+            axis = nax;
+            if (curIter++ > kMaxIter) break;
+            if (vs.n == 4) { degenerate = 13; break; }
+        }
+        if (checkSimplex) {
+            vs_update(vs);
+            gv pointOnA = vs.cP1;
+            pointOnB = vs.cP2;
+            normalInB = axis;
+            const double lenSqr = dot(axis, axis);
+            if (lenSqr < kRelError2) degenerate = 5;
+            if (lenSqr > kEps * kEps) {
+                const double rlen = 1.0 / ug_sqrt(lenSqr);
+                normalInB = scl(normalInB, rlen);
+                const double s = ug_sqrt(squaredDistance);
+                pointOnA = sub(pointOnA, scl(axis, marginA / s));
+                pointOnB = add(pointOnB, scl(axis, marginB / s));
+                distance = (1.0 / rlen) - margin;
+                isValid = true;
+                orgNormalInB = normalInB;
+            }
+        }
+    }
+    const bool catchDegenerate = degenerate && ((distance + margin) < kPenTol);
+    if ((!isValid || catchDegenerate) || status == 0) {
+        gv tA, tB;
+        axis = V3(0, 0, 0);
+        const bool isValid2 = calc_pen_depth(E, A, B, TA, TB, axis, tA, tB);
+        if (dot(axis, axis) != 0.0) {
+            if (isValid2) {
+                gv tn = sub(tB, tA);
+                double lenSqr = dot(tn, tn);
+                if (lenSqr <= kEps * kEps) { tn = axis; lenSqr = dot(axis, axis); }
+                if (lenSqr > kEps * kEps) {
+                    tn = mulinv(tn, ug_sqrt(lenSqr));
+                    const double distance2 = -len(sub(tA, tB));
+                    if (!isValid || distance2 < distance) {
+                        distance = distance2;
+                        pointOnB = tB;
+                        normalInB = tn;
+                        isValid = true;
+                    }
+                }
+            } else if (dot(axis, axis) > 0.0) {
+                const double distance2 = len(sub(tA, tB)) - margin;
+                if (!isValid || distance2 < distance) {
+                    distance = distance2;
+                    pointOnB = add(tB, scl(axis, marginB));
+                    normalInB = mulinv(axis, len(axis));
+                    isValid = true;
+                }
+            }
+        }
+    }
+    if (!(isValid && (distance < 0 || distance * distance < maxd2))) return false;
+    {
+        double d2 = 0.0;
+        const bool org = dot(orgNormalInB, orgNormalInB) != 0.0;
+        if (org) {
+            const gv w = sub(xfa(TA, support0(A, mtv(TA.R, neg(orgNormalInB)))), xfa(TB, support0(B, mtv(TB.R, orgNormalInB))));
+            d2 = dot(orgNormalInB, w) - margin;
+        }
+        const gv w1 = sub(xfa(TA, support0(A, mtv(TA.R, normalInB))), xfa(TB, support0(B, mtv(TB.R, neg(normalInB)))));
+        const double d1 = dot(neg(normalInB), w1) - margin;
+        const gv w0 = sub(xfa(TA, support0(A, mtv(TA.R, neg(normalInB)))), xfa(TB, support0(B, mtv(TB.R, normalInB))));
+        const double d0 = dot(normalInB, w0) - margin;
+        if (d1 > d0) normalInB = V3(normalInB.x * -1.0, normalInB.y * -1.0, normalInB.z * -1.0);
+        if (org && d2 > d0 && d2 > d1 && d2 > distance) {
+            normalInB = orgNormalInB;
+            distance = d2;
+        }
+    }
+    nOut = normalInB;
+    pOut = add(pointOnB, off);
+    dOut = distance;
+    return true;
+}
+
+} /* namespace ugk */
+
+#endif

@@ -49,6 +49,13 @@
 #define UG_GEOM_FULL 1       /* the full geometry, explicitly (the default) */
 #define UG_GEOM_LOD 2        /* the collision LOD */
 #define UG_GEOM_IS_FULL(flags) (((flags) & UG_GEOM_LOD) == 0)
+/* contact generation.  The default (neither bit, or UG_CONTACT_GJK) is Bullet's own convex-convex path, the one
+ * PyBullet takes for the robot's mesh hulls (btConvexConvexAlgorithm: GJK + EPA, one new point per pair and substep
+ * into the persistent manifold).  UG_CONTACT_VIH keeps rounds 1-3's vertex-in-hull generator
+ * (up to 4 points per pair and substep from hull vertices against face planes). */
+#define UG_CONTACT_GJK 4
+#define UG_CONTACT_VIH 8
+#define UG_CONTACT_IS_GJK(flags) (((flags) & UG_CONTACT_VIH) == 0)
 
 #define UG_MT_WORDS 625      /* MT19937 state (624) + index, uint32, contiguous per env */
 
