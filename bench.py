@@ -52,6 +52,8 @@ def _oracle_sample(task, n, threads, seconds, flags=0, robot="ur5_robotiq_85"):
     from urgym_amd.envs import spaces_for
     lib_path = LIB_PATH_R140 if robot == "ur5_robotiq_140" else LIB_PATH
     olib = lambda: lib(lib_path)  # noqa: E731
+    olib().ugo_set_threads.argtypes = [ctypes.c_int]
+    olib().ugo_set_threads(threads)
     envs = [OracleEnv(task, 20241220 + i, lib_path=lib_path, flags=flags) for i in range(n)]
     for e in envs:
         e.reset()
@@ -75,42 +77,47 @@ def _oracle_sample(task, n, threads, seconds, flags=0, robot="ur5_robotiq_85"):
 
 def cpu_baseline(task, seconds=10.0, seconds_1core=5.0, flags=0, robot="ur5_robotiq_85"):
     """CPU restatement (oracle/, test infrastructure) timed on this host's cores: bounded samples of the same
-    workload (same task, random actions, autoreset) -- all cores with OpenMP (one env per thread at a time,
-    4 envs per thread) and the 1-env / 1-core analogue of config A."""
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    os.environ["OMP_NUM_THREADS"] = str(threads)
-    n = 4 * threads
-    steps, substeps, dt = _oracle_sample(task, n, threads, seconds, flags, robot)
+    workload (same task, random actions, autoreset) -- every core this process may run on (os.sched_getaffinity;
+    OpenMP, 4 envs per thread), the 16-thread figure of rounds 2-3 beside it for continuity, and the 1-env / 1-core
+    analogue of config A."""
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    n = 4 * cores
+    steps, substeps, dt = _oracle_sample(task, n, cores, seconds, flags, robot)
+    t16 = min(16, cores)
+    s16, sub16, dt16 = _oracle_sample(task, 4 * t16, t16, 0.6 * seconds, flags, robot)
     s1, sub1, dt1 = _oracle_sample(task, 1, 1, seconds_1core, flags, robot)
-    return {"value": steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
             "cpu_model": cpu_model(),
             "sample": f"{TASK_NAMES[task]} x {n} envs, {steps} env-steps incl. autoresets ({substeps} substeps) in "
-                      f"{dt:.1f}s; C restatement (oracle/), OpenMP {threads} threads",
+                      f"{dt:.1f}s; C restatement (oracle/), OpenMP {cores} threads (every core of the affinity mask)",
+            "threads_16": {"value": s16 / dt16, "unit": "env-steps/s", "cores": t16,
+                           "sample": f"{4 * t16} envs, {s16} env-steps ({sub16} substeps) in {dt16:.1f}s"},
             "one_core": {"value": s1 / dt1, "unit": "env-steps/s", "cores": 1,
                          "sample": f"1 env, {s1} env-steps ({sub1} substeps) in {dt1:.1f}s, 1 thread"}}
 
 
-def pmc_traffic(task, n, geometry):
+def pmc_traffic(task, n, geometry, contact):
     """HBM bytes per k_step launch from the committed PMC summary of this workload (profiles/traffic_k_step.json,
     tools/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes), keyed on (task, envs,
-    geometry); a record without a geometry key is a round-2 LOD measurement."""
+    geometry, contact); a record without a geometry key is a round-2 LOD measurement, one without a contact key a
+    vertex-in-hull (rounds 1-3) one."""
     path = os.path.join(ROOT, "profiles", "traffic_k_step.json")
     try:
         t = json.load(open(path))
     except (OSError, ValueError):
         return None, None
     for rec in (t if isinstance(t, list) else [t]):
-        if (rec.get("task"), rec.get("envs"), rec.get("geometry", "lod")) == (task, n, geometry):
+        if (rec.get("task"), rec.get("envs"), rec.get("geometry", "lod"), rec.get("contact", "vih")) == (task, n, geometry, contact):
             return float(rec["hbm_bytes_per_launch"]), \
                 f"profiles/traffic_k_step.json ({rec.get('source', 'rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE')})"
     return None, None
 
 
-def work_model(task, geometry):
+def work_model(task, geometry, contact):
     """FP64 FLOPs per substep / per env-step outside substeps (profiles/work_model.json, tools/opcount.py), counted
-    on the restatement in the same geometry mode"""
+    on the restatement in the same geometry and contact mode"""
     try:
-        key = "tasks_full" if geometry == "full" else "tasks"
+        key = ("tasks_full" if geometry == "full" else "tasks") + ("_gjk" if contact == "gjk" else "")
         m = json.load(open(os.path.join(ROOT, "profiles", "work_model.json")))[key][str(task)]
         return float(m["F_sub"]), float(m["F_nonsub_per_env_step"])
     except (OSError, ValueError, KeyError):
@@ -144,6 +151,9 @@ def main(argv=None):
     ap.add_argument("--geometry", choices=("full", "lod"), default="full",
                     help="collision geometry: full (default: every vertex of PyBullet's mesh hulls, a true cylinder disc) "
                          "or lod (<= 48-vertex hulls, a 16-gon disc prism: URGYM_FLAG_LOD_GEOMETRY)")
+    ap.add_argument("--contact", choices=("gjk", "vih"), default="gjk",
+                    help="contact generation: gjk (default: Bullet's convex-convex GJK / EPA pair detector, one new point per "
+                         "pair and substep) or vih (rounds 1-3's vertex-in-hull generator: URGYM_FLAG_CONTACT_VIH)")
     ap.add_argument("--robot", choices=("ur5_robotiq_85", "ur5_robotiq_140"), default="ur5_robotiq_85",
                     help="arm + gripper (robot.py): UR5Robotiq85 (every registered env; default) or UR5Robotiq140")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -169,9 +179,9 @@ def main(argv=None):
         world = dist.get_world_size()
     dev = torch.device("cuda", gpu)
 
-    from urgym_amd._native import GEOM_LOD, Sim
+    from urgym_amd._native import CONTACT_VIH, GEOM_LOD, Sim
     n = args.envs
-    geom_flags = GEOM_LOD if args.geometry == "lod" else 0
+    geom_flags = (GEOM_LOD if args.geometry == "lod" else 0) | (CONTACT_VIH if args.contact == "vih" else 0)
     sim = Sim(args.task, n, device=gpu, seed=20241220, env_offset=rank * n, flags=geom_flags, robot=args.robot)
     sim.set_autoreset(True, MAX_STEPS[args.task])
     sim.reset()
@@ -191,7 +201,8 @@ def main(argv=None):
     sub = torch.zeros(n, dtype=torch.int32, device=dev)
     stream = torch.cuda.ExternalStream(sim.L.urgym_stream(sim.h), device=dev)
     if world > 1:
-        from urgym_amd.parallel import gather_returns
+        from urgym_amd.parallel import ReturnGather
+        gat = ReturnGather(n, O, dev)
 
     def one_step(t, e=None):
         sim.step_device(acts[t].data_ptr(), obs.data_ptr(), fin.data_ptr(), rew.data_ptr(), term.data_ptr(),
@@ -199,9 +210,9 @@ def main(argv=None):
         if e is not None:
             e.record(stream)
         if world > 1:
-            # returns gathered over RCCL (xGMI): obs | reward | terminated | truncated, global env-id order
+            # every return gathered over RCCL (xGMI) into one preallocated global buffer, global env-id order
             with torch.cuda.stream(stream):
-                gather_returns(obs, rew, term, trunc)
+                gat.gather(obs, fin, rew, term, trunc, succ, sub)
 
     sub_tot = torch.zeros((), dtype=torch.int64, device=dev)
     res_tot = torch.zeros((), dtype=torch.int64, device=dev)
@@ -255,7 +266,7 @@ def main(argv=None):
     value = env_steps / dt
     # roofline of the dominant kernel (k_step): FP64 VALU, algorithmic FLOPs per launch from the op-counted
     # restatement (profiles/work_model.json) with this run's substep count, over the HIP-event launch time
-    F_sub, F_non = work_model(args.task, args.geometry)
+    F_sub, F_non = work_model(args.task, args.geometry, args.contact)
     flops_per_launch = None
     if F_sub is not None:
         flops_per_launch = (F_sub * substeps + F_non * env_steps) / (K * world)
@@ -263,7 +274,7 @@ def main(argv=None):
     S = state_bytes()
     bytes_per_env = 2 * S + 4 * A + 8 * O * 2 + 8 + 3 + 4
     achieved_gbs = bytes_per_env * n / (avg_kernel_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args.task, n, args.geometry)
+    traffic, traffic_src = pmc_traffic(args.task, n, args.geometry, args.contact)
     if args.robot != "ur5_robotiq_85":  # the PMC record and the work model were measured on the Robotiq-85 build
         traffic, traffic_src = None, None
     if flops_per_launch is not None:
@@ -298,6 +309,7 @@ def main(argv=None):
         "config": {"workload": f"{TASK_NAMES[args.task]} x {n} envs per GPU, autoreset, max_episode_steps "
                                f"{MAX_STEPS[args.task]}", "envs_per_gpu": n, "total_envs": n * world,
                    "parallelism": f"env-dp{world}", "world_size": world, "geometry": args.geometry,
+                   "contact": args.contact,
                    "backend": args.backend if world > 1 else None, "robot": args.robot},
         "rep_values": [env_steps / x[0] for x in reps],
         "substeps_per_env_step": substeps / env_steps,

@@ -50,6 +50,13 @@ urgym_handle* urgym_create(int task_id, int n_envs, int device_ordinal, int prec
  * Both are bit-identical to the CPU restatement's same mode; both flags together are an error. */
 #define URGYM_FLAG_FULL_GEOMETRY 1 /* == UG_GEOM_FULL (urgym_amd/csrc/ug_layout.h) */
 #define URGYM_FLAG_LOD_GEOMETRY 2  /* == UG_GEOM_LOD */
+/* Contact generation.  The default (0 or URGYM_FLAG_CONTACT_GJK) is the path PyBullet takes for the robot's mesh hulls
+ * (no URDF_INITIALIZE_SAT_FEATURES, robot.py:186-187): btConvexConvexAlgorithm's GJK + EPA pair detector, one new point
+ * per pair and substep merged into the persistent manifold, for every pair without a dedicated Bullet algorithm
+ * (sphere-sphere, sphere-box and box-box keep theirs).  URGYM_FLAG_CONTACT_VIH selects rounds 1-3's vertex-in-hull
+ * generator (up to 4 points per pair and substep).  Both flags together are an error. */
+#define URGYM_FLAG_CONTACT_GJK 4   /* == UG_CONTACT_GJK */
+#define URGYM_FLAG_CONTACT_VIH 8   /* == UG_CONTACT_VIH */
 urgym_handle* urgym_create_ex(int task_id, int n_envs, int device_ordinal, int precision, uint32_t seed,
                               int env_offset, int flags);
 
@@ -185,6 +192,11 @@ int urgym_debug_prof(urgym_handle* h, unsigned long long* out16, int reset);
  * Delassus rows, w and impulses there. */
 int urgym_debug_workspace(urgym_handle* h, int env, double* out, int count);
 int urgym_debug_ws_doubles(void);
+/* Test aid, no reference counterpart: n convex-convex queries (Bullet's btGjkPairDetector as the kernels run it,
+ * one wave per query) on the current device.  Query i = 39 doubles: for shape A then B kind (UG_SHAPE_*), hull vertex
+ * start, vertex count, implicit dimensions[3], margin, R[9] (row-major), p[3]; then the contact breaking threshold.
+ * out: n x 7 (normal on B, point on B, distance), ok: n (1 = a point).  Returns 0 on success. */
+int urgym_debug_gjk(int n, const double* q, double* out, int* ok);
 
 #ifdef __cplusplus
 }

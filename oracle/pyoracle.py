@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libugoracle.so")
+# URGYM_ORACLE_LIB: another build of the restatement (make -C oracle asan -> tools/oracle_asan.sh)
+LIB_PATH = os.environ.get("URGYM_ORACLE_LIB") or os.path.join(_HERE, "_build", "libugoracle.so")
 LIB_PATH_R140 = os.path.join(_HERE, "_build", "libugoracle_r140.so")  # the UR5Robotiq140 restatement
 
 _libs = {}

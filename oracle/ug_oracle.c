@@ -396,8 +396,9 @@ static void build_scene(scene* s, int variant, int flags) {
         c->full = s->full;
         /* URDF2Bullet keeps a link's single collision shape bare only when its frame is the link's inertial frame
          * (child transform identity); otherwise the link collides through a btCompoundShape [ext] */
-        c->compound = memcmp(c->R.m, c->aR.m, sizeof(c->R.m)) != 0 || c->P.x != c->aP.x || c->P.y != c->aP.y ||
-                      c->P.z != c->aP.z;
+        int same = c->P.x == c->aP.x && c->P.y == c->aP.y && c->P.z == c->aP.z;
+        for (int i = 0; i < 9; i++) same = same && c->R.m[i] == c->aR.m[i];
+        c->compound = !same;
     }
     int nrobot = s->ncol;
     int statics[8], nstat = 0;
@@ -894,18 +895,51 @@ int ugo_gjk_pair(int kA, int v0A, int nvA, const double* impA, double mA, const 
     out[6] = d;
     return 1;
 }
+/* debug aid (tools/debug_gjk.py): the convex-convex queries of this thread, as urgym_debug_gjk packs them, with
+ * their results (ok, normal, point, distance) */
+#define GREC_MAX 8192
+#define GREC_DOUBLES 47
+static __thread int g_rec_on, g_rec_n;
+static __thread double g_rec[GREC_MAX * GREC_DOUBLES];
+void ugo_gjk_record(int on) {
+    if (on) g_rec_n = 0;
+    g_rec_on = on;
+}
+int ugo_gjk_records(double* out, int max) {
+    const int n = g_rec_n < max ? g_rec_n : max;
+    memcpy(out, g_rec, sizeof(double) * GREC_DOUBLES * (size_t)n);
+    return g_rec_n;
+}
+static void grec_shape(double* q, const gshape* g, int v0, const xf* T) {
+    q[0] = g->kind; q[1] = v0; q[2] = g->nv; q[3] = g->imp.x; q[4] = g->imp.y; q[5] = g->imp.z; q[6] = g->margin;
+    for (int i = 0; i < 9; i++) q[7 + i] = T->R.m[i];
+    q[16] = T->p.x; q[17] = T->p.y; q[18] = T->p.z;
+}
+static int gjk_pair_rec(const gshape* A, int va, const xf* TA, const gshape* B, int vb, const xf* TB, double thr, v3* n,
+                        v3* p, double* d) {
+    const int ok = gjk_pair(A, TA, B, TB, thr, n, p, d);
+    if (g_rec_on && g_rec_n < GREC_MAX) {
+        double* q = g_rec + GREC_DOUBLES * g_rec_n++;
+        grec_shape(q, A, va, TA);
+        grec_shape(q + 19, B, vb, TB);
+        q[38] = thr;
+        q[39] = ok;
+        q[40] = n->x; q[41] = n->y; q[42] = n->z; q[43] = p->x; q[44] = p->y; q[45] = p->z; q[46] = *d;
+    }
+    return ok;
+}
 static void nc_gjk(const xf* TA, const collider* A, const xf* TB, const collider* B, double thr, candlist* out) {
     gshape ga, gb;
     gshape_of(A, &ga);
     gshape_of(B, &gb);
-    v3 n, p;
-    double d;
+    v3 n = V(0, 0, 0), p = V(0, 0, 0);
+    double d = 0.0;
     if (A->kind == UG_SHAPE_SPHERE && B->kind != UG_SHAPE_SPHERE) {
         /* the sphere-first pair order of this restatement: B is GJK's shape A, the result turned into (A, B) */
-        if (gjk_pair(&gb, TB, &ga, TA, thr, &n, &p, &d)) cand_add(out, vneg(n), vadd(p, vscale(n, d)), d);
+        if (gjk_pair_rec(&gb, B->v0, TB, &ga, A->v0, TA, thr, &n, &p, &d)) cand_add(out, vneg(n), vadd(p, vscale(n, d)), d);
         return;
     }
-    if (gjk_pair(&ga, TA, &gb, TB, thr, &n, &p, &d)) cand_add(out, n, p, d);
+    if (gjk_pair_rec(&ga, A->v0, TA, &gb, B->v0, TB, thr, &n, &p, &d)) cand_add(out, n, p, d);
 }
 
 /* btSphereBoxCollisionAlgorithm::getSphereDistance [ext]: sphere A, box B */
@@ -2333,12 +2367,27 @@ static int state_finite(const ugo_env* e);
 /* wait_until_stable (env_ball_balance_v0.py:94-103): returns substeps taken.  A state that went non-finite
  * ends the loop at once (the step's non-finite guard then terminates the episode) instead of spinning the
  * remaining substeps on NaNs. */
+static void trace_substep(const ugo_env* e);
+/* the non-finite guard voids a runaway state: q, qd and the active objects' state become NaN and the contacts are
+ * dropped, so what a step returns once the guard fired does not depend on how the first NaN spread (the kernels
+ * clamp with v_min / v_max, which drop a NaN operand that C's selects keep) */
+static void poison(ugo_env* e) {
+    for (int i = 0; i < NB; i++) e->q[i] = e->qd[i] = NAN;
+    for (int o = 0; o < e->sc.nobj; o++) {
+        if (!e->oactive[o]) continue;
+        e->opos[o] = V(NAN, NAN, NAN);
+        e->oquat[o] = Q(NAN, NAN, NAN, NAN);
+        e->ov[o] = e->ow[o] = V(NAN, NAN, NAN);
+    }
+    e->nman = 0;
+}
 static int wait_until_stable(ugo_env* e) {
     double pos[NB];
     memcpy(pos, e->q, sizeof(pos));
     for (int i = 0; i < UG_STABLE_STEPS; i++) {
+        trace_substep(e);
         substep(e);
-        if (!state_finite(e)) return i + 1;
+        if (!state_finite(e)) { poison(e); return i + 1; }
         double a[NB];
         for (int j = 0; j < NB; j++) a[j] = ug_fabs(pos[j] - e->q[j]);
         if (np_sum12(a) < UG_STABLE_EPS) return i + 1;
@@ -2492,7 +2541,7 @@ static int robot_reset(ugo_env* e) {
     while (n < 10) {
         substep(e);
         n++;
-        if (!state_finite(e)) break; /* as wait_until_stable: no substeps on NaNs */
+        if (!state_finite(e)) { poison(e); break; } /* as wait_until_stable: no substeps on NaNs */
     }
     open_gripper(e, 100.0);
     return n;
@@ -2894,7 +2943,7 @@ static int bx_step(ugo_env* e, const float* a, double* obs, double* rew, uint8_t
     while (n < UG_BX_STEPS) { /* :128-129 a fixed 120 substeps */
         substep(e);
         n++;
-        if (!state_finite(e)) break;
+        if (!state_finite(e)) { poison(e); break; }
     }
     int bc = e->sc.ocol[1];
     int press = ugg_box_press(e->ow[1].x, e->button_mode, robot_contact(e, bc, 0, UG_NL - 1), robot_contact(e, bc, 9, 18));
@@ -2926,6 +2975,23 @@ ugo_env* ugo_create_ex(int task, uint32_t seed, int flags) {
 }
 void ugo_destroy(ugo_env* e) { free(e); }
 void ugo_substep(ugo_env* e) { substep(e); }
+/* debug aid (tools/debug_gjk.py): the state before every substep of this thread's next calls (up to 600) */
+#define TRACE_MAX 600
+static __thread int g_trace_on, g_trace_n;
+static __thread double* g_trace;
+void ugo_trace(int on) {
+    if (!g_trace) g_trace = (double*)malloc(sizeof(double) * STATE_DIM * TRACE_MAX);
+    if (on) g_trace_n = 0;
+    g_trace_on = on;
+}
+int ugo_traced(double* out, int max) {
+    const int n = g_trace_n < max ? g_trace_n : max;
+    if (n) memcpy(out, g_trace, sizeof(double) * STATE_DIM * (size_t)n);
+    return g_trace_n;
+}
+static void trace_substep(const ugo_env* e) {
+    if (g_trace_on && g_trace_n < TRACE_MAX) ugo_get_state(e, g_trace + (size_t)STATE_DIM * g_trace_n++);
+}
 /* non-finite state guard (failure detection): q, qd and the active objects' state */
 static int state_finite(const ugo_env* e) {
     for (int i = 0; i < NB; i++)
@@ -3057,6 +3123,10 @@ int ugo_contact_points(const ugo_env* e, int bodyA, int bodyB, int linkA, int li
                     t2 = V(-n.z * t1.y, n.z * t1.x, a * kk);
                 }
                 if (swap) { v3 t = pA; pA = pB; pB = t; n = vneg(n); }
+                if (s->task == UG_TASK_BOX) { /* world coordinates (the restatement keeps the robot base at the origin) */
+                    pA.y = pA.y + UG_BX_ROBOT_Y;
+                    pB.y = pB.y + UG_BX_ROBOT_Y;
+                }
                 o[0] = 0.0;
                 o[1] = swap ? eb : ea; o[2] = swap ? ea : eb;
                 o[3] = swap ? lb : la; o[4] = swap ? la : lb;
@@ -3093,7 +3163,8 @@ int ugo_camera(const ugo_env* e, const float* view16, const float* proj16, int W
         const xf O = owner_xf(e, &k, c->owner);
         const xf T = shape_xf(&O, c);
         for (int m = 0; m < 9; m++) R[ci][m] = T.R.m[m];
-        P[ci][0] = T.p.x; P[ci][1] = T.p.y; P[ci][2] = T.p.z;
+        /* world coordinates: Box-v0's frame has the robot base at the origin (world y + UG_BX_ROBOT_Y) */
+        P[ci][0] = T.p.x; P[ci][1] = s->task == UG_TASK_BOX ? T.p.y + UG_BX_ROBOT_Y : T.p.y; P[ci][2] = T.p.z;
         rad[ci] = ugr_radius(c->kind, c->half, UG_HULL_V + 3 * c->v0, c->nv);
         ugr_hull_box(UG_HULL_V + 3 * c->v0, c->kind == UG_SHAPE_HULL ? c->nv : 0, box[ci]);
         on[ci] = collider_active(e, c) != 0;
@@ -3245,6 +3316,15 @@ void ugo_link_state(const ugo_env* e, int link, double* pos7) {
 }
 void ugo_ik(const ugo_env* e, const double* tp, const double* to, double* q_out) {
     ik_solve(e->q, V(tp[0], tp[1], tp[2]), Q(to[0], to[1], to[2], to[3]), q_out);
+}
+/* OpenMP threads of the next ugo_batch_step calls from this thread (bench.py's all-core and 16-thread samples) */
+void ugo_set_threads(int n) {
+#ifdef _OPENMP
+    extern void omp_set_num_threads(int);
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
 }
 long ugo_batch_step(ugo_env** envs, int n, const float* actions, double* obs, double* reward, uint8_t* terminated,
                     uint8_t* success, int32_t* substeps, int autoreset, int max_episode_steps, int32_t* elapsed) {

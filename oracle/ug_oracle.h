@@ -105,6 +105,15 @@ int ugo_g_tb_reward(const float* a, const double* b1, const double* b2, double p
  * Returns 1 when a point is reported. */
 int ugo_gjk_pair(int kA, int v0A, int nvA, const double* impA, double mA, const double* RA, const double* pA, int kB, int v0B,
                  int nvB, const double* impB, double mB, const double* RB, const double* pB, double thr, double* out);
+/* debug aid: record this thread's convex-convex queries (urgym_debug_gjk's 39-double packing + ok + normal, point,
+ * distance = 47 doubles each, up to 512); ugo_gjk_records returns how many were recorded */
+void ugo_gjk_record(int on);
+/* debug aid: record the state (UG_STATE_DIM doubles) before every wait_until_stable substep, up to 600 */
+void ugo_trace(int on);
+int ugo_traced(double* out, int max);
+int ugo_gjk_records(double* out, int max);
+/* OpenMP threads of this thread's next ugo_batch_step calls */
+void ugo_set_threads(int n);
 /* batched CPU baseline: n envs, OpenMP over envs; returns total substeps */
 long ugo_batch_step(ugo_env** envs, int n, const float* actions, double* obs, double* reward,
                     uint8_t* terminated, uint8_t* success, int32_t* substeps, int autoreset,

@@ -19,10 +19,12 @@ def main():
     off, n = shard(total, world, rank)
     ids = torch.arange(off, off + n, dtype=torch.float64)
     obs = ids[:, None] * 10 + torch.arange(od, dtype=torch.float64)[None, :]
-    o, r, t, tr = gather_returns(obs, ids * 0.5, (ids.long() % 3) == 0, (ids.long() % 5) == 0)
+    g = gather_returns(obs, ids * 0.5, (ids.long() % 3) == 0, (ids.long() % 5) == 0, final_obs=-obs,
+                       success=(ids.long() % 7) == 0, substeps=ids.to(torch.int32) + 10)
     if rank == 0:
-        json.dump({"world": world, "obs": o.tolist(), "rew": r.tolist(), "term": t.tolist(), "trunc": tr.tolist()},
-                  open(out, "w"))
+        json.dump({"world": world, "obs": g["obs"].tolist(), "rew": g["reward"].tolist(), "term": g["terminated"].tolist(),
+                   "trunc": g["truncated"].tolist(), "final": g["final_obs"].tolist(), "succ": g["success"].tolist(),
+                   "sub": g["substeps"].tolist()}, open(out, "w"))
     dist.barrier()
     dist.destroy_process_group()
 

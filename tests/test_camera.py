@@ -103,3 +103,23 @@ def test_renderer_analytic_sphere_depth():
     expect = 0.5 * ((A * -d_eye + B) / d_eye) + 0.5  # clip z = A z_eye + B, w = -z_eye, z_eye = -d_eye
     c = cam.rgbd_2_world(W / 2, H / 2, expect)
     np.testing.assert_allclose(c, ball + [0, 0, 0.02], atol=1e-6)
+
+
+def test_box_scene_renders_in_world_coordinates():
+    """Box-v0 keeps the robot base at the origin internally (the box base at world y = 0 sits at y = -0.5 there); the
+    camera's matrices are in world coordinates, so the closed door's lid top -- world (0, 0, 0.105): door joint at
+    z 0.1, lid half height 0.005, skew-box-button.urdf -- must land under a camera looking straight down at it."""
+    env = OracleEnv(7, 3)
+    env.reset()
+    W = H = 33
+    cam = Camera((0.0, 0.0, 0.6), (0.0, 0.0, 0.105), (0, 1, 0), 0.05, 2.0, (W, H), 20)
+    rgb, depth, seg = env.camera(cam.view_matrix, cam.projection_matrix, W, H)
+    assert seg[16, 16] == 1  # the door link (object 0)
+    np.testing.assert_allclose(cam.rgbd_2_world(W / 2, H / 2, depth[16, 16]), [0.0, 0.0, 0.105], atol=2e-6)
+    # getContactPoints positions are world positions too: the closed lid (bottom face at z 0.095) rests on the button's
+    # top (z 0.095) around the box's world origin
+    env.step(np.zeros(8, np.float32))
+    pts = env.contact_points(1, 2)
+    assert len(pts) >= 1
+    for p in pts:
+        assert np.hypot(p[5], p[6]) < 0.02 + 1e-9 and abs(p[7] - 0.095) < 1e-3  # within the button's radius

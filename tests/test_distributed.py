@@ -21,16 +21,21 @@ def _worker(rank, world, port, total, obs_dim, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from urgym_amd.parallel import gather_returns, shard
+    from urgym_amd.parallel import ReturnGather, shard
     off, n = shard(total, world, rank)
     ids = torch.arange(off, off + n, dtype=torch.float64)
     obs = ids[:, None] * 10 + torch.arange(obs_dim, dtype=torch.float64)[None, :]
     rew = ids * 0.5
     term = (ids.long() % 3) == 0
     trunc = (ids.long() % 5) == 0
-    o, r, t, tr = gather_returns(obs, rew, term, trunc)
+    # the bench's form: one ReturnGather, several steps through the same preallocated buffers
+    g = ReturnGather(n, obs_dim, "cpu")
+    for step in range(3):
+        v = g.gather(obs + step, -obs, rew, term, trunc, (ids.long() % 7) == 0, ids.to(torch.int32) + step)
+    d = g.decoded()
+    assert v["obs"].data_ptr() == g.recv.data_ptr()  # views of the preallocated buffer
     if rank == 0:
-        q.put((o.numpy(), r.numpy(), t.numpy(), tr.numpy()))
+        q.put({k: x.numpy().copy() for k, x in d.items()})
     dist.barrier()
     dist.destroy_process_group()
 
@@ -51,14 +56,16 @@ def test_gather_returns_world2_gloo():
     procs = [ctx.Process(target=_worker, args=(r, world, port, total, od, q)) for r in range(world)]
     for p in procs:
         p.start()
-    o, r, t, tr = q.get(timeout=120)
+    d = q.get(timeout=120)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     ids = np.arange(total)
-    assert np.array_equal(o, ids[:, None] * 10.0 + np.arange(od)[None, :])
-    assert np.array_equal(r, ids * 0.5)
-    assert np.array_equal(t, ids % 3 == 0) and np.array_equal(tr, ids % 5 == 0)
+    obs = ids[:, None] * 10.0 + np.arange(od)[None, :]
+    assert np.array_equal(d["obs"], obs + 2) and np.array_equal(d["final_obs"], -obs)
+    assert np.array_equal(d["reward"], ids * 0.5)
+    assert np.array_equal(d["terminated"], ids % 3 == 0) and np.array_equal(d["truncated"], ids % 5 == 0)
+    assert np.array_equal(d["success"], ids % 7 == 0) and np.array_equal(d["substeps"], ids + 2)
 
 
 def test_spawn_ranks_world2(tmp_path):
@@ -79,6 +86,8 @@ def test_spawn_ranks_world2(tmp_path):
     assert np.array_equal(np.array(g["obs"]), ids[:, None] * 10.0 + np.arange(od)[None, :])
     assert np.array_equal(np.array(g["rew"]), ids * 0.5)
     assert np.array_equal(np.array(g["term"]), ids % 3 == 0) and np.array_equal(np.array(g["trunc"]), ids % 5 == 0)
+    assert np.array_equal(np.array(g["final"]), -(ids[:, None] * 10.0 + np.arange(od)[None, :]))
+    assert np.array_equal(np.array(g["succ"]), ids % 7 == 0) and np.array_equal(np.array(g["sub"]), ids + 10)
 
 
 def test_bench_gpus_flag_spawns_or_refuses(monkeypatch):

@@ -1,11 +1,14 @@
 """The failure branches, driven on purpose: crafted states that overflow the manifold
 capacity (16) and the row capacity (128), run a wait_until_stable loop into its 480-substep cap ("did not stabilize",
-env_ball_balance_v0.py:102-103), and trigger the split-impulse pass (penetration deeper than 0.04).  Each case runs
-one env-step on the GPU and in the CPU restatement from the same crafted state: every output, the flags, the event
-counters and the final state are bit-identical, and the counter the case targets is > 0.
+env_ball_balance_v0.py:102-103), trigger the split-impulse pass (penetration deeper than 0.04) and drive the
+non-finite guard.  Each case runs one env-step on the GPU and in the CPU restatement from the same crafted state: every
+output, the flags, the event counters and the final state are bit-identical, and the counter the case targets is > 0.
 
-The states were found with the restatement in the default (full) geometry (arm folded into the table; a CubesGrasp
-joint move across the whole pan range against the joint's current motion; a cube 3 cm inside the table)."""
+The states were found with the restatement: the arm folded into the table, a CubesGrasp joint move across the whole pan
+range against the joint's current motion, a cube 3 cm inside the table.  The default contact generation (Bullet's
+GJK / EPA, one new point per pair and substep) fills fewer rows than rounds 1-3's vertex-in-hull generator: its folds
+overflow the manifold capacity, and the row capacity (the same row-build code in both modes) is driven with the
+vertex-in-hull mode's folds (URGYM_FLAG_CONTACT_VIH); no finite GJK fold found in 700 random poses fills 128 rows."""
 import numpy as np
 import pytest
 
@@ -25,15 +28,15 @@ def mods(built):
     return Sim, OracleEnv
 
 
-def crafted_step(Sim, OracleEnv, task, edits, action):
+def crafted_step(Sim, OracleEnv, task, edits, action, flags=0, finite=True):
     """reset n = len(edits) envs, apply edit k to env k's state on both sides, one env-step with `action`;
     returns (GPU outputs, flags, stat increments)"""
     n = len(edits)
-    sim = Sim(task, n, seed=SEED)
+    sim = Sim(task, n, seed=SEED, flags=flags)
     sim.set_autoreset(False, 0)
     sim.reset()
     st = sim.get_state()
-    ref = [OracleEnv(task, SEED + i) for i in range(n)]
+    ref = [OracleEnv(task, SEED + i, flags=flags) for i in range(n)]
     for i, (r, edit) in enumerate(zip(ref, edits)):
         r.reset()
         assert np.array_equal(st[i], r.get_state()), i
@@ -48,38 +51,74 @@ def crafted_step(Sim, OracleEnv, task, edits, action):
     got = sim.get_state()
     for i, r in enumerate(ref):
         o, rew, term, succ, ns = r.step(acts[i])
-        assert np.array_equal(out["obs"][i], o) and out["reward"][i] == rew, i
+        assert np.array_equal(out["obs"][i], o, equal_nan=True) and out["reward"][i] == rew, (i, out["obs"][i], o)
         assert bool(out["terminated"][i]) == term and bool(out["success"][i]) == succ, i
         assert out["substeps"][i] == ns, (i, out["substeps"][i], ns)
         assert fl[i] == r.flags(), (i, fl[i], r.flags())
         assert np.array_equal(sim.stats()[i], r.stats()), (i, sim.stats()[i], r.stats())
-        assert np.array_equal(got[i], r.get_state()), i
-        assert np.all(np.isfinite(got[i]))
+        assert np.array_equal(got[i], r.get_state(), equal_nan=True), i
+        if finite:
+            assert np.all(np.isfinite(got[i]))
     sim.close()
     return out, fl, d
 
 
-def _fold(q1, q2):
+def _fold(q1, q2, q3=None):
     def edit(s):
         s[LY.F_Q + 1] = q1
         s[LY.F_Q + 2] = q2
+        if q3 is not None:
+            s[LY.F_Q + 3] = q3
         s[LY.F_QD:LY.F_QD + 12] = 0.0
     return edit
 
 
-# (shoulder lift, elbow) folds that stay finite with the default (full) geometry and overflow both capacities;
-# the last of each task also runs its wait_until_stable into the 480 cap
-POSES = {0: [(0.5, 0.0), (0.5, 2.5), (0.8, 2.5), (1.0, 2.0), (0.3, 1.5)],
-         1: [(-0.5, 1.5), (-0.3, 1.5), (0.3, 0.0), (0.0, 2.5), (0.3, 1.5)]}
+CONTACT_VIH = 8
+# (shoulder lift, elbow) folds that stay finite and overflow both capacities with the vertex-in-hull generator; the
+# last of each task also runs its wait_until_stable into the 480 cap
+POSES_VIH = {0: [(0.5, 0.0), (0.5, 2.5), (0.8, 2.5), (1.0, 2.0), (0.3, 1.5)],
+             1: [(-0.5, 1.5), (-0.3, 1.5), (0.3, 0.0), (0.0, 2.5), (0.3, 1.5)]}
+# the same for the default (GJK / EPA) contacts: finite folds overflowing the manifold capacity
+POSES = {0: [(0.5, 0.0), (0.8, 2.5), (0.3, 1.5)], 1: [(-0.5, 1.5), (-0.3, 1.5), (0.3, 0.0), (0.0, 2.5)]}
 
 
 @pytest.mark.parametrize("task", [0, 1])
-def test_manifold_and_row_capacity_overflow(mods, task):
-    """the arm folded into the table: more than 16 touching pairs and more than 128 contact rows.  The capacity
-    counters and the DROPPED flag fire (and, for the deepest poses, the 480 cap and the split pass too), equal to
-    the restatement's."""
+def test_manifold_capacity_overflow(mods, task):
+    """the arm folded into the table (default contacts): more than 16 touching pairs.  The manifold-capacity counter,
+    the DROPPED flag and the split pass fire (BallBalance's folds also reach the 480 cap), equal to the
+    restatement's."""
     Sim, OracleEnv = mods
     out, fl, d = crafted_step(Sim, OracleEnv, task, [_fold(*p) for p in POSES[task]], np.zeros(3))
+    assert (d[:, MANCAP] > 0).sum() >= 3, d.tolist()
+    assert np.all((fl & FLAG_DROPPED) != 0), fl.tolist()
+    assert (d[:, SPLIT] > 0).all(), d.tolist()
+    assert np.array_equal((d[:, UNSTABLE] > 0), (fl & FLAG_UNSTABLE) != 0)
+    if task == 0:
+        assert (d[:, UNSTABLE] > 0).any(), d.tolist()
+
+
+FLAG_NONFINITE = 2
+
+
+def test_nonfinite_guard_on_runaway_folds(mods):
+    """folds whose one-point-per-pair contacts deep inside the table run away (joint velocities past 1e20 within a few
+    dozen substeps, then inf / NaN): the non-finite guard ends the env-step at the first non-finite substep on both
+    sides -- same substep count, NONFINITE flag and counter, the same non-finite observation and state (the runaway
+    angles, 1e21 rad, take the same sin / cos quadrant in both builds: ug__rem_pio2's exact quadrant)"""
+    Sim, OracleEnv = mods
+    out, fl, d = crafted_step(Sim, OracleEnv, 0, [_fold(0.5, 0.0), _fold(0.5, 2.5), _fold(0.8, 2.5), _fold(1.0, 2.0)],
+                              np.zeros(3), finite=False)
+    assert (fl[[1, 3]] & FLAG_NONFINITE).all() and (d[[1, 3], NONFINITE] == 1).all(), (fl.tolist(), d.tolist())
+    assert not (fl[[0, 2]] & FLAG_NONFINITE).any()
+
+
+@pytest.mark.parametrize("task", [0, 1])
+def test_manifold_and_row_capacity_overflow_vih(mods, task):
+    """the vertex-in-hull generator (up to 4 points per pair and substep): more than 16 touching pairs and more than
+    128 contact rows.  The capacity counters and the DROPPED flag fire (and, for the deepest poses, the 480 cap and
+    the split pass too), equal to the restatement's same mode."""
+    Sim, OracleEnv = mods
+    out, fl, d = crafted_step(Sim, OracleEnv, task, [_fold(*p) for p in POSES_VIH[task]], np.zeros(3), flags=CONTACT_VIH)
     assert (d[:, MANCAP] > 0).sum() >= 3 and (d[:, ROWCAP] > 0).sum() >= 4, d.tolist()
     assert np.all((fl & FLAG_DROPPED) != 0), fl.tolist()
     assert (d[:, SPLIT] > 0).all() and (d[:, UNSTABLE] > 0).any(), d.tolist()

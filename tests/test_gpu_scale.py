@@ -102,7 +102,8 @@ def test_config_e_eight_shards_equal_one_65536_handle(mods):
 
 def test_gloo_ranks_gather_real_sim_outputs(mods, tmp_path):
     """two ranks (torch.distributed.run children on this GPU, gloo) step their halves of a BallBalance batch and
-    all-gather obs | reward | terminated | truncated each step; the gathered batches equal one handle stepping the
+    all-gather every return (obs, final_obs, reward, terminated, truncated, success, substeps) each step through one
+    ReturnGather; the gathered batches equal one handle stepping the
     whole batch with the same action stream (autoreset through truncation at 4 steps)."""
     Sim, _ = mods
     from urgym_amd.parallel import spawn_ranks
@@ -123,6 +124,10 @@ def test_gloo_ranks_gather_real_sim_outputs(mods, tmp_path):
         assert np.array_equal(g["reward"][t], r["reward"]), t
         assert np.array_equal(g["terminated"][t], r["terminated"].astype(bool)), t
         assert np.array_equal(g["truncated"][t], r["truncated"].astype(bool)), t
+        assert np.array_equal(g["success"][t], r["success"].astype(bool)), t
+        assert np.array_equal(g["substeps"][t], r["substeps"]), t
+        done = r["terminated"].astype(bool) | r["truncated"].astype(bool)
+        assert np.array_equal(g["final_obs"][t][done], r["final_obs"][done]), t  # the autoreset envs' terminal obs
     assert g["truncated"].any()
     sim.close()
 

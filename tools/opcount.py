@@ -210,9 +210,11 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "work_model.json"))
     ap.add_argument("--geometry", choices=("full", "lod"), default="full",
                     help="collision geometry of the counted trajectories: the counts land in tasks_full / tasks (lod)")
+    ap.add_argument("--contact", choices=("gjk", "vih"), default="gjk",
+                    help="contact generation of the counted trajectories: gjk (default) lands in tasks_full_gjk / tasks_gjk")
     args = ap.parse_args()
-    key = "tasks_full" if args.geometry == "full" else "tasks"
-    flags = 0 if args.geometry == "full" else 2  # UG_GEOM_LOD
+    key = ("tasks_full" if args.geometry == "full" else "tasks") + ("_gjk" if args.contact == "gjk" else "")
+    flags = (0 if args.geometry == "full" else 2) | (8 if args.contact == "vih" else 0)  # UG_GEOM_LOD, UG_CONTACT_VIH
     sys.path.insert(0, ROOT)
     from oracle import pyoracle
     from urgym_amd.envs import spaces_for
@@ -220,12 +222,14 @@ def main():
                      "(random actions in the action space, seeds 20241220 + env, autoreset at max_episode_steps); "
                      "FLOPs = add + sub + mul + div + sqrt + 2*fma, counted by tools/opcount.py (LLVM-IR op counters). "
                      "bench.py: achieved = F_sub * substeps + F_nonsub_per_env_step * env_steps per launch. "
-                     "tasks: the collision LOD (URGYM_FLAG_LOD_GEOMETRY); tasks_full: the default full geometry.",
-             "tasks": {}, "tasks_full": {}}
+                     "tasks: the collision LOD (URGYM_FLAG_LOD_GEOMETRY); tasks_full: the default full geometry; "
+                     "both with rounds 1-3's vertex-in-hull contacts (URGYM_FLAG_CONTACT_VIH); the _gjk keys: the same "
+                     "geometries with the default convex-convex GJK / EPA contacts.",
+             "tasks": {}, "tasks_full": {}, "tasks_gjk": {}, "tasks_full_gjk": {}}
     if os.path.exists(args.out):
         old = json.load(open(args.out))
-        model["tasks"] = old.get("tasks", {})
-        model["tasks_full"] = old.get("tasks_full", {})
+        for k in ("tasks", "tasks_full", "tasks_gjk", "tasks_full_gjk"):
+            model[k] = old.get(k, {})
     with tempfile.TemporaryDirectory() as tmp:
         so = build(tmp)
         pyoracle.LIB_PATH = so

@@ -1,4 +1,4 @@
-"""Summarise tools/pmc_mix.sh passes: per counter, the average over k_step launches and per wave (4096 waves per
+"""Summarise the tools/gpu.sh pmcmix passes: per counter, the average over k_step launches and per wave (4096 waves per
 launch at the default bench size).  usage: python tools/pmc_mix_summary.py <pmc_mix outdir> <out.csv> [waves]"""
 import collections
 import csv

@@ -19,12 +19,13 @@ SYMBOLS = [
     "urgym_link_state", "urgym_ik", "urgym_last_kernel_ms", "urgym_debug_prof", "urgym_debug_workspace",
     "urgym_debug_ws_doubles", "urgym_set_reward_type", "urgym_get_flags", "urgym_flags_device", "urgym_get_stats",
     "urgym_get_rng", "urgym_set_rng", "urgym_contact_points", "urgym_set_button_mode",
-    "urgym_camera_shot", "urgym_camera_shot_device",
+    "urgym_camera_shot", "urgym_camera_shot_device", "urgym_debug_gjk",
 ]
 
 # UG_FLAG_* / UG_STAT_* (urgym_amd/csrc/ug_layout.h)
 FLAG_UNSTABLE, FLAG_NONFINITE, FLAG_DROPPED = 1, 2, 4
 GEOM_FULL, GEOM_LOD = 1, 2  # urgym_create_ex flags: the full geometry (the default) / the collision LOD
+CONTACT_GJK, CONTACT_VIH = 4, 8  # contact generation: Bullet's GJK / EPA (the default) / rounds 1-3's vertex-in-hull
 STAT_NAMES = ["unstable_waits", "split_substeps", "row_capacity_substeps", "manifold_capacity_substeps",
               "nonfinite_terminations", "substeps", "reserved6", "reserved7"]
 CONTACT_FIELDS = 24  # pybullet getContactPoints tuple, flattened
@@ -46,7 +47,7 @@ def lib(robot="ur5_robotiq_85"):
                            "no CPU fallback exists")
     # torch, when installed, is loaded first: it bundles its own HIP runtime, and importing it after this library
     # has initialised the /opt/rocm runtime leaves torch.cuda unavailable in the process (measured on MI355X,
-    # tools/gpu_diag.sh); the other order works, and the device tensors / streams of vec.py need torch's side
+    # tools/gpu.sh history: round 3's load-order diagnosis); the other order works, and the device tensors / streams of vec.py need torch's side
     try:
         import torch  # noqa: F401
     except Exception:  # pragma: no cover - torch is part of this image
@@ -82,6 +83,7 @@ def lib(robot="ur5_robotiq_85"):
     L.urgym_debug_prof.argtypes = [P, P, I]
     L.urgym_debug_workspace.argtypes = [P, I, P, I]
     L.urgym_debug_ws_doubles.argtypes = []
+    L.urgym_debug_gjk.argtypes = [I, P, P, P]
     L.urgym_set_reward_type.argtypes = [P, I]
     L.urgym_set_button_mode.argtypes = [P, I]
     L.urgym_get_flags.argtypes = [P, P]

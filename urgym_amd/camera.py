@@ -50,6 +50,9 @@ def compute_projection_matrix_fov(fov, aspect, near, far):
     return tuple(float(v) for v in m)
 
 
+_MAX_BATCH = 65535  # envs per urgym_camera_shot call (include/urgym.h)
+
+
 class Camera:
     """utilities.py:62-74: a fixed camera; `shot()` renders the env it is attached to (the env classes attach it, or
     call `attach(sim, env)`), `shot(sim, env)` any env of a handle."""
@@ -99,11 +102,13 @@ class Camera:
         depth = np.zeros((count, H, W), np.float32)
         seg = np.zeros((count, H, W), np.int32)
         v, p = self._mats()
-        rc = sim.L.urgym_camera_shot(sim.h, env0, count, v.ctypes.data_as(ctypes.c_void_p),
-                                     p.ctypes.data_as(ctypes.c_void_p), W, H, SEG_LINK if link_index else 0,
-                                     rgb.ctypes.data_as(ctypes.c_void_p), depth.ctypes.data_as(ctypes.c_void_p),
-                                     seg.ctypes.data_as(ctypes.c_void_p))
-        sim._chk(rc, "urgym_camera_shot")
+        for c0 in range(0, count, _MAX_BATCH):  # one launch per 65,535 envs (the kernel's grid.y bound)
+            c = min(_MAX_BATCH, count - c0)
+            rc = sim.L.urgym_camera_shot(sim.h, env0 + c0, c, v.ctypes.data_as(ctypes.c_void_p),
+                                         p.ctypes.data_as(ctypes.c_void_p), W, H, SEG_LINK if link_index else 0,
+                                         rgb[c0:].ctypes.data_as(ctypes.c_void_p), depth[c0:].ctypes.data_as(ctypes.c_void_p),
+                                         seg[c0:].ctypes.data_as(ctypes.c_void_p))
+            sim._chk(rc, "urgym_camera_shot")
         return rgb, depth, seg
 
     def shot(self, sim=None, env=None, link_index=False):

@@ -40,12 +40,28 @@ __device__ static void box_collider(Collider* c, double hx, double hy, double hz
     c->rolling = 0.0;
     c->owner = -100; c->ent = 0;
     c->link = -1;
+    c->gjkbox = 0;
+    c->compound = 0;
 }
 __device__ static double safe_margin(double hx, double hy, double hz) {
     double m = hx < hy ? hx : hy;
     m = m < hz ? m : hz;
     m = 0.1 * m;
     return m < 0.04 ? m : 0.04;
+}
+/* Bullet's shape parameters for GJK (oracle gjk_params) */
+__device__ static void gjk_params(Collider* c) {
+    c->gimp = V(0, 0, 0);
+    c->gmargin = c->margin;
+    if (c->kind == UG_SHAPE_SPHERE) c->gmargin = c->half[0];
+    else if (c->kind == UG_SHAPE_BOX) c->gimp = V(c->half[0] - c->margin, c->half[1] - c->margin, c->half[2] - c->margin);
+    else if (c->kind == UG_SHAPE_CYL) {
+        const double r = c->half[0], hh = c->half[2];
+        double m = 0.1 * (r < hh ? r : hh);
+        if (m > 0.04) m = 0.04;
+        c->gmargin = m;
+        c->gimp = V(r - m, r - m, hh - m);
+    }
 }
 __device__ static void add_pair(Scene* s, int a, int b) {
     PairDef* p = &s->pair[s->npair++];
@@ -68,6 +84,7 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
     s->task = task;
     s->variant = variant;
     s->full = UG_GEOM_IS_FULL(flags);
+    s->gjk = UG_CONTACT_IS_GJK(flags);
     s->gravity = task == UG_TASK_CUBESGRASP ? -10.0 : -9.8;
     s->nobj = 0;
     s->ncol = 0;
@@ -104,6 +121,11 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
         c->owner = UG_LINK_BODY[l];
         c->ent = 0;
         c->link = l;
+        c->gjkbox = 0;
+        /* a link whose collision frame is not its inertial frame collides through a btCompoundShape (oracle) */
+        bool same = c->P.x == c->aP.x && c->P.y == c->aP.y && c->P.z == c->aP.z;
+        for (int i = 0; i < 9; i++) same = same && c->R.m[i] == c->aR.m[i];
+        c->compound = !same;
     }
     int nrobot = s->ncol;
     int statics[8], nstat = 0;
@@ -153,6 +175,7 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
         c->P = V(0.0, 0.0, -UG_PLANE_HALF_Z); c->aP = c->P;
         c->disc = ug_sqrt(15.0 * 15.0 * 2.0 + 25.0) + 5.0;
         c->owner = -100; c->ent = 11;
+        c->compound = 1;
         statics[nstat++] = s->ncol++;
     }
     if (task == UG_TASK_GOLF) {
@@ -218,6 +241,7 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
         c->P = V(0.0, 0.0, -0.5 - UG_PLANE_HALF_Z); c->aP = c->P;
         c->disc = ug_sqrt(15.0 * 15.0 * 2.0 + 25.0) + 5.0;
         c->owner = -100; c->ent = 11;
+        c->compound = 1;
         statics[nstat++] = s->ncol++;
     }
     if (task == UG_TASK_GOLF) {
@@ -226,6 +250,7 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
                      UG_GF_PITCH_HZ + UG_URDF_MARGIN, UG_URDF_MARGIN, UG_DEFAULT_FRICTION);
         c->P = V(UG_GF_PITCH_X, UG_GF_PITCH_Y, UG_GF_PITCH_Z); c->aP = c->P;
         c->owner = -100; c->ent = 12;
+        c->gjkbox = 1;
         statics[nstat++] = s->ncol++;
     }
     if (task == UG_TASK_BOX) {
@@ -256,6 +281,7 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
         c->P = V(B[0], B[1], B[2]); c->aP = c->P;
         c->disc = ddisc;
         c->owner = -2; c->ent = 1;
+        c->compound = 1;
         s->ocol[0] = s->ncol++;
         for (int i = 0; i < 3; i++) {
             const double* H = &UG_BX_HANDLE[4 * i];
@@ -266,6 +292,7 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
             if (i == 2) { double qh[4]; ugj_box_h3_quat(qh); c->R = qmat(Q(qh[0], qh[1], qh[2], qh[3])); c->aR = c->R; }
             c->disc = ddisc;
             c->owner = -2; c->ent = 1;
+            c->compound = 1;
         }
         s->oncol[0] = 4;
         c = &s->col[s->ncol];
@@ -293,6 +320,7 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
             c->P = V(UG_BX_WALL_POS[3 * w], UG_BX_WALL_POS[3 * w + 1] + by, UG_BX_WALL_POS[3 * w + 2]); c->aP = c->P;
             c->disc = wdisc;
             c->owner = -100; c->ent = 13;
+            c->compound = 1;
             statics[nstat++] = s->ncol++;
         }
         c = &s->col[s->ncol];
@@ -300,6 +328,7 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
         c->P = V(0.0, by, -UG_PLANE_HALF_Z); c->aP = c->P;
         c->disc = ug_sqrt(15.0 * 15.0 * 2.0 + 25.0) + 5.0;
         c->owner = -100; c->ent = 11;
+        c->compound = 1;
         statics[nstat++] = s->ncol++;
     }
     for (int o = 0; o < s->nobj; o++)
@@ -326,6 +355,33 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
                 if (task == UG_TASK_BOX && !(o == 1 && s->col[statics[t]].ent == 11)) continue;
                 add_pair(s, c, statics[t]);
             }
+    for (int i = 0; i < s->ncol; i++) gjk_params(&s->col[i]);
+}
+
+// development / test aid: one convex-convex query per wave (urgym_debug_gjk, tests/test_gpu_gjk.py).  Query i packs
+// 39 doubles: per shape kind, v0, nv, imp[3], margin, R[9], p[3], then thr.
+__global__ void __launch_bounds__(TEAM, 1) k_gjk_query(const double* q, int n, double* out, int* ok, ugk::EpaMem* E) {
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    const double* Q = q + (size_t)i * 39;
+    ugk::GShape S[2];
+    ugk::gx T[2];
+    for (int k = 0; k < 2; k++) {
+        const double* P = Q + 19 * k;
+        S[k].kind = (int)P[0]; S[k].v0 = (int)P[1]; S[k].nv = (int)P[2];
+        S[k].imp = ugk::V3(P[3], P[4], P[5]);
+        S[k].margin = P[6];
+        for (int j = 0; j < 9; j++) T[k].R.m[j] = P[7 + j];
+        T[k].p = ugk::V3(P[16], P[17], P[18]);
+    }
+    ugk::gv nn, pp;
+    double d = 0.0;
+    const bool r = ugk::gjk_pair(E + i, S[0], T[0], S[1], T[1], Q[38], nn, pp, d);
+    if (threadIdx.x == 0) {
+        ok[i] = r ? 1 : 0;
+        double* o = out + (size_t)i * 7;
+        o[0] = nn.x; o[1] = nn.y; o[2] = nn.z; o[3] = pp.x; o[4] = pp.y; o[5] = pp.z; o[6] = d;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -355,7 +411,7 @@ __global__ void __launch_bounds__(TEAM, 1) k_reset(const Scene* sc, double* S, u
     io.autoreset = 0;
     io.trunc = 0;
     PROF_T0(t_tot);
-    int ns = team_run(sc, ws + (size_t)i * WS_STRIDE(sc->full), G_RESET, io);
+    int ns = team_run(sc, ws + (size_t)i * WS_STRIDE(sc->full, sc->gjk), G_RESET, io);
     PROF_ADD(PF_TOTAL, t_tot);
     team_store(Si, stats + (size_t)i * UG_NSTAT, flags + i);
     team_prof_flush();
@@ -388,7 +444,7 @@ __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, ui
     io.trunc = (max_steps > 0 && el >= max_steps) ? 1 : 0;
     io.reset_done = 0;
     PROF_T0(t_tot);
-    int ns = team_run(sc, ws + (size_t)i * WS_STRIDE(sc->full), G_STEP, io);
+    int ns = team_run(sc, ws + (size_t)i * WS_STRIDE(sc->full, sc->gjk), G_STEP, io);
     PROF_ADD(PF_TOTAL, t_tot);
     team_store(Si, stats + (size_t)i * UG_NSTAT, flags + i);
     team_prof_flush();
@@ -447,7 +503,7 @@ __global__ void __launch_bounds__(TEAM, 1) k_substep(const Scene* sc, double* S,
     if (i >= n) return;
     double* Si = S + (size_t)i * UG_STATE_DIM;
     team_load(Si, stats + (size_t)i * UG_NSTAT);
-    team_substep(sc, ws + (size_t)i * WS_STRIDE(sc->full));
+    team_substep(sc, ws + (size_t)i * WS_STRIDE(sc->full, sc->gjk));
     team_store(Si, stats + (size_t)i * UG_NSTAT, nullptr);
 }
 
@@ -529,6 +585,10 @@ __global__ void __launch_bounds__(WAVE) k_contacts(const Scene* sc, const double
                     t2 = V(-nn.z * t1.y, nn.z * t1.x, a * kk);
                 }
                 if (swap) { v3 t = pA; pA = pB; pB = t; nn = vneg(nn); }
+                if (sc->task == UG_TASK_BOX) { /* Box-v0 keeps the robot base at the origin: back to world y */
+                    pA.y = pA.y + UG_BX_ROBOT_Y;
+                    pB.y = pB.y + UG_BX_ROBOT_Y;
+                }
                 o[0] = 0.0;
                 o[1] = swap ? eb : ea; o[2] = swap ? ea : eb;
                 o[3] = swap ? lb : la; o[4] = swap ? la : lb;
@@ -565,7 +625,9 @@ __global__ void __launch_bounds__(WAVE) k_camera_pose(const Scene* sc, const dou
     const XF T = shape_xf(owner_xf(e, k, c.owner), c);
     double* r = rec + ((size_t)blockIdx.x * MAXCOL + lane) * CAM_REC;
     for (int m = 0; m < 9; m++) r[m] = T.R.m[m];
-    r[9] = T.p.x; r[10] = T.p.y; r[11] = T.p.z;
+    /* the camera's view matrix is in world coordinates: Box-v0's poses are stored with the robot base at the origin
+     * (scene_data.h), so they move back by the base's world offset */
+    r[9] = T.p.x; r[10] = sc->task == UG_TASK_BOX ? T.p.y + UG_BX_ROBOT_Y : T.p.y; r[11] = T.p.z;
     r[12] = ugr_radius(c.kind, c.half, UG_HULL_V + 3 * c.v0, c.nv);
     ugr_hull_box(UG_HULL_V + 3 * c.v0, c.kind == UG_SHAPE_HULL ? c.nv : 0, r + 13);
     r[19] = collider_active(e, c) ? 1.0 : 0.0;
@@ -689,7 +751,7 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     size_t N = (size_t)n;
     HIPCHK(h, hipMalloc(&h->d_state, sizeof(double) * UG_STATE_DIM * N));
     HIPCHK(h, hipMalloc(&h->d_mt, sizeof(uint32_t) * UG_MT_WORDS * N));
-    HIPCHK(h, hipMalloc(&h->d_ws, sizeof(double) * WS_STRIDE(UG_GEOM_IS_FULL(flags)) * N));
+    HIPCHK(h, hipMalloc(&h->d_ws, sizeof(double) * WS_STRIDE(UG_GEOM_IS_FULL(flags), UG_CONTACT_IS_GJK(flags)) * N));
     HIPCHK(h, hipMalloc(&h->d_elapsed, sizeof(int) * N));
     HIPCHK(h, hipMalloc(&h->d_act, sizeof(float) * 9 * N));
     HIPCHK(h, hipMalloc(&h->d_obs, sizeof(double) * 17 * N));
@@ -708,7 +770,7 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     HIPCHK(h, hipMalloc(&h->d_flags, N));
     HIPCHK(h, hipMemsetAsync(h->d_stats, 0, sizeof(int) * UG_NSTAT * N, h->stream));
     /* the workspace starts zeroed: its separation certificates (WS_PC) must read "none" until written */
-    HIPCHK(h, hipMemsetAsync(h->d_ws, 0, sizeof(double) * WS_STRIDE(UG_GEOM_IS_FULL(flags)) * N, h->stream));
+    HIPCHK(h, hipMemsetAsync(h->d_ws, 0, sizeof(double) * WS_STRIDE(UG_GEOM_IS_FULL(flags), UG_CONTACT_IS_GJK(flags)) * N, h->stream));
     HIPCHK(h, hipMemsetAsync(h->d_flags, 0, N, h->stream));
     k_iota<<<grid_of(n), WAVE, 0, h->stream>>>(h->d_order, h->d_prio, n);
     HIPCHK(h, hipGetLastError());
@@ -729,8 +791,9 @@ urgym_handle* urgym_create(int task, int n, int dev, int precision, uint32_t see
 }
 
 urgym_handle* urgym_create_ex(int task, int n, int dev, int precision, uint32_t seed, int env_offset, int flags) {
-    if ((flags & ~(URGYM_FLAG_FULL_GEOMETRY | URGYM_FLAG_LOD_GEOMETRY)) ||
-        (flags & URGYM_FLAG_FULL_GEOMETRY && flags & URGYM_FLAG_LOD_GEOMETRY)) {
+    if ((flags & ~(URGYM_FLAG_FULL_GEOMETRY | URGYM_FLAG_LOD_GEOMETRY | URGYM_FLAG_CONTACT_GJK | URGYM_FLAG_CONTACT_VIH)) ||
+        (flags & URGYM_FLAG_FULL_GEOMETRY && flags & URGYM_FLAG_LOD_GEOMETRY) ||
+        (flags & URGYM_FLAG_CONTACT_GJK && flags & URGYM_FLAG_CONTACT_VIH)) {
         fail(nullptr, "urgym_create_ex: invalid flags " + std::to_string(flags));
         return nullptr;
     }
@@ -1081,12 +1144,33 @@ int urgym_debug_prof(urgym_handle* h, unsigned long long* out16, int reset) {
 
 // Development aid: copy env's per-env workspace (count doubles from its start) to the host.
 int urgym_debug_workspace(urgym_handle* h, int env, double* out, int count) {
-    if (!h || !out || env < 0 || env >= h->n || count < 0 || count > (int)WS_STRIDE(UG_GEOM_IS_FULL(h->flags))) return -1;
+    if (!h || !out || env < 0 || env >= h->n || count < 0 || count > (int)WS_STRIDE(UG_GEOM_IS_FULL(h->flags), UG_CONTACT_IS_GJK(h->flags))) return -1;
     HIPCHK(h, hipSetDevice(h->dev));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    HIPCHK(h, hipMemcpy(out, h->d_ws + (size_t)env * WS_STRIDE(UG_GEOM_IS_FULL(h->flags)), sizeof(double) * count, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy(out, h->d_ws + (size_t)env * WS_STRIDE(UG_GEOM_IS_FULL(h->flags), UG_CONTACT_IS_GJK(h->flags)), sizeof(double) * count, hipMemcpyDeviceToHost));
     return 0;
 }
-int urgym_debug_ws_doubles(void) { return (int)WS_STRIDE(0); } /* the LOD stride (the full geometry adds 7,488 doubles) */
+int urgym_debug_ws_doubles(void) { return (int)WS_STRIDE(0, 0); } /* the LOD vertex-in-hull stride */
+
+// Test aid: n convex-convex queries (39 doubles each, k_gjk_query) on device 0; out n x 7, ok n.
+int urgym_debug_gjk(int n, const double* q, double* out, int* ok) {
+    if (n <= 0 || !q || !out || !ok) return -1;
+    double *dq = nullptr, *dout = nullptr;
+    int* dok = nullptr;
+    ugk::EpaMem* E = nullptr;
+    if (hipMalloc(&dq, sizeof(double) * 39 * n) != hipSuccess || hipMalloc(&dout, sizeof(double) * 7 * n) != hipSuccess ||
+        hipMalloc(&dok, sizeof(int) * n) != hipSuccess || hipMalloc(&E, sizeof(ugk::EpaMem) * n) != hipSuccess)
+        return -1;
+    int rc = 0;
+    if (hipMemcpy(dq, q, sizeof(double) * 39 * n, hipMemcpyHostToDevice) != hipSuccess) rc = -1;
+    if (!rc) {
+        hipLaunchKernelGGL(k_gjk_query, dim3(n), dim3(TEAM), 0, 0, dq, n, dout, dok, E);
+        if (hipDeviceSynchronize() != hipSuccess) rc = -1;
+    }
+    if (!rc && hipMemcpy(out, dout, sizeof(double) * 7 * n, hipMemcpyDeviceToHost) != hipSuccess) rc = -1;
+    if (!rc && hipMemcpy(ok, dok, sizeof(int) * n, hipMemcpyDeviceToHost) != hipSuccess) rc = -1;
+    hipFree(dq); hipFree(dout); hipFree(dok); hipFree(E);
+    return rc;
+}
 
 }  // extern "C"

@@ -82,7 +82,10 @@ UG_HD int ug__rem_pio2(double x, double* y0, double* y1) {
     double yy0 = r - w;
     *y0 = yy0;
     *y1 = (r - yy0) - w;
-    return (int)fn;
+    /* the quadrant fn mod 4, exact for every integer-valued fn: (int)fn is undefined past 2^31 (x86 returns INT_MIN,
+     * gfx950 saturates), which made a runaway state's angles differ between the two builds; NaN gives quadrant 0 */
+    const double q4 = fn - 4.0 * __builtin_floor(fn * 0.25);
+    return q4 >= 0.0 && q4 < 4.0 ? (int)q4 : 0;
 }
 UG_HD double ug_sin(double x) {
     if (ug_fabs(x) <= 7.85398163397448278999e-01) return ug__ksin(x, 0.0);

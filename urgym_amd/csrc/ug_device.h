@@ -226,6 +226,11 @@ struct Collider {
     double disc;
     double friction, restitution, rolling;
     int owner, ent, link;
+    /* the convex-convex path (UG_CONTACT_GJK, ug_gjk.h): Bullet's shape as GJK sees it (oracle build_scene) */
+    v3 gimp;        /* box / cylinder implicit dimensions (outer minus margin) */
+    double gmargin; /* getMargin(): collision margin, a sphere's radius */
+    int gjkbox;     /* a convex mesh kept as its box (the Golf pitch): every pair of it is convex-convex */
+    int compound;   /* btCompoundShape collision object: its child manifolds are refreshed before the narrowphase */
 };
 struct PairDef { int a, b; double thr, friction, restitution, rolling; };
 struct Scene {
@@ -246,6 +251,7 @@ struct Scene {
     int sparse; /* reward_type != 'dense' (urgym_set_reward_type) */
     int button_mode; /* Box-v0 button_touch_mode (UG_BX_TOUCH_*, urgym_set_button_mode) */
     int full;   /* full-geometry mode (UG_GEOM_FULL): robot hulls with every vertex and face */
+    int gjk;    /* contact generation: 1 Bullet's convex-convex GJK / EPA (the default), 0 vertex-in-hull */
 };
 
 struct CPoint { v3 lpA, lpB, n; double dist, imp, imp1, imp2; };

@@ -29,6 +29,8 @@
 #include "ug_device.h"
 #include "prio_model.h"
 #include "ug_glue.h"
+#define UGK_FN __device__ static inline
+#include "ug_gjk.h"
 
 namespace ugd {
 
@@ -75,11 +77,16 @@ static_assert(UG_FULL_HULL_MAXV + 64 + 8 <= FC_MAX, "a full hull pair's candidat
 #ifdef UG_DEBUG_DUMP /* development aid: team_pgs dumps A, w and impulses after the workspace proper */
 #define WS_DBG WS_FULL_DOUBLES
 #define WS_DOUBLES (WS_DBG + MAXROWS * MAXROWS + 8 * MAXROWS)
-#define WS_STRIDE(full) ((size_t)WS_DOUBLES)
+#define WS_STRIDE_VIH(full) ((size_t)WS_DOUBLES)
 #else
 #define WS_DOUBLES WS_FULL_DOUBLES
-#define WS_STRIDE(full) ((size_t)((full) ? WS_FULL_DOUBLES : WS_LOD_DOUBLES))
+#define WS_STRIDE_VIH(full) ((size_t)((full) ? WS_FULL_DOUBLES : WS_LOD_DOUBLES))
 #endif
+/* the convex-convex path (UG_CONTACT_GJK): the penetration solver's store (ug_gjk.h EpaMem: btGjkEpa2's 132 support
+ * vertices, 256 faces and their lists, the horizon walk's stack) after everything else */
+#define WS_EPA WS_DOUBLES
+#define EPA_DOUBLES ((sizeof(ugk::EpaMem) + sizeof(double) - 1) / sizeof(double))
+#define WS_STRIDE(full, gjk) ((gjk) ? (size_t)(WS_EPA + EPA_DOUBLES) : WS_STRIDE_VIH(full))
 
 #define MAXOV 26 /* pairs per lane-per-pair pass: their working manifolds share LDS with the rows (Shared::pm) */
 #define NBOXSLOT 5 /* box-box pairs run per round, one LDS clip-buffer slot each (they share the hull candidates' LDS) */
@@ -265,6 +272,26 @@ __device__ __forceinline__ void wave_best(double& v, int& idx, bool want_max) {
     v = bv;
     idx = bi;
 }
+
+} /* namespace ugd */
+/* ug_gjk.h's hull support on the wave: lane l dots vertices l, l + 64, ... (each lane keeps its first maximum), then
+ * the DPP arg-max keeps the larger value and, on a tie, the lower index -- btVector3::maxDot's first maximum over the
+ * whole hull.  Called by every lane of the env's wave (the GJK runs uniformly). */
+UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
+    const int lane = threadIdx.x;
+    double best = -__builtin_inf();
+    int bi = 0x7fffffff;
+    for (int i = lane; i < nv; i += TEAM) {
+        const double* p = &UG_HULL_V[3 * (v0 + i)];
+        const double dd = p[0] * d.x + p[1] * d.y + p[2] * d.z;
+        if (dd > best) { best = dd; bi = i; }
+    }
+    ugd::wave_best(best, bi, true);
+    if (bi == 0x7fffffff) bi = 0;
+    const double* p = &UG_HULL_V[3 * (v0 + bi)];
+    return ugk::V3(p[0], p[1], p[2]);
+}
+namespace ugd {
 
 /* ---------------- env-state helpers (lane-serial) ---------------- */
 __device__ static XF owner_xf(const EnvState& e, const Kin& k, int owner) {
@@ -558,8 +585,13 @@ __device__ __forceinline__ void gc_publish() { /* the wave's workspace stores, v
 /* candidate i to the workspace list, and to the LDS list (g_sh.hc) while it fits: a pair that ends with at most 64
  * candidates is reduced from LDS (team_reduce4), a larger one from the workspace (team_reduce4_g) */
 __device__ __forceinline__ void fc_put(gdouble* gc, int i, const Cand& c) {
-    gc_put(gc, i, c);
+    if (i < FC_MAX) gc_put(gc, i, c); /* beyond the list's capacity a candidate is dropped, as the oracle's cand_add */
     if (i < 64) g_sh.hc[i] = c;
+}
+/* the list length after a chunk's m candidates were appended at n (capped at the capacity, oracle cand_add) */
+__device__ __forceinline__ int fc_count(int n, unsigned long long m) {
+    const int t = n + __popcll(m);
+    return t < FC_MAX ? t : FC_MAX;
 }
 __device__ __forceinline__ static void team_reduce4(int n, int k);
 __device__ __forceinline__ void fc_reduce(int n, int k, gdouble* gc);
@@ -707,7 +739,7 @@ __device__ __forceinline__ static void team_hull_box_full(const HullArg& A, cons
         }
         const unsigned long long vb = ballot(vvalid);
         if (vvalid) fc_put(gc, n + lane_prefix(vb), vc);
-        n += __popcll(vb);
+        n = fc_count(n, vb);
     }
     PROF_ADD(PF_HB_VERT, t_hv);
     PROF_T0(t_hc);
@@ -778,7 +810,7 @@ __device__ __forceinline__ static void team_hull_box_full(const HullArg& A, cons
     }
     const unsigned long long cb = ballot(cvalid);
     if (cvalid) fc_put(gc, n + lane_prefix(cb), cc);
-    n += __popcll(cb);
+    n = fc_count(n, cb);
     if (n == 0) {
         /* candidate-free: certify when every box corner clears its face of A and the whole hull lies beyond one box
          * face plane, each by a positive margin (a vertex beyond a face plane by more than thr + margin is that far
@@ -846,7 +878,7 @@ __device__ __forceinline__ static void team_hull_hull_full(const HullArg& A, con
         }
         const unsigned long long m = ballot(valid);
         if (valid) fc_put(gc, n + lane_prefix(m), ac);
-        n += __popcll(m);
+        n = fc_count(n, m);
     }
     const m3 RBA = mtm(TA.R, TB.R);
     const v3 pBA = mtv(TA.R, vsub(TB.p, TA.p));
@@ -873,7 +905,7 @@ __device__ __forceinline__ static void team_hull_hull_full(const HullArg& A, con
         }
         const unsigned long long m = ballot(valid);
         if (valid) fc_put(gc, n + lane_prefix(m), bc);
-        n += __popcll(m);
+        n = fc_count(n, m);
     }
     fc_reduce(n, k, gc);
 }
@@ -948,7 +980,7 @@ __device__ __forceinline__ static void team_poly_cyl(int k, bool swapped, gdoubl
         }
         const unsigned long long m = ballot(valid);
         if (valid) fc_put(gc, n + lane_prefix(m), c);
-        n += __popcll(m);
+        n = fc_count(n, m);
     }
     const m3 RBA = mtm(TA.R, TB.R);
     const v3 pBA = mtv(TA.R, vsub(TB.p, TA.p));
@@ -1056,7 +1088,7 @@ __device__ __forceinline__ static void team_poly_cyl(int k, bool swapped, gdoubl
         }
         const unsigned long long m = ballot(valid);
         if (valid) fc_put(gc, n + lane_prefix(m), c);
-        n += __popcll(m);
+        n = fc_count(n, m);
 #ifdef UG_PROF
         PROF_CNT(PC_CYIT, (int)wave_max_d((double)iters));
 #endif
@@ -1398,7 +1430,60 @@ __device__ __forceinline__ static void team_box_box(const XF& TA, const double (
 /* performDiscreteCollisionDetection (oracle collide()), team version.  ws: this env's global workspace. */
 /* FULL: the full-geometry instantiation (UG_GEOM_FULL); the LOD one has no calls into the full-hull functions, so
  * its register allocation is that of the LOD path alone */
-template <bool FULL>
+/* the convex-convex path: pairs without a dedicated Bullet algorithm (oracle pair_is_gjk) */
+__device__ __forceinline__ static bool pair_is_gjk(const Collider& A, const Collider& B) {
+    if (A.gjkbox || B.gjkbox) return true;
+    const bool pa = A.kind == UG_SHAPE_SPHERE || A.kind == UG_SHAPE_BOX;
+    const bool pb = B.kind == UG_SHAPE_SPHERE || B.kind == UG_SHAPE_BOX;
+    return !(pa && pb);
+}
+__device__ __forceinline__ static ugk::GShape gshape_of(const Collider& c) {
+    ugk::GShape g;
+    g.kind = c.kind;
+    g.v0 = c.v0;
+    g.nv = c.kind == UG_SHAPE_HULL ? c.nv : 0;
+    g.imp = ugk::V3(c.gimp.x, c.gimp.y, c.gimp.z);
+    g.margin = c.gmargin;
+    return g;
+}
+__device__ __forceinline__ static ugk::gx to_gx(const XF& T) {
+    ugk::gx r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.R.m[i] = T.R.m[i];
+    r.p = ugk::V3(T.p.x, T.p.y, T.p.z);
+    return r;
+}
+/* pair k of the pass (sh.pinfo[k]) through btGjkPairDetector on the whole wave (ug_gjk.h): at most one point, written
+ * to cand k in this restatement's pair order (a sphere-first pair runs with the sphere as GJK's B, then flipped --
+ * oracle nc_gjk) */
+__device__ __noinline__ static void team_gjk(const Scene* s, int k, ugk::EpaMem* E) {
+    Shared& sh = g_sh;
+    const int a = sh.pinfo[k].a, b = sh.pinfo[k].b;
+    const Collider& A = s->col[a];
+    const Collider& B = s->col[b];
+    const ugk::GShape ga = gshape_of(A), gb = gshape_of(B);
+    const ugk::gx TA = to_gx(sh.pinfo[k].TA), TB = to_gx(sh.pinfo[k].TB);
+    const double thr = sh.pinfo[k].thr;
+    const bool swap = A.kind == UG_SHAPE_SPHERE && B.kind != UG_SHAPE_SPHERE;
+    ugk::gv n, p;
+    double d = 0.0;
+    const bool ok = swap ? ugk::gjk_pair(E, gb, TB, ga, TA, thr, n, p, d) : ugk::gjk_pair(E, ga, TA, gb, TB, thr, n, p, d);
+    v3 cn = V(n.x, n.y, n.z), cp = V(p.x, p.y, p.z);
+    if (swap) {
+        cp = vadd(cp, vscale(cn, d));
+        cn = vneg(cn);
+    }
+    if (threadIdx.x == 0) {
+        sh.u.cand.n[k] = ok ? 1 : 0;
+        sh.u.cand.c[k][0].n = cn;
+        sh.u.cand.c[k][0].pB = cp;
+        sh.u.cand.c[k][0].d = d;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <bool FULL, bool GJK>
 __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
@@ -1463,10 +1548,11 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
             pi.a = P.a; pi.b = P.b; pi.ka = A.kind; pi.kb = B.kind;
             sh.pinfo[lane] = pi;
             hk = A.kind == UG_SHAPE_HULL && (B.kind == UG_SHAPE_BOX || B.kind == UG_SHAPE_HULL);
-            if (FULL) /* the disc cylinder against a polytope, either side */
+            if (GJK) hk = pair_is_gjk(A, B); /* the wave runs the pair's GJK / EPA */
+            else if (FULL) /* the disc cylinder against a polytope, either side */
                 hk = hk || (B.kind == UG_SHAPE_CYL && (A.kind == UG_SHAPE_HULL || A.kind == UG_SHAPE_BOX)) ||
                      (A.kind == UG_SHAPE_CYL && B.kind == UG_SHAPE_BOX);
-            if (FULL && A.kind == UG_SHAPE_HULL && (B.kind == UG_SHAPE_BOX || B.kind == UG_SHAPE_CYL) && A.nv > TEAM) {
+            if (!GJK && FULL && A.kind == UG_SHAPE_HULL && (B.kind == UG_SHAPE_BOX || B.kind == UG_SHAPE_CYL) && A.nv > TEAM) {
                 /* the pair's separation certificate (team_hull_box_full / team_poly_cyl): while no point of either
                  * shape can have moved by its slack since, the evaluation would find no candidate -- skip it.  Every
                  * A vertex lies within rA of A's origin and every point of B within rB of B's, so a point moves by at
@@ -1511,6 +1597,11 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         if (lane == 0) sh.is[3] = c0; /* the pass's first pair (team_poly_cyl's certificate slot) */
         for (unsigned long long hm = ballot(hk); hm != 0ull; hm &= hm - 1ull) {
             const int k = __builtin_ctzll(hm);
+            if (GJK) {
+                team_gjk(s, k, (ugk::EpaMem*)(ws + WS_EPA));
+                PROF_CNT(PC_HULL, 1);
+                continue;
+            }
             const PairInfo pi = sh.pinfo[k];
             if (FULL && (pi.kb == UG_SHAPE_CYL || pi.ka == UG_SHAPE_CYL))
                 team_poly_cyl(k, pi.ka == UG_SHAPE_CYL, (gdouble*)(ws + WS_FC));
@@ -1570,8 +1661,11 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
             CandList L;
             L.n = 0;
             L.c = (LCand*)&sh.u.cand.c[lane][0];
-            isbb = A.kind == UG_SHAPE_BOX && B.kind == UG_SHAPE_BOX;
-            if ((A.kind == UG_SHAPE_HULL && (B.kind == UG_SHAPE_BOX || B.kind == UG_SHAPE_HULL)) ||
+            const bool gj = GJK && pair_is_gjk(A, B);
+            isbb = A.kind == UG_SHAPE_BOX && B.kind == UG_SHAPE_BOX && !gj;
+            if (gj) {
+                L.n = sh.u.cand.n[lane]; /* team_gjk wrote it */
+            } else if ((A.kind == UG_SHAPE_HULL && (B.kind == UG_SHAPE_BOX || B.kind == UG_SHAPE_HULL)) ||
                 (FULL && ((B.kind == UG_SHAPE_CYL && A.kind != UG_SHAPE_SPHERE) || A.kind == UG_SHAPE_CYL))) {
                 L.n = sh.u.cand.n[lane]; /* team_hull_box / team_hull_hull / team_poly_cyl wrote them */
             } else if (FULL && A.kind == UG_SHAPE_SPHERE && B.kind == UG_SHAPE_CYL) {
@@ -1638,6 +1732,8 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
             L.n = sh.u.cand.n[lane];
             L.c = (LCand*)&sh.u.cand.c[lane][0];
             PROF_T0(t_pm);
+            /* a compound collision object refreshes its child manifolds before the narrowphase (oracle collide) */
+            if (GJK && (s->col[P.a].compound || s->col[P.b].compound) && M.npts) manifold_refresh(M, sh.O[P.a], sh.O[P.b], P.thr);
             for (int i = 0; i < L.n; i++) {
                 Cand c;
                 c.n = ldv(L.c[i].n);
@@ -3509,8 +3605,13 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     __syncthreads();
     PROF_ADD(PF_FK, t_col);
     const double ov0 = e.overflow;
-    if (s->full) team_collide<true>(s, ws);
-    else team_collide<false>(s, ws);
+    if (s->gjk) {
+        if (s->full) team_collide<true, true>(s, ws);
+        else team_collide<false, true>(s, ws);
+    } else {
+        if (s->full) team_collide<true, false>(s, ws);
+        else team_collide<false, false>(s, ws);
+    }
     const double ov1 = e.overflow;
     if (lane == 0) {
         sh.stats[UG_STAT_SUBSTEPS]++;
@@ -4071,6 +4172,19 @@ __device__ __forceinline__ static int team_nonfinite(const Scene* s) {
     }
     return ballot(bad) != 0ull;
 }
+/* the non-finite guard voids a runaway state (oracle poison): q, qd and the active objects' state NaN, no contacts */
+__device__ __forceinline__ static void team_poison(const Scene* s) {
+    EnvState& e = g_sh.e;
+    const int lane = threadIdx.x;
+    if (lane < NB) { e.q[lane] = __builtin_nan(""); e.qd[lane] = __builtin_nan(""); }
+    const int j = lane - NB;
+    if (j >= 0 && j < MAXOBJ * UG_OBJ_DOUBLES) {
+        const int o = j / UG_OBJ_DOUBLES;
+        if (o < s->nobj && e.oactive[o] != 0.0) (&e.obj[0].pos.x)[j] = __builtin_nan("");
+    }
+    if (lane == 0) e.nman = 0.0;
+    __syncthreads();
+}
 /* runs the program from pc0 to the end; returns physics substeps taken */
 __device__ __forceinline__ static int team_run(const Scene* s, double* ws, int pc0, RunIO& io) {
     Shared& sh = g_sh;
@@ -4097,7 +4211,10 @@ __device__ __forceinline__ static int team_run(const Scene* s, double* ws, int p
             team_substep(s, ws);
             ns++;
             /* a non-finite state ends the loop at once (oracle wait_until_stable / robot_reset) */
-            if (team_nonfinite(s)) break;
+            if (team_nonfinite(s)) {
+                team_poison(s);
+                break;
+            }
             if (loop == L_FIXED10 || loop == L_FIXED120) { /* robot.reset's 10 substeps / Box's 120 per step */
                 if (i + 1 == (loop == L_FIXED10 ? 10 : UG_BX_STEPS)) break;
                 continue;

@@ -107,12 +107,21 @@ class URGymVectorEnv(_VecBase):
         self.max_episode_steps = max_episode_steps or 0
         self.sim.set_autoreset(True, self.max_episode_steps)
         self.render_mode = render_mode  # accepted; there is no GUI ('human' opens no window: documented deviation)
-        self.camera, self.camera_obs = camera, None
+        self.camera, self._camera_obs, self._camera_dirty = camera, None, False
 
     def _shoot(self):
-        if self.camera is not None and self.task in _CAMERA_TASKS:  # every env's image, one launch
+        # the reference shoots in get_observation but returns only the vector observation (env_cubes_grasp_v0.py,
+        # env_box_v0.py): the batch is rendered when camera_obs is first read after a reset / step -- the same state
+        # -- instead of copying every env's image to the host on every call
+        self._camera_dirty = self.camera is not None and self.task in _CAMERA_TASKS
+
+    @property
+    def camera_obs(self):
+        if self._camera_dirty:  # every env's image, one launch per 65,535 envs
             rgb, depth, seg = self.camera.shot_batch(self.sim)
-            self.camera_obs = dict(rgb=rgb, depth=depth, seg=seg)
+            self._camera_obs = dict(rgb=rgb, depth=depth, seg=seg)
+            self._camera_dirty = False
+        return self._camera_obs
 
     def reset(self, *, seed=None, options=None):
         obs = self.sim.reset()

@@ -4,9 +4,10 @@ Environments are independent, so the path shards with no exchange inside a
 step: rank r owns the contiguous env-id range [r*n, (r+1)*n), seeds env i's
 MT19937 stream with seed + i (results are independent of the world size), and
 runs its shard on its own GPU.  The only collective is the per-step all-gather
-of the returns (obs | reward | terminated | truncated) for a consumer that
-needs the whole batch (a central policy): torch.distributed backend "nccl" is
-RCCL over xGMI on MI355X; tests use "gloo" on CPU.
+of the returns (obs | final_obs | reward | terminated | truncated | is_success |
+substeps, ReturnGather) for a consumer that needs the whole batch (a central
+policy): torch.distributed backend "nccl" is RCCL over xGMI on MI355X; tests use
+"gloo" on CPU.
 """
 import os
 import socket
@@ -49,26 +50,56 @@ def shard(total_envs, world_size, rank):
     return rank * n, n
 
 
-def pack_returns(obs, reward, terminated, truncated):
-    """One contiguous FP64 [n, obs_dim + 3] buffer per step -> a single all-gather."""
+FIELDS = ("obs", "final_obs", "reward", "terminated", "truncated", "success", "substeps")
+
+
+class ReturnGather:
+    """The per-step all-gather of a rank's returns for a consumer of the whole batch (a central policy, an autoreset
+    learner): obs | final_obs | reward | terminated | truncated | is_success | substeps (final_obs is the
+    terminal observation of an autoreset env, env_*'s step() return before the reset) packed into ONE preallocated FP64
+    row per env and moved with a single dist.all_gather_into_tensor (RCCL over xGMI with the nccl backend, straight
+    from HBM; gloo through host memory) into a preallocated global buffer.  gather() returns views of that buffer in
+    global env-id order (rank-major): no per-step allocation, list or concatenation."""
+
+    def __init__(self, n_local, obs_dim, device, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.o = obs_dim
+        self.width = 2 * obs_dim + 5
+        host = dist.get_backend(group) == "gloo"
+        dev = torch.device("cpu") if host else torch.device(device)
+        self.send = torch.zeros(n_local, self.width, dtype=torch.float64, device=dev)
+        self.recv = torch.zeros(self.world * n_local, self.width, dtype=torch.float64, device=dev)
+        o = obs_dim
+        self.views = {"obs": self.recv[:, :o], "final_obs": self.recv[:, o:2 * o], "reward": self.recv[:, 2 * o],
+                      "terminated": self.recv[:, 2 * o + 1], "truncated": self.recv[:, 2 * o + 2],
+                      "success": self.recv[:, 2 * o + 3], "substeps": self.recv[:, 2 * o + 4]}
+
+    def gather(self, obs, final_obs, reward, terminated, truncated, success, substeps):
+        o, b = self.o, self.send
+        b[:, :o].copy_(obs)
+        b[:, o:2 * o].copy_(final_obs)
+        b[:, 2 * o].copy_(reward)
+        b[:, 2 * o + 1].copy_(terminated)
+        b[:, 2 * o + 2].copy_(truncated)
+        b[:, 2 * o + 3].copy_(success)
+        b[:, 2 * o + 4].copy_(substeps)
+        dist.all_gather_into_tensor(self.recv, b, group=self.group)
+        return self.views
+
+    def decoded(self):
+        """the last gather with the flags as bool and the substep counts as int32 (host-side consumers)"""
+        v = self.views
+        return {"obs": v["obs"], "final_obs": v["final_obs"], "reward": v["reward"], "terminated": v["terminated"] > 0.5,
+                "truncated": v["truncated"] > 0.5, "success": v["success"] > 0.5, "substeps": v["substeps"].to(torch.int32)}
+
+
+def gather_returns(obs, reward, terminated, truncated, final_obs=None, success=None, substeps=None, group=None):
+    """One-off form of ReturnGather (tests, scripts): every field gathered, missing ones as zeros; returns the
+    decoded dict in global env-id order.  Per-step loops keep one ReturnGather instead."""
     n, o = obs.shape
-    buf = torch.empty(n, o + 3, dtype=torch.float64, device=obs.device)
-    buf[:, :o] = obs
-    buf[:, o] = reward
-    buf[:, o + 1] = terminated.to(torch.float64)
-    buf[:, o + 2] = truncated.to(torch.float64)
-    return buf
-
-
-def gather_returns(obs, reward, terminated, truncated, group=None):
-    """All-gather every rank's returns; result is in global env-id order (rank-major).  RCCL gathers HBM
-    buffers directly; under gloo (CPU tests, single-GPU rehearsals) the buffer goes through host memory."""
-    buf = pack_returns(obs, reward, terminated, truncated)
-    if dist.get_backend(group) == "gloo" and buf.is_cuda:
-        buf = buf.cpu()
-    world = dist.get_world_size(group)
-    out = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(out, buf, group=group)
-    full = torch.cat(out, 0)
-    o = obs.shape[1]
-    return full[:, :o], full[:, o], full[:, o + 1] > 0.5, full[:, o + 2] > 0.5
+    g = ReturnGather(n, o, obs.device, group)
+    z = torch.zeros(n, dtype=torch.float64)
+    g.gather(obs, obs if final_obs is None else final_obs, reward, terminated, truncated, z if success is None else success,
+             z if substeps is None else substeps)
+    return g.decoded()
