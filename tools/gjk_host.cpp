@@ -26,6 +26,28 @@ UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
     return ugk::V3(p[0], p[1], p[2]);
 }
 
+UGK_FN void ugk_epa_reset_lists(ugk::EpaMem* E) {
+    for (int i = 0; i < ugk::kEpaMaxFaces; i++) {
+        E->stock[i] = ugk::kEpaMaxFaces - 1 - i;
+        E->fc[i].inhull = 0;
+    }
+}
+/* m_hull's first minimum of d * d: the largest stamp among the minima; a NaN at the root (the largest stamp) wins */
+UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E) {
+    int root = -1;
+    for (int f = 0; f < ugk::kEpaMaxFaces; f++)
+        if (E->fc[f].inhull && (root < 0 || E->fc[f].stamp > E->fc[root].stamp)) root = f;
+    double mind = E->fc[root].d * E->fc[root].d;
+    if (mind != mind) return root;
+    int best = root;
+    for (int f = 0; f < ugk::kEpaMaxFaces; f++) {
+        if (!E->fc[f].inhull) continue;
+        const double sqd = E->fc[f].d * E->fc[f].d;
+        if (sqd < mind || (sqd == mind && E->fc[f].stamp > E->fc[best].stamp)) { best = f; mind = sqd; }
+    }
+    return best;
+}
+
 static ugk::EpaMem g_epa;
 
 /* shape: kind, v0, nv, imp[3], margin; pose: R (row-major 9), p (3).  out: n[3], pB[3], d.  Returns 1 with a point. */

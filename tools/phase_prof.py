@@ -35,13 +35,15 @@ def main():
     ap.add_argument("--task", type=int, default=0)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--geometry", choices=("lod", "full"), default="full")
+    ap.add_argument("--contact", choices=("gjk", "vih"), default="gjk")
     a = ap.parse_args()
-    from urgym_amd._native import GEOM_LOD, Sim
-    sim = Sim(a.task, a.envs, seed=20241220, flags=GEOM_LOD if a.geometry == "lod" else 0)
+    from urgym_amd._native import CONTACT_VIH, GEOM_LOD, Sim
+    sim = Sim(a.task, a.envs, seed=20241220,
+              flags=(GEOM_LOD if a.geometry == "lod" else 0) | (CONTACT_VIH if a.contact == "vih" else 0))
     from urgym_amd.envs import spaces_for
     _, asp = spaces_for(a.task)
     sim.set_autoreset(True, 500)
-    buf = np.zeros(80, np.uint64)
+    buf = np.zeros(96, np.uint64)
     sim.reset()
     sim.sync()
     rc = sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
@@ -84,6 +86,12 @@ def main():
               "sw_fric_prep", "sw_fric", "sw_res", "pr_lookup", "pr_narrow", "pr_manifold", "pr_store", "integrate", "pr_boxbox", "hull_sphere",
               "cyl_pairs", "cyl_pass1", "cyl_pass2", "cyl_survivors", "cyl_scan_iters"):
         out[k + "_cycles_per_substep"] = d[k] / max(d["substeps"], 1)
+    gj = dict(zip(["gjk_queries", "gjk_epa_queries", "gjk_iterations", "gjk_ccd_iterations", "gjk_hull_supports",
+                   "gjk_hull_support_cycles", "epa_iterations", "gjk_cycles_reporting_queries", "gjk_penetration_cycles",
+                   "gjk_ccd_cycles", "gjk_classic_cycles", "epa_gjk_cycles", "epa_setup_cycles", "epa_support_cycles",
+                   "epa_expand_cycles", "epa_findbest_cycles"], [float(x) for x in buf[80:96]]))
+    out["gjk_per_substep"] = {k: v / max(d["substeps"], 1) for k, v in gj.items()}
+    out["gjk_cycles_per_hull_support"] = gj["gjk_hull_support_cycles"] / max(gj["gjk_hull_supports"], 1)
     print(json.dumps(out, indent=1))
     sim.close()
 

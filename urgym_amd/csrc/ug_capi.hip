@@ -62,6 +62,18 @@ __device__ static void gjk_params(Collider* c) {
         c->gmargin = m;
         c->gimp = V(r - m, r - m, hh - m);
     }
+    /* the certificate's rotation bound (team_collide): every core support point lies within gradius of the origin */
+    double r2 = 0.0;
+    if (c->kind == UG_SHAPE_HULL) {
+        for (int i = 0; i < c->nv; i++) {
+            const double* v = &UG_HULL_V[3 * (c->v0 + i)];
+            const double x = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+            r2 = x > r2 ? x : r2;
+        }
+    } else if (c->kind == UG_SHAPE_BOX || c->kind == UG_SHAPE_CYL) {
+        r2 = c->gimp.x * c->gimp.x + c->gimp.y * c->gimp.y + c->gimp.z * c->gimp.z;
+    }
+    c->gradius = ug_sqrt(r2) * (1.0 + 1e-12) + 1e-15;
 }
 __device__ static void add_pair(Scene* s, int a, int b) {
     PairDef* p = &s->pair[s->npair++];

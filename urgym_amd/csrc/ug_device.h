@@ -230,6 +230,7 @@ struct Collider {
     v3 gimp;        /* box / cylinder implicit dimensions (outer minus margin) */
     double gmargin; /* getMargin(): collision margin, a sphere's radius */
     int gjkbox;     /* a convex mesh kept as its box (the Golf pitch): every pair of it is convex-convex */
+    double gradius; /* the largest distance of a core support point from the shape origin (certificate bound) */
     int compound;   /* btCompoundShape collision object: its child manifolds are refreshed before the narrowphase */
 };
 struct PairDef { int a, b; double thr, friction, restitution, rolling; };

@@ -26,6 +26,12 @@
 #include "scene_data.h"
 #include "ug_detmath.h"
 
+#ifndef UGK_COUNT /* the includer's event counter and timer hooks (the kernels' -DUG_PROF build) */
+#define UGK_COUNT(k, v) do { } while (0)
+#define UGK_T0(v)
+#define UGK_ADD(k, v) do { } while (0)
+#endif
+
 namespace ugk {
 
 struct gv { double x, y, z; };
@@ -340,7 +346,10 @@ UGK_FN bool vs_in(const Voronoi& s, gv w) {
 
 /* ---------------- btGjkEpa2: GJK + EPA in the global workspace ---------------- */
 struct ESv { gv d, w; };
-struct EFace { gv n; double d; int c[3], f[3], l[2], e[3], pass; };
+/* a face; Bullet's two intrusive lists become: the free faces a stack (m_stock is only ever popped at its root and
+ * pushed there), the hull a membership flag plus an append stamp (m_hull's list order is most recently appended
+ * first, so its first minimum is the largest stamp among the minima -- what ugk_epa_findbest returns) */
+struct EFace { gv n; double d; int c[3], f[3], e[3], pass, inhull, stamp; };
 struct EpaMem {
     ESv sv[4 + kEpaMaxVertices]; /* [0, 4) the GJK's store, then the EPA's */
     EFace fc[kEpaMaxFaces];
@@ -349,6 +358,7 @@ struct EpaMem {
     int srank[2];
     int freev[4];
     int stk[3 * kEpaMaxFaces];   /* expand()'s frames: face, edge, stage */
+    int stock[kEpaMaxFaces];     /* the free faces, top = the list root */
 };
 struct Mink { GShape s0, s1; gm toshape1; gx toshape0; bool margins; };
 UGK_FN gv mk_ls(const Mink& M, int i, gv d) {
@@ -613,25 +623,30 @@ UGK_FN bool g2_enclose(EpaMem* E, Gjk2& g, const Mink& M) {
     return false;
 }
 
-struct Epa { int status, nextsv, hroot, hcount, sroot, scount; gv normal; double depth; int rc[3]; double rp[3]; int rrank; };
+struct Epa { int status, nextsv, hcount, nstock, stampctr; gv normal; double depth; int rc[3]; double rp[3]; int rrank; };
+
+} /* namespace ugk */
+/* the includer's EPA list hooks: the free-face stack set to Bullet's initial order (faces 0, 1, 2, ... popped first) and
+ * every face out of the hull; the hull face with the smallest d * d, ties to the largest stamp (m_hull's first
+ * minimum), except that a NaN at the list root keeps the root (Bullet's loop never replaces a NaN) */
+UGK_FN void ugk_epa_reset_lists(ugk::EpaMem* E);
+UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E);
+namespace ugk {
+
 UGK_FN void e_bind(EpaMem* E, int fa, int ea, int fb, int eb) {
     E->fc[fa].e[ea] = eb; E->fc[fa].f[ea] = fb;
     E->fc[fb].e[eb] = ea; E->fc[fb].f[eb] = fa;
 }
-UGK_FN void e_append(EpaMem* E, int& root, int& count, int f) {
-    E->fc[f].l[0] = -1;
-    E->fc[f].l[1] = root;
-    if (root >= 0) E->fc[root].l[0] = f;
-    root = f;
-    count++;
+UGK_FN void h_append(EpaMem* E, Epa& P, int f) {
+    E->fc[f].inhull = 1;
+    E->fc[f].stamp = ++P.stampctr;
+    P.hcount++;
 }
-UGK_FN void e_remove(EpaMem* E, int& root, int& count, int f) {
-    const int l0 = E->fc[f].l[0], l1 = E->fc[f].l[1];
-    if (l1 >= 0) E->fc[l1].l[0] = l0;
-    if (l0 >= 0) E->fc[l0].l[1] = l1;
-    if (f == root) root = l1;
-    count--;
+UGK_FN void h_remove(EpaMem* E, Epa& P, int f) {
+    E->fc[f].inhull = 0;
+    P.hcount--;
 }
+UGK_FN void s_push(EpaMem* E, Epa& P, int f) { E->stock[P.nstock++] = f; }
 UGK_FN bool e_edgedist(EpaMem* E, gv fn, int a, int b, double& dist) {
     const gv aw = E->sv[a].w, bw = E->sv[b].w;
     const gv ba = sub(bw, aw);
@@ -652,10 +667,9 @@ UGK_FN bool e_edgedist(EpaMem* E, gv fn, int a, int b, double& dist) {
     return false;
 }
 UGK_FN int e_newface(EpaMem* E, Epa& P, int a, int b, int c, bool forced) {
-    if (P.sroot >= 0) {
-        const int f = P.sroot;
-        e_remove(E, P.sroot, P.scount, f);
-        e_append(E, P.hroot, P.hcount, f);
+    if (P.nstock > 0) {
+        const int f = E->stock[--P.nstock];
+        h_append(E, P, f);
         EFace& F = E->fc[f];
         F.pass = 0;
         F.c[0] = a; F.c[1] = b; F.c[2] = c;
@@ -673,21 +687,12 @@ UGK_FN int e_newface(EpaMem* E, Epa& P, int a, int b, int c, bool forced) {
             F.n = n;
             P.status = EPA_DEGENERATED;
         }
-        e_remove(E, P.hroot, P.hcount, f);
-        e_append(E, P.sroot, P.scount, f);
+        h_remove(E, P, f);
+        s_push(E, P, f);
         return -1;
     }
-    P.status = P.sroot >= 0 ? EPA_OUTOFVERTICES : EPA_OUTOFFACES;
+    P.status = P.nstock > 0 ? EPA_OUTOFVERTICES : EPA_OUTOFFACES;
     return -1;
-}
-UGK_FN int e_findbest(EpaMem* E, const Epa& P) {
-    int minf = P.hroot;
-    double mind = E->fc[minf].d * E->fc[minf].d;
-    for (int f = E->fc[minf].l[1]; f >= 0; f = E->fc[f].l[1]) {
-        const double sqd = E->fc[f].d * E->fc[f].d;
-        if (sqd < mind) { minf = f; mind = sqd; }
-    }
-    return minf;
 }
 /* EPA::expand as an explicit depth-first walk: frame (face, edge, stage); stage 0 = entry, 1 = the first neighbour's
  * answer is in r, 2 = the second's.  The same visits, face allocations and list operations as the recursion. */
@@ -732,8 +737,8 @@ UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, int f0, int e0, int& hc
             continue;
         }
         if (r) {
-            e_remove(E, P.hroot, P.hcount, f);
-            e_append(E, P.sroot, P.scount, f);
+            h_remove(E, P, f);
+            s_push(E, P, f);
         }
         sp--;
     }
@@ -742,12 +747,9 @@ UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, int f0, int e0, int& hc
 /* EPA::Evaluate */
 UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
     const int s = g.simplex;
+    UGK_T0(t_setup);
     if (E->srank[s] > 1 && g2_enclose(E, g, M)) {
-        while (P.hroot >= 0) {
-            const int f = P.hroot;
-            e_remove(E, P.hroot, P.hcount, f);
-            e_append(E, P.sroot, P.scount, f);
-        }
+        /* Bullet first moves every hull face back to the stock: a fresh EPA (e_init) has none */
         P.status = EPA_VALID;
         P.nextsv = 0;
         int* c = E->sc[s];
@@ -764,7 +766,8 @@ UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
         tetra[2] = e_newface(E, P, c[2], c[1], c[3], true);
         tetra[3] = e_newface(E, P, c[0], c[2], c[3], true);
         if (P.hcount == 4) {
-            int best = e_findbest(E, P);
+            int best = ugk_epa_findbest(E);
+            UGK_ADD(PF_EPA_SETUP, t_setup);
             EFace outer = E->fc[best];
             int pass = 0;
             e_bind(E, tetra[0], 0, tetra[1], 0);
@@ -775,21 +778,28 @@ UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
             e_bind(E, tetra[2], 2, tetra[3], 1);
             P.status = EPA_VALID;
             for (int it = 0; it < kEpaMaxIterations; it++) {
+                UGK_COUNT(PC_EPA_IT, 1);
                 if (P.nextsv >= kEpaMaxVertices) { P.status = EPA_OUTOFVERTICES; break; }
                 int hcf = -1, hff = -1, hnf = 0;
                 const int w = 4 + P.nextsv++;
                 bool valid = true;
                 E->fc[best].pass = ++pass;
+                UGK_T0(t_sup);
                 g2_getsupport(E, M, E->fc[best].n, w);
+                UGK_ADD(PF_EPA_SUP, t_sup);
                 const double wdist = dot(E->fc[best].n, E->sv[w].w) - E->fc[best].d;
                 if (!(wdist > kEpaAccuracy)) { P.status = EPA_ACCURACYREACHED; break; }
+                UGK_T0(t_exp);
                 for (int j = 0; j < 3 && valid; j++)
                     valid = e_expand(E, P, pass, w, E->fc[best].f[j], E->fc[best].e[j], hcf, hff, hnf) && valid;
+                UGK_ADD(PF_EPA_EXPAND, t_exp);
                 if (!(valid && hnf >= 3)) { P.status = EPA_INVALIDHULL; break; }
                 e_bind(E, hcf, 1, hff, 2);
-                e_remove(E, P.hroot, P.hcount, best);
-                e_append(E, P.sroot, P.scount, best);
-                best = e_findbest(E, P);
+                h_remove(E, P, best);
+                s_push(E, P, best);
+                UGK_T0(t_best);
+                best = ugk_epa_findbest(E);
+                UGK_ADD(PF_EPA_BEST, t_best);
                 outer = E->fc[best];
             }
             const gv projection = scl(outer.n, outer.d);
@@ -824,16 +834,20 @@ UGK_FN void e_init(EpaMem* E, Epa& P) {
     P.normal = V3(0, 0, 0);
     P.depth = 0;
     P.nextsv = 0;
-    P.hroot = P.sroot = -1;
-    P.hcount = P.scount = 0;
-    for (int i = 0; i < kEpaMaxFaces; i++) e_append(E, P.sroot, P.scount, kEpaMaxFaces - i - 1);
+    P.hcount = 0;
+    P.nstock = kEpaMaxFaces;
+    P.stampctr = 0;
+    ugk_epa_reset_lists(E); /* stock[i] = 255 - i (face 0 on top), no face in the hull */
 }
 struct Res { gv w0, w1, normal; double distance; };
 UGK_FN bool g2_penetration(EpaMem* E, const GShape& s0, const gx& w0, const GShape& s1, const gx& w1, gv guess, Res& r) {
     Mink M;
     mk_init(M, s0, w0, s1, w1, true);
     Gjk2 g;
-    if (g2_evaluate(E, g, M, neg(guess)) == GJK_INSIDE) {
+    UGK_T0(t_g2);
+    const int gs = g2_evaluate(E, g, M, neg(guess));
+    UGK_ADD(PF_EPA_GJK, t_g2);
+    if (gs == GJK_INSIDE) {
         Epa P;
         e_init(E, P);
         if (e_evaluate(E, P, g, M, neg(guess)) != EPA_FAILED) {
@@ -1046,7 +1060,9 @@ UGK_FN gv support_ab(const GShape& A, const gx& TA, const GShape& B, const gx& T
 
 /* btGjkPairDetector::getClosestPointsNonVirtual: one point (normal on B, point on B, distance) or none */
 UGK_FN bool gjk_pair(EpaMem* E, const GShape& A, const gx& TA0, const GShape& B, const gx& TB0, double thr, gv& nOut,
-                           gv& pOut, double& dOut) {
+                           gv& pOut, double& dOut, gv* sepAxis = nullptr) {
+    UGK_COUNT(PC_GJK, 1);
+    UGK_T0(t_all);
     const double marginA = A.margin, marginB = B.margin;
     double maxd2 = marginA + marginB + thr;
     maxd2 *= maxd2;
@@ -1061,6 +1077,7 @@ UGK_FN bool gjk_pair(EpaMem* E, const GShape& A, const gx& TA0, const GShape& B,
     int degenerate = 0, status = -2;
     gv orgNormalInB = V3(0, 0, 0);
     const double margin = marginA + marginB;
+    UGK_T0(t_ccd);
     {
         Ccd s;
         gv dir = V3(1, 0, 0);
@@ -1070,6 +1087,7 @@ UGK_FN bool gjk_pair(EpaMem* E, const GShape& A, const gx& TA0, const GShape& B,
         s.n = 1;
         dir = neg(sup);
         for (int it = 0; it < kMaxIter; it++) {
+            UGK_COUNT(PC_GJK_CCD, 1);
             sup = support_ab(A, TA, B, TB, dir);
             if (dot(sup, dir) < 0) { status = -1; break; }
             if (s.n == 1) s.p1 = sup;
@@ -1084,12 +1102,15 @@ UGK_FN bool gjk_pair(EpaMem* E, const GShape& A, const gx& TA0, const GShape& B,
             if (dot(dir, dir) < kEps * kEps) { status = -1; break; }
         }
     }
+    UGK_ADD(PF_GJK_CCD, t_ccd);
+    UGK_T0(t_cls);
     Voronoi vs;
     vs_reset(vs);
     {
         double squaredDistance = kLarge, delta = 0.0;
         int curIter = 0;
         for (;;) {
+            UGK_COUNT(PC_GJK_IT, 1);
             const gv pW = xfa(TA, support0(A, mtv(TA.R, neg(axis))));
             const gv qW = xfa(TB, support0(B, mtv(TB.R, axis)));
             const gv w = sub(pW, qW);
@@ -1129,11 +1150,18 @@ UGK_FN bool gjk_pair(EpaMem* E, const GShape& A, const gx& TA0, const GShape& B,
             }
         }
     }
+    UGK_ADD(PF_GJK_CLASSIC, t_cls);
+    /* the classic GJK's last separating axis (from B towards A): the caller's separation certificate, when the query
+     * ends without a point it keeps (an observer only: nothing below reads it) */
+    if (sepAxis) *sepAxis = status == 0 ? V3(0, 0, 0) : axis;
     const bool catchDegenerate = degenerate && ((distance + margin) < kPenTol);
     if ((!isValid || catchDegenerate) || status == 0) {
+        UGK_COUNT(PC_GJK_EPA, 1);
+        UGK_T0(t_pen);
         gv tA, tB;
         axis = V3(0, 0, 0);
         const bool isValid2 = calc_pen_depth(E, A, B, TA, TB, axis, tA, tB);
+        UGK_ADD(PF_GJK_PEN, t_pen);
         if (dot(axis, axis) != 0.0) {
             if (isValid2) {
                 gv tn = sub(tB, tA);
@@ -1181,6 +1209,7 @@ UGK_FN bool gjk_pair(EpaMem* E, const GShape& A, const gx& TA0, const GShape& B,
     nOut = normalInB;
     pOut = add(pointOnB, off);
     dOut = distance;
+    UGK_ADD(PF_GJK_ALL, t_all);
     return true;
 }
 

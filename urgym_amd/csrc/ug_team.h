@@ -29,15 +29,13 @@
 #include "ug_device.h"
 #include "prio_model.h"
 #include "ug_glue.h"
-#define UGK_FN __device__ static inline
-#include "ug_gjk.h"
 
 namespace ugd {
 
 #define TEAM 64
 typedef __attribute__((address_space(1))) const double gcdouble;
 typedef __attribute__((address_space(1))) double gdouble;
-#define UG_NPROF 80 /* phase accumulators of the -DUG_PROF build */
+#define UG_NPROF 96 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* a row's J and M^-1 J^T over the NVP = 32 dof slots (robot 12, objects 3 x 6, 2 zero pads) */
@@ -86,7 +84,12 @@ static_assert(UG_FULL_HULL_MAXV + 64 + 8 <= FC_MAX, "a full hull pair's candidat
  * vertices, 256 faces and their lists, the horizon walk's stack) after everything else */
 #define WS_EPA WS_DOUBLES
 #define EPA_DOUBLES ((sizeof(ugk::EpaMem) + sizeof(double) - 1) / sizeof(double))
-#define WS_STRIDE(full, gjk) ((gjk) ? (size_t)(WS_EPA + EPA_DOUBLES) : WS_STRIDE_VIH(full))
+/* the convex-convex path's separation certificates, per pair: [0] valid, [1..3] the separating axis n in B's frame,
+ * [4] A's core extent along -n at the evaluation, [5] B's core extent along n, [6..14] R_AB, [15..17] p_AB (A's pose in
+ * B's frame then); GJK's (A, B) order (a sphere-first pair swapped) */
+#define GC_DOUBLES 18
+#define WS_GC (WS_EPA + EPA_DOUBLES)
+#define WS_STRIDE(full, gjk) ((gjk) ? (size_t)(WS_GC + GC_DOUBLES * MAXPAIR) : WS_STRIDE_VIH(full))
 
 #define MAXOV 26 /* pairs per lane-per-pair pass: their working manifolds share LDS with the rows (Shared::pm) */
 #define NBOXSLOT 5 /* box-box pairs run per round, one LDS clip-buffer slot each (they share the hull candidates' LDS) */
@@ -195,12 +198,31 @@ enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_
        PC_FREE, PF_FREE_COL, PF_FREE_DYN, PF_FREE_ROWS, PF_FREE_PGS, PF_FREE_INT,
        PF_FREE_PSETUP, PF_FREE_PSWEEP, PF_FREE_PPOST, PF_PR_BB, PF_HS, PC_CYPAIR, PF_CY1, PF_CY2, PC_CYSV, PC_CYIT,
        /* the contact-free substeps' share of these sub-phase counters (UG_FREE_SPLIT below) */
-       PF_FREE_SUB0 = 64 };
+       PF_FREE_SUB0 = 64,
+       /* the convex-convex path (ug_gjk.h): queries, penetration-path queries, classic GJK / libccd iterations, hull
+        * support queries and their cycles */
+       PC_GJK = 80, PC_GJK_EPA, PC_GJK_IT, PC_GJK_CCD, PC_GJK_SUP, PF_GJK_SUP,
+       /* EPA iterations, cycles: the whole query, the penetration path, the libccd test, the classic GJK */
+       PC_EPA_IT, PF_GJK_ALL, PF_GJK_PEN, PF_GJK_CCD, PF_GJK_CLASSIC,
+       /* inside the penetration path: btGjkEpa2's GJK, the EPA setup (enclose + tetrahedron), its iterations' support,
+        * horizon walk and findbest, the witnesses */
+       PF_EPA_GJK, PF_EPA_SETUP, PF_EPA_SUP, PF_EPA_EXPAND, PF_EPA_BEST };
 #define UG_FREE_SPLIT_N 14
 #ifdef UG_PROF
 __device__ static const int kFreeSplit[UG_FREE_SPLIT_N] = {PF_FK, PF_BROAD, PF_HULL, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST,
                                                            PF_PAIRS, PC_OVL, PC_HULL, PF_RDYN, PF_LDL, PF_ENUM, PF_UNIT};
 #endif
+
+} /* namespace ugd */
+/* the convex-convex narrowphase (Bullet's GJK / EPA pair detector), run by the whole wave per pair */
+#define UGK_FN __device__ static inline
+#ifdef UG_PROF /* its event counters (PC_GJK_*) and phase timers, lane 0 of the env's wave */
+#define UGK_COUNT(k, v) do { if (threadIdx.x == 0) ugd::g_sh.prof[ugd::k] += (unsigned long long)(v); } while (0)
+#define UGK_T0(v) const unsigned long long v = __builtin_readcyclecounter()
+#define UGK_ADD(k, v) UGK_COUNT(k, __builtin_readcyclecounter() - (v))
+#endif
+#include "ug_gjk.h"
+namespace ugd {
 
 /* ---------------- wave helpers ---------------- */
 template <int CTRL>
@@ -279,17 +301,67 @@ __device__ __forceinline__ void wave_best(double& v, int& idx, bool want_max) {
  * whole hull.  Called by every lane of the env's wave (the GJK runs uniformly). */
 UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
     const int lane = threadIdx.x;
+    PROF_T0(t_sup);
     double best = -__builtin_inf();
     int bi = 0x7fffffff;
-    for (int i = lane; i < nv; i += TEAM) {
-        const double* p = &UG_HULL_V[3 * (v0 + i)];
-        const double dd = p[0] * d.x + p[1] * d.y + p[2] * d.z;
-        if (dd > best) { best = dd; bi = i; }
+    /* four vertices per trip: their loads in flight together (the hull is L2-resident, the latency is the cost) */
+    for (int i0 = lane; i0 < nv; i0 += 4 * TEAM) {
+        double x[4], y[4], z[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int i = i0 + k * TEAM < nv ? i0 + k * TEAM : i0;
+            const double* p = &UG_HULL_V[3 * (v0 + i)];
+            x[k] = p[0]; y[k] = p[1]; z[k] = p[2];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const double dd = x[k] * d.x + y[k] * d.y + z[k] * d.z;
+            if (i0 + k * TEAM < nv && dd > best) { best = dd; bi = i0 + k * TEAM; }
+        }
     }
     ugd::wave_best(best, bi, true);
     if (bi == 0x7fffffff) bi = 0;
     const double* p = &UG_HULL_V[3 * (v0 + bi)];
+#ifdef UG_PROF
+    if (lane == 0) {
+        ugd::g_sh.prof[ugd::PF_GJK_SUP] += __builtin_readcyclecounter() - t_sup;
+        ugd::g_sh.prof[ugd::PC_GJK_SUP] += 1;
+    }
+#endif
     return ugk::V3(p[0], p[1], p[2]);
+}
+
+/* ug_gjk.h's EPA list hooks on the wave: the free-face stack and the hull flags reset lane-parallel (published to the
+ * wave's later loads), and m_hull's first minimum (smallest d * d, ties to the largest append stamp; a NaN at the root
+ * keeps the root) as a lane-strided scan + DPP arg-min instead of a pointer chase through the workspace */
+UGK_FN void ugk_epa_reset_lists(ugk::EpaMem* E) {
+    for (int i = threadIdx.x; i < ugk::kEpaMaxFaces; i += TEAM) {
+        E->stock[i] = ugk::kEpaMaxFaces - 1 - i;
+        E->fc[i].inhull = 0;
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+}
+UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E) {
+    const int lane = threadIdx.x;
+    double rs = -1.0;
+    int rf = 0x7fffffff;
+    for (int f = lane; f < ugk::kEpaMaxFaces; f += TEAM)
+        if (E->fc[f].inhull && (rf == 0x7fffffff || (double)E->fc[f].stamp > rs)) { rs = (double)E->fc[f].stamp; rf = f; }
+    ugd::wave_best(rs, rf, true); /* the root: the largest stamp */
+    const double rd = E->fc[rf].d;
+    if ((rd * rd) != (rd * rd)) return rf;
+    double bv = 0.0;
+    int bi = 0x7fffffff;
+    for (int f = lane; f < ugk::kEpaMaxFaces; f += TEAM) {
+        if (!E->fc[f].inhull) continue;
+        const double d = E->fc[f].d, sqd = d * d;
+        if (sqd != sqd) continue;
+        const int key = ((1 << 20) - E->fc[f].stamp) * ugk::kEpaMaxFaces + f; /* lower key = larger stamp */
+        if (bi == 0x7fffffff || sqd < bv || (sqd == bv && key < bi)) { bv = sqd; bi = key; }
+    }
+    ugd::wave_best(bv, bi, false);
+    return bi & (ugk::kEpaMaxFaces - 1);
 }
 namespace ugd {
 
@@ -1456,18 +1528,45 @@ __device__ __forceinline__ static ugk::gx to_gx(const XF& T) {
 /* pair k of the pass (sh.pinfo[k]) through btGjkPairDetector on the whole wave (ug_gjk.h): at most one point, written
  * to cand k in this restatement's pair order (a sphere-first pair runs with the sphere as GJK's B, then flipped --
  * oracle nc_gjk) */
-__device__ __noinline__ static void team_gjk(const Scene* s, int k, ugk::EpaMem* E) {
+/* pair k of the pass (sh.pinfo[k]) through btGjkPairDetector on the whole wave (ug_gjk.h): at most one point, written
+ * to cand k in this restatement's pair order (a sphere-first pair runs with the sphere as GJK's B, then flipped --
+ * oracle nc_gjk).  A query that ends without a point the manifold keeps leaves a separation certificate: the
+ * separating axis n (the reported normal, or the classic GJK's last axis) with both cores' extents along it, and the
+ * relative pose; while the motion bound in team_collide proves that the margin-expanded shapes stay farther apart than
+ * the contact threshold, the query would again add nothing, and the pair is skipped. */
+__device__ __noinline__ static void team_gjk(const Scene* s, int k, ugk::EpaMem* E, gdouble* gc) {
     Shared& sh = g_sh;
     const int a = sh.pinfo[k].a, b = sh.pinfo[k].b;
     const Collider& A = s->col[a];
     const Collider& B = s->col[b];
-    const ugk::GShape ga = gshape_of(A), gb = gshape_of(B);
-    const ugk::gx TA = to_gx(sh.pinfo[k].TA), TB = to_gx(sh.pinfo[k].TB);
-    const double thr = sh.pinfo[k].thr;
     const bool swap = A.kind == UG_SHAPE_SPHERE && B.kind != UG_SHAPE_SPHERE;
-    ugk::gv n, p;
+    const ugk::GShape g0 = gshape_of(swap ? B : A), g1 = gshape_of(swap ? A : B);
+    const ugk::gx T0 = to_gx(swap ? sh.pinfo[k].TB : sh.pinfo[k].TA), T1 = to_gx(swap ? sh.pinfo[k].TA : sh.pinfo[k].TB);
+    const double thr = sh.pinfo[k].thr;
+    ugk::gv n, p, ax = ugk::V3(0, 0, 0);
     double d = 0.0;
-    const bool ok = swap ? ugk::gjk_pair(E, gb, TB, ga, TA, thr, n, p, d) : ugk::gjk_pair(E, ga, TA, gb, TB, thr, n, p, d);
+    const bool ok = ugk::gjk_pair(E, g0, T0, g1, T1, thr, n, p, d, &ax);
+    /* certificate (GJK's order): the axis of a dropped point or of the classic GJK */
+    const bool kept = ok && !(d > thr);
+    ugk::gv u = ok ? n : ax;
+    const double ul = ugk::dot(u, u);
+    bool cert = !kept && ul > 1e-24;
+    if (cert) {
+        u = ugk::mulinv(u, ug_sqrt(ul));
+        const ugk::gv dA = ugk::mtv(T0.R, ugk::neg(u)), dB = ugk::mtv(T1.R, u);
+        const double hA = ugk::dot(dA, ugk::support0(g0, dA)), hB = ugk::dot(dB, ugk::support0(g1, dB));
+        if (threadIdx.x == 0) {
+            const ugk::gm R = ugk::mtm(T1.R, T0.R);
+            const ugk::gv pp = ugk::mtv(T1.R, ugk::sub(T0.p, T1.p));
+            gc[0] = 1.0;
+            gc[1] = dB.x; gc[2] = dB.y; gc[3] = dB.z;
+            gc[4] = hA; gc[5] = hB;
+            for (int i = 0; i < 9; i++) gc[6 + i] = R.m[i];
+            gc[15] = pp.x; gc[16] = pp.y; gc[17] = pp.z;
+        }
+    } else if (threadIdx.x == 0) {
+        gc[0] = 0.0;
+    }
     v3 cn = V(n.x, n.y, n.z), cp = V(p.x, p.y, p.z);
     if (swap) {
         cp = vadd(cp, vscale(cn, d));
@@ -1549,6 +1648,36 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
             sh.pinfo[lane] = pi;
             hk = A.kind == UG_SHAPE_HULL && (B.kind == UG_SHAPE_BOX || B.kind == UG_SHAPE_HULL);
             if (GJK) hk = pair_is_gjk(A, B); /* the wave runs the pair's GJK / EPA */
+            if (GJK && hk) {
+                /* its separation certificate (team_gjk): with R_AB, p_AB now, A's extent along -n grows by at most
+                 * ||(R_AB - R_AB0)^T n|| times A's support radius, B's along n (B-fixed) not at all, so the cores stay
+                 * at least s = n . p_AB - hA - that - hB apart; past the margins and the threshold GJK adds no point */
+                const gcdouble* gc = (gcdouble*)(ws + WS_GC) + GC_DOUBLES * p;
+                if (gc[0] > 0.0) {
+                    const bool sw = A.kind == UG_SHAPE_SPHERE && B.kind != UG_SHAPE_SPHERE;
+                    const XF& G0 = sw ? pi.TB : pi.TA;
+                    const XF& G1 = sw ? pi.TA : pi.TB;
+                    const Collider& C0 = sw ? B : A;
+                    const Collider& C1 = sw ? A : B;
+                    const m3 R = mtm(G1.R, G0.R);
+                    const v3 pp = mtv(G1.R, vsub(G0.p, G1.p));
+                    const v3 nb = V(gc[1], gc[2], gc[3]);
+                    v3 w = V(0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < 3; i++) {
+                        const double ni = i == 0 ? nb.x : (i == 1 ? nb.y : nb.z);
+                        w.x += (R.m[3 * i] - gc[6 + 3 * i]) * ni;
+                        w.y += (R.m[3 * i + 1] - gc[7 + 3 * i]) * ni;
+                        w.z += (R.m[3 * i + 2] - gc[8 + 3 * i]) * ni;
+                    }
+                    const double sep = vdot(nb, pp) - gc[4] - vlen(w) * C0.gradius - gc[5];
+                    if (sep - C0.gmargin - C1.gmargin - P.thr > 1e-9 * (1.0 + ug_fabs(sep))) {
+                        hk = 0;
+                        certd = true;
+                        sh.u.cand.n[lane] = 0;
+                    }
+                }
+            }
             else if (FULL) /* the disc cylinder against a polytope, either side */
                 hk = hk || (B.kind == UG_SHAPE_CYL && (A.kind == UG_SHAPE_HULL || A.kind == UG_SHAPE_BOX)) ||
                      (A.kind == UG_SHAPE_CYL && B.kind == UG_SHAPE_BOX);
@@ -1598,7 +1727,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         for (unsigned long long hm = ballot(hk); hm != 0ull; hm &= hm - 1ull) {
             const int k = __builtin_ctzll(hm);
             if (GJK) {
-                team_gjk(s, k, (ugk::EpaMem*)(ws + WS_EPA));
+                team_gjk(s, k, (ugk::EpaMem*)(ws + WS_EPA), (gdouble*)(ws + WS_GC) + GC_DOUBLES * sh.ov[c0 + k]);
                 PROF_CNT(PC_HULL, 1);
                 continue;
             }
