@@ -75,12 +75,28 @@ def _oracle_sample(task, n, threads, seconds, flags=0, robot="ur5_robotiq_85"):
     return steps, substeps, time.perf_counter() - t0
 
 
+def usable_cores():
+    """(cores this process can keep busy, how that was found): the affinity mask, capped by the cgroup v2 CPU quota
+    (cpu.max "quota period") -- the GPU box's mask lists the whole machine while its quota is the box's share, and
+    threads past the quota only queue"""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+            if quota < aff:
+                return quota, f"cgroup cpu.max quota {quota} of {aff} affinity cores"
+    except (OSError, ValueError):
+        pass
+    return aff, f"every core of the affinity mask ({aff})"
+
+
 def cpu_baseline(task, seconds=10.0, seconds_1core=5.0, flags=0, robot="ur5_robotiq_85"):
     """CPU restatement (oracle/, test infrastructure) timed on this host's cores: bounded samples of the same
-    workload (same task, random actions, autoreset) -- every core this process may run on (os.sched_getaffinity;
-    OpenMP, 4 envs per thread), the 16-thread figure of rounds 2-3 beside it for continuity, and the 1-env / 1-core
-    analogue of config A."""
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    workload (same task, random actions, autoreset) -- every core this process may use (usable_cores: the affinity
+    mask within the cgroup quota; OpenMP, 4 envs per thread), the 16-thread figure of rounds 2-3 beside it for
+    continuity, and the 1-env / 1-core analogue of config A."""
+    cores, how = usable_cores()
     n = 4 * cores
     steps, substeps, dt = _oracle_sample(task, n, cores, seconds, flags, robot)
     t16 = min(16, cores)
@@ -89,7 +105,7 @@ def cpu_baseline(task, seconds=10.0, seconds_1core=5.0, flags=0, robot="ur5_robo
     return {"value": steps / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
             "cpu_model": cpu_model(),
             "sample": f"{TASK_NAMES[task]} x {n} envs, {steps} env-steps incl. autoresets ({substeps} substeps) in "
-                      f"{dt:.1f}s; C restatement (oracle/), OpenMP {cores} threads (every core of the affinity mask)",
+                      f"{dt:.1f}s; C restatement (oracle/), OpenMP {cores} threads ({how})",
             "threads_16": {"value": s16 / dt16, "unit": "env-steps/s", "cores": t16,
                            "sample": f"{4 * t16} envs, {s16} env-steps ({sub16} substeps) in {dt16:.1f}s"},
             "one_core": {"value": s1 / dt1, "unit": "env-steps/s", "cores": 1,

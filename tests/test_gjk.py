@@ -28,7 +28,10 @@ ARGS = [ctypes.c_int, ctypes.c_int, ctypes.c_int, DP, ctypes.c_double, DP, DP,
 
 
 def _lib(name, fn):
-    L = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", name))
+    path = os.path.join(ROOT, "oracle", "_build", name)
+    if name == "libugoracle.so" and os.environ.get("URGYM_ORACLE_LIB"):  # tools/oracle_asan.sh's instrumented build
+        path = os.environ["URGYM_ORACLE_LIB"]
+    L = ctypes.CDLL(path)
     f = getattr(L, fn)
     f.argtypes = ARGS
     f.restype = ctypes.c_int

@@ -14,7 +14,7 @@
 #endif
 #include "../urgym_amd/csrc/ug_gjk.h"
 
-UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
+UGK_FN ugk::gv ugk_hull_support(int v0, int nv, int, ugk::gv d) {
     double best = -__builtin_inf();
     int bi = 0;
     for (int i = 0; i < nv; i++) {

@@ -66,12 +66,12 @@ UGK_FN bool veq(gv a, gv b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
 UGK_FN gv vsel(bool c, gv a, gv b) { return V3(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
 
 /* a convex shape as GJK sees it (kind: UG_SHAPE_*; imp: box / cylinder implicit dimensions; margin: getMargin) */
-struct GShape { int kind, v0, nv; gv imp; double margin; };
+struct GShape { int kind, v0, nv; gv imp; double margin; int c0 = -1; }; /* c0: a full hull's first chunk sphere, or -1 */
 
 } /* namespace ugk */
 
 /* the includer's hull support: the vertex of hull [v0, v0 + nv) with the first maximal dot product with d */
-UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d);
+UGK_FN ugk::gv ugk_hull_support(int v0, int nv, int c0, ugk::gv d);
 
 namespace ugk {
 
@@ -100,7 +100,7 @@ UGK_FN gv support0(const GShape& s, gv d) {
         }
         return V3(s.imp.x, 0.0, z);
     }
-    return ugk_hull_support(s.v0, s.nv, d);
+    return ugk_hull_support(s.v0, s.nv, s.c0, d);
 }
 /* localGetSupportVertexNonVirtual */
 UGK_FN gv support(const GShape& s, gv d) {

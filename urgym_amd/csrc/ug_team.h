@@ -83,12 +83,13 @@ static_assert(UG_FULL_HULL_MAXV + 64 + 8 <= FC_MAX, "a full hull pair's candidat
 /* the convex-convex path (UG_CONTACT_GJK): the penetration solver's store (ug_gjk.h EpaMem: btGjkEpa2's 132 support
  * vertices, 256 faces and their lists, the horizon walk's stack) after everything else */
 #define WS_EPA WS_DOUBLES
+#define UG_GJK_G 16 /* lanes per GJK pair (ugd::GJK_G): the wave runs 64 / UG_GJK_G pairs at once, one store each */
 #define EPA_DOUBLES ((sizeof(ugk::EpaMem) + sizeof(double) - 1) / sizeof(double))
 /* the convex-convex path's separation certificates, per pair: [0] valid, [1..3] the separating axis n in B's frame,
  * [4] A's core extent along -n at the evaluation, [5] B's core extent along n, [6..14] R_AB, [15..17] p_AB (A's pose in
  * B's frame then); GJK's (A, B) order (a sphere-first pair swapped) */
 #define GC_DOUBLES 18
-#define WS_GC (WS_EPA + EPA_DOUBLES)
+#define WS_GC (WS_EPA + EPA_DOUBLES * (64 / UG_GJK_G)) /* one EPA store per GJK lane group */
 #define WS_STRIDE(full, gjk) ((gjk) ? (size_t)(WS_GC + GC_DOUBLES * MAXPAIR) : WS_STRIDE_VIH(full))
 
 #define MAXOV 26 /* pairs per lane-per-pair pass: their working manifolds share LDS with the rows (Shared::pm) */
@@ -217,7 +218,8 @@ __device__ static const int kFreeSplit[UG_FREE_SPLIT_N] = {PF_FK, PF_BROAD, PF_H
 /* the convex-convex narrowphase (Bullet's GJK / EPA pair detector), run by the whole wave per pair */
 #define UGK_FN __device__ static inline
 #ifdef UG_PROF /* its event counters (PC_GJK_*) and phase timers, lane 0 of the env's wave */
-#define UGK_COUNT(k, v) do { if (threadIdx.x == 0) ugd::g_sh.prof[ugd::k] += (unsigned long long)(v); } while (0)
+/* summed over the lane groups that run pairs at once (LDS atomics): work, not wall time */
+#define UGK_COUNT(k, v) do { if ((threadIdx.x & (UG_GJK_G - 1)) == 0) atomicAdd(&ugd::g_sh.prof[ugd::k], (unsigned long long)(v)); } while (0)
 #define UGK_T0(v) const unsigned long long v = __builtin_readcyclecounter()
 #define UGK_ADD(k, v) UGK_COUNT(k, __builtin_readcyclecounter() - (v))
 #endif
@@ -295,37 +297,93 @@ __device__ __forceinline__ void wave_best(double& v, int& idx, bool want_max) {
     idx = bi;
 }
 
+/* The GJK / EPA of one pair runs on a group of GJK_G lanes (one DPP row): the wave runs up to GJK_NG pairs at once,
+ * each group uniform within itself (every lane of it computes the same values), the groups diverging as their pairs'
+ * iterations differ.  group_best is wave_best over the group's row. */
+constexpr int GJK_G = UG_GJK_G, GJK_NG = TEAM / GJK_G;
+static_assert(TEAM == 64, "WS_GC counts 64 lanes");
+static_assert(GJK_G == 16 || GJK_G == TEAM, "a GJK lane group is one DPP row or the wave");
+__device__ __forceinline__ void group_best(double& v, int& idx, bool want_max) {
+    if (GJK_G == TEAM) {
+        wave_best(v, idx, want_max);
+        return;
+    }
+#define STEP(CTRL)                                               \
+    {                                                            \
+        double w = dpp<CTRL>(v);                                 \
+        int j = dppi<CTRL>(idx);                                 \
+        if (!better(v, idx, w, j, want_max)) { v = w; idx = j; } \
+    }
+    STEP(0xB1) STEP(0x4E) STEP(0x141) STEP(0x140)
+#undef STEP
+}
+
 } /* namespace ugd */
-/* ug_gjk.h's hull support on the wave: lane l dots vertices l, l + 64, ... (each lane keeps its first maximum), then
- * the DPP arg-max keeps the larger value and, on a tie, the lower index -- btVector3::maxDot's first maximum over the
- * whole hull.  Called by every lane of the env's wave (the GJK runs uniformly). */
-UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
-    const int lane = threadIdx.x;
-    PROF_T0(t_sup);
-    double best = -__builtin_inf();
-    int bi = 0x7fffffff;
-    /* four vertices per trip: their loads in flight together (the hull is L2-resident, the latency is the cost) */
-    for (int i0 = lane; i0 < nv; i0 += 4 * TEAM) {
-        double x[4], y[4], z[4];
+/* ug_gjk.h's hull support on the lane group: btVector3::maxDot's first maximum (the largest dot product, on a tie the
+ * lowest vertex index) over the whole hull, called by every lane of the group (its GJK runs uniformly).  Lane l of the
+ * group dots vertices l, l + G, ... of a vertex range keeping its first maximum, and the DPP arg-max keeps the larger
+ * value and, on a tie, the lower index.  A full hull of more than two 64-vertex chunks is culled by its chunk spheres
+ * (UG_HULL_CS): the chunk with the largest bound c . d + r |d| first, then only the chunks whose bound reaches the best
+ * value found (>=, so a tie at a lower index in another chunk is still seen); the bound carries a 1e-12 relative slack
+ * over the dot products' rounding, so a skipped chunk cannot hold the maximum. */
+__device__ __forceinline__ void hs_scan(int v0, int lo, int hi, ugk::gv d, int gl, double& best, int& bi) {
+    constexpr int G = ugd::GJK_G, U = G == TEAM ? 4 : 8;
+    /* U vertices per trip: their loads in flight together (the hull is cache-resident, the latency is the cost) */
+    for (int i0 = lo + gl; i0 < hi; i0 += U * G) {
+        double x[U], y[U], z[U];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int i = i0 + k * TEAM < nv ? i0 + k * TEAM : i0;
+        for (int k = 0; k < U; k++) {
+            const int i = i0 + k * G < hi ? i0 + k * G : i0;
             const double* p = &UG_HULL_V[3 * (v0 + i)];
             x[k] = p[0]; y[k] = p[1]; z[k] = p[2];
         }
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < U; k++) {
             const double dd = x[k] * d.x + y[k] * d.y + z[k] * d.z;
-            if (i0 + k * TEAM < nv && dd > best) { best = dd; bi = i0 + k * TEAM; }
+            const int i = i0 + k * G;
+            if (i < hi && (bi == 0x7fffffff || dd > best || (dd == best && i < bi))) { best = dd; bi = i; }
         }
     }
-    ugd::wave_best(best, bi, true);
+}
+UGK_FN ugk::gv ugk_hull_support(int v0, int nv, int c0, ugk::gv d) {
+    constexpr int G = ugd::GJK_G;
+    const int gl = threadIdx.x & (G - 1);
+    PROF_T0(t_sup);
+    double best = -__builtin_inf();
+    int bi = 0x7fffffff;
+    const int nch = (nv + TEAM - 1) / TEAM;
+    const double dl1 = ug_fabs(d.x) + ug_fabs(d.y) + ug_fabs(d.z);
+    if (nch <= 2 || nch > G || c0 < 0 || !(dl1 < 1e300)) {
+        hs_scan(v0, 0, nv, d, gl, best, bi);
+    } else {
+        double b = -__builtin_inf();
+        int ci = 0x7fffffff;
+        if (gl < nch) {
+            const double* S = &UG_HULL_CS[4 * (c0 + gl)];
+            const double dn = ug_sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
+            b = S[0] * d.x + S[1] * d.y + S[2] * d.z + S[3] * dn +
+                1e-12 * (ug_fabs(S[0]) + ug_fabs(S[1]) + ug_fabs(S[2]) + S[3]) * dl1;
+            ci = gl;
+        }
+        double bb = b;
+        int c1 = ci;
+        ugd::group_best(bb, c1, true);
+        hs_scan(v0, TEAM * c1, TEAM * c1 + TEAM < nv ? TEAM * c1 + TEAM : nv, d, gl, best, bi);
+        ugd::group_best(best, bi, true);
+        const int gb = threadIdx.x & ~(G - 1);
+        unsigned long long more = (ugd::ballot(gl < nch && gl != c1 && b >= best) >> gb) & ((1ull << G) - 1ull);
+        for (; more != 0ull; more &= more - 1ull) {
+            const int c = __builtin_ctzll(more);
+            hs_scan(v0, TEAM * c, TEAM * c + TEAM < nv ? TEAM * c + TEAM : nv, d, gl, best, bi);
+        }
+    }
+    ugd::group_best(best, bi, true);
     if (bi == 0x7fffffff) bi = 0;
     const double* p = &UG_HULL_V[3 * (v0 + bi)];
 #ifdef UG_PROF
-    if (lane == 0) {
-        ugd::g_sh.prof[ugd::PF_GJK_SUP] += __builtin_readcyclecounter() - t_sup;
-        ugd::g_sh.prof[ugd::PC_GJK_SUP] += 1;
+    if (gl == 0) {
+        atomicAdd(&ugd::g_sh.prof[ugd::PF_GJK_SUP], __builtin_readcyclecounter() - t_sup);
+        atomicAdd(&ugd::g_sh.prof[ugd::PC_GJK_SUP], 1ull);
     }
 #endif
     return ugk::V3(p[0], p[1], p[2]);
@@ -335,7 +393,7 @@ UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
  * wave's later loads), and m_hull's first minimum (smallest d * d, ties to the largest append stamp; a NaN at the root
  * keeps the root) as a lane-strided scan + DPP arg-min instead of a pointer chase through the workspace */
 UGK_FN void ugk_epa_reset_lists(ugk::EpaMem* E) {
-    for (int i = threadIdx.x; i < ugk::kEpaMaxFaces; i += TEAM) {
+    for (int i = threadIdx.x & (ugd::GJK_G - 1); i < ugk::kEpaMaxFaces; i += ugd::GJK_G) {
         E->stock[i] = ugk::kEpaMaxFaces - 1 - i;
         E->fc[i].inhull = 0;
     }
@@ -343,24 +401,24 @@ UGK_FN void ugk_epa_reset_lists(ugk::EpaMem* E) {
     __builtin_amdgcn_wave_barrier();
 }
 UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E) {
-    const int lane = threadIdx.x;
-    double rs = -1.0;
-    int rf = 0x7fffffff;
-    for (int f = lane; f < ugk::kEpaMaxFaces; f += TEAM)
-        if (E->fc[f].inhull && (rf == 0x7fffffff || (double)E->fc[f].stamp > rs)) { rs = (double)E->fc[f].stamp; rf = f; }
-    ugd::wave_best(rs, rf, true); /* the root: the largest stamp */
+    constexpr int G = ugd::GJK_G;
+    const int gl = threadIdx.x & (G - 1);
+    /* one pass over the lane's faces (all loads in flight): the root candidate and the arg-min together */
+    double rs = -1.0, bv = 0.0;
+    int rf = 0x7fffffff, bi = 0x7fffffff;
+#pragma unroll
+    for (int f = gl; f < ugk::kEpaMaxFaces; f += G) {
+        const int in = E->fc[f].inhull, st = E->fc[f].stamp;
+        const double d = E->fc[f].d, sqd = d * d;
+        if (in && (rf == 0x7fffffff || (double)st > rs)) { rs = (double)st; rf = f; }
+        const int key = ((1 << 20) - st) * ugk::kEpaMaxFaces + f; /* lower key = larger stamp */
+        if (in && sqd == sqd && (bi == 0x7fffffff || sqd < bv || (sqd == bv && key < bi))) { bv = sqd; bi = key; }
+    }
+    ugd::group_best(rs, rf, true); /* the root: the largest stamp */
+    if (rf == 0x7fffffff) return 0;
     const double rd = E->fc[rf].d;
     if ((rd * rd) != (rd * rd)) return rf;
-    double bv = 0.0;
-    int bi = 0x7fffffff;
-    for (int f = lane; f < ugk::kEpaMaxFaces; f += TEAM) {
-        if (!E->fc[f].inhull) continue;
-        const double d = E->fc[f].d, sqd = d * d;
-        if (sqd != sqd) continue;
-        const int key = ((1 << 20) - E->fc[f].stamp) * ugk::kEpaMaxFaces + f; /* lower key = larger stamp */
-        if (bi == 0x7fffffff || sqd < bv || (sqd == bv && key < bi)) { bv = sqd; bi = key; }
-    }
-    ugd::wave_best(bv, bi, false);
+    ugd::group_best(bv, bi, false);
     return bi & (ugk::kEpaMaxFaces - 1);
 }
 namespace ugd {
@@ -1516,6 +1574,7 @@ __device__ __forceinline__ static ugk::GShape gshape_of(const Collider& c) {
     g.nv = c.kind == UG_SHAPE_HULL ? c.nv : 0;
     g.imp = ugk::V3(c.gimp.x, c.gimp.y, c.gimp.z);
     g.margin = c.gmargin;
+    g.c0 = c.kind == UG_SHAPE_HULL && c.nv > 2 * TEAM ? c.c0 : -1; /* a full hull's chunk spheres (ugk_hull_support) */
     return g;
 }
 __device__ __forceinline__ static ugk::gx to_gx(const XF& T) {
@@ -1545,6 +1604,7 @@ __device__ __noinline__ static void team_gjk(const Scene* s, int k, ugk::EpaMem*
     const double thr = sh.pinfo[k].thr;
     ugk::gv n, p, ax = ugk::V3(0, 0, 0);
     double d = 0.0;
+    const bool lead = (threadIdx.x & (GJK_G - 1)) == 0; /* the group's writer */
     const bool ok = ugk::gjk_pair(E, g0, T0, g1, T1, thr, n, p, d, &ax);
     /* certificate (GJK's order): the axis of a dropped point or of the classic GJK */
     const bool kept = ok && !(d > thr);
@@ -1555,7 +1615,7 @@ __device__ __noinline__ static void team_gjk(const Scene* s, int k, ugk::EpaMem*
         u = ugk::mulinv(u, ug_sqrt(ul));
         const ugk::gv dA = ugk::mtv(T0.R, ugk::neg(u)), dB = ugk::mtv(T1.R, u);
         const double hA = ugk::dot(dA, ugk::support0(g0, dA)), hB = ugk::dot(dB, ugk::support0(g1, dB));
-        if (threadIdx.x == 0) {
+        if (lead) {
             const ugk::gm R = ugk::mtm(T1.R, T0.R);
             const ugk::gv pp = ugk::mtv(T1.R, ugk::sub(T0.p, T1.p));
             gc[0] = 1.0;
@@ -1564,7 +1624,7 @@ __device__ __noinline__ static void team_gjk(const Scene* s, int k, ugk::EpaMem*
             for (int i = 0; i < 9; i++) gc[6 + i] = R.m[i];
             gc[15] = pp.x; gc[16] = pp.y; gc[17] = pp.z;
         }
-    } else if (threadIdx.x == 0) {
+    } else if (lead) {
         gc[0] = 0.0;
     }
     v3 cn = V(n.x, n.y, n.z), cp = V(p.x, p.y, p.z);
@@ -1572,7 +1632,7 @@ __device__ __noinline__ static void team_gjk(const Scene* s, int k, ugk::EpaMem*
         cp = vadd(cp, vscale(cn, d));
         cn = vneg(cn);
     }
-    if (threadIdx.x == 0) {
+    if (lead) {
         sh.u.cand.n[k] = ok ? 1 : 0;
         sh.u.cand.c[k][0].n = cn;
         sh.u.cand.c[k][0].pB = cp;
@@ -1724,13 +1784,24 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) sh.is[3] = c0; /* the pass's first pair (team_poly_cyl's certificate slot) */
-        for (unsigned long long hm = ballot(hk); hm != 0ull; hm &= hm - 1ull) {
-            const int k = __builtin_ctzll(hm);
-            if (GJK) {
-                team_gjk(s, k, (ugk::EpaMem*)(ws + WS_EPA), (gdouble*)(ws + WS_GC) + GC_DOUBLES * sh.ov[c0 + k]);
-                PROF_CNT(PC_HULL, 1);
-                continue;
+        if (GJK) {
+            /* the GJK pairs in rounds of GJK_NG: group g runs the round's g-th pair on its own EPA store */
+            const unsigned long long hq = ballot(hk);
+            const int nq = __popcll(hq), g = lane / GJK_G;
+            for (int r0 = 0; r0 < nq; r0 += GJK_NG) {
+                if (r0 + g < nq) {
+                    unsigned long long m = hq;
+                    for (int j = 0; j < r0 + g; j++) m &= m - 1ull;
+                    const int k = __builtin_ctzll(m);
+                    team_gjk(s, k, (ugk::EpaMem*)(ws + WS_EPA) + g, (gdouble*)(ws + WS_GC) + GC_DOUBLES * sh.ov[c0 + k]);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
             }
+            PROF_CNT(PC_HULL, nq);
+        }
+        for (unsigned long long hm = GJK ? 0ull : ballot(hk); hm != 0ull; hm &= hm - 1ull) {
+            const int k = __builtin_ctzll(hm);
             const PairInfo pi = sh.pinfo[k];
             if (FULL && (pi.kb == UG_SHAPE_CYL || pi.ka == UG_SHAPE_CYL))
                 team_poly_cyl(k, pi.ka == UG_SHAPE_CYL, (gdouble*)(ws + WS_FC));
