@@ -14,7 +14,7 @@
 #endif
 #include "../urgym_amd/csrc/ug_gjk.h"
 
-UGK_FN ugk::gv ugk_hull_support(int v0, int nv, int, ugk::gv d) {
+UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
     double best = -__builtin_inf();
     int bi = 0;
     for (int i = 0; i < nv; i++) {
@@ -26,26 +26,20 @@ UGK_FN ugk::gv ugk_hull_support(int v0, int nv, int, ugk::gv d) {
     return ugk::V3(p[0], p[1], p[2]);
 }
 
-UGK_FN void ugk_epa_reset_lists(ugk::EpaMem* E) {
-    for (int i = 0; i < ugk::kEpaMaxFaces; i++) {
-        E->stock[i] = ugk::kEpaMaxFaces - 1 - i;
-        E->fc[i].inhull = 0;
-    }
-}
-/* m_hull's first minimum of d * d: the largest stamp among the minima; a NaN at the root (the largest stamp) wins */
-UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E) {
-    int root = -1;
-    for (int f = 0; f < ugk::kEpaMaxFaces; f++)
-        if (E->fc[f].inhull && (root < 0 || E->fc[f].stamp > E->fc[root].stamp)) root = f;
-    double mind = E->fc[root].d * E->fc[root].d;
-    if (mind != mind) return root;
+/* m_hull's first minimum of d * d over the hull array: the largest stamp among the minima; a NaN at the root (the
+ * largest stamp) wins */
+UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E, int hcount) {
+    int root = 0;
+    for (int i = 1; i < hcount; i++)
+        if (E->hl[i].stamp > E->hl[root].stamp) root = i;
+    double mind = E->hl[root].d * E->hl[root].d;
+    if (mind != mind) return E->hl[root].f;
     int best = root;
-    for (int f = 0; f < ugk::kEpaMaxFaces; f++) {
-        if (!E->fc[f].inhull) continue;
-        const double sqd = E->fc[f].d * E->fc[f].d;
-        if (sqd < mind || (sqd == mind && E->fc[f].stamp > E->fc[best].stamp)) { best = f; mind = sqd; }
+    for (int i = 0; i < hcount; i++) {
+        const double sqd = E->hl[i].d * E->hl[i].d;
+        if (sqd < mind || (sqd == mind && E->hl[i].stamp > E->hl[best].stamp)) { best = i; mind = sqd; }
     }
-    return best;
+    return E->hl[best].f;
 }
 
 static ugk::EpaMem g_epa;

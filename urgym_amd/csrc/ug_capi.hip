@@ -383,9 +383,6 @@ __global__ void __launch_bounds__(TEAM, 1) k_gjk_query(const double* q, int n, d
         S[k].kind = (int)P[0]; S[k].v0 = (int)P[1]; S[k].nv = (int)P[2];
         S[k].imp = ugk::V3(P[3], P[4], P[5]);
         S[k].margin = P[6];
-        S[k].c0 = -1; /* a full hull (its first vertex a full hull's) takes its chunk spheres, as in the sims */
-        for (int si = 0; si < UG_NSHAPE; si++)
-            if (S[k].kind == UG_SHAPE_HULL && S[k].nv > 2 * TEAM && UG_SHAPE_FV0[si] == S[k].v0) S[k].c0 = UG_SHAPE_FC0[si];
         for (int j = 0; j < 9; j++) T[k].R.m[j] = P[7 + j];
         T[k].p = ugk::V3(P[16], P[17], P[18]);
     }

@@ -66,12 +66,12 @@ UGK_FN bool veq(gv a, gv b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
 UGK_FN gv vsel(bool c, gv a, gv b) { return V3(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
 
 /* a convex shape as GJK sees it (kind: UG_SHAPE_*; imp: box / cylinder implicit dimensions; margin: getMargin) */
-struct GShape { int kind, v0, nv; gv imp; double margin; int c0 = -1; }; /* c0: a full hull's first chunk sphere, or -1 */
+struct GShape { int kind, v0, nv; gv imp; double margin; };
 
 } /* namespace ugk */
 
 /* the includer's hull support: the vertex of hull [v0, v0 + nv) with the first maximal dot product with d */
-UGK_FN ugk::gv ugk_hull_support(int v0, int nv, int c0, ugk::gv d);
+UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d);
 
 namespace ugk {
 
@@ -100,7 +100,7 @@ UGK_FN gv support0(const GShape& s, gv d) {
         }
         return V3(s.imp.x, 0.0, z);
     }
-    return ugk_hull_support(s.v0, s.nv, s.c0, d);
+    return ugk_hull_support(s.v0, s.nv, d);
 }
 /* localGetSupportVertexNonVirtual */
 UGK_FN gv support(const GShape& s, gv d) {
@@ -347,9 +347,12 @@ UGK_FN bool vs_in(const Voronoi& s, gv w) {
 /* ---------------- btGjkEpa2: GJK + EPA in the global workspace ---------------- */
 struct ESv { gv d, w; };
 /* a face; Bullet's two intrusive lists become: the free faces a stack (m_stock is only ever popped at its root and
- * pushed there), the hull a membership flag plus an append stamp (m_hull's list order is most recently appended
- * first, so its first minimum is the largest stamp among the minima -- what ugk_epa_findbest returns) */
-struct EFace { gv n; double d; int c[3], f[3], e[3], pass, inhull, stamp; };
+ * pushed there; it starts as faces 0, 1, 2, ... from the root, kept implicit as a 'fresh' counter below the pushed
+ * ones), the hull an unordered array of (d, append stamp, face) with swap-removal (m_hull's list order is most
+ * recently appended first, so its first minimum is the largest stamp among the minima -- what ugk_epa_findbest
+ * returns from the array) */
+struct EFace { gv n; double d; int c[3], f[3], e[3], pass; };
+struct EHull { double d; int stamp, f; };
 struct EpaMem {
     ESv sv[4 + kEpaMaxVertices]; /* [0, 4) the GJK's store, then the EPA's */
     EFace fc[kEpaMaxFaces];
@@ -357,8 +360,10 @@ struct EpaMem {
     double sp[2][4];
     int srank[2];
     int freev[4];
-    int stk[3 * kEpaMaxFaces];   /* expand()'s frames: face, edge, stage */
-    int stock[kEpaMaxFaces];     /* the free faces, top = the list root */
+    EHull hl[kEpaMaxFaces];      /* the hull faces [0, hcount), unordered */
+    int hpos[kEpaMaxFaces];      /* a hull face's slot in hl */
+    int stk[kEpaMaxFaces];       /* expand()'s parent frames, packed (e_frame) */
+    int stock[kEpaMaxFaces];     /* the faces pushed back to the stock, top = the list root */
 };
 struct Mink { GShape s0, s1; gm toshape1; gx toshape0; bool margins; };
 UGK_FN gv mk_ls(const Mink& M, int i, gv d) {
@@ -623,32 +628,35 @@ UGK_FN bool g2_enclose(EpaMem* E, Gjk2& g, const Mink& M) {
     return false;
 }
 
-struct Epa { int status, nextsv, hcount, nstock, stampctr; gv normal; double depth; int rc[3]; double rp[3]; int rrank; };
+struct Epa { int status, nextsv, hcount, nstock, nfresh, stampctr; gv normal; double depth; int rc[3]; double rp[3]; int rrank; };
 
 } /* namespace ugk */
-/* the includer's EPA list hooks: the free-face stack set to Bullet's initial order (faces 0, 1, 2, ... popped first) and
- * every face out of the hull; the hull face with the smallest d * d, ties to the largest stamp (m_hull's first
- * minimum), except that a NaN at the list root keeps the root (Bullet's loop never replaces a NaN) */
-UGK_FN void ugk_epa_reset_lists(ugk::EpaMem* E);
-UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E);
+/* the includer's EPA hook: of the hull faces hl[0, hcount), the one with the smallest d * d, ties to the largest stamp
+ * (m_hull's first minimum), except that a NaN at the list root (the largest stamp) keeps the root (Bullet's loop never
+ * replaces a NaN) */
+UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E, int hcount);
 namespace ugk {
 
 UGK_FN void e_bind(EpaMem* E, int fa, int ea, int fb, int eb) {
     E->fc[fa].e[ea] = eb; E->fc[fa].f[ea] = fb;
     E->fc[fb].e[eb] = ea; E->fc[fb].f[eb] = fa;
 }
-UGK_FN void h_append(EpaMem* E, Epa& P, int f) {
-    E->fc[f].inhull = 1;
-    E->fc[f].stamp = ++P.stampctr;
-    P.hcount++;
+UGK_FN void h_append(EpaMem* E, Epa& P, int f, double d, int stamp) {
+    EHull h;
+    h.d = d; h.stamp = stamp; h.f = f;
+    E->hl[P.hcount] = h;
+    E->hpos[f] = P.hcount++;
 }
 UGK_FN void h_remove(EpaMem* E, Epa& P, int f) {
-    E->fc[f].inhull = 0;
-    P.hcount--;
+    const int i = E->hpos[f], last = --P.hcount;
+    if (i != last) {
+        const EHull t = E->hl[last];
+        E->hl[i] = t;
+        E->hpos[t.f] = i;
+    }
 }
 UGK_FN void s_push(EpaMem* E, Epa& P, int f) { E->stock[P.nstock++] = f; }
-UGK_FN bool e_edgedist(EpaMem* E, gv fn, int a, int b, double& dist) {
-    const gv aw = E->sv[a].w, bw = E->sv[b].w;
+UGK_FN bool e_edgedist(gv aw, gv bw, gv fn, double& dist) {
     const gv ba = sub(bw, aw);
     const gv n_ab = cross(ba, fn);
     if (dot(aw, n_ab) < 0) {
@@ -667,48 +675,55 @@ UGK_FN bool e_edgedist(EpaMem* E, gv fn, int a, int b, double& dist) {
     return false;
 }
 UGK_FN int e_newface(EpaMem* E, Epa& P, int a, int b, int c, bool forced) {
-    if (P.nstock > 0) {
-        const int f = E->stock[--P.nstock];
-        h_append(E, P, f);
+    if (P.nstock > 0 || P.nfresh < kEpaMaxFaces) {
+        const int f = P.nstock > 0 ? E->stock[P.nstock - 1] : P.nfresh;
+        if (P.nstock > 0) P.nstock--;
+        else P.nfresh++;
+        const int stamp = ++P.stampctr; /* m_hull.append: the face joins the hull before its plane is known */
+        const gv aw = E->sv[a].w, bw = E->sv[b].w, cw = E->sv[c].w;
         EFace& F = E->fc[f];
         F.pass = 0;
         F.c[0] = a; F.c[1] = b; F.c[2] = c;
-        const gv n = cross(sub(E->sv[b].w, E->sv[a].w), sub(E->sv[c].w, E->sv[a].w));
+        const gv n = cross(sub(bw, aw), sub(cw, aw));
         const double l = len(n);
         if (l > kEpaAccuracy) {
             double d;
-            if (!(e_edgedist(E, n, a, b, d) || e_edgedist(E, n, b, c, d) || e_edgedist(E, n, c, a, d)))
-                d = dot(E->sv[a].w, n) / l;
+            if (!(e_edgedist(aw, bw, n, d) || e_edgedist(bw, cw, n, d) || e_edgedist(cw, aw, n, d)))
+                d = dot(aw, n) / l;
             F.d = d;
             F.n = mulinv(n, l);
-            if (forced || d >= -kEpaPlaneEps) return f;
+            if (forced || d >= -kEpaPlaneEps) {
+                h_append(E, P, f, d, stamp);
+                return f;
+            }
             P.status = EPA_NONCONVEX;
         } else {
             F.n = n;
             P.status = EPA_DEGENERATED;
         }
-        h_remove(E, P, f);
-        s_push(E, P, f);
+        s_push(E, P, f); /* m_hull.remove + m_stock.append: back on top of the stock */
         return -1;
     }
-    P.status = P.nstock > 0 ? EPA_OUTOFVERTICES : EPA_OUTOFFACES;
+    P.status = EPA_OUTOFFACES;
     return -1;
 }
-/* EPA::expand as an explicit depth-first walk: frame (face, edge, stage); stage 0 = entry, 1 = the first neighbour's
- * answer is in r, 2 = the second's.  The same visits, face allocations and list operations as the recursion. */
-UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, int f0, int e0, int& hcf, int& hff, int& hnf) {
-    int sp = 0;
+/* EPA::expand as an explicit depth-first walk.  The current frame (face, edge, stage; stage 0 = entry, 1 = the first
+ * neighbour's answer is in r, 2 = the second's) lives in registers, its parents on E->stk packed as face | edge << 8 |
+ * stage << 10 | second neighbour << 12 | its edge << 20 (read at entry: a visited face's other edges are not rebound
+ * while its subtree runs, the pass mark stops every re-entry).  The same visits, face allocations and list operations
+ * as the recursion. */
+UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, gv ww, int f0, int e0, int& hcf, int& hff, int& hnf) {
+    int sp = 0, f = f0, e = e0, stage = 0, f2 = 0, e2 = 0;
     bool r = false;
-    E->stk[0] = f0; E->stk[1] = e0; E->stk[2] = 0;
-    sp = 1;
-    while (sp > 0) {
-        int* fr = &E->stk[3 * (sp - 1)];
-        const int f = fr[0], e = fr[1], stage = fr[2];
-        const int e1 = e == 2 ? 0 : e + 1, e2 = e == 0 ? 2 : e - 1;
+    for (;;) {
+        bool pop = true;
         if (stage == 0) {
-            if (E->fc[f].pass == pass) { r = false; sp--; continue; }
-            if ((dot(E->fc[f].n, E->sv[w].w) - E->fc[f].d) < -kEpaPlaneEps) {
-                const int nf = e_newface(E, P, E->fc[f].c[e1], E->fc[f].c[e], w, false);
+            const EFace F = E->fc[f]; /* the face's record in one batch of loads */
+            const int e1 = e == 2 ? 0 : e + 1, em = e == 0 ? 2 : e - 1;
+            if (F.pass == pass) {
+                r = false;
+            } else if ((dot(F.n, ww) - F.d) < -kEpaPlaneEps) {
+                const int nf = e_newface(E, P, F.c[e1], F.c[e], w, false);
                 r = false;
                 if (nf >= 0) {
                     e_bind(E, nf, 0, f, e);
@@ -718,29 +733,34 @@ UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, int f0, int e0, int& hc
                     hnf++;
                     r = true;
                 }
-                sp--;
-                continue;
+            } else {
+                E->fc[f].pass = pass;
+                E->stk[sp++] = f | (e << 8) | (1 << 10) | (F.f[em] << 12) | (F.e[em] << 20);
+                f = F.f[e1];
+                e = F.e[e1];
+                pop = false;
             }
-            E->fc[f].pass = pass;
-            fr[2] = 1;
-            int* ch = &E->stk[3 * sp];
-            ch[0] = E->fc[f].f[e1]; ch[1] = E->fc[f].e[e1]; ch[2] = 0;
-            sp++;
-            continue;
-        }
-        if (stage == 1) {
-            if (!r) { sp--; continue; }
-            fr[2] = 2;
-            int* ch = &E->stk[3 * sp];
-            ch[0] = E->fc[f].f[e2]; ch[1] = E->fc[f].e[e2]; ch[2] = 0;
-            sp++;
-            continue;
-        }
-        if (r) {
+        } else if (stage == 1) {
+            if (r) {
+                E->stk[sp++] = f | (e << 8) | (2 << 10);
+                f = f2;
+                e = e2;
+                stage = 0;
+                pop = false;
+            }
+        } else if (r) {
             h_remove(E, P, f);
             s_push(E, P, f);
         }
-        sp--;
+        if (pop) {
+            if (sp == 0) break;
+            const int fr = E->stk[--sp];
+            f = fr & 255;
+            e = (fr >> 8) & 3;
+            stage = (fr >> 10) & 3;
+            f2 = (fr >> 12) & 255;
+            e2 = (fr >> 20) & 3;
+        }
     }
     return r;
 }
@@ -766,7 +786,7 @@ UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
         tetra[2] = e_newface(E, P, c[2], c[1], c[3], true);
         tetra[3] = e_newface(E, P, c[0], c[2], c[3], true);
         if (P.hcount == 4) {
-            int best = ugk_epa_findbest(E);
+            int best = ugk_epa_findbest(E, P.hcount);
             UGK_ADD(PF_EPA_SETUP, t_setup);
             EFace outer = E->fc[best];
             int pass = 0;
@@ -787,18 +807,20 @@ UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
                 UGK_T0(t_sup);
                 g2_getsupport(E, M, E->fc[best].n, w);
                 UGK_ADD(PF_EPA_SUP, t_sup);
-                const double wdist = dot(E->fc[best].n, E->sv[w].w) - E->fc[best].d;
+                const gv ww = E->sv[w].w;
+                const EFace B = E->fc[best];
+                const double wdist = dot(B.n, ww) - B.d;
                 if (!(wdist > kEpaAccuracy)) { P.status = EPA_ACCURACYREACHED; break; }
                 UGK_T0(t_exp);
                 for (int j = 0; j < 3 && valid; j++)
-                    valid = e_expand(E, P, pass, w, E->fc[best].f[j], E->fc[best].e[j], hcf, hff, hnf) && valid;
+                    valid = e_expand(E, P, pass, w, ww, B.f[j], B.e[j], hcf, hff, hnf) && valid;
                 UGK_ADD(PF_EPA_EXPAND, t_exp);
                 if (!(valid && hnf >= 3)) { P.status = EPA_INVALIDHULL; break; }
                 e_bind(E, hcf, 1, hff, 2);
                 h_remove(E, P, best);
                 s_push(E, P, best);
                 UGK_T0(t_best);
-                best = ugk_epa_findbest(E);
+                best = ugk_epa_findbest(E, P.hcount);
                 UGK_ADD(PF_EPA_BEST, t_best);
                 outer = E->fc[best];
             }
@@ -835,9 +857,9 @@ UGK_FN void e_init(EpaMem* E, Epa& P) {
     P.depth = 0;
     P.nextsv = 0;
     P.hcount = 0;
-    P.nstock = kEpaMaxFaces;
+    P.nstock = 0; /* the stock: faces 0, 1, 2, ... from the root (fresh), nothing pushed back yet */
+    P.nfresh = 0;
     P.stampctr = 0;
-    ugk_epa_reset_lists(E); /* stock[i] = 255 - i (face 0 on top), no face in the hull */
 }
 struct Res { gv w0, w1, normal; double distance; };
 UGK_FN bool g2_penetration(EpaMem* E, const GShape& s0, const gx& w0, const GShape& s1, const gx& w1, gv guess, Res& r) {

@@ -322,10 +322,9 @@ __device__ __forceinline__ void group_best(double& v, int& idx, bool want_max) {
 /* ug_gjk.h's hull support on the lane group: btVector3::maxDot's first maximum (the largest dot product, on a tie the
  * lowest vertex index) over the whole hull, called by every lane of the group (its GJK runs uniformly).  Lane l of the
  * group dots vertices l, l + G, ... of a vertex range keeping its first maximum, and the DPP arg-max keeps the larger
- * value and, on a tie, the lower index.  A full hull of more than two 64-vertex chunks is culled by its chunk spheres
- * (UG_HULL_CS): the chunk with the largest bound c . d + r |d| first, then only the chunks whose bound reaches the best
- * value found (>=, so a tie at a lower index in another chunk is still seen); the bound carries a 1e-12 relative slack
- * over the dot products' rounding, so a skipped chunk cannot hold the maximum. */
+ * value and, on a tie, the lower index.  (Culling a full hull's 64-vertex chunks by their bounding spheres -- the
+ * best-bound chunk first, then every chunk whose bound reaches its maximum -- measured 2.2x slower per support on
+ * BallBalance: the spheres overlap, most chunks pass, and each pass is a serial load + reduction.) */
 __device__ __forceinline__ void hs_scan(int v0, int lo, int hi, ugk::gv d, int gl, double& best, int& bi) {
     constexpr int G = ugd::GJK_G, U = G == TEAM ? 4 : 8;
     /* U vertices per trip: their loads in flight together (the hull is cache-resident, the latency is the cost) */
@@ -345,38 +344,13 @@ __device__ __forceinline__ void hs_scan(int v0, int lo, int hi, ugk::gv d, int g
         }
     }
 }
-UGK_FN ugk::gv ugk_hull_support(int v0, int nv, int c0, ugk::gv d) {
+UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
     constexpr int G = ugd::GJK_G;
     const int gl = threadIdx.x & (G - 1);
     PROF_T0(t_sup);
     double best = -__builtin_inf();
     int bi = 0x7fffffff;
-    const int nch = (nv + TEAM - 1) / TEAM;
-    const double dl1 = ug_fabs(d.x) + ug_fabs(d.y) + ug_fabs(d.z);
-    if (nch <= 2 || nch > G || c0 < 0 || !(dl1 < 1e300)) {
-        hs_scan(v0, 0, nv, d, gl, best, bi);
-    } else {
-        double b = -__builtin_inf();
-        int ci = 0x7fffffff;
-        if (gl < nch) {
-            const double* S = &UG_HULL_CS[4 * (c0 + gl)];
-            const double dn = ug_sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
-            b = S[0] * d.x + S[1] * d.y + S[2] * d.z + S[3] * dn +
-                1e-12 * (ug_fabs(S[0]) + ug_fabs(S[1]) + ug_fabs(S[2]) + S[3]) * dl1;
-            ci = gl;
-        }
-        double bb = b;
-        int c1 = ci;
-        ugd::group_best(bb, c1, true);
-        hs_scan(v0, TEAM * c1, TEAM * c1 + TEAM < nv ? TEAM * c1 + TEAM : nv, d, gl, best, bi);
-        ugd::group_best(best, bi, true);
-        const int gb = threadIdx.x & ~(G - 1);
-        unsigned long long more = (ugd::ballot(gl < nch && gl != c1 && b >= best) >> gb) & ((1ull << G) - 1ull);
-        for (; more != 0ull; more &= more - 1ull) {
-            const int c = __builtin_ctzll(more);
-            hs_scan(v0, TEAM * c, TEAM * c + TEAM < nv ? TEAM * c + TEAM : nv, d, gl, best, bi);
-        }
-    }
+    hs_scan(v0, 0, nv, d, gl, best, bi);
     ugd::group_best(best, bi, true);
     if (bi == 0x7fffffff) bi = 0;
     const double* p = &UG_HULL_V[3 * (v0 + bi)];
@@ -389,35 +363,28 @@ UGK_FN ugk::gv ugk_hull_support(int v0, int nv, int c0, ugk::gv d) {
     return ugk::V3(p[0], p[1], p[2]);
 }
 
-/* ug_gjk.h's EPA list hooks on the wave: the free-face stack and the hull flags reset lane-parallel (published to the
- * wave's later loads), and m_hull's first minimum (smallest d * d, ties to the largest append stamp; a NaN at the root
- * keeps the root) as a lane-strided scan + DPP arg-min instead of a pointer chase through the workspace */
-UGK_FN void ugk_epa_reset_lists(ugk::EpaMem* E) {
-    for (int i = threadIdx.x & (ugd::GJK_G - 1); i < ugk::kEpaMaxFaces; i += ugd::GJK_G) {
-        E->stock[i] = ugk::kEpaMaxFaces - 1 - i;
-        E->fc[i].inhull = 0;
-    }
-    __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
-}
-UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E) {
+/* ug_gjk.h's EPA hook on the lane group: m_hull's first minimum (smallest d * d, ties to the largest append stamp; a
+ * NaN at the root -- the largest stamp -- keeps the root) as a lane-strided scan of the hull array + a DPP arg-min of
+ * the key (d * d, (2^20 - stamp) * 256 + face); the root is looked up only when some face of the hull has a NaN plane */
+UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E, int hcount) {
     constexpr int G = ugd::GJK_G;
     const int gl = threadIdx.x & (G - 1);
-    /* one pass over the lane's faces (all loads in flight): the root candidate and the arg-min together */
-    double rs = -1.0, bv = 0.0;
-    int rf = 0x7fffffff, bi = 0x7fffffff;
-#pragma unroll
-    for (int f = gl; f < ugk::kEpaMaxFaces; f += G) {
-        const int in = E->fc[f].inhull, st = E->fc[f].stamp;
-        const double d = E->fc[f].d, sqd = d * d;
-        if (in && (rf == 0x7fffffff || (double)st > rs)) { rs = (double)st; rf = f; }
-        const int key = ((1 << 20) - st) * ugk::kEpaMaxFaces + f; /* lower key = larger stamp */
-        if (in && sqd == sqd && (bi == 0x7fffffff || sqd < bv || (sqd == bv && key < bi))) { bv = sqd; bi = key; }
+    double bv = 0.0, rs = -1.0;
+    int bi = 0x7fffffff, ri = 0x7fffffff;
+    bool nan = false;
+    for (int i = gl; i < hcount; i += G) {
+        const ugk::EHull h = E->hl[i];
+        const double sqd = h.d * h.d;
+        if (ri == 0x7fffffff || (double)h.stamp > rs) { rs = (double)h.stamp; ri = i; }
+        if (sqd != sqd) { nan = true; continue; }
+        const int key = ((1 << 20) - h.stamp) * ugk::kEpaMaxFaces + h.f; /* lower key = larger stamp */
+        if (bi == 0x7fffffff || sqd < bv || (sqd == bv && key < bi)) { bv = sqd; bi = key; }
     }
-    ugd::group_best(rs, rf, true); /* the root: the largest stamp */
-    if (rf == 0x7fffffff) return 0;
-    const double rd = E->fc[rf].d;
-    if ((rd * rd) != (rd * rd)) return rf;
+    if ((ugd::ballot(nan) >> (threadIdx.x & ~(G - 1))) & ((1ull << G) - 1ull)) {
+        ugd::group_best(rs, ri, true); /* the root: the largest stamp */
+        const ugk::EHull h = E->hl[ri];
+        if ((h.d * h.d) != (h.d * h.d)) return h.f;
+    }
     ugd::group_best(bv, bi, false);
     return bi & (ugk::kEpaMaxFaces - 1);
 }
@@ -1574,7 +1541,6 @@ __device__ __forceinline__ static ugk::GShape gshape_of(const Collider& c) {
     g.nv = c.kind == UG_SHAPE_HULL ? c.nv : 0;
     g.imp = ugk::V3(c.gimp.x, c.gimp.y, c.gimp.z);
     g.margin = c.gmargin;
-    g.c0 = c.kind == UG_SHAPE_HULL && c.nv > 2 * TEAM ? c.c0 : -1; /* a full hull's chunk spheres (ugk_hull_support) */
     return g;
 }
 __device__ __forceinline__ static ugk::gx to_gx(const XF& T) {
