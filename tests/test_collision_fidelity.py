@@ -1,5 +1,5 @@
 """The collision-fidelity builds of the restatement (tools/collision_fidelity.py, oracle/ug_fidelity.h): the
-Bullet-polyhedral narrowphase pinned by box-box known answers (face contact: 4 clipped corners at the penetration
+Bullet SAT-polyhedral narrowphase (the sat variant) pinned by box-box known answers (face contact: 4 clipped corners at the penetration
 depth; edge-edge: one contact at the crossing), and every variant steps each task family with finite state.
 These builds measure the product's collision substitutes (profiles/collision_fidelity.json);
 they need the reference meshes, so the module skips where /root/reference is absent (the GPU box)."""
@@ -31,7 +31,7 @@ def _rot(axis, ang):
 
 
 def _box_box(fid, ha, Ra, pa, hb, Rb, pb, thr=0.02):
-    L = ctypes.CDLL(fid.LIBS["bullet"])
+    L = ctypes.CDLL(fid.LIBS["sat"])
     P = ctypes.c_void_p
     L.ugo_fid_box_box.argtypes = [P] * 6 + [ctypes.c_double, P, ctypes.c_int]
     arrs = [np.ascontiguousarray(x, np.float64) for x in (ha, Ra, pa, hb, Rb, pb)]
@@ -77,7 +77,7 @@ def test_variants_step_finite(fid, task):
     e0.reset()
     s0 = e0.get_state()
     acts = fid.actions(task, 2, 3)
-    for v in ("lod", "bullet"):
+    for v in ("lod", "vih", "sat"):
         e = OracleEnv(task, 1000, lib_path=fid.LIBS.get(v), flags=fid.FLAGS.get(v, 0))
         e.set_state(s0)
         for a in acts:

@@ -13,6 +13,8 @@
 #   bash tools/gpu.sh profile <tag> [bench.py args...]  rocprofv3 kernel trace + stats, FETCH_SIZE / WRITE_SIZE PMC
 #                                                       passes (one counter group per run), traffic json, bench line
 #   bash tools/gpu.sh pmcmix <tag> [bench.py args...]   instruction-mix / stall PMC passes
+#   bash tools/gpu.sh world8 <tag> [bench.py args...]   the 8-rank path rehearsed on this one GPU: 8 gloo ranks
+#                                                       (torch.distributed.run, 127.0.0.1) -> <tag>/world8.json
 #   bash tools/gpu.sh final <tag>                       round-end check: whole suite, smoke, headline bench
 # Several jobs in one call: gpurun -- 'bash tools/gpu.sh tests t1 tests/test_gpu_gjk.py && bash tools/gpu.sh bench t1'
 set -u
@@ -74,6 +76,11 @@ pmcmix)
             > "$OUT/p$i.log" 2>&1 || { echo "PASS $i FAILED"; exit 1; }
     done
     echo PMC_MIX_OK ;;
+world8)
+    timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29533 bench.py --gpus 8 --backend gloo --no-cpu-baseline "$@" > "$OUT/world8.json" \
+        2> "$OUT/world8.err"; rc=$?
+    echo "[world8] rc=$rc"; cut -c1-400 "$OUT/world8.json"; exit $rc ;;
 final)
     bash tools/gpu.sh tests "$TAG" && bash tools/gpu.sh smoke "$TAG" && bash tools/gpu.sh bench "$TAG" ;;
 *)
