@@ -15,6 +15,8 @@
 #   bash tools/gpu.sh pmcmix <tag> [bench.py args...]   instruction-mix / stall PMC passes
 #   bash tools/gpu.sh world8 <tag> [bench.py args...]   the 8-rank path rehearsed on this one GPU: 8 gloo ranks
 #                                                       (torch.distributed.run, 127.0.0.1) -> <tag>/world8.json
+#   bash tools/gpu.sh icache <tag> [bench.py args...]   instruction-cache PMC pass (SQC_ICACHE_*, SQ_IFETCH) after
+#                                                       listing the box's counters -> <tag>/counters.txt, <tag>/ic/
 #   bash tools/gpu.sh final <tag>                       round-end check: whole suite, smoke, headline bench
 # Several jobs in one call: gpurun -- 'bash tools/gpu.sh tests t1 tests/test_gpu_gjk.py && bash tools/gpu.sh bench t1'
 set -u
@@ -76,6 +78,25 @@ pmcmix)
             > "$OUT/p$i.log" 2>&1 || { echo "PASS $i FAILED"; exit 1; }
     done
     echo PMC_MIX_OK ;;
+icache)
+    ARGS="${*:---steps 5 --warmup 2 --reps 1 --no-cpu-baseline}"
+    timeout -s KILL 60 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
+    G=""
+    for c in SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE; do
+        grep -qw "$c" "$OUT/counters.txt" && G="$G $c"
+    done
+    echo "icache counters:$G"
+    [ -n "$G" ] || exit 0
+    timeout -s KILL 180 rocprofv3 --pmc $G --output-format csv -d "$OUT/ic" -o run -- python3 bench.py $ARGS \
+        > "$OUT/ic.log" 2>&1 || { echo "ICACHE PASS FAILED"; exit 1; }
+    G2=""
+    for c in SQ_IFETCH SQ_IFETCH_LEVEL SQ_WAIT_INST_ANY SQ_WAVE_CYCLES; do
+        grep -qw "$c" "$OUT/counters.txt" && G2="$G2 $c"
+    done
+    [ -n "$G2" ] || exit 0
+    timeout -s KILL 180 rocprofv3 --pmc $G2 --output-format csv -d "$OUT/if" -o run -- python3 bench.py $ARGS \
+        > "$OUT/if.log" 2>&1 || { echo "IFETCH PASS FAILED"; exit 1; }
+    echo ICACHE_OK ;;
 world8)
     timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29533 bench.py --gpus 8 --backend gloo --no-cpu-baseline "$@" > "$OUT/world8.json" \
