@@ -26,6 +26,8 @@ UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
     return ugk::V3(p[0], p[1], p[2]);
 }
 
+UGK_FN void ugk_ls_put(int* mem, ugk::LStack&, int i, int v) { mem[i] = v; }
+UGK_FN int ugk_ls_get(const int* mem, const ugk::LStack&, int i) { return mem[i]; }
 /* m_hull's first minimum of d * d over the hull array: the largest stamp among the minima; a NaN at the root (the
  * largest stamp) wins */
 UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E, int hcount) {

@@ -628,13 +628,19 @@ UGK_FN bool g2_enclose(EpaMem* E, Gjk2& g, const Mink& M) {
     return false;
 }
 
-struct Epa { int status, nextsv, hcount, nstock, nfresh, stampctr; gv normal; double depth; int rc[3]; double rp[3]; int rrank; };
+/* a small stack of ints (the free-face stack, expand()'s parent frames) whose lowest slots may live in registers */
+struct LStack { int reg; };
+struct Epa { int status, nextsv, hcount, nstock, nfresh, stampctr; LStack stock; gv normal; double depth; int rc[3]; double rp[3]; int rrank; };
 
 } /* namespace ugk */
 /* the includer's EPA hook: of the hull faces hl[0, hcount), the one with the smallest d * d, ties to the largest stamp
  * (m_hull's first minimum), except that a NaN at the list root (the largest stamp) keeps the root (Bullet's loop never
  * replaces a NaN) */
 UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E, int hcount);
+/* the includer's LStack hooks: slot i of the stack whose memory is mem (the kernels hold slots [0, 16) in the lane
+ * group's registers, lane i slot i) */
+UGK_FN void ugk_ls_put(int* mem, ugk::LStack& s, int i, int v);
+UGK_FN int ugk_ls_get(const int* mem, const ugk::LStack& s, int i);
 namespace ugk {
 
 UGK_FN void e_bind(EpaMem* E, int fa, int ea, int fb, int eb) {
@@ -655,7 +661,7 @@ UGK_FN void h_remove(EpaMem* E, Epa& P, int f) {
         E->hpos[t.f] = i;
     }
 }
-UGK_FN void s_push(EpaMem* E, Epa& P, int f) { E->stock[P.nstock++] = f; }
+UGK_FN void s_push(EpaMem* E, Epa& P, int f) { ugk_ls_put(E->stock, P.stock, P.nstock++, f); }
 UGK_FN bool e_edgedist(gv aw, gv bw, gv fn, double& dist) {
     const gv ba = sub(bw, aw);
     const gv n_ab = cross(ba, fn);
@@ -676,7 +682,7 @@ UGK_FN bool e_edgedist(gv aw, gv bw, gv fn, double& dist) {
 }
 UGK_FN int e_newface(EpaMem* E, Epa& P, int a, int b, int c, bool forced) {
     if (P.nstock > 0 || P.nfresh < kEpaMaxFaces) {
-        const int f = P.nstock > 0 ? E->stock[P.nstock - 1] : P.nfresh;
+        const int f = P.nstock > 0 ? ugk_ls_get(E->stock, P.stock, P.nstock - 1) : P.nfresh;
         if (P.nstock > 0) P.nstock--;
         else P.nfresh++;
         const int stamp = ++P.stampctr; /* m_hull.append: the face joins the hull before its plane is known */
@@ -715,6 +721,8 @@ UGK_FN int e_newface(EpaMem* E, Epa& P, int a, int b, int c, bool forced) {
 UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, gv ww, int f0, int e0, int& hcf, int& hff, int& hnf) {
     int sp = 0, f = f0, e = e0, stage = 0, f2 = 0, e2 = 0;
     bool r = false;
+    LStack fs;
+    fs.reg = 0;
     for (;;) {
         bool pop = true;
         if (stage == 0) {
@@ -735,14 +743,14 @@ UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, gv ww, int f0, int e0, 
                 }
             } else {
                 E->fc[f].pass = pass;
-                E->stk[sp++] = f | (e << 8) | (1 << 10) | (F.f[em] << 12) | (F.e[em] << 20);
+                ugk_ls_put(E->stk, fs, sp++, f | (e << 8) | (1 << 10) | (F.f[em] << 12) | (F.e[em] << 20));
                 f = F.f[e1];
                 e = F.e[e1];
                 pop = false;
             }
         } else if (stage == 1) {
             if (r) {
-                E->stk[sp++] = f | (e << 8) | (2 << 10);
+                ugk_ls_put(E->stk, fs, sp++, f | (e << 8) | (2 << 10));
                 f = f2;
                 e = e2;
                 stage = 0;
@@ -754,7 +762,7 @@ UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, gv ww, int f0, int e0, 
         }
         if (pop) {
             if (sp == 0) break;
-            const int fr = E->stk[--sp];
+            const int fr = ugk_ls_get(E->stk, fs, --sp);
             f = fr & 255;
             e = (fr >> 8) & 3;
             stage = (fr >> 10) & 3;
@@ -858,6 +866,7 @@ UGK_FN void e_init(EpaMem* E, Epa& P) {
     P.nextsv = 0;
     P.hcount = 0;
     P.nstock = 0; /* the stock: faces 0, 1, 2, ... from the root (fresh), nothing pushed back yet */
+    P.stock.reg = 0;
     P.nfresh = 0;
     P.stampctr = 0;
 }

@@ -326,7 +326,7 @@ __device__ __forceinline__ void group_best(double& v, int& idx, bool want_max) {
  * best-bound chunk first, then every chunk whose bound reaches its maximum -- measured 2.2x slower per support on
  * BallBalance: the spheres overlap, most chunks pass, and each pass is a serial load + reduction.) */
 __device__ __forceinline__ void hs_scan(int v0, int lo, int hi, ugk::gv d, int gl, double& best, int& bi) {
-    constexpr int G = ugd::GJK_G, U = G == TEAM ? 4 : 8;
+    constexpr int G = ugd::GJK_G, U = G == TEAM ? 4 : 8; /* 16 measured the same (r4l) */
     /* U vertices per trip: their loads in flight together (the hull is cache-resident, the latency is the cost) */
     for (int i0 = lo + gl; i0 < hi; i0 += U * G) {
         double x[U], y[U], z[U];
@@ -363,6 +363,19 @@ UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
     return ugk::V3(p[0], p[1], p[2]);
 }
 
+/* ug_gjk.h's small stacks on the lane group: slots [0, GJK_G) in one register, lane i of the group holding slot i
+ * (read back through ds_bpermute, an LDS-crossbar hop instead of a workspace round trip), deeper slots in memory */
+UGK_FN void ugk_ls_put(int* mem, ugk::LStack& s, int i, int v) {
+    if (i < ugd::GJK_G) {
+        if ((int)(threadIdx.x & (ugd::GJK_G - 1)) == i) s.reg = v;
+    } else {
+        mem[i] = v;
+    }
+}
+UGK_FN int ugk_ls_get(const int* mem, const ugk::LStack& s, int i) {
+    if (i < ugd::GJK_G) return __shfl(s.reg, (int)(threadIdx.x & ~(ugd::GJK_G - 1)) + i, TEAM);
+    return mem[i];
+}
 /* ug_gjk.h's EPA hook on the lane group: m_hull's first minimum (smallest d * d, ties to the largest append stamp; a
  * NaN at the root -- the largest stamp -- keeps the root) as a lane-strided scan of the hull array + a DPP arg-min of
  * the key (d * d, (2^20 - stamp) * 256 + face); the root is looked up only when some face of the hull has a NaN plane */
