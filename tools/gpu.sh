@@ -9,7 +9,7 @@
 #   bash tools/gpu.sh sweep <tag> [bench.py args...]    every task at its BASELINE size -> <tag>/task<N>.json
 #   bash tools/gpu.sh phase <tag> [phase_prof args...]  phase cycles of the profiling build -> <tag>/phase.txt
 #   bash tools/gpu.sh chain <tag> [task envs]           reset-chain / step-chain timings -> <tag>/chain.txt
-#   bash tools/gpu.sh timeline <tag> [envs steps]       k_step block timeline -> <tag>/timeline.txt
+#   bash tools/gpu.sh timeline <tag> [timeline args]    k_step block timeline + schedule predictions -> <tag>/timeline.txt, .json
 #   bash tools/gpu.sh profile <tag> [bench.py args...]  rocprofv3 kernel trace + stats, FETCH_SIZE / WRITE_SIZE PMC
 #                                                       passes (one counter group per run), traffic json, bench line
 #   bash tools/gpu.sh pmcmix <tag> [bench.py args...]   instruction-mix / stall PMC passes
@@ -52,7 +52,7 @@ phase)
 chain)
     step 300 "$OUT/chain.txt" python tools/chain_bench.py "${1:-0}" "${2:-4096}" ;;
 timeline)
-    step 300 "$OUT/timeline.txt" python tools/timeline.py "${1:-4096}" "${2:-20}" ;;
+    step 300 "$OUT/timeline.txt" python tools/timeline.py --json "$OUT/timeline.json" "$@" ;;
 profile)
     timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
         python3 bench.py --no-cpu-baseline "$@" > "$OUT/trace.log" 2>&1 || { echo TRACE_FAIL; exit 1; }
