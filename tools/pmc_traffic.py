@@ -1,7 +1,7 @@
 """Reduce rocprofv3 FETCH_SIZE / WRITE_SIZE passes to HBM bytes per k_step launch.
 
 usage: python tools/pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> <out.json>
-       [--task T --envs N --steps K --warmup W --geometry G]
+       [--task T --envs N --steps K --warmup W --geometry G --contact C]
 
 Units and corrections follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section): both counters are in
 KB; on gfx950 FETCH_SIZE tallies 128-B requests at 64 B, so it is doubled; WRITE_SIZE is taken as is.
@@ -30,12 +30,14 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--geometry", choices=("full", "lod"), default="full")
+    ap.add_argument("--contact", choices=("gjk", "vih"), default="gjk")
     a, _ = ap.parse_known_args()
     f_kb, nf = per_launch(a.fetch, "FETCH_SIZE")
     w_kb, nw = per_launch(a.write, "WRITE_SIZE")
     fetch_b = 2.0 * f_kb * 1024.0  # gfx950: FETCH_SIZE reports half of the bytes read
     write_b = w_kb * 1024.0
-    out = {"kernel": "k_step", "task": a.task, "envs": a.envs, "geometry": a.geometry, "steps": a.steps, "warmup": a.warmup,
+    out = {"kernel": "k_step", "task": a.task, "envs": a.envs, "geometry": a.geometry, "contact": a.contact,
+           "steps": a.steps, "warmup": a.warmup,
            "launches": [nf, nw], "fetch_size_kb_avg": f_kb, "write_size_kb_avg": w_kb,
            "hbm_bytes_per_launch": fetch_b + write_b, "read_bytes_per_launch": fetch_b,
            "write_bytes_per_launch": write_b,

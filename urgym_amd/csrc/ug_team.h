@@ -1572,7 +1572,7 @@ __device__ __forceinline__ static ugk::gx to_gx(const XF& T) {
  * separating axis n (the reported normal, or the classic GJK's last axis) with both cores' extents along it, and the
  * relative pose; while the motion bound in team_collide proves that the margin-expanded shapes stay farther apart than
  * the contact threshold, the query would again add nothing, and the pair is skipped. */
-__device__ __noinline__ static void team_gjk(const Scene* s, int k, ugk::EpaMem* E, gdouble* gc) {
+__device__ __forceinline__ static void gjk_one(const Scene* s, int k, ugk::EpaMem* E, gdouble* gc) {
     Shared& sh = g_sh;
     const int a = sh.pinfo[k].a, b = sh.pinfo[k].b;
     const Collider& A = s->col[a];
@@ -1619,6 +1619,24 @@ __device__ __noinline__ static void team_gjk(const Scene* s, int k, ugk::EpaMem*
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
+}
+
+/* the GJK pairs of a pair chunk (bits of hq), in rounds of GJK_NG: lane group g runs the round's g-th pair on its own
+ * EPA store.  One call per chunk: the callee-saved registers this solver needs are saved once per substep with GJK
+ * pairs, not once per pair (they were 441 dwords per lane per call, most of the k_step's HBM traffic). */
+__device__ __noinline__ static void team_gjk(const Scene* s, unsigned long long hq, int c0, double* ws) {
+    Shared& sh = g_sh;
+    const int nq = __popcll(hq), g = threadIdx.x / GJK_G;
+    for (int r0 = 0; r0 < nq; r0 += GJK_NG) {
+        if (r0 + g < nq) {
+            unsigned long long m = hq;
+            for (int j = 0; j < r0 + g; j++) m &= m - 1ull;
+            const int k = __builtin_ctzll(m);
+            gjk_one(s, k, (ugk::EpaMem*)(ws + WS_EPA) + g, (gdouble*)(ws + WS_GC) + GC_DOUBLES * sh.ov[c0 + k]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    }
 }
 
 template <bool FULL, bool GJK>
@@ -1764,20 +1782,9 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) sh.is[3] = c0; /* the pass's first pair (team_poly_cyl's certificate slot) */
         if (GJK) {
-            /* the GJK pairs in rounds of GJK_NG: group g runs the round's g-th pair on its own EPA store */
             const unsigned long long hq = ballot(hk);
-            const int nq = __popcll(hq), g = lane / GJK_G;
-            for (int r0 = 0; r0 < nq; r0 += GJK_NG) {
-                if (r0 + g < nq) {
-                    unsigned long long m = hq;
-                    for (int j = 0; j < r0 + g; j++) m &= m - 1ull;
-                    const int k = __builtin_ctzll(m);
-                    team_gjk(s, k, (ugk::EpaMem*)(ws + WS_EPA) + g, (gdouble*)(ws + WS_GC) + GC_DOUBLES * sh.ov[c0 + k]);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_wave_barrier();
-            }
-            PROF_CNT(PC_HULL, nq);
+            if (hq) team_gjk(s, hq, c0, ws);
+            PROF_CNT(PC_HULL, __popcll(hq));
         }
         for (unsigned long long hm = GJK ? 0ull : ballot(hk); hm != 0ull; hm &= hm - 1ull) {
             const int k = __builtin_ctzll(hm);
