@@ -1119,13 +1119,17 @@ UGK_FN bool gjk_pair(EpaMem* E, const GShape& A, const gx& TA0, const GShape& B,
         dir = neg(sup);
         for (int it = 0; it < kMaxIter; it++) {
             UGK_COUNT(PC_GJK_CCD, 1);
+            UGK_T0(t_cs);
             sup = support_ab(A, TA, B, TB, dir);
+            UGK_ADD(PF_CCD_SUP, t_cs);
             if (dot(sup, dir) < 0) { status = -1; break; }
             if (s.n == 1) s.p1 = sup;
             else if (s.n == 2) s.p2 = sup;
             else s.p3 = sup;
             s.n++;
+            UGK_T0(t_cd);
             const int res = ccd_do(s, dir);
+            UGK_ADD(PF_CCD_DO, t_cd);
             if (res == 1) { status = 0; break; }
             if (res == -1) { status = -1; break; }
             if (fuzzy0(dot(dir, dir))) status = -1;
@@ -1142,9 +1146,12 @@ UGK_FN bool gjk_pair(EpaMem* E, const GShape& A, const gx& TA0, const GShape& B,
         int curIter = 0;
         for (;;) {
             UGK_COUNT(PC_GJK_IT, 1);
+            UGK_T0(t_ks);
             const gv pW = xfa(TA, support0(A, mtv(TA.R, neg(axis))));
             const gv qW = xfa(TB, support0(B, mtv(TB.R, axis)));
             const gv w = sub(pW, qW);
+            UGK_ADD(PF_CLS_SUP, t_ks);
+            UGK_T0(t_kv);
             delta = dot(axis, w);
             if (delta > 0.0 && delta * delta > squaredDistance * maxd2) { degenerate = 10; checkSimplex = true; break; }
             if (vs_in(vs, w)) { degenerate = 1; checkSimplex = true; break; }
@@ -1152,6 +1159,7 @@ UGK_FN bool gjk_pair(EpaMem* E, const GShape& A, const gx& TA0, const GShape& B,
             if (f0 <= f1) { degenerate = f0 <= 0.0 ? 2 : 11; checkSimplex = true; break; }
             vs_add(vs, w, pW, qW);
             const bool ok = vs_update(vs);
+            UGK_ADD(PF_CLS_VS, t_kv);
             const gv nax = vs.cV;
             if (!ok) { degenerate = 3; checkSimplex = true; break; }
             if (dot(nax, nax) < kRelError2) { axis = nax; degenerate = 6; checkSimplex = true; break; }

@@ -35,7 +35,7 @@ namespace ugd {
 #define TEAM 64
 typedef __attribute__((address_space(1))) const double gcdouble;
 typedef __attribute__((address_space(1))) double gdouble;
-#define UG_NPROF 96 /* phase accumulators of the -DUG_PROF build */
+#define UG_NPROF 100 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* a row's J and M^-1 J^T over the NVP = 32 dof slots (robot 12, objects 3 x 6, 2 zero pads) */
@@ -83,7 +83,9 @@ static_assert(UG_FULL_HULL_MAXV + 64 + 8 <= FC_MAX, "a full hull pair's candidat
 /* the convex-convex path (UG_CONTACT_GJK): the penetration solver's store (ug_gjk.h EpaMem: btGjkEpa2's 132 support
  * vertices, 256 faces and their lists, the horizon walk's stack) after everything else */
 #define WS_EPA WS_DOUBLES
+#ifndef UG_GJK_G /* (-DUG_GJK_G=64: one pair per wave, the profiling build's serial view of the solver) */
 #define UG_GJK_G 16 /* lanes per GJK pair (ugd::GJK_G): the wave runs 64 / UG_GJK_G pairs at once, one store each */
+#endif
 #define EPA_DOUBLES ((sizeof(ugk::EpaMem) + sizeof(double) - 1) / sizeof(double))
 /* the convex-convex path's separation certificates, per pair: [0] valid, [1..3] the separating axis n in B's frame,
  * [4] A's core extent along -n at the evaluation, [5] B's core extent along n, [6..14] R_AB, [15..17] p_AB (A's pose in
@@ -207,7 +209,9 @@ enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_
        PC_EPA_IT, PF_GJK_ALL, PF_GJK_PEN, PF_GJK_CCD, PF_GJK_CLASSIC,
        /* inside the penetration path: btGjkEpa2's GJK, the EPA setup (enclose + tetrahedron), its iterations' support,
         * horizon walk and findbest, the witnesses */
-       PF_EPA_GJK, PF_EPA_SETUP, PF_EPA_SUP, PF_EPA_EXPAND, PF_EPA_BEST };
+       PF_EPA_GJK, PF_EPA_SETUP, PF_EPA_SUP, PF_EPA_EXPAND, PF_EPA_BEST,
+       /* inside the libccd test and the classic GJK: the support pairs, the simplex work */
+       PF_CCD_SUP, PF_CCD_DO, PF_CLS_SUP, PF_CLS_VS };
 #define UG_FREE_SPLIT_N 14
 #ifdef UG_PROF
 __device__ static const int kFreeSplit[UG_FREE_SPLIT_N] = {PF_FK, PF_BROAD, PF_HULL, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST,
@@ -325,14 +329,14 @@ __device__ __forceinline__ void group_best(double& v, int& idx, bool want_max) {
  * value and, on a tie, the lower index.  (Culling a full hull's 64-vertex chunks by their bounding spheres -- the
  * best-bound chunk first, then every chunk whose bound reaches its maximum -- measured 2.2x slower per support on
  * BallBalance: the spheres overlap, most chunks pass, and each pass is a serial load + reduction.) */
-__device__ __forceinline__ void hs_scan(int v0, int lo, int hi, ugk::gv d, int gl, double& best, int& bi) {
+__device__ __forceinline__ void hs_scan(int v0, int nv, ugk::gv d, int gl, double& best, int& bi, ugk::gv& bv) {
     constexpr int G = ugd::GJK_G, U = G == TEAM ? 4 : 8; /* 16 measured the same (r4l) */
     /* U vertices per trip: their loads in flight together (the hull is cache-resident, the latency is the cost) */
-    for (int i0 = lo + gl; i0 < hi; i0 += U * G) {
+    for (int i0 = gl; i0 < nv; i0 += U * G) {
         double x[U], y[U], z[U];
 #pragma unroll
         for (int k = 0; k < U; k++) {
-            const int i = i0 + k * G < hi ? i0 + k * G : i0;
+            const int i = i0 + k * G < nv ? i0 + k * G : i0;
             const double* p = &UG_HULL_V[3 * (v0 + i)];
             x[k] = p[0]; y[k] = p[1]; z[k] = p[2];
         }
@@ -340,7 +344,11 @@ __device__ __forceinline__ void hs_scan(int v0, int lo, int hi, ugk::gv d, int g
         for (int k = 0; k < U; k++) {
             const double dd = x[k] * d.x + y[k] * d.y + z[k] * d.z;
             const int i = i0 + k * G;
-            if (i < hi && (bi == 0x7fffffff || dd > best || (dd == best && i < bi))) { best = dd; bi = i; }
+            if (i < nv && (dd > best || (dd == best && i < bi))) { /* maxDot's test: a NaN never wins */
+                best = dd;
+                bi = i;
+                bv = ugk::V3(x[k], y[k], z[k]);
+            }
         }
     }
 }
@@ -350,17 +358,24 @@ UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
     PROF_T0(t_sup);
     double best = -__builtin_inf();
     int bi = 0x7fffffff;
-    hs_scan(v0, 0, nv, d, gl, best, bi);
+    ugk::gv bv = ugk::V3(0.0, 0.0, 0.0);
+    hs_scan(v0, nv, d, gl, best, bi, bv);
     ugd::group_best(best, bi, true);
-    if (bi == 0x7fffffff) bi = 0;
-    const double* p = &UG_HULL_V[3 * (v0 + bi)];
+    ugk::gv r;
+    if (bi == 0x7fffffff) { /* no comparable dot product (a NaN direction): vertex 0, as maxDot leaves it */
+        const double* p = &UG_HULL_V[3 * v0];
+        r = ugk::V3(p[0], p[1], p[2]);
+    } else { /* the winner's coordinates from the lane that dotted it (vertex i sits in lane i mod G) */
+        const int src = (int)(threadIdx.x & ~(G - 1)) + (bi & (G - 1));
+        r = ugk::V3(__shfl(bv.x, src, TEAM), __shfl(bv.y, src, TEAM), __shfl(bv.z, src, TEAM));
+    }
 #ifdef UG_PROF
     if (gl == 0) {
         atomicAdd(&ugd::g_sh.prof[ugd::PF_GJK_SUP], __builtin_readcyclecounter() - t_sup);
         atomicAdd(&ugd::g_sh.prof[ugd::PC_GJK_SUP], 1ull);
     }
 #endif
-    return ugk::V3(p[0], p[1], p[2]);
+    return r;
 }
 
 /* ug_gjk.h's small stacks on the lane group: slots [0, GJK_G) in one register, lane i of the group holding slot i
