@@ -141,3 +141,57 @@ def test_box_refuses_lod(mods):
     from urgym_amd._native import GEOM_LOD
     with pytest.raises(RuntimeError):
         Sim(TASK, 2, flags=GEOM_LOD)
+
+
+# arm offsets from the reset pose (shoulder pan .. wrist 3) that press the gripper's hulls 0.6-3.7 cm into the door
+# compound (its box and handle cylinders) -- found with the restatement (the hull-cylinder pass's
+# candidate list under a deep press, team_poly_cyl's FC_MAX cap)
+DOOR_PRESS = [[0.0, 0.502, 0.248, -0.339, -0.245, -1.029], [-0.213, 0.156, 0.637, -1.129, 0.122, 0.396],
+              [-0.17, 0.619, 0.338, 0.981, -1.024, -0.772], [-0.549, 0.362, 0.42, 0.227, 0.907, 0.257],
+              [-0.23, 0.718, 0.007, 0.699, -0.419, 0.375], [-0.033, 0.623, 0.059, 0.415, -0.855, 0.259]]
+
+
+@pytest.mark.parametrize("contact", ["gjk", "vih"])
+def test_box_gripper_pressed_into_the_door(mods, contact):
+    """the gripper's full hulls pushed into the door's box and handle cylinders: after one substep the restatement
+    reports contacts deeper than 5 mm, and two env-steps from those states are bit-exact on the GPU (state,
+    observation, reward, substeps, contact tuples) in both contact modes"""
+    Sim, OracleEnv = mods
+    from urgym_amd import layout as LY
+    from urgym_amd._native import CONTACT_VIH
+    fl = CONTACT_VIH if contact == "vih" else 0
+    n = len(DOOR_PRESS)
+    sim = Sim(TASK, n, seed=SEED, flags=fl)
+    sim.set_autoreset(False, 0)
+    sim.reset()
+    st = sim.get_state()
+    ref = [OracleEnv(TASK, SEED + i, flags=fl) for i in range(n)]
+    deepest = []
+    for i, r in enumerate(ref):
+        r.reset()
+        assert np.array_equal(st[i], r.get_state()), i
+        st[i, LY.F_Q:LY.F_Q + 6] += DOOR_PRESS[i]
+        st[i, LY.F_QD:LY.F_QD + 12] = 0.0
+        probe = OracleEnv(TASK, SEED + i, flags=fl)
+        probe.reset()
+        probe.set_state(st[i])
+        probe.substep()
+        cp = probe.contact_points()
+        m = cp[(cp[:, 3] >= 8) & (cp[:, 2] == 1)]
+        deepest.append(m[:, 14].min() if len(m) else 0.0)
+        r.set_state(st[i])
+    assert min(deepest) < -0.02 and sum(d < -0.005 for d in deepest) >= 5, deepest
+    sim.set_state(st)
+    rng = np.random.default_rng(7)
+    for t in range(2):
+        act = _actions(rng, n)
+        out = sim.step(act)
+        got = sim.get_state()
+        cps, cnt = sim.contact_points()
+        for i, r in enumerate(ref):
+            o, rew, term, succ, ns = r.step(act[i])
+            assert np.array_equal(out["obs"][i], o) and out["reward"][i] == rew, (t, i)
+            assert out["substeps"][i] == ns and np.array_equal(got[i], r.get_state()), (t, i)
+            rc = r.contact_points()
+            assert cnt[i] == len(rc) and np.array_equal(cps[i, :cnt[i]], rc), (t, i)
+    sim.close()

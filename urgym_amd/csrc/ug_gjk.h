@@ -145,13 +145,14 @@ UGK_FN void vs_add(Voronoi& s, gv w, gv p, gv q) {
     }
     s.n++;
 }
-/* removeVertex(I): n--, slot I <- slot n (I a compile-time index, n a run-time one) */
+/* removeVertex(I): n--, slot I <- slot n (I a compile-time index, n a run-time one; vs_reduce removes slot I only
+ * while n > I, so the source is a slot j >= I: slot I itself when it was the last) */
 template <int I>
 UGK_FN void vs_remove(Voronoi& s) {
     s.n--;
     gv w = s.W[I], p = s.P[I], q = s.Q[I];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
+    for (int j = I + 1; j < 4; j++) {
         const bool h = j == s.n;
         w = vsel(h, s.W[j], w);
         p = vsel(h, s.P[j], p);
