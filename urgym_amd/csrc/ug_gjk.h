@@ -72,6 +72,14 @@ struct GShape { int kind, v0, nv; gv imp; double margin; };
 
 /* the includer's hull support: the vertex of hull [v0, v0 + nv) with the first maximal dot product with d */
 UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d);
+#ifdef UGK_GROUP_PARALLEL
+/* the includer's lane-group hooks (kernels): this lane's index in its group, and v as lane j of the group holds it.
+ * With them the solver evaluates a few independent sub-results on separate lanes at once (the tetrahedron's faces,
+ * libccd's five triangle distances) and reads them back in the serial order; the host build runs them in turn. */
+UGK_FN int ugk_glane();
+UGK_FN double ugk_gread(double v, int j);
+UGK_FN int ugk_greadi(int v, int j);
+#endif
 
 namespace ugk {
 
@@ -219,6 +227,50 @@ UGK_FN int vs_outside(gv p, gv a, gv b, gv c, gv d) {
 UGK_FN bool vs_tet(gv p, gv a, gv b, gv c, gv d, Sub& fr) {
     fr.closest = p;
     fr.used = UA | UB | UC | UD;
+#ifdef UGK_GROUP_PARALLEL
+    {
+        /* lane j of the group takes face j (ABC, ACD, ADB, BDC with its opposite vertex): its outside test and its
+         * closest point, all four at once; the serial selection then runs on the gathered values */
+        const int j = ugk_glane() & 3;
+        const gv x = j == 3 ? b : a;
+        const gv y = j == 0 ? b : (j == 1 ? c : d);
+        const gv z = j == 0 ? c : (j == 1 ? d : (j == 2 ? b : c));
+        const gv w = j == 0 ? d : (j == 1 ? b : (j == 2 ? c : a));
+        const int oj = vs_outside(p, x, y, z, w);
+        Sub t;
+        vs_tri(p, x, y, z, t);
+        const double sqj = dot(sub(t.closest, p), sub(t.closest, p));
+        const int o0 = ugk_greadi(oj, 0), o1 = ugk_greadi(oj, 1), o2 = ugk_greadi(oj, 2), o3 = ugk_greadi(oj, 3);
+        if (o0 < 0 || o1 < 0 || o2 < 0 || o3 < 0) { fr.degenerate = 1; return false; }
+        if (!o0 && !o1 && !o2 && !o3) return false;
+        const double s0 = ugk_gread(sqj, 0), s1 = ugk_gread(sqj, 1), s2 = ugk_gread(sqj, 2), s3 = ugk_gread(sqj, 3);
+        double best = 3.4028234663852886e+38; /* FLT_MAX */
+        int k = -1;
+        if (o0 && s0 < best) { best = s0; k = 0; }
+        if (o1 && s1 < best) { best = s1; k = 1; }
+        if (o2 && s2 < best) { best = s2; k = 2; }
+        if (o3 && s3 < best) { best = s3; k = 3; }
+        if (k >= 0) {
+            fr.closest = V3(ugk_gread(t.closest.x, k), ugk_gread(t.closest.y, k), ugk_gread(t.closest.z, k));
+            const int u = ugk_greadi(t.used, k);
+            const double b0 = ugk_gread(t.bc[0], k), b1 = ugk_gread(t.bc[1], k), b2 = ugk_gread(t.bc[2], k);
+            if (k == 0) {
+                fr.used = u & (UA | UB | UC);
+                sub_set(fr, b0, b1, b2, 0);
+            } else if (k == 1) {
+                fr.used = ((u & UA) ? UA : 0) | ((u & UB) ? UC : 0) | ((u & UC) ? UD : 0);
+                sub_set(fr, b0, 0, b1, b2);
+            } else if (k == 2) {
+                fr.used = ((u & UA) ? UA : 0) | ((u & UC) ? UB : 0) | ((u & UB) ? UD : 0);
+                sub_set(fr, b0, b2, 0, b1);
+            } else {
+                fr.used = ((u & UA) ? UB : 0) | ((u & UC) ? UC : 0) | ((u & UB) ? UD : 0);
+                sub_set(fr, 0, b0, b2, b1);
+            }
+        }
+        return true;
+    }
+#endif
     const int oABC = vs_outside(p, a, b, c, d);
     const int oACD = vs_outside(p, a, c, d, b);
     const int oADB = vs_outside(p, a, d, b, c);
@@ -1060,12 +1112,23 @@ UGK_FN int ccd_do(Ccd& s, gv& dir) {
     if (s.n == 3) return ccd_do3(s, s.p2, dir);
     /* size 4: A = p3, B = p2, C = p1, D = p0 */
     const gv A = s.p3, B = s.p2, C = s.p1, D = s.p0;
-    if (fuzzy0(tri_dist2(A, B, C, D))) return -1;
     const gv O = V3(0.0, 0.0, 0.0);
+#ifdef UGK_GROUP_PARALLEL
+    {
+        /* the five distances on lanes 0..4 of the group at once (the others repeat lane 2's), tested in order */
+        const int j = ugk_glane();
+        const double rj = tri_dist2(j == 0 ? A : O, (j == 0 || j == 4) ? B : A, (j == 1 || j == 3) ? B : C, j == 1 ? C : D);
+        if (fuzzy0(ugk_gread(rj, 0))) return -1;
+        if (fuzzy0(ugk_gread(rj, 1)) || fuzzy0(ugk_gread(rj, 2)) || fuzzy0(ugk_gread(rj, 3)) || fuzzy0(ugk_gread(rj, 4)))
+            return 1;
+    }
+#else
+    if (fuzzy0(tri_dist2(A, B, C, D))) return -1;
     if (fuzzy0(tri_dist2(O, A, B, C))) return 1;
     if (fuzzy0(tri_dist2(O, A, C, D))) return 1;
     if (fuzzy0(tri_dist2(O, A, B, D))) return 1;
     if (fuzzy0(tri_dist2(O, B, C, D))) return 1;
+#endif
     const gv AO = neg1(A);
     const gv AB = sub(B, A), AC = sub(C, A), AD = sub(D, A);
     const gv ABC = cross(AB, AC), ACD = cross(AC, AD), ADB = cross(AD, AB);

@@ -221,6 +221,7 @@ __device__ static const int kFreeSplit[UG_FREE_SPLIT_N] = {PF_FK, PF_BROAD, PF_H
 } /* namespace ugd */
 /* the convex-convex narrowphase (Bullet's GJK / EPA pair detector), run by the whole wave per pair */
 #define UGK_FN __device__ static inline
+#define UGK_GROUP_PARALLEL 1
 #ifdef UG_PROF /* its event counters (PC_GJK_*) and phase timers, lane 0 of the env's wave */
 /* summed over the lane groups that run pairs at once (LDS atomics): work, not wall time */
 #define UGK_COUNT(k, v) do { if ((threadIdx.x & (UG_GJK_G - 1)) == 0) atomicAdd(&ugd::g_sh.prof[ugd::k], (unsigned long long)(v)); } while (0)
@@ -377,6 +378,11 @@ UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
 #endif
     return r;
 }
+
+/* ug_gjk.h's lane-group hooks: the lane's index in its group, a value as another lane of the group holds it */
+UGK_FN int ugk_glane() { return (int)(threadIdx.x & (ugd::GJK_G - 1)); }
+UGK_FN double ugk_gread(double v, int j) { return __shfl(v, (int)(threadIdx.x & ~(ugd::GJK_G - 1)) + j, TEAM); }
+UGK_FN int ugk_greadi(int v, int j) { return __shfl(v, (int)(threadIdx.x & ~(ugd::GJK_G - 1)) + j, TEAM); }
 
 /* ug_gjk.h's small stacks on the lane group: slots [0, GJK_G) in one register, lane i of the group holding slot i
  * (read back through ds_bpermute, an LDS-crossbar hop instead of a workspace round trip), deeper slots in memory */
