@@ -26,22 +26,25 @@ UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
     return ugk::V3(p[0], p[1], p[2]);
 }
 
+UGK_FN ugk::EFace* ugk_face(ugk::EpaMem* E, int f) { return &E->fc[f]; }
+UGK_FN ugk::EHull* ugk_hull(ugk::EpaMem* E, int i) { return &E->hl[i]; }
 UGK_FN void ugk_ls_put(int* mem, ugk::LStack&, int i, int v) { mem[i] = v; }
 UGK_FN int ugk_ls_get(const int* mem, const ugk::LStack&, int i) { return mem[i]; }
 /* m_hull's first minimum of d * d over the hull array: the largest stamp among the minima; a NaN at the root (the
  * largest stamp) wins */
 UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E, int hcount) {
+    const ugk::EHull* h = E->hl; /* the host keeps every hull slot in E */
     int root = 0;
     for (int i = 1; i < hcount; i++)
-        if (E->hl[i].stamp > E->hl[root].stamp) root = i;
-    double mind = E->hl[root].d * E->hl[root].d;
-    if (mind != mind) return E->hl[root].f;
+        if (h[i].stamp > h[root].stamp) root = i;
+    double mind = h[root].d * h[root].d;
+    if (mind != mind) return h[root].f;
     int best = root;
     for (int i = 0; i < hcount; i++) {
-        const double sqd = E->hl[i].d * E->hl[i].d;
-        if (sqd < mind || (sqd == mind && E->hl[i].stamp > E->hl[best].stamp)) { best = i; mind = sqd; }
+        const double sqd = h[i].d * h[i].d;
+        if (sqd < mind || (sqd == mind && h[i].stamp > h[best].stamp)) { best = i; mind = sqd; }
     }
-    return E->hl[best].f;
+    return h[best].f;
 }
 
 static ugk::EpaMem g_epa;

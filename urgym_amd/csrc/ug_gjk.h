@@ -404,7 +404,16 @@ struct ESv { gv d, w; };
  * ones), the hull an unordered array of (d, append stamp, face) with swap-removal (m_hull's list order is most
  * recently appended first, so its first minimum is the largest stamp among the minima -- what ugk_epa_findbest
  * returns from the array) */
-struct EFace { gv n; double d; int c[3], f[3], e[3], pass; };
+struct EFace {
+    gv n;
+    double d;
+    unsigned char c[3], f[3]; /* vertex ids (< 132), neighbour faces (< 256) */
+    unsigned char e3;         /* the neighbours' edge indices, 2 bits each */
+    unsigned char pass;       /* expand()'s visit mark (<= 255 iterations) */
+};
+static_assert(sizeof(EFace) == 40, "the compact face record");
+UGK_FN int fe(const EFace& F, int j) { return (F.e3 >> (2 * j)) & 3; }
+UGK_FN void set_fe(EFace& F, int j, int v) { F.e3 = (unsigned char)((F.e3 & ~(3 << (2 * j))) | (v << (2 * j))); }
 struct EHull { double d; int stamp, f; };
 struct EpaMem {
     ESv sv[4 + kEpaMaxVertices]; /* [0, 4) the GJK's store, then the EPA's */
@@ -418,6 +427,12 @@ struct EpaMem {
     int stk[kEpaMaxFaces];       /* expand()'s parent frames, packed (e_frame) */
     int stock[kEpaMaxFaces];     /* the faces pushed back to the stock, top = the list root */
 };
+} /* namespace ugk */
+/* the includer's EPA record hooks: face f's record and hull slot i (the kernels keep the first few of each in LDS,
+ * the rest in E) */
+UGK_FN ugk::EFace* ugk_face(ugk::EpaMem* E, int f);
+UGK_FN ugk::EHull* ugk_hull(ugk::EpaMem* E, int i);
+namespace ugk {
 struct Mink { GShape s0, s1; gm toshape1; gx toshape0; bool margins; };
 UGK_FN gv mk_ls(const Mink& M, int i, gv d) {
     const GShape& s = i ? M.s1 : M.s0;
@@ -697,20 +712,22 @@ UGK_FN int ugk_ls_get(const int* mem, const ugk::LStack& s, int i);
 namespace ugk {
 
 UGK_FN void e_bind(EpaMem* E, int fa, int ea, int fb, int eb) {
-    E->fc[fa].e[ea] = eb; E->fc[fa].f[ea] = fb;
-    E->fc[fb].e[eb] = ea; E->fc[fb].f[eb] = fa;
+    EFace* A = ugk_face(E, fa);
+    EFace* B = ugk_face(E, fb);
+    set_fe(*A, ea, eb); A->f[ea] = (unsigned char)fb;
+    set_fe(*B, eb, ea); B->f[eb] = (unsigned char)fa;
 }
 UGK_FN void h_append(EpaMem* E, Epa& P, int f, double d, int stamp) {
     EHull h;
     h.d = d; h.stamp = stamp; h.f = f;
-    E->hl[P.hcount] = h;
+    *ugk_hull(E, P.hcount) = h;
     E->hpos[f] = P.hcount++;
 }
 UGK_FN void h_remove(EpaMem* E, Epa& P, int f) {
     const int i = E->hpos[f], last = --P.hcount;
     if (i != last) {
-        const EHull t = E->hl[last];
-        E->hl[i] = t;
+        const EHull t = *ugk_hull(E, last);
+        *ugk_hull(E, i) = t;
         E->hpos[t.f] = i;
     }
 }
@@ -740,9 +757,9 @@ UGK_FN int e_newface(EpaMem* E, Epa& P, int a, int b, int c, bool forced) {
         else P.nfresh++;
         const int stamp = ++P.stampctr; /* m_hull.append: the face joins the hull before its plane is known */
         const gv aw = E->sv[a].w, bw = E->sv[b].w, cw = E->sv[c].w;
-        EFace& F = E->fc[f];
+        EFace& F = *ugk_face(E, f);
         F.pass = 0;
-        F.c[0] = a; F.c[1] = b; F.c[2] = c;
+        F.c[0] = (unsigned char)a; F.c[1] = (unsigned char)b; F.c[2] = (unsigned char)c;
         const gv n = cross(sub(bw, aw), sub(cw, aw));
         const double l = len(n);
         if (l > kEpaAccuracy) {
@@ -779,7 +796,7 @@ UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, gv ww, int f0, int e0, 
     for (;;) {
         bool pop = true;
         if (stage == 0) {
-            const EFace F = E->fc[f]; /* the face's record in one batch of loads */
+            const EFace F = *ugk_face(E, f); /* the face's record in one batch of loads */
             const int e1 = e == 2 ? 0 : e + 1, em = e == 0 ? 2 : e - 1;
             if (F.pass == pass) {
                 r = false;
@@ -795,10 +812,10 @@ UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, gv ww, int f0, int e0, 
                     r = true;
                 }
             } else {
-                E->fc[f].pass = pass;
-                ugk_ls_put(E->stk, fs, sp++, f | (e << 8) | (1 << 10) | (F.f[em] << 12) | (F.e[em] << 20));
+                ugk_face(E, f)->pass = (unsigned char)pass;
+                ugk_ls_put(E->stk, fs, sp++, f | (e << 8) | (1 << 10) | (F.f[em] << 12) | (fe(F, em) << 20));
                 f = F.f[e1];
-                e = F.e[e1];
+                e = fe(F, e1);
                 pop = false;
             }
         } else if (stage == 1) {
@@ -849,7 +866,7 @@ UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
         if (P.hcount == 4) {
             int best = ugk_epa_findbest(E, P.hcount);
             UGK_ADD(PF_EPA_SETUP, t_setup);
-            EFace outer = E->fc[best];
+            EFace outer = *ugk_face(E, best);
             int pass = 0;
             e_bind(E, tetra[0], 0, tetra[1], 0);
             e_bind(E, tetra[0], 1, tetra[2], 0);
@@ -864,17 +881,17 @@ UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
                 int hcf = -1, hff = -1, hnf = 0;
                 const int w = 4 + P.nextsv++;
                 bool valid = true;
-                E->fc[best].pass = ++pass;
+                ugk_face(E, best)->pass = (unsigned char)(++pass);
                 UGK_T0(t_sup);
-                g2_getsupport(E, M, E->fc[best].n, w);
+                g2_getsupport(E, M, ugk_face(E, best)->n, w);
                 UGK_ADD(PF_EPA_SUP, t_sup);
                 const gv ww = E->sv[w].w;
-                const EFace B = E->fc[best];
+                const EFace B = *ugk_face(E, best);
                 const double wdist = dot(B.n, ww) - B.d;
                 if (!(wdist > kEpaAccuracy)) { P.status = EPA_ACCURACYREACHED; break; }
                 UGK_T0(t_exp);
                 for (int j = 0; j < 3 && valid; j++)
-                    valid = e_expand(E, P, pass, w, ww, B.f[j], B.e[j], hcf, hff, hnf) && valid;
+                    valid = e_expand(E, P, pass, w, ww, B.f[j], fe(B, j), hcf, hff, hnf) && valid;
                 UGK_ADD(PF_EPA_EXPAND, t_exp);
                 if (!(valid && hnf >= 3)) { P.status = EPA_INVALIDHULL; break; }
                 e_bind(E, hcf, 1, hff, 2);
@@ -883,7 +900,7 @@ UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
                 UGK_T0(t_best);
                 best = ugk_epa_findbest(E, P.hcount);
                 UGK_ADD(PF_EPA_BEST, t_best);
-                outer = E->fc[best];
+                outer = *ugk_face(E, best);
             }
             const gv projection = scl(outer.n, outer.d);
             P.normal = outer.n;

@@ -379,6 +379,28 @@ UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
     return r;
 }
 
+/* ug_gjk.h's EPA record hooks: each lane group keeps its first UG_EPA_LDS_FACES face records and UG_EPA_LDS_HULL hull
+ * slots in LDS the GJK stage does not use -- the hull-candidate / box-clip union (written only after team_gjk) and the
+ * tail of the rows union past the pair records (the working manifolds overwrite it only after team_gjk) -- and the
+ * rest in its workspace store; the records are reached through generic (flat) pointers either way */
+#define UG_EPA_LDS_FACES 22
+#define UG_EPA_LDS_HULL 42
+#define UG_EPA_HULL_OFF (((sizeof(ugd::PairInfo) * MAXOV) + 15) & ~(size_t)15)
+static_assert(ugd::GJK_NG * UG_EPA_LDS_FACES * sizeof(ugk::EFace) <= sizeof(ugd::Cand) * 64, "EPA face tier in hc");
+static_assert(UG_EPA_HULL_OFF + ugd::GJK_NG * UG_EPA_LDS_HULL * sizeof(ugk::EHull) <= sizeof(ugd::RowS) * MAXROWS,
+              "EPA hull tier in the rows union");
+UGK_FN ugk::EFace* ugk_face(ugk::EpaMem* E, int f) {
+    if (f < UG_EPA_LDS_FACES)
+        return (ugk::EFace*)(void*)&ugd::g_sh.hc[0] + (int)(threadIdx.x / ugd::GJK_G) * UG_EPA_LDS_FACES + f;
+    return &E->fc[f];
+}
+UGK_FN ugk::EHull* ugk_hull(ugk::EpaMem* E, int i) {
+    if (i < UG_EPA_LDS_HULL)
+        return (ugk::EHull*)(void*)((char*)(void*)&ugd::g_sh.rs[0] + UG_EPA_HULL_OFF) +
+               (int)(threadIdx.x / ugd::GJK_G) * UG_EPA_LDS_HULL + i;
+    return &E->hl[i];
+}
+
 /* ug_gjk.h's lane-group hooks: the lane's index in its group, a value as another lane of the group holds it */
 UGK_FN int ugk_glane() { return (int)(threadIdx.x & (ugd::GJK_G - 1)); }
 UGK_FN double ugk_gread(double v, int j) { return __shfl(v, (int)(threadIdx.x & ~(ugd::GJK_G - 1)) + j, TEAM); }
@@ -407,7 +429,7 @@ UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E, int hcount) {
     int bi = 0x7fffffff, ri = 0x7fffffff;
     bool nan = false;
     for (int i = gl; i < hcount; i += G) {
-        const ugk::EHull h = E->hl[i];
+        const ugk::EHull h = *ugk_hull(const_cast<ugk::EpaMem*>(E), i);
         const double sqd = h.d * h.d;
         if (ri == 0x7fffffff || (double)h.stamp > rs) { rs = (double)h.stamp; ri = i; }
         if (sqd != sqd) { nan = true; continue; }
@@ -416,7 +438,7 @@ UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E, int hcount) {
     }
     if ((ugd::ballot(nan) >> (threadIdx.x & ~(G - 1))) & ((1ull << G) - 1ull)) {
         ugd::group_best(rs, ri, true); /* the root: the largest stamp */
-        const ugk::EHull h = E->hl[ri];
+        const ugk::EHull h = *ugk_hull(const_cast<ugk::EpaMem*>(E), ri);
         if ((h.d * h.d) != (h.d * h.d)) return h.f;
     }
     ugd::group_best(bv, bi, false);
