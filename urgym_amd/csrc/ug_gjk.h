@@ -423,7 +423,7 @@ struct EpaMem {
     int srank[2];
     int freev[4];
     EHull hl[kEpaMaxFaces];      /* the hull faces [0, hcount), unordered */
-    int hpos[kEpaMaxFaces];      /* a hull face's slot in hl */
+    unsigned char hpos[kEpaMaxFaces]; /* a hull face's slot in hl (< 256) */
     int stk[kEpaMaxFaces];       /* expand()'s parent frames, packed (e_frame) */
     int stock[kEpaMaxFaces];     /* the faces pushed back to the stock, top = the list root */
 };
@@ -432,6 +432,7 @@ struct EpaMem {
  * the rest in E) */
 UGK_FN ugk::EFace* ugk_face(ugk::EpaMem* E, int f);
 UGK_FN ugk::EHull* ugk_hull(ugk::EpaMem* E, int i);
+UGK_FN unsigned char* ugk_hpos(ugk::EpaMem* E); /* the hull-slot table, kEpaMaxFaces entries */
 namespace ugk {
 struct Mink { GShape s0, s1; gm toshape1; gx toshape0; bool margins; };
 UGK_FN gv mk_ls(const Mink& M, int i, gv d) {
@@ -721,14 +722,15 @@ UGK_FN void h_append(EpaMem* E, Epa& P, int f, double d, int stamp) {
     EHull h;
     h.d = d; h.stamp = stamp; h.f = f;
     *ugk_hull(E, P.hcount) = h;
-    E->hpos[f] = P.hcount++;
+    ugk_hpos(E)[f] = (unsigned char)P.hcount++;
 }
 UGK_FN void h_remove(EpaMem* E, Epa& P, int f) {
-    const int i = E->hpos[f], last = --P.hcount;
+    unsigned char* hp = ugk_hpos(E);
+    const int i = hp[f], last = --P.hcount;
     if (i != last) {
         const EHull t = *ugk_hull(E, last);
         *ugk_hull(E, i) = t;
-        E->hpos[t.f] = i;
+        hp[t.f] = (unsigned char)i;
     }
 }
 UGK_FN void s_push(EpaMem* E, Epa& P, int f) { ugk_ls_put(E->stock, P.stock, P.nstock++, f); }

@@ -394,6 +394,11 @@ UGK_FN ugk::EFace* ugk_face(ugk::EpaMem* E, int f) {
         return (ugk::EFace*)(void*)&ugd::g_sh.hc[0] + (int)(threadIdx.x / ugd::GJK_G) * UG_EPA_LDS_FACES + f;
     return &E->fc[f];
 }
+/* the hull-slot table (one byte per face) in the mass matrix's LDS, dead from FK to serial_pre (which rebuilds it) */
+static_assert(ugd::GJK_NG * ugk::kEpaMaxFaces <= sizeof(double) * NB * NB, "EPA hull-slot tables in LDL");
+UGK_FN unsigned char* ugk_hpos(ugk::EpaMem*) {
+    return (unsigned char*)(void*)&ugd::g_sh.LDL[0] + (int)(threadIdx.x / ugd::GJK_G) * ugk::kEpaMaxFaces;
+}
 UGK_FN ugk::EHull* ugk_hull(ugk::EpaMem* E, int i) {
     if (i < UG_EPA_LDS_HULL)
         return (ugk::EHull*)(void*)((char*)(void*)&ugd::g_sh.rs[0] + UG_EPA_HULL_OFF) +
