@@ -29,6 +29,7 @@ UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
 UGK_FN ugk::EFace* ugk_face(ugk::EpaMem* E, int f) { return &E->fc[f]; }
 UGK_FN ugk::EHull* ugk_hull(ugk::EpaMem* E, int i) { return &E->hl[i]; }
 UGK_FN unsigned char* ugk_hpos(ugk::EpaMem* E) { return E->hpos; }
+UGK_FN ugk::ESv* ugk_sv(ugk::EpaMem* E, int i) { return &E->sv[i]; }
 UGK_FN void ugk_ls_put(int* mem, ugk::LStack&, int i, int v) { mem[i] = v; }
 UGK_FN int ugk_ls_get(const int* mem, const ugk::LStack&, int i) { return mem[i]; }
 /* m_hull's first minimum of d * d over the hull array: the largest stamp among the minima; a NaN at the root (the

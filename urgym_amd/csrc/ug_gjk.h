@@ -433,6 +433,7 @@ struct EpaMem {
 UGK_FN ugk::EFace* ugk_face(ugk::EpaMem* E, int f);
 UGK_FN ugk::EHull* ugk_hull(ugk::EpaMem* E, int i);
 UGK_FN unsigned char* ugk_hpos(ugk::EpaMem* E); /* the hull-slot table, kEpaMaxFaces entries */
+UGK_FN ugk::ESv* ugk_sv(ugk::EpaMem* E, int i); /* support vertex i (the GJK's store 0..3, then the EPA's) */
 namespace ugk {
 struct Mink { GShape s0, s1; gm toshape1; gx toshape0; bool margins; };
 UGK_FN gv mk_ls(const Mink& M, int i, gv d) {
@@ -462,8 +463,8 @@ enum { EPA_VALID = 0, EPA_TOUCHING, EPA_DEGENERATED, EPA_NONCONVEX, EPA_INVALIDH
 
 UGK_FN void g2_getsupport(EpaMem* E, const Mink& M, gv d, int sv) {
     const gv dd = mulinv(d, len(d));
-    E->sv[sv].d = dd;
-    E->sv[sv].w = mk_support(M, dd);
+    ugk_sv(E, sv)->d = dd;
+    ugk_sv(E, sv)->w = mk_support(M, dd);
 }
 UGK_FN void g2_remove(EpaMem* E, Gjk2& g, int s) { E->freev[g.nfree++] = E->sc[s][--E->srank[s]]; }
 UGK_FN void g2_append(EpaMem* E, Gjk2& g, const Mink& M, int s, gv v) {
@@ -581,7 +582,7 @@ UGK_FN int g2_evaluate(EpaMem* E, Gjk2& g, const Mink& M, gv guess) {
     const double sqrl = dot(g.ray, g.ray);
     g2_append(E, g, M, 0, sqrl > 0 ? neg(g.ray) : V3(1, 0, 0));
     E->sp[0][0] = 1;
-    g.ray = E->sv[E->sc[0][0]].w;
+    g.ray = ugk_sv(E, E->sc[0][0])->w;
     sqdist = sqrl;
     lastw[0] = lastw[1] = lastw[2] = lastw[3] = g.ray;
     do {
@@ -589,7 +590,7 @@ UGK_FN int g2_evaluate(EpaMem* E, Gjk2& g, const Mink& M, gv guess) {
         const double rl = len(g.ray);
         if (rl < kGjkMinDist) { g.status = GJK_INSIDE; break; }
         g2_append(E, g, M, cs, neg(g.ray));
-        const gv w = E->sv[E->sc[cs][E->srank[cs] - 1]].w;
+        const gv w = ugk_sv(E, E->sc[cs][E->srank[cs] - 1])->w;
         bool found = false;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -606,10 +607,10 @@ UGK_FN int g2_evaluate(EpaMem* E, Gjk2& g, const Mink& M, gv guess) {
         double weights[4];
         int mask = 0;
         const int rank = E->srank[cs];
-        const gv w0 = E->sv[E->sc[cs][0]].w, w1 = E->sv[E->sc[cs][1]].w;
+        const gv w0 = ugk_sv(E, E->sc[cs][0])->w, w1 = ugk_sv(E, E->sc[cs][1])->w;
         if (rank == 2) sqdist = g2_proj2(w0, w1, weights, mask);
-        else if (rank == 3) sqdist = g2_proj3(w0, w1, E->sv[E->sc[cs][2]].w, weights, mask);
-        else if (rank == 4) sqdist = g2_proj4(w0, w1, E->sv[E->sc[cs][2]].w, E->sv[E->sc[cs][3]].w, weights, mask);
+        else if (rank == 3) sqdist = g2_proj3(w0, w1, ugk_sv(E, E->sc[cs][2])->w, weights, mask);
+        else if (rank == 4) sqdist = g2_proj4(w0, w1, ugk_sv(E, E->sc[cs][2])->w, ugk_sv(E, E->sc[cs][3])->w, weights, mask);
         if (sqdist >= 0) {
             E->srank[ns] = 0;
             g.ray = V3(0, 0, 0);
@@ -621,7 +622,7 @@ UGK_FN int g2_evaluate(EpaMem* E, Gjk2& g, const Mink& M, gv guess) {
                     const int r = E->srank[ns]++;
                     E->sc[ns][r] = E->sc[cs][i];
                     E->sp[ns][r] = weights[i];
-                    g.ray = add(g.ray, scl(E->sv[E->sc[cs][i]].w, weights[i]));
+                    g.ray = add(g.ray, scl(ugk_sv(E, E->sc[cs][i])->w, weights[i]));
                 } else {
                     E->freev[g.nfree++] = E->sc[cs][i];
                 }
@@ -642,13 +643,13 @@ UGK_FN int g2_evaluate(EpaMem* E, Gjk2& g, const Mink& M, gv guess) {
 UGK_FN gv g2_axis(int i) { return V3(i == 0 ? 1.0 : 0.0, i == 1 ? 1.0 : 0.0, i == 2 ? 1.0 : 0.0); }
 UGK_FN bool g2_enc4(EpaMem* E, const Gjk2& g) {
     const int s = g.simplex;
-    const gv w3 = E->sv[E->sc[s][3]].w;
-    return ug_fabs(g2_det(sub(E->sv[E->sc[s][0]].w, w3), sub(E->sv[E->sc[s][1]].w, w3), sub(E->sv[E->sc[s][2]].w, w3))) > 0;
+    const gv w3 = ugk_sv(E, E->sc[s][3])->w;
+    return ug_fabs(g2_det(sub(ugk_sv(E, E->sc[s][0])->w, w3), sub(ugk_sv(E, E->sc[s][1])->w, w3), sub(ugk_sv(E, E->sc[s][2])->w, w3))) > 0;
 }
 UGK_FN bool g2_enc3(EpaMem* E, Gjk2& g, const Mink& M) {
     const int s = g.simplex;
-    const gv w0 = E->sv[E->sc[s][0]].w;
-    const gv n = cross(sub(E->sv[E->sc[s][1]].w, w0), sub(E->sv[E->sc[s][2]].w, w0));
+    const gv w0 = ugk_sv(E, E->sc[s][0])->w;
+    const gv n = cross(sub(ugk_sv(E, E->sc[s][1])->w, w0), sub(ugk_sv(E, E->sc[s][2])->w, w0));
     if (dot(n, n) > 0) {
         g2_append(E, g, M, s, n);
         if (g2_enc4(E, g)) return true;
@@ -661,7 +662,7 @@ UGK_FN bool g2_enc3(EpaMem* E, Gjk2& g, const Mink& M) {
 }
 UGK_FN bool g2_enc2(EpaMem* E, Gjk2& g, const Mink& M) {
     const int s = g.simplex;
-    const gv d = sub(E->sv[E->sc[s][1]].w, E->sv[E->sc[s][0]].w);
+    const gv d = sub(ugk_sv(E, E->sc[s][1])->w, ugk_sv(E, E->sc[s][0])->w);
     for (int i = 0; i < 3; i++) {
         const gv p = cross(d, g2_axis(i));
         if (dot(p, p) > 0) {
@@ -758,7 +759,7 @@ UGK_FN int e_newface(EpaMem* E, Epa& P, int a, int b, int c, bool forced) {
         if (P.nstock > 0) P.nstock--;
         else P.nfresh++;
         const int stamp = ++P.stampctr; /* m_hull.append: the face joins the hull before its plane is known */
-        const gv aw = E->sv[a].w, bw = E->sv[b].w, cw = E->sv[c].w;
+        const gv aw = ugk_sv(E, a)->w, bw = ugk_sv(E, b)->w, cw = ugk_sv(E, c)->w;
         EFace& F = *ugk_face(E, f);
         F.pass = 0;
         F.c[0] = (unsigned char)a; F.c[1] = (unsigned char)b; F.c[2] = (unsigned char)c;
@@ -854,8 +855,8 @@ UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
         P.nextsv = 0;
         int* c = E->sc[s];
         {
-            const gv w3 = E->sv[c[3]].w;
-            if (g2_det(sub(E->sv[c[0]].w, w3), sub(E->sv[c[1]].w, w3), sub(E->sv[c[2]].w, w3)) < 0) {
+            const gv w3 = ugk_sv(E, c[3])->w;
+            if (g2_det(sub(ugk_sv(E, c[0])->w, w3), sub(ugk_sv(E, c[1])->w, w3), sub(ugk_sv(E, c[2])->w, w3)) < 0) {
                 const int t = c[0]; c[0] = c[1]; c[1] = t;
                 const double tp = E->sp[s][0]; E->sp[s][0] = E->sp[s][1]; E->sp[s][1] = tp;
             }
@@ -887,7 +888,7 @@ UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
                 UGK_T0(t_sup);
                 g2_getsupport(E, M, ugk_face(E, best)->n, w);
                 UGK_ADD(PF_EPA_SUP, t_sup);
-                const gv ww = E->sv[w].w;
+                const gv ww = ugk_sv(E, w)->w;
                 const EFace B = *ugk_face(E, best);
                 const double wdist = dot(B.n, ww) - B.d;
                 if (!(wdist > kEpaAccuracy)) { P.status = EPA_ACCURACYREACHED; break; }
@@ -909,8 +910,8 @@ UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
             P.depth = outer.d;
             P.rrank = 3;
             P.rc[0] = outer.c[0]; P.rc[1] = outer.c[1]; P.rc[2] = outer.c[2];
-            const gv a = sub(E->sv[outer.c[0]].w, projection), b = sub(E->sv[outer.c[1]].w, projection),
-                     cc = sub(E->sv[outer.c[2]].w, projection);
+            const gv a = sub(ugk_sv(E, outer.c[0])->w, projection), b = sub(ugk_sv(E, outer.c[1])->w, projection),
+                     cc = sub(ugk_sv(E, outer.c[2])->w, projection);
             P.rp[0] = len(cross(b, cc));
             P.rp[1] = len(cross(cc, a));
             P.rp[2] = len(cross(a, b));
@@ -955,7 +956,7 @@ UGK_FN bool g2_penetration(EpaMem* E, const GShape& s0, const gx& w0, const GSha
         e_init(E, P);
         if (e_evaluate(E, P, g, M, neg(guess)) != EPA_FAILED) {
             gv a = V3(0, 0, 0);
-            for (int i = 0; i < P.rrank; i++) a = add(a, scl(mk_support0(M, E->sv[P.rc[i]].d), P.rp[i]));
+            for (int i = 0; i < P.rrank; i++) a = add(a, scl(mk_support0(M, ugk_sv(E, P.rc[i])->d), P.rp[i]));
             r.w0 = xfa(w0, a);
             r.w1 = xfa(w0, sub(a, scl(P.normal, P.depth)));
             r.normal = neg(P.normal);
@@ -974,7 +975,7 @@ UGK_FN bool g2_distance(EpaMem* E, const GShape& s0, const gx& w0, const GShape&
         const int s = g.simplex;
         for (int i = 0; i < E->srank[s]; i++) {
             const double p = E->sp[s][i];
-            const gv d = E->sv[E->sc[s][i]].d;
+            const gv d = ugk_sv(E, E->sc[s][i])->d;
             a = add(a, scl(mk_support0(M, d), p));
             b = add(b, scl(mk_support1(M, neg(d)), p));
         }

@@ -394,6 +394,14 @@ UGK_FN ugk::EFace* ugk_face(ugk::EpaMem* E, int f) {
         return (ugk::EFace*)(void*)&ugd::g_sh.hc[0] + (int)(threadIdx.x / ugd::GJK_G) * UG_EPA_LDS_FACES + f;
     return &E->fc[f];
 }
+/* the btGjkEpa2 GJK's four-vertex store (support vertices 0..3, every GJK iteration's reads and writes) in the
+ * velocity / impulse vectors' LDS (v0 | dvout | dvsout: written by serial_pre and after the PGS, dead during collision) */
+static_assert(ugd::GJK_NG * 4 * sizeof(ugk::ESv) <= 3 * sizeof(double) * NVP, "the GJK stores in v0 | dvout | dvsout");
+static_assert(offsetof(ugd::Shared, dvsout) == offsetof(ugd::Shared, v0) + 2 * sizeof(double) * NVP, "v0, dvout, dvsout adjacent");
+UGK_FN ugk::ESv* ugk_sv(ugk::EpaMem* E, int i) {
+    if (i < 4) return (ugk::ESv*)(void*)&ugd::g_sh.v0[0] + (int)(threadIdx.x / ugd::GJK_G) * 4 + i;
+    return &E->sv[i];
+}
 /* the hull-slot table (one byte per face) in the mass matrix's LDS, dead from FK to serial_pre (which rebuilds it) */
 static_assert(ugd::GJK_NG * ugk::kEpaMaxFaces <= sizeof(double) * NB * NB, "EPA hull-slot tables in LDL");
 UGK_FN unsigned char* ugk_hpos(ugk::EpaMem*) {
