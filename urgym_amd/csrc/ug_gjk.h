@@ -79,6 +79,8 @@ UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d);
 UGK_FN int ugk_glane();
 UGK_FN double ugk_gread(double v, int j);
 UGK_FN int ugk_greadi(int v, int j);
+UGK_FN bool ugk_gany(bool p); /* p on any lane of the group */
+UGK_FN int ugk_gsize();       /* lanes per group */
 #endif
 
 namespace ugk {
@@ -426,6 +428,8 @@ struct EpaMem {
     unsigned char hpos[kEpaMaxFaces]; /* a hull face's slot in hl (< 256) */
     int stk[kEpaMaxFaces];       /* expand()'s parent frames, packed (e_frame) */
     int stock[kEpaMaxFaces];     /* the faces pushed back to the stock, top = the list root */
+    int evm[2 * kEpaMaxFaces];   /* e_expand_group's event log and marked faces beyond their register slots */
+    int mkm[kEpaMaxFaces];
 };
 } /* namespace ugk */
 /* the includer's EPA record hooks: face f's record and hull slot i (the kernels keep the first few of each in LDS,
@@ -753,6 +757,21 @@ UGK_FN bool e_edgedist(gv aw, gv bw, gv fn, double& dist) {
     }
     return false;
 }
+/* a new face's plane from its vertices: false when degenerate (|n| <= EPA_ACCURACY: nOut = the raw normal) */
+UGK_FN bool e_plane(gv aw, gv bw, gv cw, gv& nOut, double& dOut) {
+    const gv n = cross(sub(bw, aw), sub(cw, aw));
+    const double l = len(n);
+    if (l > kEpaAccuracy) {
+        double d;
+        if (!(e_edgedist(aw, bw, n, d) || e_edgedist(bw, cw, n, d) || e_edgedist(cw, aw, n, d)))
+            d = dot(aw, n) / l;
+        dOut = d;
+        nOut = mulinv(n, l);
+        return true;
+    }
+    nOut = n;
+    return false;
+}
 UGK_FN int e_newface(EpaMem* E, Epa& P, int a, int b, int c, bool forced) {
     if (P.nstock > 0 || P.nfresh < kEpaMaxFaces) {
         const int f = P.nstock > 0 ? ugk_ls_get(E->stock, P.stock, P.nstock - 1) : P.nfresh;
@@ -763,21 +782,18 @@ UGK_FN int e_newface(EpaMem* E, Epa& P, int a, int b, int c, bool forced) {
         EFace& F = *ugk_face(E, f);
         F.pass = 0;
         F.c[0] = (unsigned char)a; F.c[1] = (unsigned char)b; F.c[2] = (unsigned char)c;
-        const gv n = cross(sub(bw, aw), sub(cw, aw));
-        const double l = len(n);
-        if (l > kEpaAccuracy) {
-            double d;
-            if (!(e_edgedist(aw, bw, n, d) || e_edgedist(bw, cw, n, d) || e_edgedist(cw, aw, n, d)))
-                d = dot(aw, n) / l;
+        gv n;
+        double d = 0.0;
+        const bool nondeg = e_plane(aw, bw, cw, n, d);
+        F.n = n;
+        if (nondeg) {
             F.d = d;
-            F.n = mulinv(n, l);
             if (forced || d >= -kEpaPlaneEps) {
                 h_append(E, P, f, d, stamp);
                 return f;
             }
             P.status = EPA_NONCONVEX;
         } else {
-            F.n = n;
             P.status = EPA_DEGENERATED;
         }
         s_push(E, P, f); /* m_hull.remove + m_stock.append: back on top of the stock */
@@ -845,6 +861,119 @@ UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, gv ww, int f0, int e0, 
     }
     return r;
 }
+#ifdef UGK_GROUP_PARALLEL
+/* One EPA iteration's three expand() calls with the new faces' planes computed on separate lanes of the group.
+ * The walk runs first and logs, in its order, the faces it would create (horizon edge: its vertices and the
+ * neighbour it binds to) and the visible faces it would return to the stock, assuming every new face succeeds: the
+ * walk's decisions never read what those calls change (a new face only rebinds the horizon face's edge, which the
+ * walk never descends through; a removed face is never reached again).  Then lane k computes event k's plane; when
+ * none is degenerate or non-convex (and the faces suffice) the log is replayed in order -- stock pops and pushes,
+ * stamps, records, hull appends / removals, bindings -- which is exactly what the serial walk does.  Otherwise the
+ * walk's marks are cleared and the serial expand() runs. */
+UGK_FN bool e_walk(EpaMem* E, int pass, gv ww, int f0, int e0, LStack& ev, int& nev, int& nnew, LStack& mk, int& nmk) {
+    int sp = 0, f = f0, e = e0, stage = 0, f2 = 0, e2 = 0;
+    bool r = false;
+    LStack fs;
+    fs.reg = 0;
+    for (;;) {
+        bool pop = true;
+        if (stage == 0) {
+            const EFace F = *ugk_face(E, f);
+            const int e1 = e == 2 ? 0 : e + 1, em = e == 0 ? 2 : e - 1;
+            if (F.pass == pass) {
+                r = false;
+            } else if ((dot(F.n, ww) - F.d) < -kEpaPlaneEps) {
+                ugk_ls_put(E->evm, ev, nev++, f | (e << 8) | (F.c[e1] << 10) | (F.c[e] << 18));
+                nnew++;
+                r = true;
+            } else {
+                ugk_face(E, f)->pass = (unsigned char)pass;
+                ugk_ls_put(E->mkm, mk, nmk++, f);
+                ugk_ls_put(E->stk, fs, sp++, f | (e << 8) | (1 << 10) | (F.f[em] << 12) | (fe(F, em) << 20));
+                f = F.f[e1];
+                e = fe(F, e1);
+                pop = false;
+            }
+        } else if (stage == 1) {
+            if (r) {
+                ugk_ls_put(E->stk, fs, sp++, f | (e << 8) | (2 << 10));
+                f = f2;
+                e = e2;
+                stage = 0;
+                pop = false;
+            }
+        } else if (r) {
+            ugk_ls_put(E->evm, ev, nev++, f | (1 << 28)); /* back to the stock */
+        }
+        if (pop) {
+            if (sp == 0) break;
+            const int fr = ugk_ls_get(E->stk, fs, --sp);
+            f = fr & 255;
+            e = (fr >> 8) & 3;
+            stage = (fr >> 10) & 3;
+            f2 = (fr >> 12) & 255;
+            e2 = (fr >> 20) & 3;
+        }
+    }
+    return r;
+}
+UGK_FN bool e_expand_group(EpaMem* E, Epa& P, int pass, int w, gv ww, const EFace& B, int& hcf, int& hff, int& hnf) {
+    LStack ev, mk;
+    ev.reg = 0;
+    mk.reg = 0;
+    int nev = 0, nnew = 0, nmk = 0;
+    bool valid = true;
+    for (int j = 0; j < 3 && valid; j++) valid = e_walk(E, pass, ww, B.f[j], fe(B, j), ev, nev, nnew, mk, nmk) && valid;
+    /* lane k: event k's plane (its own register slot holds the event) */
+    const int k = ugk_glane();
+    const int my = ev.reg;
+    gv pn = V3(0.0, 0.0, 0.0);
+    double pd = 0.0;
+    bool fail = false;
+    if (k < nev && !((my >> 28) & 1)) {
+        const int a = (my >> 10) & 255, b = (my >> 18) & 255;
+        const bool nondeg = e_plane(ugk_sv(E, a)->w, ugk_sv(E, b)->w, ww, pn, pd);
+        fail = !nondeg || !(pd >= -kEpaPlaneEps);
+    }
+    const bool serial = ugk_gany(fail) || nev > ugk_gsize() || nnew > P.nstock + (kEpaMaxFaces - P.nfresh);
+    if (serial) {
+        for (int i = 0; i < nmk; i++) ugk_face(E, ugk_ls_get(E->mkm, mk, i))->pass = 0;
+        hcf = -1;
+        hff = -1;
+        hnf = 0;
+        valid = true;
+        for (int j = 0; j < 3 && valid; j++) valid = e_expand(E, P, pass, w, ww, B.f[j], fe(B, j), hcf, hff, hnf) && valid;
+        return valid;
+    }
+    for (int i = 0; i < nev; i++) {
+        const int x = ugk_greadi(my, i);
+        const int f = x & 255;
+        if ((x >> 28) & 1) {
+            h_remove(E, P, f);
+            s_push(E, P, f);
+            continue;
+        }
+        const int e = (x >> 8) & 3;
+        const int nf = P.nstock > 0 ? ugk_ls_get(E->stock, P.stock, P.nstock - 1) : P.nfresh;
+        if (P.nstock > 0) P.nstock--;
+        else P.nfresh++;
+        const int stamp = ++P.stampctr;
+        EFace& F = *ugk_face(E, nf);
+        F.pass = 0;
+        F.c[0] = (unsigned char)((x >> 10) & 255); F.c[1] = (unsigned char)((x >> 18) & 255); F.c[2] = (unsigned char)w;
+        const double d = ugk_gread(pd, i);
+        F.n = V3(ugk_gread(pn.x, i), ugk_gread(pn.y, i), ugk_gread(pn.z, i));
+        F.d = d;
+        h_append(E, P, nf, d, stamp);
+        e_bind(E, nf, 0, f, e);
+        if (hcf >= 0) e_bind(E, hcf, 1, nf, 2);
+        else hff = nf;
+        hcf = nf;
+        hnf++;
+    }
+    return valid;
+}
+#endif
 /* EPA::Evaluate */
 UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
     const int s = g.simplex;
@@ -893,8 +1022,12 @@ UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
                 const double wdist = dot(B.n, ww) - B.d;
                 if (!(wdist > kEpaAccuracy)) { P.status = EPA_ACCURACYREACHED; break; }
                 UGK_T0(t_exp);
+#ifdef UGK_GROUP_PARALLEL
+                valid = e_expand_group(E, P, pass, w, ww, B, hcf, hff, hnf);
+#else
                 for (int j = 0; j < 3 && valid; j++)
                     valid = e_expand(E, P, pass, w, ww, B.f[j], fe(B, j), hcf, hff, hnf) && valid;
+#endif
                 UGK_ADD(PF_EPA_EXPAND, t_exp);
                 if (!(valid && hnf >= 3)) { P.status = EPA_INVALIDHULL; break; }
                 e_bind(E, hcf, 1, hff, 2);

@@ -35,7 +35,7 @@ namespace ugd {
 #define TEAM 64
 typedef __attribute__((address_space(1))) const double gcdouble;
 typedef __attribute__((address_space(1))) double gdouble;
-#define UG_NPROF 100 /* phase accumulators of the -DUG_PROF build */
+#define UG_NPROF 102 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* a row's J and M^-1 J^T over the NVP = 32 dof slots (robot 12, objects 3 x 6, 2 zero pads) */
@@ -211,7 +211,9 @@ enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_
         * horizon walk and findbest, the witnesses */
        PF_EPA_GJK, PF_EPA_SETUP, PF_EPA_SUP, PF_EPA_EXPAND, PF_EPA_BEST,
        /* inside the libccd test and the classic GJK: the support pairs, the simplex work */
-       PF_CCD_SUP, PF_CCD_DO, PF_CLS_SUP, PF_CLS_VS };
+       PF_CCD_SUP, PF_CCD_DO, PF_CLS_SUP, PF_CLS_VS,
+       /* EPA face-record accesses served from LDS / from the workspace */
+       PC_EPA_FLDS, PC_EPA_FGLOB };
 #define UG_FREE_SPLIT_N 14
 #ifdef UG_PROF
 __device__ static const int kFreeSplit[UG_FREE_SPLIT_N] = {PF_FK, PF_BROAD, PF_HULL, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST,
@@ -390,6 +392,10 @@ static_assert(ugd::GJK_NG * UG_EPA_LDS_FACES * sizeof(ugk::EFace) <= sizeof(ugd:
 static_assert(UG_EPA_HULL_OFF + ugd::GJK_NG * UG_EPA_LDS_HULL * sizeof(ugk::EHull) <= sizeof(ugd::RowS) * MAXROWS,
               "EPA hull tier in the rows union");
 UGK_FN ugk::EFace* ugk_face(ugk::EpaMem* E, int f) {
+#ifdef UG_PROF
+    if (f < UG_EPA_LDS_FACES) UGK_COUNT(PC_EPA_FLDS, 1);
+    else UGK_COUNT(PC_EPA_FGLOB, 1);
+#endif
     if (f < UG_EPA_LDS_FACES)
         return (ugk::EFace*)(void*)&ugd::g_sh.hc[0] + (int)(threadIdx.x / ugd::GJK_G) * UG_EPA_LDS_FACES + f;
     return &E->fc[f];
@@ -418,6 +424,10 @@ UGK_FN ugk::EHull* ugk_hull(ugk::EpaMem* E, int i) {
 UGK_FN int ugk_glane() { return (int)(threadIdx.x & (ugd::GJK_G - 1)); }
 UGK_FN double ugk_gread(double v, int j) { return __shfl(v, (int)(threadIdx.x & ~(ugd::GJK_G - 1)) + j, TEAM); }
 UGK_FN int ugk_greadi(int v, int j) { return __shfl(v, (int)(threadIdx.x & ~(ugd::GJK_G - 1)) + j, TEAM); }
+UGK_FN bool ugk_gany(bool p) {
+    return ((ugd::ballot(p) >> (threadIdx.x & ~(ugd::GJK_G - 1))) & ((1ull << ugd::GJK_G) - 1ull)) != 0ull;
+}
+UGK_FN int ugk_gsize() { return ugd::GJK_G; }
 
 /* ug_gjk.h's small stacks on the lane group: slots [0, GJK_G) in one register, lane i of the group holding slot i
  * (read back through ds_bpermute, an LDS-crossbar hop instead of a workspace round trip), deeper slots in memory */
