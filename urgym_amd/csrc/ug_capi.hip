@@ -388,7 +388,7 @@ __global__ void __launch_bounds__(TEAM, 1) k_gjk_query(const double* q, int n, d
     }
     ugk::gv nn, pp;
     double d = 0.0;
-    const bool r = ugk::gjk_pair(E + i, S[0], T[0], S[1], T[1], Q[38], nn, pp, d);
+    const bool r = ugk::gjk_pair((UGK_GMEM ugk::EpaMem*)(E + i), S[0], T[0], S[1], T[1], Q[38], nn, pp, d);
     if (threadIdx.x == 0) {
         ok[i] = r ? 1 : 0;
         double* o = out + (size_t)i * 7;

@@ -26,6 +26,15 @@
 #include "scene_data.h"
 #include "ug_detmath.h"
 
+#ifndef UGK_GMEM /* the address space of the EPA store (the kernels: global, so its accesses are global_*, not flat_*) */
+#define UGK_GMEM
+#endif
+#ifndef UGK_OPAQUE /* the includer's register pin: the value stays in registers, never re-read from where it came */
+#define UGK_OPAQUE(x)
+#endif
+#ifndef UGK_LMEM /* the address space of the hull-slot table (the kernels: LDS) */
+#define UGK_LMEM
+#endif
 #ifndef UGK_COUNT /* the includer's event counter and timer hooks (the kernels' -DUG_PROF build) */
 #define UGK_COUNT(k, v) do { } while (0)
 #define UGK_T0(v)
@@ -95,6 +104,7 @@ constexpr double kGjkMinDist = 1e-12, kGjkDupEps = 1e-12, kGjkAccuracy = 1e-12;
 constexpr int kGjkMaxIterations = 128;
 constexpr double kEpaAccuracy = 1e-12, kEpaPlaneEps = 0.00001;
 constexpr int kEpaMaxVertices = 128, kEpaMaxFaces = 256, kEpaMaxIterations = 255;
+constexpr int kTetra = 4 + kEpaMaxVertices; /* E->sv slots of the EPA's first tetrahedron */
 
 /* localGetSupportVertexWithoutMarginNonVirtual */
 UGK_FN gv support0(const GShape& s, gv d) {
@@ -409,7 +419,7 @@ struct ESv { gv d, w; };
 struct EFace {
     gv n;
     double d;
-    unsigned char c[3], f[3]; /* vertex ids (< 132), neighbour faces (< 256) */
+    unsigned char c[3], f[3]; /* vertex ids (< 136), neighbour faces (< 256) */
     unsigned char e3;         /* the neighbours' edge indices, 2 bits each */
     unsigned char pass;       /* expand()'s visit mark (<= 255 iterations) */
 };
@@ -417,8 +427,16 @@ static_assert(sizeof(EFace) == 40, "the compact face record");
 UGK_FN int fe(const EFace& F, int j) { return (F.e3 >> (2 * j)) & 3; }
 UGK_FN void set_fe(EFace& F, int j, int v) { F.e3 = (unsigned char)((F.e3 & ~(3 << (2 * j))) | (v << (2 * j))); }
 struct EHull { double d; int stamp, f; };
+/* copies in and out of the store's address space (a struct does not convert between address spaces implicitly) */
+UGK_FN gv ldw(const UGK_GMEM ESv& s) { return V3(s.w.x, s.w.y, s.w.z); }
+UGK_FN gv ldd(const UGK_GMEM ESv& s) { return V3(s.d.x, s.d.y, s.d.z); }
+UGK_FN ESv ldsv(const UGK_GMEM ESv& s) { ESv v; v.d = ldd(s); v.w = ldw(s); return v; }
+UGK_FN void stsv(UGK_GMEM ESv& s, const ESv& v) {
+    s.d.x = v.d.x; s.d.y = v.d.y; s.d.z = v.d.z;
+    s.w.x = v.w.x; s.w.y = v.w.y; s.w.z = v.w.z;
+}
 struct EpaMem {
-    ESv sv[4 + kEpaMaxVertices]; /* [0, 4) the GJK's store, then the EPA's */
+    ESv sv[4 + kEpaMaxVertices + 4]; /* [0, 4) the GJK's store, then the EPA's, [132, 136) its first tetrahedron */
     EFace fc[kEpaMaxFaces];
     int sc[2][4];                /* the GJK's two simplices: vertex indices, weights, ranks */
     double sp[2][4];
@@ -434,10 +452,17 @@ struct EpaMem {
 } /* namespace ugk */
 /* the includer's EPA record hooks: face f's record and hull slot i (the kernels keep the first few of each in LDS,
  * the rest in E) */
-UGK_FN ugk::EFace* ugk_face(ugk::EpaMem* E, int f);
-UGK_FN ugk::EHull* ugk_hull(ugk::EpaMem* E, int i);
-UGK_FN unsigned char* ugk_hpos(ugk::EpaMem* E); /* the hull-slot table, kEpaMaxFaces entries */
-UGK_FN ugk::ESv* ugk_sv(ugk::EpaMem* E, int i); /* support vertex i (the GJK's store 0..3, then the EPA's) */
+UGK_FN ugk::EFace ugk_face_get(UGK_GMEM ugk::EpaMem* E, int f);
+UGK_FN void ugk_face_put(UGK_GMEM ugk::EpaMem* E, int f, const ugk::EFace& F);
+UGK_FN void ugk_face_pass(UGK_GMEM ugk::EpaMem* E, int f, int pass);
+UGK_FN void ugk_face_link(UGK_GMEM ugk::EpaMem* E, int f, int j, int nf, int ne); /* neighbour j of face f := (nf, edge ne) */
+UGK_FN ugk::EHull ugk_hull_get(UGK_GMEM ugk::EpaMem* E, int i);
+UGK_FN void ugk_hull_put(UGK_GMEM ugk::EpaMem* E, int i, const ugk::EHull& h);
+UGK_FN UGK_LMEM unsigned char* ugk_hpos(UGK_GMEM ugk::EpaMem* E); /* the hull-slot table, kEpaMaxFaces entries */
+/* support vertices: the btGjkEpa2 GJK's store 0..3 (svl: the kernels keep it in LDS) and the EPA's (svg, in E: the
+ * EPA copies the GJK's final simplex to 132..135 first, so it never reads the store) */
+UGK_FN ugk::ESv ugk_svl_get(UGK_GMEM ugk::EpaMem* E, int i);
+UGK_FN void ugk_svl_put(UGK_GMEM ugk::EpaMem* E, int i, const ugk::ESv& v);
 namespace ugk {
 struct Mink { GShape s0, s1; gm toshape1; gx toshape0; bool margins; };
 UGK_FN gv mk_ls(const Mink& M, int i, gv d) {
@@ -465,13 +490,16 @@ enum { GJK_VALID = 0, GJK_INSIDE, GJK_FAILED };
 enum { EPA_VALID = 0, EPA_TOUCHING, EPA_DEGENERATED, EPA_NONCONVEX, EPA_INVALIDHULL, EPA_OUTOFFACES, EPA_OUTOFVERTICES,
        EPA_ACCURACYREACHED, EPA_FALLBACK, EPA_FAILED };
 
-UGK_FN void g2_getsupport(EpaMem* E, const Mink& M, gv d, int sv) {
+UGK_FN ESv g2_support(const Mink& M, gv d) {
     const gv dd = mulinv(d, len(d));
-    ugk_sv(E, sv)->d = dd;
-    ugk_sv(E, sv)->w = mk_support(M, dd);
+    ESv v;
+    v.d = dd;
+    v.w = mk_support(M, dd);
+    return v;
 }
-UGK_FN void g2_remove(EpaMem* E, Gjk2& g, int s) { E->freev[g.nfree++] = E->sc[s][--E->srank[s]]; }
-UGK_FN void g2_append(EpaMem* E, Gjk2& g, const Mink& M, int s, gv v) {
+UGK_FN void g2_getsupport(UGK_GMEM EpaMem* E, const Mink& M, gv d, int sv) { ugk_svl_put(E, sv, g2_support(M, d)); }
+UGK_FN void g2_remove(UGK_GMEM EpaMem* E, Gjk2& g, int s) { E->freev[g.nfree++] = E->sc[s][--E->srank[s]]; }
+UGK_FN void g2_append(UGK_GMEM EpaMem* E, Gjk2& g, const Mink& M, int s, gv v) {
     const int r = E->srank[s];
     E->sp[s][r] = 0;
     E->sc[s][r] = E->freev[--g.nfree];
@@ -571,7 +599,7 @@ UGK_FN double g2_proj4(gv a, gv b, gv c, gv d, double* w, int& m) {
     return -1;
 }
 /* GJK::Evaluate */
-UGK_FN int g2_evaluate(EpaMem* E, Gjk2& g, const Mink& M, gv guess) {
+UGK_FN int g2_evaluate(UGK_GMEM EpaMem* E, Gjk2& g, const Mink& M, gv guess) {
     int iterations = 0;
     double sqdist = 0, alpha = 0;
     gv lastw[4];
@@ -586,7 +614,7 @@ UGK_FN int g2_evaluate(EpaMem* E, Gjk2& g, const Mink& M, gv guess) {
     const double sqrl = dot(g.ray, g.ray);
     g2_append(E, g, M, 0, sqrl > 0 ? neg(g.ray) : V3(1, 0, 0));
     E->sp[0][0] = 1;
-    g.ray = ugk_sv(E, E->sc[0][0])->w;
+    g.ray = ugk_svl_get(E, E->sc[0][0]).w;
     sqdist = sqrl;
     lastw[0] = lastw[1] = lastw[2] = lastw[3] = g.ray;
     do {
@@ -594,7 +622,7 @@ UGK_FN int g2_evaluate(EpaMem* E, Gjk2& g, const Mink& M, gv guess) {
         const double rl = len(g.ray);
         if (rl < kGjkMinDist) { g.status = GJK_INSIDE; break; }
         g2_append(E, g, M, cs, neg(g.ray));
-        const gv w = ugk_sv(E, E->sc[cs][E->srank[cs] - 1])->w;
+        const gv w = ugk_svl_get(E, E->sc[cs][E->srank[cs] - 1]).w;
         bool found = false;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -611,10 +639,10 @@ UGK_FN int g2_evaluate(EpaMem* E, Gjk2& g, const Mink& M, gv guess) {
         double weights[4];
         int mask = 0;
         const int rank = E->srank[cs];
-        const gv w0 = ugk_sv(E, E->sc[cs][0])->w, w1 = ugk_sv(E, E->sc[cs][1])->w;
+        const gv w0 = ugk_svl_get(E, E->sc[cs][0]).w, w1 = ugk_svl_get(E, E->sc[cs][1]).w;
         if (rank == 2) sqdist = g2_proj2(w0, w1, weights, mask);
-        else if (rank == 3) sqdist = g2_proj3(w0, w1, ugk_sv(E, E->sc[cs][2])->w, weights, mask);
-        else if (rank == 4) sqdist = g2_proj4(w0, w1, ugk_sv(E, E->sc[cs][2])->w, ugk_sv(E, E->sc[cs][3])->w, weights, mask);
+        else if (rank == 3) sqdist = g2_proj3(w0, w1, ugk_svl_get(E, E->sc[cs][2]).w, weights, mask);
+        else if (rank == 4) sqdist = g2_proj4(w0, w1, ugk_svl_get(E, E->sc[cs][2]).w, ugk_svl_get(E, E->sc[cs][3]).w, weights, mask);
         if (sqdist >= 0) {
             E->srank[ns] = 0;
             g.ray = V3(0, 0, 0);
@@ -626,7 +654,7 @@ UGK_FN int g2_evaluate(EpaMem* E, Gjk2& g, const Mink& M, gv guess) {
                     const int r = E->srank[ns]++;
                     E->sc[ns][r] = E->sc[cs][i];
                     E->sp[ns][r] = weights[i];
-                    g.ray = add(g.ray, scl(ugk_sv(E, E->sc[cs][i])->w, weights[i]));
+                    g.ray = add(g.ray, scl(ugk_svl_get(E, E->sc[cs][i]).w, weights[i]));
                 } else {
                     E->freev[g.nfree++] = E->sc[cs][i];
                 }
@@ -645,15 +673,15 @@ UGK_FN int g2_evaluate(EpaMem* E, Gjk2& g, const Mink& M, gv guess) {
 }
 /* GJK::EncloseOrigin, its recursion unrolled by rank (rank r tries the simplices of rank r + 1) */
 UGK_FN gv g2_axis(int i) { return V3(i == 0 ? 1.0 : 0.0, i == 1 ? 1.0 : 0.0, i == 2 ? 1.0 : 0.0); }
-UGK_FN bool g2_enc4(EpaMem* E, const Gjk2& g) {
+UGK_FN bool g2_enc4(UGK_GMEM EpaMem* E, const Gjk2& g) {
     const int s = g.simplex;
-    const gv w3 = ugk_sv(E, E->sc[s][3])->w;
-    return ug_fabs(g2_det(sub(ugk_sv(E, E->sc[s][0])->w, w3), sub(ugk_sv(E, E->sc[s][1])->w, w3), sub(ugk_sv(E, E->sc[s][2])->w, w3))) > 0;
+    const gv w3 = ugk_svl_get(E, E->sc[s][3]).w;
+    return ug_fabs(g2_det(sub(ugk_svl_get(E, E->sc[s][0]).w, w3), sub(ugk_svl_get(E, E->sc[s][1]).w, w3), sub(ugk_svl_get(E, E->sc[s][2]).w, w3))) > 0;
 }
-UGK_FN bool g2_enc3(EpaMem* E, Gjk2& g, const Mink& M) {
+UGK_FN bool g2_enc3(UGK_GMEM EpaMem* E, Gjk2& g, const Mink& M) {
     const int s = g.simplex;
-    const gv w0 = ugk_sv(E, E->sc[s][0])->w;
-    const gv n = cross(sub(ugk_sv(E, E->sc[s][1])->w, w0), sub(ugk_sv(E, E->sc[s][2])->w, w0));
+    const gv w0 = ugk_svl_get(E, E->sc[s][0]).w;
+    const gv n = cross(sub(ugk_svl_get(E, E->sc[s][1]).w, w0), sub(ugk_svl_get(E, E->sc[s][2]).w, w0));
     if (dot(n, n) > 0) {
         g2_append(E, g, M, s, n);
         if (g2_enc4(E, g)) return true;
@@ -664,9 +692,9 @@ UGK_FN bool g2_enc3(EpaMem* E, Gjk2& g, const Mink& M) {
     }
     return false;
 }
-UGK_FN bool g2_enc2(EpaMem* E, Gjk2& g, const Mink& M) {
+UGK_FN bool g2_enc2(UGK_GMEM EpaMem* E, Gjk2& g, const Mink& M) {
     const int s = g.simplex;
-    const gv d = sub(ugk_sv(E, E->sc[s][1])->w, ugk_sv(E, E->sc[s][0])->w);
+    const gv d = sub(ugk_svl_get(E, E->sc[s][1]).w, ugk_svl_get(E, E->sc[s][0]).w);
     for (int i = 0; i < 3; i++) {
         const gv p = cross(d, g2_axis(i));
         if (dot(p, p) > 0) {
@@ -680,7 +708,7 @@ UGK_FN bool g2_enc2(EpaMem* E, Gjk2& g, const Mink& M) {
     }
     return false;
 }
-UGK_FN bool g2_enc1(EpaMem* E, Gjk2& g, const Mink& M) {
+UGK_FN bool g2_enc1(UGK_GMEM EpaMem* E, Gjk2& g, const Mink& M) {
     const int s = g.simplex;
     for (int i = 0; i < 3; i++) {
         const gv axis = g2_axis(i);
@@ -693,7 +721,7 @@ UGK_FN bool g2_enc1(EpaMem* E, Gjk2& g, const Mink& M) {
     }
     return false;
 }
-UGK_FN bool g2_enclose(EpaMem* E, Gjk2& g, const Mink& M) {
+UGK_FN bool g2_enclose(UGK_GMEM EpaMem* E, Gjk2& g, const Mink& M) {
     const int r = E->srank[g.simplex];
     if (r == 1) return g2_enc1(E, g, M);
     if (r == 2) return g2_enc2(E, g, M);
@@ -710,35 +738,33 @@ struct Epa { int status, nextsv, hcount, nstock, nfresh, stampctr; LStack stock;
 /* the includer's EPA hook: of the hull faces hl[0, hcount), the one with the smallest d * d, ties to the largest stamp
  * (m_hull's first minimum), except that a NaN at the list root (the largest stamp) keeps the root (Bullet's loop never
  * replaces a NaN) */
-UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E, int hcount);
+UGK_FN int ugk_epa_findbest(const UGK_GMEM ugk::EpaMem* E, int hcount);
 /* the includer's LStack hooks: slot i of the stack whose memory is mem (the kernels hold slots [0, 16) in the lane
  * group's registers, lane i slot i) */
-UGK_FN void ugk_ls_put(int* mem, ugk::LStack& s, int i, int v);
-UGK_FN int ugk_ls_get(const int* mem, const ugk::LStack& s, int i);
+UGK_FN void ugk_ls_put(UGK_GMEM int* mem, ugk::LStack& s, int i, int v);
+UGK_FN int ugk_ls_get(const UGK_GMEM int* mem, const ugk::LStack& s, int i);
 namespace ugk {
 
-UGK_FN void e_bind(EpaMem* E, int fa, int ea, int fb, int eb) {
-    EFace* A = ugk_face(E, fa);
-    EFace* B = ugk_face(E, fb);
-    set_fe(*A, ea, eb); A->f[ea] = (unsigned char)fb;
-    set_fe(*B, eb, ea); B->f[eb] = (unsigned char)fa;
+UGK_FN void e_bind(UGK_GMEM EpaMem* E, int fa, int ea, int fb, int eb) {
+    ugk_face_link(E, fa, ea, fb, eb);
+    ugk_face_link(E, fb, eb, fa, ea);
 }
-UGK_FN void h_append(EpaMem* E, Epa& P, int f, double d, int stamp) {
+UGK_FN void h_append(UGK_GMEM EpaMem* E, Epa& P, int f, double d, int stamp) {
     EHull h;
     h.d = d; h.stamp = stamp; h.f = f;
-    *ugk_hull(E, P.hcount) = h;
+    ugk_hull_put(E, P.hcount, h);
     ugk_hpos(E)[f] = (unsigned char)P.hcount++;
 }
-UGK_FN void h_remove(EpaMem* E, Epa& P, int f) {
-    unsigned char* hp = ugk_hpos(E);
+UGK_FN void h_remove(UGK_GMEM EpaMem* E, Epa& P, int f) {
+    UGK_LMEM unsigned char* hp = ugk_hpos(E);
     const int i = hp[f], last = --P.hcount;
     if (i != last) {
-        const EHull t = *ugk_hull(E, last);
-        *ugk_hull(E, i) = t;
+        const EHull t = ugk_hull_get(E, last);
+        ugk_hull_put(E, i, t);
         hp[t.f] = (unsigned char)i;
     }
 }
-UGK_FN void s_push(EpaMem* E, Epa& P, int f) { ugk_ls_put(E->stock, P.stock, P.nstock++, f); }
+UGK_FN void s_push(UGK_GMEM EpaMem* E, Epa& P, int f) { ugk_ls_put(E->stock, P.stock, P.nstock++, f); }
 UGK_FN bool e_edgedist(gv aw, gv bw, gv fn, double& dist) {
     const gv ba = sub(bw, aw);
     const gv n_ab = cross(ba, fn);
@@ -772,22 +798,26 @@ UGK_FN bool e_plane(gv aw, gv bw, gv cw, gv& nOut, double& dOut) {
     nOut = n;
     return false;
 }
-UGK_FN int e_newface(EpaMem* E, Epa& P, int a, int b, int c, bool forced) {
+UGK_FN int e_newface(UGK_GMEM EpaMem* E, Epa& P, int a, int b, int c, bool forced) {
     if (P.nstock > 0 || P.nfresh < kEpaMaxFaces) {
         const int f = P.nstock > 0 ? ugk_ls_get(E->stock, P.stock, P.nstock - 1) : P.nfresh;
         if (P.nstock > 0) P.nstock--;
         else P.nfresh++;
         const int stamp = ++P.stampctr; /* m_hull.append: the face joins the hull before its plane is known */
-        const gv aw = ugk_sv(E, a)->w, bw = ugk_sv(E, b)->w, cw = ugk_sv(E, c)->w;
-        EFace& F = *ugk_face(E, f);
+        const gv aw = ldw(E->sv[a]), bw = ldw(E->sv[b]), cw = ldw(E->sv[c]);
+        EFace F; /* its three links are all set by e_bind before the hull is read again */
+        F.f[0] = F.f[1] = F.f[2] = 0;
+        F.e3 = 0;
+        F.d = 0.0;
         F.pass = 0;
         F.c[0] = (unsigned char)a; F.c[1] = (unsigned char)b; F.c[2] = (unsigned char)c;
         gv n;
         double d = 0.0;
         const bool nondeg = e_plane(aw, bw, cw, n, d);
         F.n = n;
+        if (nondeg) F.d = d;
+        ugk_face_put(E, f, F);
         if (nondeg) {
-            F.d = d;
             if (forced || d >= -kEpaPlaneEps) {
                 h_append(E, P, f, d, stamp);
                 return f;
@@ -807,7 +837,7 @@ UGK_FN int e_newface(EpaMem* E, Epa& P, int a, int b, int c, bool forced) {
  * stage << 10 | second neighbour << 12 | its edge << 20 (read at entry: a visited face's other edges are not rebound
  * while its subtree runs, the pass mark stops every re-entry).  The same visits, face allocations and list operations
  * as the recursion. */
-UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, gv ww, int f0, int e0, int& hcf, int& hff, int& hnf) {
+UGK_FN bool e_expand(UGK_GMEM EpaMem* E, Epa& P, int pass, int w, gv ww, int f0, int e0, int& hcf, int& hff, int& hnf) {
     int sp = 0, f = f0, e = e0, stage = 0, f2 = 0, e2 = 0;
     bool r = false;
     LStack fs;
@@ -815,7 +845,7 @@ UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, gv ww, int f0, int e0, 
     for (;;) {
         bool pop = true;
         if (stage == 0) {
-            const EFace F = *ugk_face(E, f); /* the face's record in one batch of loads */
+            const EFace F = ugk_face_get(E, f); /* the face's record in one batch of loads */
             const int e1 = e == 2 ? 0 : e + 1, em = e == 0 ? 2 : e - 1;
             if (F.pass == pass) {
                 r = false;
@@ -831,7 +861,7 @@ UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, gv ww, int f0, int e0, 
                     r = true;
                 }
             } else {
-                ugk_face(E, f)->pass = (unsigned char)pass;
+                ugk_face_pass(E, f, pass);
                 ugk_ls_put(E->stk, fs, sp++, f | (e << 8) | (1 << 10) | (F.f[em] << 12) | (fe(F, em) << 20));
                 f = F.f[e1];
                 e = fe(F, e1);
@@ -870,7 +900,7 @@ UGK_FN bool e_expand(EpaMem* E, Epa& P, int pass, int w, gv ww, int f0, int e0, 
  * none is degenerate or non-convex (and the faces suffice) the log is replayed in order -- stock pops and pushes,
  * stamps, records, hull appends / removals, bindings -- which is exactly what the serial walk does.  Otherwise the
  * walk's marks are cleared and the serial expand() runs. */
-UGK_FN bool e_walk(EpaMem* E, int pass, gv ww, int f0, int e0, LStack& ev, int& nev, int& nnew, LStack& mk, int& nmk) {
+UGK_FN bool e_walk(UGK_GMEM EpaMem* E, int pass, gv ww, int f0, int e0, LStack& ev, int& nev, int& nnew, LStack& mk, int& nmk) {
     int sp = 0, f = f0, e = e0, stage = 0, f2 = 0, e2 = 0;
     bool r = false;
     LStack fs;
@@ -878,7 +908,7 @@ UGK_FN bool e_walk(EpaMem* E, int pass, gv ww, int f0, int e0, LStack& ev, int& 
     for (;;) {
         bool pop = true;
         if (stage == 0) {
-            const EFace F = *ugk_face(E, f);
+            const EFace F = ugk_face_get(E, f);
             const int e1 = e == 2 ? 0 : e + 1, em = e == 0 ? 2 : e - 1;
             if (F.pass == pass) {
                 r = false;
@@ -887,7 +917,7 @@ UGK_FN bool e_walk(EpaMem* E, int pass, gv ww, int f0, int e0, LStack& ev, int& 
                 nnew++;
                 r = true;
             } else {
-                ugk_face(E, f)->pass = (unsigned char)pass;
+                ugk_face_pass(E, f, pass);
                 ugk_ls_put(E->mkm, mk, nmk++, f);
                 ugk_ls_put(E->stk, fs, sp++, f | (e << 8) | (1 << 10) | (F.f[em] << 12) | (fe(F, em) << 20));
                 f = F.f[e1];
@@ -917,7 +947,7 @@ UGK_FN bool e_walk(EpaMem* E, int pass, gv ww, int f0, int e0, LStack& ev, int& 
     }
     return r;
 }
-UGK_FN bool e_expand_group(EpaMem* E, Epa& P, int pass, int w, gv ww, const EFace& B, int& hcf, int& hff, int& hnf) {
+UGK_FN bool e_expand_group(UGK_GMEM EpaMem* E, Epa& P, int pass, int w, gv ww, const EFace& B, int& hcf, int& hff, int& hnf) {
     LStack ev, mk;
     ev.reg = 0;
     mk.reg = 0;
@@ -932,12 +962,12 @@ UGK_FN bool e_expand_group(EpaMem* E, Epa& P, int pass, int w, gv ww, const EFac
     bool fail = false;
     if (k < nev && !((my >> 28) & 1)) {
         const int a = (my >> 10) & 255, b = (my >> 18) & 255;
-        const bool nondeg = e_plane(ugk_sv(E, a)->w, ugk_sv(E, b)->w, ww, pn, pd);
+        const bool nondeg = e_plane(ldw(E->sv[a]), ldw(E->sv[b]), ww, pn, pd);
         fail = !nondeg || !(pd >= -kEpaPlaneEps);
     }
     const bool serial = ugk_gany(fail) || nev > ugk_gsize() || nnew > P.nstock + (kEpaMaxFaces - P.nfresh);
     if (serial) {
-        for (int i = 0; i < nmk; i++) ugk_face(E, ugk_ls_get(E->mkm, mk, i))->pass = 0;
+        for (int i = 0; i < nmk; i++) ugk_face_pass(E, ugk_ls_get(E->mkm, mk, i), 0);
         hcf = -1;
         hff = -1;
         hnf = 0;
@@ -958,12 +988,15 @@ UGK_FN bool e_expand_group(EpaMem* E, Epa& P, int pass, int w, gv ww, const EFac
         if (P.nstock > 0) P.nstock--;
         else P.nfresh++;
         const int stamp = ++P.stampctr;
-        EFace& F = *ugk_face(E, nf);
+        EFace F;
+        F.f[0] = F.f[1] = F.f[2] = 0;
+        F.e3 = 0;
         F.pass = 0;
         F.c[0] = (unsigned char)((x >> 10) & 255); F.c[1] = (unsigned char)((x >> 18) & 255); F.c[2] = (unsigned char)w;
         const double d = ugk_gread(pd, i);
         F.n = V3(ugk_gread(pn.x, i), ugk_gread(pn.y, i), ugk_gread(pn.z, i));
         F.d = d;
+        ugk_face_put(E, nf, F);
         h_append(E, P, nf, d, stamp);
         e_bind(E, nf, 0, f, e);
         if (hcf >= 0) e_bind(E, hcf, 1, nf, 2);
@@ -975,30 +1008,32 @@ UGK_FN bool e_expand_group(EpaMem* E, Epa& P, int pass, int w, gv ww, const EFac
 }
 #endif
 /* EPA::Evaluate */
-UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
+UGK_FN int e_evaluate(UGK_GMEM EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
     const int s = g.simplex;
     UGK_T0(t_setup);
     if (E->srank[s] > 1 && g2_enclose(E, g, M)) {
         /* Bullet first moves every hull face back to the stock: a fresh EPA (e_init) has none */
         P.status = EPA_VALID;
         P.nextsv = 0;
-        int* c = E->sc[s];
+        UGK_GMEM int* c = E->sc[s];
         {
-            const gv w3 = ugk_sv(E, c[3])->w;
-            if (g2_det(sub(ugk_sv(E, c[0])->w, w3), sub(ugk_sv(E, c[1])->w, w3), sub(ugk_sv(E, c[2])->w, w3)) < 0) {
+            const gv w3 = ugk_svl_get(E, c[3]).w;
+            if (g2_det(sub(ugk_svl_get(E, c[0]).w, w3), sub(ugk_svl_get(E, c[1]).w, w3), sub(ugk_svl_get(E, c[2]).w, w3)) < 0) {
                 const int t = c[0]; c[0] = c[1]; c[1] = t;
                 const double tp = E->sp[s][0]; E->sp[s][0] = E->sp[s][1]; E->sp[s][1] = tp;
             }
         }
+        /* the simplex's vertices as EPA vertices 132..135 (the same values; the EPA only ever reads E->sv) */
+        for (int k = 0; k < 4; k++) stsv(E->sv[kTetra + k], ugk_svl_get(E, c[k]));
         int tetra[4];
-        tetra[0] = e_newface(E, P, c[0], c[1], c[2], true);
-        tetra[1] = e_newface(E, P, c[1], c[0], c[3], true);
-        tetra[2] = e_newface(E, P, c[2], c[1], c[3], true);
-        tetra[3] = e_newface(E, P, c[0], c[2], c[3], true);
+        tetra[0] = e_newface(E, P, kTetra + 0, kTetra + 1, kTetra + 2, true);
+        tetra[1] = e_newface(E, P, kTetra + 1, kTetra + 0, kTetra + 3, true);
+        tetra[2] = e_newface(E, P, kTetra + 2, kTetra + 1, kTetra + 3, true);
+        tetra[3] = e_newface(E, P, kTetra + 0, kTetra + 2, kTetra + 3, true);
         if (P.hcount == 4) {
             int best = ugk_epa_findbest(E, P.hcount);
             UGK_ADD(PF_EPA_SETUP, t_setup);
-            EFace outer = *ugk_face(E, best);
+            EFace outer = ugk_face_get(E, best);
             int pass = 0;
             e_bind(E, tetra[0], 0, tetra[1], 0);
             e_bind(E, tetra[0], 1, tetra[2], 0);
@@ -1013,12 +1048,12 @@ UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
                 int hcf = -1, hff = -1, hnf = 0;
                 const int w = 4 + P.nextsv++;
                 bool valid = true;
-                ugk_face(E, best)->pass = (unsigned char)(++pass);
+                ugk_face_pass(E, best, ++pass);
                 UGK_T0(t_sup);
-                g2_getsupport(E, M, ugk_face(E, best)->n, w);
+                stsv(E->sv[w], g2_support(M, ugk_face_get(E, best).n));
                 UGK_ADD(PF_EPA_SUP, t_sup);
-                const gv ww = ugk_sv(E, w)->w;
-                const EFace B = *ugk_face(E, best);
+                const gv ww = ldw(E->sv[w]);
+                const EFace B = ugk_face_get(E, best);
                 const double wdist = dot(B.n, ww) - B.d;
                 if (!(wdist > kEpaAccuracy)) { P.status = EPA_ACCURACYREACHED; break; }
                 UGK_T0(t_exp);
@@ -1036,15 +1071,15 @@ UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
                 UGK_T0(t_best);
                 best = ugk_epa_findbest(E, P.hcount);
                 UGK_ADD(PF_EPA_BEST, t_best);
-                outer = *ugk_face(E, best);
+                outer = ugk_face_get(E, best);
             }
             const gv projection = scl(outer.n, outer.d);
             P.normal = outer.n;
             P.depth = outer.d;
             P.rrank = 3;
             P.rc[0] = outer.c[0]; P.rc[1] = outer.c[1]; P.rc[2] = outer.c[2];
-            const gv a = sub(ugk_sv(E, outer.c[0])->w, projection), b = sub(ugk_sv(E, outer.c[1])->w, projection),
-                     cc = sub(ugk_sv(E, outer.c[2])->w, projection);
+            const gv a = sub(ldw(E->sv[outer.c[0]]), projection), b = sub(ldw(E->sv[outer.c[1]]), projection),
+                     cc = sub(ldw(E->sv[outer.c[2]]), projection);
             P.rp[0] = len(cross(b, cc));
             P.rp[1] = len(cross(cc, a));
             P.rp[2] = len(cross(a, b));
@@ -1065,7 +1100,7 @@ UGK_FN int e_evaluate(EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
     P.rp[0] = 1;
     return P.status;
 }
-UGK_FN void e_init(EpaMem* E, Epa& P) {
+UGK_FN void e_init(UGK_GMEM EpaMem* E, Epa& P) {
     P.status = EPA_FAILED;
     P.normal = V3(0, 0, 0);
     P.depth = 0;
@@ -1077,7 +1112,7 @@ UGK_FN void e_init(EpaMem* E, Epa& P) {
     P.stampctr = 0;
 }
 struct Res { gv w0, w1, normal; double distance; };
-UGK_FN bool g2_penetration(EpaMem* E, const GShape& s0, const gx& w0, const GShape& s1, const gx& w1, gv guess, Res& r) {
+UGK_FN bool g2_penetration(UGK_GMEM EpaMem* E, const GShape& s0, const gx& w0, const GShape& s1, const gx& w1, gv guess, Res& r) {
     Mink M;
     mk_init(M, s0, w0, s1, w1, true);
     Gjk2 g;
@@ -1089,7 +1124,9 @@ UGK_FN bool g2_penetration(EpaMem* E, const GShape& s0, const gx& w0, const GSha
         e_init(E, P);
         if (e_evaluate(E, P, g, M, neg(guess)) != EPA_FAILED) {
             gv a = V3(0, 0, 0);
-            for (int i = 0; i < P.rrank; i++) a = add(a, scl(mk_support0(M, ugk_sv(E, P.rc[i])->d), P.rp[i]));
+            /* the witness: EPA vertices, or the GJK store's for the fallback */
+            for (int i = 0; i < P.rrank; i++)
+                a = add(a, scl(mk_support0(M, P.rc[i] < 4 ? ugk_svl_get(E, P.rc[i]).d : ldd(E->sv[P.rc[i]])), P.rp[i]));
             r.w0 = xfa(w0, a);
             r.w1 = xfa(w0, sub(a, scl(P.normal, P.depth)));
             r.normal = neg(P.normal);
@@ -1099,7 +1136,7 @@ UGK_FN bool g2_penetration(EpaMem* E, const GShape& s0, const gx& w0, const GSha
     }
     return false;
 }
-UGK_FN bool g2_distance(EpaMem* E, const GShape& s0, const gx& w0, const GShape& s1, const gx& w1, gv guess, Res& r) {
+UGK_FN bool g2_distance(UGK_GMEM EpaMem* E, const GShape& s0, const gx& w0, const GShape& s1, const gx& w1, gv guess, Res& r) {
     Mink M;
     mk_init(M, s0, w0, s1, w1, false);
     Gjk2 g;
@@ -1108,7 +1145,7 @@ UGK_FN bool g2_distance(EpaMem* E, const GShape& s0, const gx& w0, const GShape&
         const int s = g.simplex;
         for (int i = 0; i < E->srank[s]; i++) {
             const double p = E->sp[s][i];
-            const gv d = ugk_sv(E, E->sc[s][i])->d;
+            const gv d = ugk_svl_get(E, E->sc[s][i]).d;
             a = add(a, scl(mk_support0(M, d), p));
             b = add(b, scl(mk_support1(M, neg(d)), p));
         }
@@ -1126,7 +1163,7 @@ UGK_FN gv safe_normalize(gv d) {
     return l2 >= kEps * kEps ? mulinv(d, ug_sqrt(l2)) : V3(1, 0, 0);
 }
 /* btGjkEpaPenetrationDepthSolver::calcPenDepth */
-UGK_FN bool calc_pen_depth(EpaMem* E, const GShape& A, const GShape& B, const gx& TA, const gx& TB, gv& v, gv& wA, gv& wB) {
+UGK_FN bool calc_pen_depth(UGK_GMEM EpaMem* E, const GShape& A, const GShape& B, const gx& TA, const gx& TB, gv& v, gv& wA, gv& wB) {
     for (int i = 0; i < 9; i++) {
         gv guess;
         if (i == 0) guess = safe_normalize(sub(TB.p, TA.p));
@@ -1307,14 +1344,20 @@ UGK_FN gv support_ab(const GShape& A, const gx& TA, const GShape& B, const gx& T
 }
 
 /* btGjkPairDetector::getClosestPointsNonVirtual: one point (normal on B, point on B, distance) or none */
-UGK_FN bool gjk_pair(EpaMem* E, const GShape& A, const gx& TA0, const GShape& B, const gx& TB0, double thr, gv& nOut,
-                           gv& pOut, double& dOut, gv* sepAxis = nullptr) {
+UGK_FN bool gjk_pair(UGK_GMEM EpaMem* E, const GShape& A0, const gx& TA0, const GShape& B0, const gx& TB0, double thr,
+                     gv& nOut, gv& pOut, double& dOut, gv* sepAxis = nullptr) {
     UGK_COUNT(PC_GJK, 1);
     UGK_T0(t_all);
+    const GShape A = A0, B = B0; /* by value: the caller's records are not re-read through its stack in the loops */
     const double marginA = A.margin, marginB = B.margin;
     double maxd2 = marginA + marginB + thr;
     maxd2 *= maxd2;
     gx TA = TA0, TB = TB0;
+    /* pinned: the caller's records sit on its stack, and a re-read through that generic address is a flat load that
+     * waits for every outstanding memory access of the wave */
+    for (int i = 0; i < 9; i++) { UGK_OPAQUE(TA.R.m[i]); UGK_OPAQUE(TB.R.m[i]); }
+    UGK_OPAQUE(TA.p.x); UGK_OPAQUE(TA.p.y); UGK_OPAQUE(TA.p.z);
+    UGK_OPAQUE(TB.p.x); UGK_OPAQUE(TB.p.y); UGK_OPAQUE(TB.p.z);
     const gv off = scl(add(TA.p, TB.p), 0.5);
     TA.p = sub(TA.p, off);
     TB.p = sub(TB.p, off);

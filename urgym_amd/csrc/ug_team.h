@@ -35,7 +35,7 @@ namespace ugd {
 #define TEAM 64
 typedef __attribute__((address_space(1))) const double gcdouble;
 typedef __attribute__((address_space(1))) double gdouble;
-#define UG_NPROF 102 /* phase accumulators of the -DUG_PROF build */
+#define UG_NPROF 100 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* a row's J and M^-1 J^T over the NVP = 32 dof slots (robot 12, objects 3 x 6, 2 zero pads) */
@@ -211,9 +211,7 @@ enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_
         * horizon walk and findbest, the witnesses */
        PF_EPA_GJK, PF_EPA_SETUP, PF_EPA_SUP, PF_EPA_EXPAND, PF_EPA_BEST,
        /* inside the libccd test and the classic GJK: the support pairs, the simplex work */
-       PF_CCD_SUP, PF_CCD_DO, PF_CLS_SUP, PF_CLS_VS,
-       /* EPA face-record accesses served from LDS / from the workspace */
-       PC_EPA_FLDS, PC_EPA_FGLOB };
+       PF_CCD_SUP, PF_CCD_DO, PF_CLS_SUP, PF_CLS_VS };
 #define UG_FREE_SPLIT_N 14
 #ifdef UG_PROF
 __device__ static const int kFreeSplit[UG_FREE_SPLIT_N] = {PF_FK, PF_BROAD, PF_HULL, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST,
@@ -223,6 +221,9 @@ __device__ static const int kFreeSplit[UG_FREE_SPLIT_N] = {PF_FK, PF_BROAD, PF_H
 } /* namespace ugd */
 /* the convex-convex narrowphase (Bullet's GJK / EPA pair detector), run by the whole wave per pair */
 #define UGK_FN __device__ static inline
+#define UGK_GMEM __attribute__((address_space(1)))
+#define UGK_LMEM __attribute__((address_space(3)))
+#define UGK_OPAQUE(x) __asm__ volatile("" : "+v"(x))
 #define UGK_GROUP_PARALLEL 1
 #ifdef UG_PROF /* its event counters (PC_GJK_*) and phase timers, lane 0 of the env's wave */
 /* summed over the lane groups that run pairs at once (LDS atomics): work, not wall time */
@@ -381,43 +382,63 @@ UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
     return r;
 }
 
-/* ug_gjk.h's EPA record hooks: each lane group keeps its first UG_EPA_LDS_FACES face records and UG_EPA_LDS_HULL hull
- * slots in LDS the GJK stage does not use -- the hull-candidate / box-clip union (written only after team_gjk) and the
- * tail of the rows union past the pair records (the working manifolds overwrite it only after team_gjk) -- and the
- * rest in its workspace store; the records are reached through generic (flat) pointers either way */
-#define UG_EPA_LDS_FACES 22
-#define UG_EPA_LDS_HULL 42
-#define UG_EPA_HULL_OFF (((sizeof(ugd::PairInfo) * MAXOV) + 15) & ~(size_t)15)
-static_assert(ugd::GJK_NG * UG_EPA_LDS_FACES * sizeof(ugk::EFace) <= sizeof(ugd::Cand) * 64, "EPA face tier in hc");
-static_assert(UG_EPA_HULL_OFF + ugd::GJK_NG * UG_EPA_LDS_HULL * sizeof(ugk::EHull) <= sizeof(ugd::RowS) * MAXROWS,
-              "EPA hull tier in the rows union");
-UGK_FN ugk::EFace* ugk_face(ugk::EpaMem* E, int f) {
-#ifdef UG_PROF
-    if (f < UG_EPA_LDS_FACES) UGK_COUNT(PC_EPA_FLDS, 1);
-    else UGK_COUNT(PC_EPA_FGLOB, 1);
-#endif
-    if (f < UG_EPA_LDS_FACES)
-        return (ugk::EFace*)(void*)&ugd::g_sh.hc[0] + (int)(threadIdx.x / ugd::GJK_G) * UG_EPA_LDS_FACES + f;
-    return &E->fc[f];
-}
-/* the btGjkEpa2 GJK's four-vertex store (support vertices 0..3, every GJK iteration's reads and writes) in the
- * velocity / impulse vectors' LDS (v0 | dvout | dvsout: written by serial_pre and after the PGS, dead during collision) */
+/* The EPA / btGjkEpa2 records.  The btGjkEpa2 GJK's four-vertex store and the EPA's hull-slot table live in LDS the
+ * collision stage leaves unused (v0 | dvout | dvsout, written by serial_pre and after the PGS; LDL, written by
+ * serial_pre), one slice per lane group, reached through LDS-typed pointers (ds_* instructions); the faces, hull slots
+ * and EPA vertices stay in the group's workspace store, reached through global-typed pointers (global_*).  A record
+ * that may sit in either space would need a generic pointer, and every flat access waits for all outstanding memory
+ * operations of the wave (measured: 308 full waits in the solver with LDS / workspace tiers for the faces). */
+#define UG_LDS __attribute__((address_space(3)))
 static_assert(ugd::GJK_NG * 4 * sizeof(ugk::ESv) <= 3 * sizeof(double) * NVP, "the GJK stores in v0 | dvout | dvsout");
 static_assert(offsetof(ugd::Shared, dvsout) == offsetof(ugd::Shared, v0) + 2 * sizeof(double) * NVP, "v0, dvout, dvsout adjacent");
-UGK_FN ugk::ESv* ugk_sv(ugk::EpaMem* E, int i) {
-    if (i < 4) return (ugk::ESv*)(void*)&ugd::g_sh.v0[0] + (int)(threadIdx.x / ugd::GJK_G) * 4 + i;
-    return &E->sv[i];
-}
-/* the hull-slot table (one byte per face) in the mass matrix's LDS, dead from FK to serial_pre (which rebuilds it) */
 static_assert(ugd::GJK_NG * ugk::kEpaMaxFaces <= sizeof(double) * NB * NB, "EPA hull-slot tables in LDL");
-UGK_FN unsigned char* ugk_hpos(ugk::EpaMem*) {
-    return (unsigned char*)(void*)&ugd::g_sh.LDL[0] + (int)(threadIdx.x / ugd::GJK_G) * ugk::kEpaMaxFaces;
+__device__ __forceinline__ int gjk_grp() { return (int)(threadIdx.x / ugd::GJK_G); }
+__device__ __forceinline__ UG_LDS ugk::ESv* lds_sv() { return (UG_LDS ugk::ESv*)(UG_LDS void*)&ugd::g_sh.v0[0] + gjk_grp() * 4; }
+UGK_FN ugk::ESv ugk_svl_get(UGK_GMEM ugk::EpaMem*, int i) {
+    const UG_LDS ugk::ESv& s = lds_sv()[i];
+    ugk::ESv v;
+    v.d = ugk::V3(s.d.x, s.d.y, s.d.z);
+    v.w = ugk::V3(s.w.x, s.w.y, s.w.z);
+    return v;
 }
-UGK_FN ugk::EHull* ugk_hull(ugk::EpaMem* E, int i) {
-    if (i < UG_EPA_LDS_HULL)
-        return (ugk::EHull*)(void*)((char*)(void*)&ugd::g_sh.rs[0] + UG_EPA_HULL_OFF) +
-               (int)(threadIdx.x / ugd::GJK_G) * UG_EPA_LDS_HULL + i;
-    return &E->hl[i];
+UGK_FN void ugk_svl_put(UGK_GMEM ugk::EpaMem*, int i, const ugk::ESv& v) {
+    UG_LDS ugk::ESv& s = lds_sv()[i];
+    s.d.x = v.d.x; s.d.y = v.d.y; s.d.z = v.d.z;
+    s.w.x = v.w.x; s.w.y = v.w.y; s.w.z = v.w.z;
+}
+UGK_FN UGK_LMEM unsigned char* ugk_hpos(UGK_GMEM ugk::EpaMem*) {
+    return (UGK_LMEM unsigned char*)(UGK_LMEM void*)&ugd::g_sh.LDL[0] + gjk_grp() * ugk::kEpaMaxFaces;
+}
+UGK_FN ugk::EFace ugk_face_get(UGK_GMEM ugk::EpaMem* E, int f) {
+    const UGK_GMEM ugk::EFace& G = E->fc[f];
+    ugk::EFace F;
+    F.n = ugk::V3(G.n.x, G.n.y, G.n.z);
+    F.d = G.d;
+    for (int j = 0; j < 3; j++) { F.c[j] = G.c[j]; F.f[j] = G.f[j]; }
+    F.e3 = G.e3;
+    F.pass = G.pass;
+    return F;
+}
+UGK_FN void ugk_face_put(UGK_GMEM ugk::EpaMem* E, int f, const ugk::EFace& F) {
+    UGK_GMEM ugk::EFace& G = E->fc[f];
+    G.n.x = F.n.x; G.n.y = F.n.y; G.n.z = F.n.z;
+    G.d = F.d;
+    for (int j = 0; j < 3; j++) { G.c[j] = F.c[j]; G.f[j] = F.f[j]; }
+    G.e3 = F.e3;
+    G.pass = F.pass;
+}
+UGK_FN void ugk_face_pass(UGK_GMEM ugk::EpaMem* E, int f, int pass) { E->fc[f].pass = (unsigned char)pass; }
+UGK_FN void ugk_face_link(UGK_GMEM ugk::EpaMem* E, int f, int j, int nf, int ne) {
+    E->fc[f].f[j] = (unsigned char)nf;
+    E->fc[f].e3 = (unsigned char)((E->fc[f].e3 & ~(3 << (2 * j))) | (ne << (2 * j)));
+}
+UGK_FN ugk::EHull ugk_hull_get(UGK_GMEM ugk::EpaMem* E, int i) {
+    ugk::EHull h;
+    h.d = E->hl[i].d; h.stamp = E->hl[i].stamp; h.f = E->hl[i].f;
+    return h;
+}
+UGK_FN void ugk_hull_put(UGK_GMEM ugk::EpaMem* E, int i, const ugk::EHull& h) {
+    E->hl[i].d = h.d; E->hl[i].stamp = h.stamp; E->hl[i].f = h.f;
 }
 
 /* ug_gjk.h's lane-group hooks: the lane's index in its group, a value as another lane of the group holds it */
@@ -431,28 +452,28 @@ UGK_FN int ugk_gsize() { return ugd::GJK_G; }
 
 /* ug_gjk.h's small stacks on the lane group: slots [0, GJK_G) in one register, lane i of the group holding slot i
  * (read back through ds_bpermute, an LDS-crossbar hop instead of a workspace round trip), deeper slots in memory */
-UGK_FN void ugk_ls_put(int* mem, ugk::LStack& s, int i, int v) {
+UGK_FN void ugk_ls_put(UGK_GMEM int* mem, ugk::LStack& s, int i, int v) {
     if (i < ugd::GJK_G) {
         if ((int)(threadIdx.x & (ugd::GJK_G - 1)) == i) s.reg = v;
     } else {
         mem[i] = v;
     }
 }
-UGK_FN int ugk_ls_get(const int* mem, const ugk::LStack& s, int i) {
+UGK_FN int ugk_ls_get(const UGK_GMEM int* mem, const ugk::LStack& s, int i) {
     if (i < ugd::GJK_G) return __shfl(s.reg, (int)(threadIdx.x & ~(ugd::GJK_G - 1)) + i, TEAM);
     return mem[i];
 }
 /* ug_gjk.h's EPA hook on the lane group: m_hull's first minimum (smallest d * d, ties to the largest append stamp; a
  * NaN at the root -- the largest stamp -- keeps the root) as a lane-strided scan of the hull array + a DPP arg-min of
  * the key (d * d, (2^20 - stamp) * 256 + face); the root is looked up only when some face of the hull has a NaN plane */
-UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E, int hcount) {
+UGK_FN int ugk_epa_findbest(const UGK_GMEM ugk::EpaMem* E, int hcount) {
     constexpr int G = ugd::GJK_G;
     const int gl = threadIdx.x & (G - 1);
     double bv = 0.0, rs = -1.0;
     int bi = 0x7fffffff, ri = 0x7fffffff;
     bool nan = false;
     for (int i = gl; i < hcount; i += G) {
-        const ugk::EHull h = *ugk_hull(const_cast<ugk::EpaMem*>(E), i);
+        const ugk::EHull h = ugk_hull_get(const_cast<UGK_GMEM ugk::EpaMem*>(E), i);
         const double sqd = h.d * h.d;
         if (ri == 0x7fffffff || (double)h.stamp > rs) { rs = (double)h.stamp; ri = i; }
         if (sqd != sqd) { nan = true; continue; }
@@ -461,7 +482,7 @@ UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E, int hcount) {
     }
     if ((ugd::ballot(nan) >> (threadIdx.x & ~(G - 1))) & ((1ull << G) - 1ull)) {
         ugd::group_best(rs, ri, true); /* the root: the largest stamp */
-        const ugk::EHull h = *ugk_hull(const_cast<ugk::EpaMem*>(E), ri);
+        const ugk::EHull h = ugk_hull_get(const_cast<UGK_GMEM ugk::EpaMem*>(E), ri);
         if ((h.d * h.d) != (h.d * h.d)) return h.f;
     }
     ugd::group_best(bv, bi, false);
@@ -1638,7 +1659,7 @@ __device__ __forceinline__ static ugk::gx to_gx(const XF& T) {
  * separating axis n (the reported normal, or the classic GJK's last axis) with both cores' extents along it, and the
  * relative pose; while the motion bound in team_collide proves that the margin-expanded shapes stay farther apart than
  * the contact threshold, the query would again add nothing, and the pair is skipped. */
-__device__ __forceinline__ static void gjk_one(const Scene* s, int k, ugk::EpaMem* E, gdouble* gc) {
+__device__ __forceinline__ static void gjk_one(const Scene* s, int k, UGK_GMEM ugk::EpaMem* E, gdouble* gc) {
     Shared& sh = g_sh;
     const int a = sh.pinfo[k].a, b = sh.pinfo[k].b;
     const Collider& A = s->col[a];
@@ -1698,7 +1719,7 @@ __device__ __noinline__ static void team_gjk(const Scene* s, unsigned long long 
             unsigned long long m = hq;
             for (int j = 0; j < r0 + g; j++) m &= m - 1ull;
             const int k = __builtin_ctzll(m);
-            gjk_one(s, k, (ugk::EpaMem*)(ws + WS_EPA) + g, (gdouble*)(ws + WS_GC) + GC_DOUBLES * sh.ov[c0 + k]);
+            gjk_one(s, k, (UGK_GMEM ugk::EpaMem*)(ws + WS_EPA) + g, (gdouble*)(ws + WS_GC) + GC_DOUBLES * sh.ov[c0 + k]);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
