@@ -26,17 +26,15 @@ UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
     return ugk::V3(p[0], p[1], p[2]);
 }
 
-/* the small store's capacity as the kernels' (22 faces), so the restart on the full store runs here too */
-UGK_FN int ugk_face_cap(bool L) { return L ? 22 : ugk::kEpaMaxFaces; }
-UGK_FN ugk::EFace ugk_face_get(ugk::EpaMem* E, int f, bool) { return E->fc[f]; }
-UGK_FN void ugk_face_put(ugk::EpaMem* E, int f, const ugk::EFace& F, bool) { E->fc[f] = F; }
-UGK_FN void ugk_face_pass(ugk::EpaMem* E, int f, int pass, bool) { E->fc[f].pass = (unsigned char)pass; }
-UGK_FN void ugk_face_link(ugk::EpaMem* E, int f, int j, int nf, int ne, bool) {
+UGK_FN ugk::EFace ugk_face_get(ugk::EpaMem* E, int f) { return E->fc[f]; }
+UGK_FN void ugk_face_put(ugk::EpaMem* E, int f, const ugk::EFace& F) { E->fc[f] = F; }
+UGK_FN void ugk_face_pass(ugk::EpaMem* E, int f, int pass) { E->fc[f].pass = (unsigned char)pass; }
+UGK_FN void ugk_face_link(ugk::EpaMem* E, int f, int j, int nf, int ne) {
     E->fc[f].f[j] = (unsigned char)nf;
     ugk::set_fe(E->fc[f], j, ne);
 }
-UGK_FN ugk::EHull ugk_hull_get(ugk::EpaMem* E, int i, bool) { return E->hl[i]; }
-UGK_FN void ugk_hull_put(ugk::EpaMem* E, int i, const ugk::EHull& h, bool) { E->hl[i] = h; }
+UGK_FN ugk::EHull ugk_hull_get(ugk::EpaMem* E, int i) { return E->hl[i]; }
+UGK_FN void ugk_hull_put(ugk::EpaMem* E, int i, const ugk::EHull& h) { E->hl[i] = h; }
 UGK_FN unsigned char* ugk_hpos(ugk::EpaMem* E) { return E->hpos; }
 UGK_FN ugk::ESv ugk_svl_get(ugk::EpaMem* E, int i) { return E->sv[i]; }
 UGK_FN void ugk_svl_put(ugk::EpaMem* E, int i, const ugk::ESv& v) { E->sv[i] = v; }
@@ -44,7 +42,7 @@ UGK_FN void ugk_ls_put(int* mem, ugk::LStack&, int i, int v) { mem[i] = v; }
 UGK_FN int ugk_ls_get(const int* mem, const ugk::LStack&, int i) { return mem[i]; }
 /* m_hull's first minimum of d * d over the hull array: the largest stamp among the minima; a NaN at the root (the
  * largest stamp) wins */
-UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E, int hcount, bool) {
+UGK_FN int ugk_epa_findbest(const ugk::EpaMem* E, int hcount) {
     const ugk::EHull* h = E->hl; /* the host keeps every hull slot in E */
     int root = 0;
     for (int i = 1; i < hcount; i++)

@@ -452,15 +452,12 @@ struct EpaMem {
 } /* namespace ugk */
 /* the includer's EPA record hooks: face f's record and hull slot i (the kernels keep the first few of each in LDS,
  * the rest in E) */
-/* faces and hull slots: L selects the small store (the kernels: LDS, ugk_face_cap(true) faces; an EPA that needs more
- * restarts on the full one, L = false, in E) -- a compile-time choice in every caller, so no access is generic */
-UGK_FN int ugk_face_cap(bool L);
-UGK_FN ugk::EFace ugk_face_get(UGK_GMEM ugk::EpaMem* E, int f, bool L);
-UGK_FN void ugk_face_put(UGK_GMEM ugk::EpaMem* E, int f, const ugk::EFace& F, bool L);
-UGK_FN void ugk_face_pass(UGK_GMEM ugk::EpaMem* E, int f, int pass, bool L);
-UGK_FN void ugk_face_link(UGK_GMEM ugk::EpaMem* E, int f, int j, int nf, int ne, bool L); /* neighbour j of f := (nf, ne) */
-UGK_FN ugk::EHull ugk_hull_get(UGK_GMEM ugk::EpaMem* E, int i, bool L);
-UGK_FN void ugk_hull_put(UGK_GMEM ugk::EpaMem* E, int i, const ugk::EHull& h, bool L);
+UGK_FN ugk::EFace ugk_face_get(UGK_GMEM ugk::EpaMem* E, int f);
+UGK_FN void ugk_face_put(UGK_GMEM ugk::EpaMem* E, int f, const ugk::EFace& F);
+UGK_FN void ugk_face_pass(UGK_GMEM ugk::EpaMem* E, int f, int pass);
+UGK_FN void ugk_face_link(UGK_GMEM ugk::EpaMem* E, int f, int j, int nf, int ne); /* neighbour j of face f := (nf, edge ne) */
+UGK_FN ugk::EHull ugk_hull_get(UGK_GMEM ugk::EpaMem* E, int i);
+UGK_FN void ugk_hull_put(UGK_GMEM ugk::EpaMem* E, int i, const ugk::EHull& h);
 UGK_FN UGK_LMEM unsigned char* ugk_hpos(UGK_GMEM ugk::EpaMem* E); /* the hull-slot table, kEpaMaxFaces entries */
 /* support vertices: the btGjkEpa2 GJK's store 0..3 (svl: the kernels keep it in LDS) and the EPA's (svg, in E: the
  * EPA copies the GJK's final simplex to 132..135 first, so it never reads the store) */
@@ -491,7 +488,7 @@ struct Gjk2 { /* btGjkEpa2's GJK: the scalar fields (the stores are in EpaMem) *
 };
 enum { GJK_VALID = 0, GJK_INSIDE, GJK_FAILED };
 enum { EPA_VALID = 0, EPA_TOUCHING, EPA_DEGENERATED, EPA_NONCONVEX, EPA_INVALIDHULL, EPA_OUTOFFACES, EPA_OUTOFVERTICES,
-       EPA_ACCURACYREACHED, EPA_FALLBACK, EPA_FAILED, EPA_RETRY /* the small store ran out: restart on the full one */ };
+       EPA_ACCURACYREACHED, EPA_FALLBACK, EPA_FAILED };
 
 UGK_FN ESv g2_support(const Mink& M, gv d) {
     const gv dd = mulinv(d, len(d));
@@ -741,32 +738,29 @@ struct Epa { int status, nextsv, hcount, nstock, nfresh, stampctr; LStack stock;
 /* the includer's EPA hook: of the hull faces hl[0, hcount), the one with the smallest d * d, ties to the largest stamp
  * (m_hull's first minimum), except that a NaN at the list root (the largest stamp) keeps the root (Bullet's loop never
  * replaces a NaN) */
-UGK_FN int ugk_epa_findbest(const UGK_GMEM ugk::EpaMem* E, int hcount, bool L);
+UGK_FN int ugk_epa_findbest(const UGK_GMEM ugk::EpaMem* E, int hcount);
 /* the includer's LStack hooks: slot i of the stack whose memory is mem (the kernels hold slots [0, 16) in the lane
  * group's registers, lane i slot i) */
 UGK_FN void ugk_ls_put(UGK_GMEM int* mem, ugk::LStack& s, int i, int v);
 UGK_FN int ugk_ls_get(const UGK_GMEM int* mem, const ugk::LStack& s, int i);
 namespace ugk {
 
-template <bool L>
 UGK_FN void e_bind(UGK_GMEM EpaMem* E, int fa, int ea, int fb, int eb) {
-    ugk_face_link(E, fa, ea, fb, eb, L);
-    ugk_face_link(E, fb, eb, fa, ea, L);
+    ugk_face_link(E, fa, ea, fb, eb);
+    ugk_face_link(E, fb, eb, fa, ea);
 }
-template <bool L>
 UGK_FN void h_append(UGK_GMEM EpaMem* E, Epa& P, int f, double d, int stamp) {
     EHull h;
     h.d = d; h.stamp = stamp; h.f = f;
-    ugk_hull_put(E, P.hcount, h, L);
+    ugk_hull_put(E, P.hcount, h);
     ugk_hpos(E)[f] = (unsigned char)P.hcount++;
 }
-template <bool L>
 UGK_FN void h_remove(UGK_GMEM EpaMem* E, Epa& P, int f) {
     UGK_LMEM unsigned char* hp = ugk_hpos(E);
     const int i = hp[f], last = --P.hcount;
     if (i != last) {
-        const EHull t = ugk_hull_get(E, last, L);
-        ugk_hull_put(E, i, t, L);
+        const EHull t = ugk_hull_get(E, last);
+        ugk_hull_put(E, i, t);
         hp[t.f] = (unsigned char)i;
     }
 }
@@ -804,9 +798,8 @@ UGK_FN bool e_plane(gv aw, gv bw, gv cw, gv& nOut, double& dOut) {
     nOut = n;
     return false;
 }
-template <bool L>
 UGK_FN int e_newface(UGK_GMEM EpaMem* E, Epa& P, int a, int b, int c, bool forced) {
-    if (P.nstock > 0 || P.nfresh < ugk_face_cap(L)) {
+    if (P.nstock > 0 || P.nfresh < kEpaMaxFaces) {
         const int f = P.nstock > 0 ? ugk_ls_get(E->stock, P.stock, P.nstock - 1) : P.nfresh;
         if (P.nstock > 0) P.nstock--;
         else P.nfresh++;
@@ -823,10 +816,10 @@ UGK_FN int e_newface(UGK_GMEM EpaMem* E, Epa& P, int a, int b, int c, bool force
         const bool nondeg = e_plane(aw, bw, cw, n, d);
         F.n = n;
         if (nondeg) F.d = d;
-        ugk_face_put(E, f, F, L);
+        ugk_face_put(E, f, F);
         if (nondeg) {
             if (forced || d >= -kEpaPlaneEps) {
-                h_append<L>(E, P, f, d, stamp);
+                h_append(E, P, f, d, stamp);
                 return f;
             }
             P.status = EPA_NONCONVEX;
@@ -836,7 +829,7 @@ UGK_FN int e_newface(UGK_GMEM EpaMem* E, Epa& P, int a, int b, int c, bool force
         s_push(E, P, f); /* m_hull.remove + m_stock.append: back on top of the stock */
         return -1;
     }
-    P.status = L ? EPA_RETRY : EPA_OUTOFFACES;
+    P.status = EPA_OUTOFFACES;
     return -1;
 }
 /* EPA::expand as an explicit depth-first walk.  The current frame (face, edge, stage; stage 0 = entry, 1 = the first
@@ -844,7 +837,6 @@ UGK_FN int e_newface(UGK_GMEM EpaMem* E, Epa& P, int a, int b, int c, bool force
  * stage << 10 | second neighbour << 12 | its edge << 20 (read at entry: a visited face's other edges are not rebound
  * while its subtree runs, the pass mark stops every re-entry).  The same visits, face allocations and list operations
  * as the recursion. */
-template <bool L>
 UGK_FN bool e_expand(UGK_GMEM EpaMem* E, Epa& P, int pass, int w, gv ww, int f0, int e0, int& hcf, int& hff, int& hnf) {
     int sp = 0, f = f0, e = e0, stage = 0, f2 = 0, e2 = 0;
     bool r = false;
@@ -853,23 +845,23 @@ UGK_FN bool e_expand(UGK_GMEM EpaMem* E, Epa& P, int pass, int w, gv ww, int f0,
     for (;;) {
         bool pop = true;
         if (stage == 0) {
-            const EFace F = ugk_face_get(E, f, L); /* the face's record in one batch of loads */
+            const EFace F = ugk_face_get(E, f); /* the face's record in one batch of loads */
             const int e1 = e == 2 ? 0 : e + 1, em = e == 0 ? 2 : e - 1;
             if (F.pass == pass) {
                 r = false;
             } else if ((dot(F.n, ww) - F.d) < -kEpaPlaneEps) {
-                const int nf = e_newface<L>(E, P, F.c[e1], F.c[e], w, false);
+                const int nf = e_newface(E, P, F.c[e1], F.c[e], w, false);
                 r = false;
                 if (nf >= 0) {
-                    e_bind<L>(E, nf, 0, f, e);
-                    if (hcf >= 0) e_bind<L>(E, hcf, 1, nf, 2);
+                    e_bind(E, nf, 0, f, e);
+                    if (hcf >= 0) e_bind(E, hcf, 1, nf, 2);
                     else hff = nf;
                     hcf = nf;
                     hnf++;
                     r = true;
                 }
             } else {
-                ugk_face_pass(E, f, pass, L);
+                ugk_face_pass(E, f, pass);
                 ugk_ls_put(E->stk, fs, sp++, f | (e << 8) | (1 << 10) | (F.f[em] << 12) | (fe(F, em) << 20));
                 f = F.f[e1];
                 e = fe(F, e1);
@@ -884,7 +876,7 @@ UGK_FN bool e_expand(UGK_GMEM EpaMem* E, Epa& P, int pass, int w, gv ww, int f0,
                 pop = false;
             }
         } else if (r) {
-            h_remove<L>(E, P, f);
+            h_remove(E, P, f);
             s_push(E, P, f);
         }
         if (pop) {
@@ -908,7 +900,6 @@ UGK_FN bool e_expand(UGK_GMEM EpaMem* E, Epa& P, int pass, int w, gv ww, int f0,
  * none is degenerate or non-convex (and the faces suffice) the log is replayed in order -- stock pops and pushes,
  * stamps, records, hull appends / removals, bindings -- which is exactly what the serial walk does.  Otherwise the
  * walk's marks are cleared and the serial expand() runs. */
-template <bool L>
 UGK_FN bool e_walk(UGK_GMEM EpaMem* E, int pass, gv ww, int f0, int e0, LStack& ev, int& nev, int& nnew, LStack& mk, int& nmk) {
     int sp = 0, f = f0, e = e0, stage = 0, f2 = 0, e2 = 0;
     bool r = false;
@@ -917,7 +908,7 @@ UGK_FN bool e_walk(UGK_GMEM EpaMem* E, int pass, gv ww, int f0, int e0, LStack& 
     for (;;) {
         bool pop = true;
         if (stage == 0) {
-            const EFace F = ugk_face_get(E, f, L);
+            const EFace F = ugk_face_get(E, f);
             const int e1 = e == 2 ? 0 : e + 1, em = e == 0 ? 2 : e - 1;
             if (F.pass == pass) {
                 r = false;
@@ -926,7 +917,7 @@ UGK_FN bool e_walk(UGK_GMEM EpaMem* E, int pass, gv ww, int f0, int e0, LStack& 
                 nnew++;
                 r = true;
             } else {
-                ugk_face_pass(E, f, pass, L);
+                ugk_face_pass(E, f, pass);
                 ugk_ls_put(E->mkm, mk, nmk++, f);
                 ugk_ls_put(E->stk, fs, sp++, f | (e << 8) | (1 << 10) | (F.f[em] << 12) | (fe(F, em) << 20));
                 f = F.f[e1];
@@ -956,14 +947,13 @@ UGK_FN bool e_walk(UGK_GMEM EpaMem* E, int pass, gv ww, int f0, int e0, LStack& 
     }
     return r;
 }
-template <bool L>
 UGK_FN bool e_expand_group(UGK_GMEM EpaMem* E, Epa& P, int pass, int w, gv ww, const EFace& B, int& hcf, int& hff, int& hnf) {
     LStack ev, mk;
     ev.reg = 0;
     mk.reg = 0;
     int nev = 0, nnew = 0, nmk = 0;
     bool valid = true;
-    for (int j = 0; j < 3 && valid; j++) valid = e_walk<L>(E, pass, ww, B.f[j], fe(B, j), ev, nev, nnew, mk, nmk) && valid;
+    for (int j = 0; j < 3 && valid; j++) valid = e_walk(E, pass, ww, B.f[j], fe(B, j), ev, nev, nnew, mk, nmk) && valid;
     /* lane k: event k's plane (its own register slot holds the event) */
     const int k = ugk_glane();
     const int my = ev.reg;
@@ -975,21 +965,21 @@ UGK_FN bool e_expand_group(UGK_GMEM EpaMem* E, Epa& P, int pass, int w, gv ww, c
         const bool nondeg = e_plane(ldw(E->sv[a]), ldw(E->sv[b]), ww, pn, pd);
         fail = !nondeg || !(pd >= -kEpaPlaneEps);
     }
-    const bool serial = ugk_gany(fail) || nev > ugk_gsize() || nnew > P.nstock + (ugk_face_cap(L) - P.nfresh);
+    const bool serial = ugk_gany(fail) || nev > ugk_gsize() || nnew > P.nstock + (kEpaMaxFaces - P.nfresh);
     if (serial) {
-        for (int i = 0; i < nmk; i++) ugk_face_pass(E, ugk_ls_get(E->mkm, mk, i), 0, L);
+        for (int i = 0; i < nmk; i++) ugk_face_pass(E, ugk_ls_get(E->mkm, mk, i), 0);
         hcf = -1;
         hff = -1;
         hnf = 0;
         valid = true;
-        for (int j = 0; j < 3 && valid; j++) valid = e_expand<L>(E, P, pass, w, ww, B.f[j], fe(B, j), hcf, hff, hnf) && valid;
+        for (int j = 0; j < 3 && valid; j++) valid = e_expand(E, P, pass, w, ww, B.f[j], fe(B, j), hcf, hff, hnf) && valid;
         return valid;
     }
     for (int i = 0; i < nev; i++) {
         const int x = ugk_greadi(my, i);
         const int f = x & 255;
         if ((x >> 28) & 1) {
-            h_remove<L>(E, P, f);
+            h_remove(E, P, f);
             s_push(E, P, f);
             continue;
         }
@@ -1006,10 +996,10 @@ UGK_FN bool e_expand_group(UGK_GMEM EpaMem* E, Epa& P, int pass, int w, gv ww, c
         const double d = ugk_gread(pd, i);
         F.n = V3(ugk_gread(pn.x, i), ugk_gread(pn.y, i), ugk_gread(pn.z, i));
         F.d = d;
-        ugk_face_put(E, nf, F, L);
-        h_append<L>(E, P, nf, d, stamp);
-        e_bind<L>(E, nf, 0, f, e);
-        if (hcf >= 0) e_bind<L>(E, hcf, 1, nf, 2);
+        ugk_face_put(E, nf, F);
+        h_append(E, P, nf, d, stamp);
+        e_bind(E, nf, 0, f, e);
+        if (hcf >= 0) e_bind(E, hcf, 1, nf, 2);
         else hff = nf;
         hcf = nf;
         hnf++;
@@ -1018,7 +1008,6 @@ UGK_FN bool e_expand_group(UGK_GMEM EpaMem* E, Epa& P, int pass, int w, gv ww, c
 }
 #endif
 /* EPA::Evaluate */
-template <bool L>
 UGK_FN int e_evaluate(UGK_GMEM EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv guess) {
     const int s = g.simplex;
     UGK_T0(t_setup);
@@ -1037,21 +1026,21 @@ UGK_FN int e_evaluate(UGK_GMEM EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv gue
         /* the simplex's vertices as EPA vertices 132..135 (the same values; the EPA only ever reads E->sv) */
         for (int k = 0; k < 4; k++) stsv(E->sv[kTetra + k], ugk_svl_get(E, c[k]));
         int tetra[4];
-        tetra[0] = e_newface<L>(E, P, kTetra + 0, kTetra + 1, kTetra + 2, true);
-        tetra[1] = e_newface<L>(E, P, kTetra + 1, kTetra + 0, kTetra + 3, true);
-        tetra[2] = e_newface<L>(E, P, kTetra + 2, kTetra + 1, kTetra + 3, true);
-        tetra[3] = e_newface<L>(E, P, kTetra + 0, kTetra + 2, kTetra + 3, true);
+        tetra[0] = e_newface(E, P, kTetra + 0, kTetra + 1, kTetra + 2, true);
+        tetra[1] = e_newface(E, P, kTetra + 1, kTetra + 0, kTetra + 3, true);
+        tetra[2] = e_newface(E, P, kTetra + 2, kTetra + 1, kTetra + 3, true);
+        tetra[3] = e_newface(E, P, kTetra + 0, kTetra + 2, kTetra + 3, true);
         if (P.hcount == 4) {
-            int best = ugk_epa_findbest(E, P.hcount, L);
+            int best = ugk_epa_findbest(E, P.hcount);
             UGK_ADD(PF_EPA_SETUP, t_setup);
-            EFace outer = ugk_face_get(E, best, L);
+            EFace outer = ugk_face_get(E, best);
             int pass = 0;
-            e_bind<L>(E, tetra[0], 0, tetra[1], 0);
-            e_bind<L>(E, tetra[0], 1, tetra[2], 0);
-            e_bind<L>(E, tetra[0], 2, tetra[3], 0);
-            e_bind<L>(E, tetra[1], 1, tetra[3], 2);
-            e_bind<L>(E, tetra[1], 2, tetra[2], 1);
-            e_bind<L>(E, tetra[2], 2, tetra[3], 1);
+            e_bind(E, tetra[0], 0, tetra[1], 0);
+            e_bind(E, tetra[0], 1, tetra[2], 0);
+            e_bind(E, tetra[0], 2, tetra[3], 0);
+            e_bind(E, tetra[1], 1, tetra[3], 2);
+            e_bind(E, tetra[1], 2, tetra[2], 1);
+            e_bind(E, tetra[2], 2, tetra[3], 1);
             P.status = EPA_VALID;
             for (int it = 0; it < kEpaMaxIterations; it++) {
                 UGK_COUNT(PC_EPA_IT, 1);
@@ -1059,31 +1048,30 @@ UGK_FN int e_evaluate(UGK_GMEM EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv gue
                 int hcf = -1, hff = -1, hnf = 0;
                 const int w = 4 + P.nextsv++;
                 bool valid = true;
-                ugk_face_pass(E, best, ++pass, L);
+                ugk_face_pass(E, best, ++pass);
                 UGK_T0(t_sup);
-                stsv(E->sv[w], g2_support(M, ugk_face_get(E, best, L).n));
+                stsv(E->sv[w], g2_support(M, ugk_face_get(E, best).n));
                 UGK_ADD(PF_EPA_SUP, t_sup);
                 const gv ww = ldw(E->sv[w]);
-                const EFace B = ugk_face_get(E, best, L);
+                const EFace B = ugk_face_get(E, best);
                 const double wdist = dot(B.n, ww) - B.d;
                 if (!(wdist > kEpaAccuracy)) { P.status = EPA_ACCURACYREACHED; break; }
                 UGK_T0(t_exp);
 #ifdef UGK_GROUP_PARALLEL
-                valid = e_expand_group<L>(E, P, pass, w, ww, B, hcf, hff, hnf);
+                valid = e_expand_group(E, P, pass, w, ww, B, hcf, hff, hnf);
 #else
                 for (int j = 0; j < 3 && valid; j++)
-                    valid = e_expand<L>(E, P, pass, w, ww, B.f[j], fe(B, j), hcf, hff, hnf) && valid;
+                    valid = e_expand(E, P, pass, w, ww, B.f[j], fe(B, j), hcf, hff, hnf) && valid;
 #endif
                 UGK_ADD(PF_EPA_EXPAND, t_exp);
-                if (L && P.status == EPA_RETRY) return EPA_RETRY;
                 if (!(valid && hnf >= 3)) { P.status = EPA_INVALIDHULL; break; }
-                e_bind<L>(E, hcf, 1, hff, 2);
-                h_remove<L>(E, P, best);
+                e_bind(E, hcf, 1, hff, 2);
+                h_remove(E, P, best);
                 s_push(E, P, best);
                 UGK_T0(t_best);
-                best = ugk_epa_findbest(E, P.hcount, L);
+                best = ugk_epa_findbest(E, P.hcount);
                 UGK_ADD(PF_EPA_BEST, t_best);
-                outer = ugk_face_get(E, best, L);
+                outer = ugk_face_get(E, best);
             }
             const gv projection = scl(outer.n, outer.d);
             P.normal = outer.n;
@@ -1134,12 +1122,7 @@ UGK_FN bool g2_penetration(UGK_GMEM EpaMem* E, const GShape& s0, const gx& w0, c
     if (gs == GJK_INSIDE) {
         Epa P;
         e_init(E, P);
-        int est = e_evaluate<true>(E, P, g, M, neg(guess));
-        if (est == EPA_RETRY) { /* more faces than the small store holds: the same EPA on the full one */
-            e_init(E, P);
-            est = e_evaluate<false>(E, P, g, M, neg(guess));
-        }
-        if (est != EPA_FAILED) {
+        if (e_evaluate(E, P, g, M, neg(guess)) != EPA_FAILED) {
             gv a = V3(0, 0, 0);
             /* the witness: EPA vertices, or the GJK store's for the fallback */
             for (int i = 0; i < P.rrank; i++)

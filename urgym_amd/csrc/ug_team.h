@@ -409,73 +409,36 @@ UGK_FN void ugk_svl_put(UGK_GMEM ugk::EpaMem*, int i, const ugk::ESv& v) {
 UGK_FN UGK_LMEM unsigned char* ugk_hpos(UGK_GMEM ugk::EpaMem*) {
     return (UGK_LMEM unsigned char*)(UGK_LMEM void*)&ugd::g_sh.LDL[0] + gjk_grp() * ugk::kEpaMaxFaces;
 }
-/* the small face store: each group's 22 faces in the hull-candidate / box-clip union (written only after team_gjk), its
- * 42 hull slots in the rows union past the pair records (the working manifolds overwrite it only after team_gjk) */
-#define UG_EPA_LDS_FACES 22
-#define UG_EPA_LDS_HULL 42
-#define UG_EPA_HULL_OFF (((sizeof(ugd::PairInfo) * MAXOV) + 15) & ~(size_t)15)
-static_assert(ugd::GJK_NG * UG_EPA_LDS_FACES * sizeof(ugk::EFace) <= sizeof(ugd::Cand) * 64, "EPA face store in hc");
-static_assert(UG_EPA_HULL_OFF + ugd::GJK_NG * UG_EPA_LDS_HULL * sizeof(ugk::EHull) <= sizeof(ugd::RowS) * MAXROWS,
-              "EPA hull store in the rows union");
-static_assert(UG_EPA_LDS_HULL >= UG_EPA_LDS_FACES, "every face of the small store fits its hull slots");
-__device__ __forceinline__ UG_LDS ugk::EFace* lds_faces() {
-    return (UG_LDS ugk::EFace*)(UG_LDS void*)&ugd::g_sh.hc[0] + gjk_grp() * UG_EPA_LDS_FACES;
-}
-__device__ __forceinline__ UG_LDS ugk::EHull* lds_hull() {
-    return (UG_LDS ugk::EHull*)(UG_LDS void*)((UG_LDS char*)(UG_LDS void*)&ugd::g_sh.rs[0] + UG_EPA_HULL_OFF) +
-           gjk_grp() * UG_EPA_LDS_HULL;
-}
-UGK_FN int ugk_face_cap(bool L) { return L ? UG_EPA_LDS_FACES : ugk::kEpaMaxFaces; }
-template <class FP>
-__device__ __forceinline__ ugk::EFace face_ld(FP G) {
+UGK_FN ugk::EFace ugk_face_get(UGK_GMEM ugk::EpaMem* E, int f) {
+    const UGK_GMEM ugk::EFace& G = E->fc[f];
     ugk::EFace F;
-    F.n = ugk::V3(G->n.x, G->n.y, G->n.z);
-    F.d = G->d;
-    for (int j = 0; j < 3; j++) { F.c[j] = G->c[j]; F.f[j] = G->f[j]; }
-    F.e3 = G->e3;
-    F.pass = G->pass;
+    F.n = ugk::V3(G.n.x, G.n.y, G.n.z);
+    F.d = G.d;
+    for (int j = 0; j < 3; j++) { F.c[j] = G.c[j]; F.f[j] = G.f[j]; }
+    F.e3 = G.e3;
+    F.pass = G.pass;
     return F;
 }
-template <class FP>
-__device__ __forceinline__ void face_st(FP G, const ugk::EFace& F) {
-    G->n.x = F.n.x; G->n.y = F.n.y; G->n.z = F.n.z;
-    G->d = F.d;
-    for (int j = 0; j < 3; j++) { G->c[j] = F.c[j]; G->f[j] = F.f[j]; }
-    G->e3 = F.e3;
-    G->pass = F.pass;
+UGK_FN void ugk_face_put(UGK_GMEM ugk::EpaMem* E, int f, const ugk::EFace& F) {
+    UGK_GMEM ugk::EFace& G = E->fc[f];
+    G.n.x = F.n.x; G.n.y = F.n.y; G.n.z = F.n.z;
+    G.d = F.d;
+    for (int j = 0; j < 3; j++) { G.c[j] = F.c[j]; G.f[j] = F.f[j]; }
+    G.e3 = F.e3;
+    G.pass = F.pass;
 }
-UGK_FN ugk::EFace ugk_face_get(UGK_GMEM ugk::EpaMem* E, int f, bool L) {
-    return L ? face_ld(lds_faces() + f) : face_ld(&E->fc[f]);
+UGK_FN void ugk_face_pass(UGK_GMEM ugk::EpaMem* E, int f, int pass) { E->fc[f].pass = (unsigned char)pass; }
+UGK_FN void ugk_face_link(UGK_GMEM ugk::EpaMem* E, int f, int j, int nf, int ne) {
+    E->fc[f].f[j] = (unsigned char)nf;
+    E->fc[f].e3 = (unsigned char)((E->fc[f].e3 & ~(3 << (2 * j))) | (ne << (2 * j)));
 }
-UGK_FN void ugk_face_put(UGK_GMEM ugk::EpaMem* E, int f, const ugk::EFace& F, bool L) {
-    if (L) face_st(lds_faces() + f, F);
-    else face_st(&E->fc[f], F);
-}
-UGK_FN void ugk_face_pass(UGK_GMEM ugk::EpaMem* E, int f, int pass, bool L) {
-    if (L) lds_faces()[f].pass = (unsigned char)pass;
-    else E->fc[f].pass = (unsigned char)pass;
-}
-template <class FP>
-__device__ __forceinline__ void face_link(FP G, int j, int nf, int ne) {
-    G->f[j] = (unsigned char)nf;
-    G->e3 = (unsigned char)((G->e3 & ~(3 << (2 * j))) | (ne << (2 * j)));
-}
-UGK_FN void ugk_face_link(UGK_GMEM ugk::EpaMem* E, int f, int j, int nf, int ne, bool L) {
-    if (L) face_link(lds_faces() + f, j, nf, ne);
-    else face_link(&E->fc[f], j, nf, ne);
-}
-template <class HP>
-__device__ __forceinline__ ugk::EHull hull_ld(HP p) {
+UGK_FN ugk::EHull ugk_hull_get(UGK_GMEM ugk::EpaMem* E, int i) {
     ugk::EHull h;
-    h.d = p->d; h.stamp = p->stamp; h.f = p->f;
+    h.d = E->hl[i].d; h.stamp = E->hl[i].stamp; h.f = E->hl[i].f;
     return h;
 }
-UGK_FN ugk::EHull ugk_hull_get(UGK_GMEM ugk::EpaMem* E, int i, bool L) {
-    return L ? hull_ld(lds_hull() + i) : hull_ld(&E->hl[i]);
-}
-UGK_FN void ugk_hull_put(UGK_GMEM ugk::EpaMem* E, int i, const ugk::EHull& h, bool L) {
-    if (L) { UG_LDS ugk::EHull* p = lds_hull() + i; p->d = h.d; p->stamp = h.stamp; p->f = h.f; }
-    else { UGK_GMEM ugk::EHull* p = &E->hl[i]; p->d = h.d; p->stamp = h.stamp; p->f = h.f; }
+UGK_FN void ugk_hull_put(UGK_GMEM ugk::EpaMem* E, int i, const ugk::EHull& h) {
+    E->hl[i].d = h.d; E->hl[i].stamp = h.stamp; E->hl[i].f = h.f;
 }
 
 /* ug_gjk.h's lane-group hooks: the lane's index in its group, a value as another lane of the group holds it */
@@ -503,14 +466,14 @@ UGK_FN int ugk_ls_get(const UGK_GMEM int* mem, const ugk::LStack& s, int i) {
 /* ug_gjk.h's EPA hook on the lane group: m_hull's first minimum (smallest d * d, ties to the largest append stamp; a
  * NaN at the root -- the largest stamp -- keeps the root) as a lane-strided scan of the hull array + a DPP arg-min of
  * the key (d * d, (2^20 - stamp) * 256 + face); the root is looked up only when some face of the hull has a NaN plane */
-UGK_FN int ugk_epa_findbest(const UGK_GMEM ugk::EpaMem* E, int hcount, bool L) {
+UGK_FN int ugk_epa_findbest(const UGK_GMEM ugk::EpaMem* E, int hcount) {
     constexpr int G = ugd::GJK_G;
     const int gl = threadIdx.x & (G - 1);
     double bv = 0.0, rs = -1.0;
     int bi = 0x7fffffff, ri = 0x7fffffff;
     bool nan = false;
     for (int i = gl; i < hcount; i += G) {
-        const ugk::EHull h = ugk_hull_get(const_cast<UGK_GMEM ugk::EpaMem*>(E), i, L);
+        const ugk::EHull h = ugk_hull_get(const_cast<UGK_GMEM ugk::EpaMem*>(E), i);
         const double sqd = h.d * h.d;
         if (ri == 0x7fffffff || (double)h.stamp > rs) { rs = (double)h.stamp; ri = i; }
         if (sqd != sqd) { nan = true; continue; }
@@ -519,7 +482,7 @@ UGK_FN int ugk_epa_findbest(const UGK_GMEM ugk::EpaMem* E, int hcount, bool L) {
     }
     if ((ugd::ballot(nan) >> (threadIdx.x & ~(G - 1))) & ((1ull << G) - 1ull)) {
         ugd::group_best(rs, ri, true); /* the root: the largest stamp */
-        const ugk::EHull h = ugk_hull_get(const_cast<UGK_GMEM ugk::EpaMem*>(E), ri, L);
+        const ugk::EHull h = ugk_hull_get(const_cast<UGK_GMEM ugk::EpaMem*>(E), ri);
         if ((h.d * h.d) != (h.d * h.d)) return h.f;
     }
     ugd::group_best(bv, bi, false);
