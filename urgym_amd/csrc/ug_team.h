@@ -1743,7 +1743,8 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
     /* live manifolds -> global workspace (read back per pair below; LDS list is rebuilt in place) */
     int nold = (int)e.nman;
     const double* src = (const double*)e.man;
-    for (int i = lane; i < nold * UG_MAN_DOUBLES; i += TEAM) ws[i] = src[i];
+    gdouble* const gws = (gdouble*)ws; /* global-typed: a generic store here would make later loads wait for it */
+    for (int i = lane; i < nold * UG_MAN_DOUBLES; i += TEAM) gws[i] = src[i];
     if (lane < nold) sh.oldp[lane] = (int)e.man[lane].pair;
     __threadfence_block();
     __syncthreads();
@@ -1910,14 +1911,14 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
                 if (sh.oldp[m] == p) { mo = m; break; }
             sh.pmo[lane] = mo;
             sh.pm[lane].pair = p;
-            sh.pm[lane].npts = mo >= 0 ? (int)ws[mo * UG_MAN_DOUBLES + 1] : 0;
+            sh.pm[lane].npts = mo >= 0 ? (int)gws[mo * UG_MAN_DOUBLES + 1] : 0;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         for (int i = lane; i < cn * 4 * UG_PT_DOUBLES; i += TEAM) {
             const int k = i / (4 * UG_PT_DOUBLES), f = i - k * (4 * UG_PT_DOUBLES);
             const int mo = sh.pmo[k];
-            if (mo >= 0) ((__attribute__((address_space(3))) double*)&sh.pm[k].pt[0].lpA.x)[f] = ws[mo * UG_MAN_DOUBLES + 2 + f];
+            if (mo >= 0) ((__attribute__((address_space(3))) double*)&sh.pm[k].pt[0].lpA.x)[f] = gws[mo * UG_MAN_DOUBLES + 2 + f];
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
