@@ -43,7 +43,7 @@ def main():
     from urgym_amd.envs import spaces_for
     _, asp = spaces_for(a.task)
     sim.set_autoreset(True, 500)
-    buf = np.zeros(100, np.uint64)
+    buf = np.zeros(101, np.uint64)
     sim.reset()
     sim.sync()
     rc = sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
@@ -90,7 +90,7 @@ def main():
                    "gjk_hull_support_cycles", "epa_iterations", "gjk_cycles_reporting_queries", "gjk_penetration_cycles",
                    "gjk_ccd_cycles", "gjk_classic_cycles", "epa_gjk_cycles", "epa_setup_cycles", "epa_support_cycles",
                    "epa_expand_cycles", "epa_findbest_cycles", "ccd_support_cycles", "ccd_simplex_cycles",
-                   "classic_support_cycles", "classic_simplex_cycles"], [float(x) for x in buf[80:100]]))
+                   "classic_support_cycles", "classic_simplex_cycles", "gjk_recertified"], [float(x) for x in buf[80:101]]))
     out["gjk_per_substep"] = {k: v / max(d["substeps"], 1) for k, v in gj.items()}
     out["gjk_cycles_per_hull_support"] = gj["gjk_hull_support_cycles"] / max(gj["gjk_hull_supports"], 1)
     print(json.dumps(out, indent=1))

@@ -35,7 +35,7 @@ namespace ugd {
 #define TEAM 64
 typedef __attribute__((address_space(1))) const double gcdouble;
 typedef __attribute__((address_space(1))) double gdouble;
-#define UG_NPROF 100 /* phase accumulators of the -DUG_PROF build */
+#define UG_NPROF 101 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* a row's J and M^-1 J^T over the NVP = 32 dof slots (robot 12, objects 3 x 6, 2 zero pads) */
@@ -83,9 +83,7 @@ static_assert(UG_FULL_HULL_MAXV + 64 + 8 <= FC_MAX, "a full hull pair's candidat
 /* the convex-convex path (UG_CONTACT_GJK): the penetration solver's store (ug_gjk.h EpaMem: btGjkEpa2's 132 support
  * vertices, 256 faces and their lists, the horizon walk's stack) after everything else */
 #define WS_EPA WS_DOUBLES
-#ifndef UG_GJK_G /* (-DUG_GJK_G=64: one pair per wave, the profiling build's serial view of the solver) */
 #define UG_GJK_G 16 /* lanes per GJK pair (ugd::GJK_G): the wave runs 64 / UG_GJK_G pairs at once, one store each */
-#endif
 #define EPA_DOUBLES ((sizeof(ugk::EpaMem) + sizeof(double) - 1) / sizeof(double))
 /* the convex-convex path's separation certificates, per pair: [0] valid, [1..3] the separating axis n in B's frame,
  * [4] A's core extent along -n at the evaluation, [5] B's core extent along n, [6..14] R_AB, [15..17] p_AB (A's pose in
@@ -211,7 +209,8 @@ enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_
         * horizon walk and findbest, the witnesses */
        PF_EPA_GJK, PF_EPA_SETUP, PF_EPA_SUP, PF_EPA_EXPAND, PF_EPA_BEST,
        /* inside the libccd test and the classic GJK: the support pairs, the simplex work */
-       PF_CCD_SUP, PF_CCD_DO, PF_CLS_SUP, PF_CLS_VS };
+       PF_CCD_SUP, PF_CCD_DO, PF_CLS_SUP, PF_CLS_VS,
+       PC_GJK_RECERT /* GJK pairs skipped by the exact certificate re-test (gjk_one) */ };
 #define UG_FREE_SPLIT_N 14
 #ifdef UG_PROF
 __device__ static const int kFreeSplit[UG_FREE_SPLIT_N] = {PF_FK, PF_BROAD, PF_HULL, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST,
@@ -310,7 +309,7 @@ __device__ __forceinline__ void wave_best(double& v, int& idx, bool want_max) {
  * iterations differ.  group_best is wave_best over the group's row. */
 constexpr int GJK_G = UG_GJK_G, GJK_NG = TEAM / GJK_G;
 static_assert(TEAM == 64, "WS_GC counts 64 lanes");
-static_assert(GJK_G == 16 || GJK_G == TEAM, "a GJK lane group is one DPP row or the wave");
+static_assert(GJK_G == 16, "a GJK lane group is one DPP row (the group masks and ds_bpermute reads assume it)");
 __device__ __forceinline__ void group_best(double& v, int& idx, bool want_max) {
     if (GJK_G == TEAM) {
         wave_best(v, idx, want_max);
@@ -1671,6 +1670,31 @@ __device__ __forceinline__ static void gjk_one(const Scene* s, int k, UGK_GMEM u
     ugk::gv n, p, ax = ugk::V3(0, 0, 0);
     double d = 0.0;
     const bool lead = (threadIdx.x & (GJK_G - 1)) == 0; /* the group's writer */
+    if (gc[0] > 0.0) {
+        /* the pair's certificate failed team_collide's motion bound: test it exactly instead -- A's core extent along
+         * the certified axis (fixed in B's frame) in the current pose, one support -- before the whole query.  The
+         * cores are still apart by more than the margins and the threshold along it: GJK would keep no point, so
+         * none is produced and the certificate moves to this pose. */
+        const ugk::gv nb = ugk::V3(gc[1], gc[2], gc[3]);
+        const ugk::gv uw = ugk::mv(T1.R, nb);
+        const ugk::gv dA = ugk::mtv(T0.R, ugk::neg(uw));
+        const double hA = ugk::dot(dA, ugk::support0(g0, dA));
+        const ugk::gv pp = ugk::mtv(T1.R, ugk::sub(T0.p, T1.p));
+        const double sep = ugk::dot(nb, pp) - hA - gc[5];
+        if (sep - g0.margin - g1.margin - thr > 1e-9 * (1.0 + ug_fabs(sep))) {
+            UGK_COUNT(PC_GJK_RECERT, 1);
+            if (lead) {
+                const ugk::gm R = ugk::mtm(T1.R, T0.R);
+                gc[4] = hA;
+                for (int i = 0; i < 9; i++) gc[6 + i] = R.m[i];
+                gc[15] = pp.x; gc[16] = pp.y; gc[17] = pp.z;
+                sh.u.cand.n[k] = 0;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            return;
+        }
+    }
     const bool ok = ugk::gjk_pair(E, g0, T0, g1, T1, thr, n, p, d, &ax);
     /* certificate (GJK's order): the axis of a dropped point or of the classic GJK */
     const bool kept = ok && !(d > thr);
