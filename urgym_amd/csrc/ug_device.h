@@ -869,8 +869,20 @@ DF int sort_cached(const LManifold& M, const CPoint& pt) {
         if (ug_fabs(res[i]) > bv) { bv = ug_fabs(res[i]); bi = i; }
     return bi;
 }
-DF void manifold_add(LManifold& M, const XF& TA, const XF& TB, const Cand& c, double thr) {
+/* the pair's collider poses as LDS records (g_sh.O): read through an LDS-typed reference, so the reads are ds_*
+ * instructions (a generic one would be a flat access that waits for every outstanding memory operation) */
+typedef __attribute__((address_space(3))) const XF LXF;
+DFI XF ldxf(const LXF& T) {
+    XF r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.R.m[i] = T.R.m[i];
+    r.p = V(T.p.x, T.p.y, T.p.z);
+    return r;
+}
+DFI const LXF& lxf(const XF& T) { return *(const LXF*)&T; }
+DF void manifold_add(LManifold& M, const LXF& TA0, const LXF& TB0, const Cand c, double thr) {
     if (c.d > thr) return;
+    const XF TA = ldxf(TA0), TB = ldxf(TB0);
     v3 pA = vadd(c.pB, vscale(c.n, c.d));
     CPoint np;
     np.lpA = xf_inv_apply(TA, pA);
@@ -896,7 +908,8 @@ DF void manifold_add(LManifold& M, const XF& TA, const XF& TB, const Cand& c, do
     if (ins < 0) ins = 0;
     stpt(M.pt[ins], np);
 }
-DF void manifold_refresh(LManifold& M, const XF& TA, const XF& TB, double thr) {
+DF void manifold_refresh(LManifold& M, const LXF& TA0, const LXF& TB0, double thr) {
+    const XF TA = ldxf(TA0), TB = ldxf(TB0);
     /* the world points of the first pass are kept (registers, compile-time slots) for the removal pass: the
      * removal pass visits slots in descending order and a removal only overwrites the slot just visited, so
      * every slot it reads still holds its original point */

@@ -2031,15 +2031,16 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
             L.c = (LCand*)&sh.u.cand.c[lane][0];
             PROF_T0(t_pm);
             /* a compound collision object refreshes its child manifolds before the narrowphase (oracle collide) */
-            if (GJK && (s->col[P.a].compound || s->col[P.b].compound) && M.npts) manifold_refresh(M, sh.O[P.a], sh.O[P.b], P.thr);
+            if (GJK && (s->col[P.a].compound || s->col[P.b].compound) && M.npts)
+                manifold_refresh(M, lxf(sh.O[P.a]), lxf(sh.O[P.b]), P.thr);
             for (int i = 0; i < L.n; i++) {
                 Cand c;
                 c.n = ldv(L.c[i].n);
                 c.pB = ldv(L.c[i].pB);
                 c.d = L.c[i].d;
-                manifold_add(M, sh.O[P.a], sh.O[P.b], c, P.thr);
+                manifold_add(M, lxf(sh.O[P.a]), lxf(sh.O[P.b]), c, P.thr);
             }
-            if (M.npts) manifold_refresh(M, sh.O[P.a], sh.O[P.b], P.thr);
+            if (M.npts) manifold_refresh(M, lxf(sh.O[P.a]), lxf(sh.O[P.b]), P.thr);
             has = M.npts > 0;
             PROF_ADD(PF_PR_MAN, t_pm);
         }
