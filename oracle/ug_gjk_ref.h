@@ -39,7 +39,7 @@
 #define G_GJK_ACCURACY 1e-12
 #define G_GJK_MAX_ITERATIONS 128
 #define G_EPA_ACCURACY 1e-12
-#define G_EPA_PLANE_EPS 0.00001
+#define G_EPA_PLANE_EPS 1e-14         /* btGjkEpa2.cpp, BT_USE_DOUBLE_PRECISION block (single: 0.00001) */
 #define G_EPA_MAX_VERTICES 128
 #define G_EPA_MAX_FACES (G_EPA_MAX_VERTICES * 2)
 #define G_EPA_MAX_ITERATIONS 255

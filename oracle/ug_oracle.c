@@ -2251,6 +2251,10 @@ static int pgs_bullet(rowset* rs, double* dv, double* dvs) {
 /* ======================================================================== */
 /* one p.stepSimulation()                                                    */
 /* ======================================================================== */
+/* a floating base's linear / angular velocity, per component (btMultiBody m_realBuf[0..5]) */
+static v3 vclamp_coord(v3 v) {
+    return V(ug_vclamp(v.x, UG_MAX_COORD_VEL), ug_vclamp(v.y, UG_MAX_COORD_VEL), ug_vclamp(v.z, UG_MAX_COORD_VEL));
+}
 static void substep(ugo_env* e) {
     const double dt = UG_DT;
     const scene* s = &e->sc;
@@ -2271,7 +2275,8 @@ static void substep(ugo_env* e) {
     ldlt_solve(M, NB, qdd);
     double v0[NV];
     memset(v0, 0, sizeof(v0));
-    for (int i = 0; i < NB; i++) { e->qd[i] = e->qd[i] + qdd[i] * dt; v0[i] = e->qd[i]; }
+    /* every dof velocity clamped to +-m_maxCoordinateVelocity (btMultiBody::applyDeltaVeeMultiDof [ext]) */
+    for (int i = 0; i < NB; i++) { e->qd[i] = ug_vclamp(e->qd[i] + qdd[i] * dt, UG_MAX_COORD_VEL); v0[i] = e->qd[i]; }
     /* free objects: gravity + default damping + gyroscopic (btMultiBody floating base, 0 links) */
     for (int o = 0; o < s->nobj; o++) {
         if (!e->oactive[o]) continue;
@@ -2281,14 +2286,14 @@ static void substep(ugo_env* e) {
             ugj_dynamics(&s->ojoint[o], &e->oquat[o].x, e->ov[o].x, s->gravity, &Mj, &Cj);
             e->jM[o] = Mj;
             double qdd = -Cj / Mj;
-            e->ov[o].x = e->ov[o].x + qdd * dt;
+            e->ov[o].x = ug_vclamp(e->ov[o].x + qdd * dt, UG_MAX_COORD_VEL);
             v0[NB + 6 * o] = e->ov[o].x;
             continue;
         }
         v3 v = e->ov[o];
         double vn = vlen(v);
         v3 a = vsub(V(0, 0, s->gravity), vscale(v, UG_LIN_DAMP + UG_LIN_DAMP * vn));
-        e->ov[o] = vadd(v, vscale(a, dt));
+        e->ov[o] = vclamp_coord(vadd(v, vscale(a, dt)));
         m3 R = qmat(e->oquat[o]);
         v3 wl = mtv(&R, e->ow[o]);
         v3 I = s->oinertia[o];
@@ -2296,7 +2301,7 @@ static void substep(ugo_env* e) {
         double wn = vlen(wl);
         v3 z = vadd(vscale(Iw, UG_ANG_DAMP + UG_ANG_DAMP * wn), vcross(wl, Iw));
         v3 al = V(-z.x / I.x, -z.y / I.y, -z.z / I.z);
-        e->ow[o] = vadd(e->ow[o], vscale(mv(&R, al), dt));
+        e->ow[o] = vclamp_coord(vadd(e->ow[o], vscale(mv(&R, al), dt)));
         int off = NB + 6 * o;
         v0[off] = e->ov[o].x; v0[off + 1] = e->ov[o].y; v0[off + 2] = e->ov[o].z;
         v0[off + 3] = e->ow[o].x; v0[off + 4] = e->ow[o].y; v0[off + 5] = e->ow[o].z;
@@ -2321,7 +2326,7 @@ static void substep(ugo_env* e) {
     }
     /* velocities += solver delta; positions integrate (v + split velocity) */
     for (int i = 0; i < NB; i++) {
-        e->qd[i] = e->qd[i] + dv[i];
+        e->qd[i] = ug_vclamp(e->qd[i] + dv[i], UG_MAX_COORD_VEL);
         double vi = split ? e->qd[i] + dvs[i] : e->qd[i];
         e->q[i] = e->q[i] + vi * dt;
     }
@@ -2329,14 +2334,14 @@ static void substep(ugo_env* e) {
         if (!e->oactive[o]) continue;
         int off = NB + 6 * o;
         if (s->ojoint[o].kind != UGJ_FREE) {
-            e->ov[o].x = e->ov[o].x + dv[off];
+            e->ov[o].x = ug_vclamp(e->ov[o].x + dv[off], UG_MAX_COORD_VEL);
             double vi = split ? e->ov[o].x + dvs[off] : e->ov[o].x;
             e->ow[o].x = e->ow[o].x + vi * dt;
             ugj_frame(&s->ojoint[o], e->ow[o].x, &e->oquat[o].x, &e->opos[o].x);
             continue;
         }
-        e->ov[o] = vadd(e->ov[o], V(dv[off], dv[off + 1], dv[off + 2]));
-        e->ow[o] = vadd(e->ow[o], V(dv[off + 3], dv[off + 4], dv[off + 5]));
+        e->ov[o] = vclamp_coord(vadd(e->ov[o], V(dv[off], dv[off + 1], dv[off + 2])));
+        e->ow[o] = vclamp_coord(vadd(e->ow[o], V(dv[off + 3], dv[off + 4], dv[off + 5])));
         v3 vl = e->ov[o], wa = e->ow[o];
         if (split) {
             vl = vadd(vl, V(dvs[off], dvs[off + 1], dvs[off + 2]));

@@ -100,16 +100,25 @@ def test_manifold_capacity_overflow(mods, task):
 FLAG_NONFINITE = 2
 
 
-def test_nonfinite_guard_on_runaway_folds(mods):
-    """folds whose one-point-per-pair contacts deep inside the table run away (joint velocities past 1e20 within a few
-    dozen substeps, then inf / NaN): the non-finite guard ends the env-step at the first non-finite substep on both
-    sides -- same substep count, NONFINITE flag and counter, the same non-finite observation and state (the runaway
-    angles, 1e21 rad, take the same sin / cos quadrant in both builds: ug__rem_pio2's exact quadrant)"""
+def _spin(j, w):
+    def edit(s):
+        s[LY.F_QD + j] = w
+    return edit
+
+
+def test_nonfinite_guard(mods):
+    """an absurd joint velocity (1e200 rad/s: its gyroscopic terms overflow in the first substep's RNEA, before the
+    coordinate-velocity clamp) drives the non-finite guard: it ends the env-step at the first non-finite substep on both
+    sides -- same substep count, NONFINITE flag and counter, the same non-finite observation and state.  The deep folds
+    beside it (they ran away to inf in round 4, before btMultiBody's +-100 coordinate-velocity clamp was restated) now
+    stay finite and end at the 480 cap."""
     Sim, OracleEnv = mods
-    out, fl, d = crafted_step(Sim, OracleEnv, 0, [_fold(0.5, 0.0), _fold(0.5, 2.5), _fold(0.8, 2.5), _fold(1.0, 2.0)],
+    out, fl, d = crafted_step(Sim, OracleEnv, 0, [_fold(0.5, 0.0), _spin(5, 1e200), _fold(0.5, 2.5), _fold(1.0, 2.0)],
                               np.zeros(3), finite=False)
-    assert (fl[[1, 3]] & FLAG_NONFINITE).all() and (d[[1, 3], NONFINITE] == 1).all(), (fl.tolist(), d.tolist())
-    assert not (fl[[0, 2]] & FLAG_NONFINITE).any()
+    assert (fl[1] & FLAG_NONFINITE) and d[1, NONFINITE] == 1 and out["substeps"][1] == 1, (fl.tolist(), d.tolist())
+    assert not (fl[[0, 2, 3]] & FLAG_NONFINITE).any()
+    assert np.all(np.isfinite(out["obs"][[0, 2, 3]]))
+    assert (out["substeps"][[2, 3]] == 480).all() and (fl[[2, 3]] & FLAG_UNSTABLE).all()
 
 
 @pytest.mark.parametrize("task", [0, 1])

@@ -1,6 +1,6 @@
 """The restatement alone (CPU) on tests/test_gpu_failures.py's crafted states: the arm folded into the table in both
-contact modes (manifold and row capacity overflow, the 480-substep cap, the split pass), the runaway folds that end at
-the non-finite guard, a cube sunk into the table.  Each case checks the counter it targets, as the GPU test does.  These
+contact modes (manifold and row capacity overflow, the 480-substep cap, the split pass), the deep folds the coordinate-velocity
+clamp keeps finite, an absurd joint velocity that ends at the non-finite guard, a cube sunk into the table.  Each case checks the counter it targets, as the GPU test does.  These
 are the states tools/oracle_asan.sh runs under AddressSanitizer / UBSan (make -C oracle asan), where every capacity
 branch, clamp and NaN path of oracle/ug_oracle.c executes with bounds and undefined-behaviour checks."""
 import os
@@ -46,10 +46,19 @@ def test_oracle_row_capacity_overflow_vih(task):
 
 
 def test_oracle_nonfinite_guard():
+    res = _run(0, [F._spin(5, 1e200), F._spin(0, 1e200)], np.zeros(3))
+    for o, fl, d, ns in res:
+        assert fl & F.FLAG_NONFINITE and d[F.NONFINITE] == 1 and ns == 1, (fl, d.tolist(), ns)
+        assert not np.all(np.isfinite(o))
+
+
+def test_oracle_deep_folds_stay_finite():
+    """the folds that ran away in round 4: btMultiBody's coordinate-velocity clamp (+-100, every dof, after
+    the force step and after the solve) bounds them; they end at the 480 cap with finite states"""
     res = _run(0, [F._fold(0.5, 2.5), F._fold(1.0, 2.0)], np.zeros(3))
     for o, fl, d, ns in res:
-        assert fl & F.FLAG_NONFINITE and d[F.NONFINITE] == 1, (fl, d.tolist())
-        assert not np.all(np.isfinite(o))
+        assert np.all(np.isfinite(o)) and not fl & F.FLAG_NONFINITE, (fl, d.tolist())
+        assert ns == 480 and fl & F.FLAG_UNSTABLE
 
 
 def test_oracle_split_impulse():

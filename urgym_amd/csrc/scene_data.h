@@ -61,6 +61,11 @@ UG_CONST double UG_BX_DOOR_MASSES[4] = {0.1, 0.05, 0.05, 0.1};
 #define UG_CONTACT_BREAK 0.02          /* gContactBreakingThreshold (relative to shape size) [ext] */
 #define UG_AABB_PAD 0.02               /* broadphase AABB padding [ext] */
 #define UG_LIN_DAMP 0.04               /* btMultiBody default linear damping [ext] */
+#ifndef UG_MAX_COORD_VEL /* (a -D override: the fidelity tools compare against the unclamped dynamics) */
+#define UG_MAX_COORD_VEL 100.0         /* btMultiBody m_maxCoordinateVelocity default (100.f) [ext]: every dof velocity is
+                                          clamped to +-this in applyDeltaVeeMultiDof, after the force step and after the
+                                          constraint solve's delta (processDeltaVeeMultiDof2) */
+#endif
 #define UG_ANG_DAMP 0.04               /* btMultiBody default angular damping [ext] */
 #define UG_MAX_FRICTION 10.0           /* MAX_FRICTION clamp of the combined friction [ext] */
 #define UG_ANGULAR_MOTION_THR (0.5 * 1.5707963267948966)   /* ANGULAR_MOTION_THRESHOLD [ext] */

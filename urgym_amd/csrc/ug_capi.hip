@@ -49,6 +49,16 @@ __device__ static double safe_margin(double hx, double hy, double hz) {
     m = 0.1 * m;
     return m < 0.04 ? m : 0.04;
 }
+/* the support-cell table of the hull with vertex range [v0, v0 + nv): a full hull's (tools/build_supcells.py), or none */
+__device__ static void supcell_table(int v0, int nv, int* scb, int* sck) {
+    *scb = -1;
+    *sck = 0;
+    for (int k = 0; k < UG_NSHAPE; k++)
+        if (UG_SHAPE_KIND[k] == 1 && UG_SHAPE_FNV[k] > 0 && UG_SHAPE_FV0[k] == v0 && UG_SHAPE_FNV[k] == nv) {
+            *scb = UG_SHAPE_SCB[k];
+            *sck = UG_SHAPE_SCK[k];
+        }
+}
 /* Bullet's shape parameters for GJK (oracle gjk_params) */
 __device__ static void gjk_params(Collider* c) {
     c->gimp = V(0, 0, 0);
@@ -62,6 +72,10 @@ __device__ static void gjk_params(Collider* c) {
         c->gmargin = m;
         c->gimp = V(r - m, r - m, hh - m);
     }
+    /* a full hull's support-cell table (supcell_data.h), found by its vertex range */
+    c->scb = -1;
+    c->sck = 0;
+    if (c->kind == UG_SHAPE_HULL) supcell_table(c->v0, c->nv, &c->scb, &c->sck);
     /* the certificate's rotation bound (team_collide): every core support point lies within gradius of the origin */
     double r2 = 0.0;
     if (c->kind == UG_SHAPE_HULL) {
@@ -370,11 +384,12 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
     for (int i = 0; i < s->ncol; i++) gjk_params(&s->col[i]);
 }
 
-// development / test aid: one convex-convex query per wave (urgym_debug_gjk, tests/test_gpu_gjk.py).  Query i packs
+// development / test aid: convex-convex queries as the kernels run them, one per 16-lane group (GJK_NG per wave, each
+// with its own EPA store), through the same support-cell tables (urgym_debug_gjk, tests/test_gpu_gjk.py).  Query i packs
 // 39 doubles: per shape kind, v0, nv, imp[3], margin, R[9], p[3], then thr.
 __global__ void __launch_bounds__(TEAM, 1) k_gjk_query(const double* q, int n, double* out, int* ok, ugk::EpaMem* E) {
-    const int i = blockIdx.x;
-    if (i >= n) return;
+    const int i = blockIdx.x * GJK_NG + gjk_grp();
+    if (i >= n) return; /* a whole group: its lanes leave together */
     const double* Q = q + (size_t)i * 39;
     ugk::GShape S[2];
     ugk::gx T[2];
@@ -383,13 +398,15 @@ __global__ void __launch_bounds__(TEAM, 1) k_gjk_query(const double* q, int n, d
         S[k].kind = (int)P[0]; S[k].v0 = (int)P[1]; S[k].nv = (int)P[2];
         S[k].imp = ugk::V3(P[3], P[4], P[5]);
         S[k].margin = P[6];
+        S[k].scb = -1; S[k].sck = 0;
+        if (S[k].kind == UG_SHAPE_HULL) supcell_table(S[k].v0, S[k].nv, &S[k].scb, &S[k].sck);
         for (int j = 0; j < 9; j++) T[k].R.m[j] = P[7 + j];
         T[k].p = ugk::V3(P[16], P[17], P[18]);
     }
     ugk::gv nn, pp;
     double d = 0.0;
     const bool r = ugk::gjk_pair((UGK_GMEM ugk::EpaMem*)(E + i), S[0], T[0], S[1], T[1], Q[38], nn, pp, d);
-    if (threadIdx.x == 0) {
+    if ((threadIdx.x & (GJK_G - 1)) == 0) {
         ok[i] = r ? 1 : 0;
         double* o = out + (size_t)i * 7;
         o[0] = nn.x; o[1] = nn.y; o[2] = nn.z; o[3] = pp.x; o[4] = pp.y; o[5] = pp.z; o[6] = d;
@@ -1170,17 +1187,18 @@ int urgym_debug_gjk(int n, const double* q, double* out, int* ok) {
     double *dq = nullptr, *dout = nullptr;
     int* dok = nullptr;
     ugk::EpaMem* E = nullptr;
+    int rc = 0;
     if (hipMalloc(&dq, sizeof(double) * 39 * n) != hipSuccess || hipMalloc(&dout, sizeof(double) * 7 * n) != hipSuccess ||
         hipMalloc(&dok, sizeof(int) * n) != hipSuccess || hipMalloc(&E, sizeof(ugk::EpaMem) * n) != hipSuccess)
-        return -1;
-    int rc = 0;
-    if (hipMemcpy(dq, q, sizeof(double) * 39 * n, hipMemcpyHostToDevice) != hipSuccess) rc = -1;
+        rc = -1;
+    if (!rc && hipMemcpy(dq, q, sizeof(double) * 39 * n, hipMemcpyHostToDevice) != hipSuccess) rc = -1;
     if (!rc) {
-        hipLaunchKernelGGL(k_gjk_query, dim3(n), dim3(TEAM), 0, 0, dq, n, dout, dok, E);
-        if (hipDeviceSynchronize() != hipSuccess) rc = -1;
+        hipLaunchKernelGGL(k_gjk_query, dim3((n + GJK_NG - 1) / GJK_NG), dim3(TEAM), 0, 0, dq, n, dout, dok, E);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = -1;
     }
     if (!rc && hipMemcpy(out, dout, sizeof(double) * 7 * n, hipMemcpyDeviceToHost) != hipSuccess) rc = -1;
     if (!rc && hipMemcpy(ok, dok, sizeof(int) * n, hipMemcpyDeviceToHost) != hipSuccess) rc = -1;
+    /* hipFree(nullptr) is a no-op: every path frees whatever was allocated */
     hipFree(dq); hipFree(dout); hipFree(dok); hipFree(E);
     return rc;
 }

@@ -32,6 +32,8 @@ UG_HD double ug_rint(double x) { return __builtin_rint(x); }
 UG_HD double ug_min(double a, double b) { return a < b ? a : b; }
 UG_HD double ug_max(double a, double b) { return a > b ? a : b; }
 UG_HD double ug_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+/* btClamp(v, -m, m) as btMultiBody::applyDeltaVeeMultiDof applies it to every dof velocity [ext] (a NaN passes) */
+UG_HD double ug_vclamp(double v, double m) { return v < -m ? -m : (m < v ? m : v); }
 /* numpy.linalg.norm of a 3-vector as this image's numpy computes it (OpenBLAS ddot: fused
  * multiply-adds in element order, then sqrt) -- checked against numpy in tests/test_oracle_kat.py */
 UG_HD double ug_norm3(double x, double y, double z) { return __builtin_sqrt(__builtin_fma(z, z, __builtin_fma(y, y, x * x))); }

@@ -17,8 +17,10 @@
 #define UG_CONST static __constant__ const
 #ifdef UG_ROBOT_R140 /* the UR5Robotiq140 build (liburgym_r140.so, robot.py:221-240) */
 #include "model_data_r140.h"
+#include "supcell_data_r140.h"
 #else
 #include "model_data.h"
+#include "supcell_data.h"
 #endif
 #include "scene_data.h"
 #include "ug_detmath.h"
@@ -46,6 +48,10 @@ struct q4 { double x, y, z, w; };
 
 DFI v3 V(double x, double y, double z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
 DFI v3 vadd(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+/* a floating base's linear / angular velocity clamped per component to +-m_maxCoordinateVelocity (oracle vclamp_coord) */
+DFI v3 vclamp_coord(v3 v) {
+    return V(ug_vclamp(v.x, UG_MAX_COORD_VEL), ug_vclamp(v.y, UG_MAX_COORD_VEL), ug_vclamp(v.z, UG_MAX_COORD_VEL));
+}
 DFI v3 vsub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
 DFI v3 vscale(v3 a, double s) { return V(a.x * s, a.y * s, a.z * s); }
 DFI v3 vneg(v3 a) { return V(-a.x, -a.y, -a.z); }
@@ -232,6 +238,7 @@ struct Collider {
     int gjkbox;     /* a convex mesh kept as its box (the Golf pitch): every pair of it is convex-convex */
     double gradius; /* the largest distance of a core support point from the shape origin (certificate bound) */
     int compound;   /* btCompoundShape collision object: its child manifolds are refreshed before the narrowphase */
+    int scb, sck;   /* a full hull's support-cell table (first cell, K; scb -1: none), set with the GJK parameters */
 };
 struct PairDef { int a, b; double thr, friction, restitution, rolling; };
 struct Scene {

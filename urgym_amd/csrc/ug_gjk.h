@@ -9,8 +9,9 @@
  *
  * How it runs on CDNA4: every lane of the env's wavefront executes the same (uniform) scalar chain, so the wave is
  * one pair's solver; the only wave-parallel step is the hull support query (max-dot over up to 865 vertices), which
- * the includer supplies as ugk_hull_support(v0, nv, d) (ug_team.h: lane-strided dot products + a DPP arg-max with
- * the lowest index winning ties, as btVector3::maxDot's first maximum).  The common path (intersection test, Voronoi
+ * the includer supplies as ugk_hull_support(shape, d) (ug_team.h: the direction cell's candidate list from the full
+ * hulls' support-cell tables, ug_supcell.h / tools/build_supcells.py, or every vertex; lane-strided dot products + a
+ * DPP arg-max with the lowest index winning ties, as btVector3::maxDot's first maximum).  The common path (intersection test, Voronoi
  * GJK, normal fix) keeps its small state in registers: every run-time index into the simplex arrays is an explicit
  * select, so no private array is dynamically indexed.  The penetration path (btGjkEpa2 GJK + EPA:
  * 132 support vertices, 256 faces, their lists) lives in the env's global workspace (EpaMem, L2-resident); EPA's
@@ -74,13 +75,15 @@ UGK_FN gv xfa(const gx& T, gv x) { return add(mv(T.R, x), T.p); }
 UGK_FN bool veq(gv a, gv b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
 UGK_FN gv vsel(bool c, gv a, gv b) { return V3(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
 
-/* a convex shape as GJK sees it (kind: UG_SHAPE_*; imp: box / cylinder implicit dimensions; margin: getMargin) */
-struct GShape { int kind, v0, nv; gv imp; double margin; };
+/* a convex shape as GJK sees it (kind: UG_SHAPE_*; imp: box / cylinder implicit dimensions; margin: getMargin;
+ * scb, sck: a hull's support-cell table -- first cell in UG_SC_IDX and K -- or scb = -1 for none, supcell_data.h) */
+struct GShape { int kind, v0, nv; gv imp; double margin; int scb, sck; };
 
 } /* namespace ugk */
 
-/* the includer's hull support: the vertex of hull [v0, v0 + nv) with the first maximal dot product with d */
-UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d);
+/* the includer's hull support: the vertex of hull [s.v0, s.v0 + s.nv) with the first maximal dot product with d
+ * (btVector3::maxDot), over the whole hull or over the direction cell's candidates (s.scb >= 0, ug_supcell.h) */
+UGK_FN ugk::gv ugk_hull_support(const ugk::GShape& s, ugk::gv d);
 #ifdef UGK_GROUP_PARALLEL
 /* the includer's lane-group hooks (kernels): this lane's index in its group, and v as lane j of the group holds it.
  * With them the solver evaluates a few independent sub-results on separate lanes at once (the tetrahedron's faces,
@@ -102,7 +105,7 @@ constexpr double kEqVertex = (double)1e-12f;
 constexpr int kMaxIter = 1000;
 constexpr double kGjkMinDist = 1e-12, kGjkDupEps = 1e-12, kGjkAccuracy = 1e-12;
 constexpr int kGjkMaxIterations = 128;
-constexpr double kEpaAccuracy = 1e-12, kEpaPlaneEps = 0.00001;
+constexpr double kEpaAccuracy = 1e-12, kEpaPlaneEps = 1e-14; /* btGjkEpa2.cpp double block (single: 1e-4, 1e-5) */
 constexpr int kEpaMaxVertices = 128, kEpaMaxFaces = 256, kEpaMaxIterations = 255;
 constexpr int kTetra = 4 + kEpaMaxVertices; /* E->sv slots of the EPA's first tetrahedron */
 
@@ -120,7 +123,7 @@ UGK_FN gv support0(const GShape& s, gv d) {
         }
         return V3(s.imp.x, 0.0, z);
     }
-    return ugk_hull_support(s.v0, s.nv, d);
+    return ugk_hull_support(s, d);
 }
 /* localGetSupportVertexNonVirtual */
 UGK_FN gv support(const GShape& s, gv d) {

@@ -355,22 +355,61 @@ __device__ __forceinline__ void hs_scan(int v0, int nv, ugk::gv d, int gl, doubl
         }
     }
 }
-UGK_FN ugk::gv ugk_hull_support(int v0, int nv, ugk::gv d) {
+#define UGK_RCPF(x) __builtin_amdgcn_rcpf(x)
+#include "ug_supcell.h"
+/* the direction cell's candidates (supcell_data.h): lane l of the group dots candidate l of the cell's list (a longer
+ * list in trips of G), keeping its first maximum with the candidate's key (vertex index x G + lane: the lower vertex
+ * wins a tie, and the key names the lane that holds the winner's coordinates) */
+__device__ __forceinline__ void hs_cells(int v0, int scb, int cell, ugk::gv d, int gl, double& best, int& key, ugk::gv& bv) {
+    constexpr int G = ugd::GJK_G;
+    static_assert(UG_SC_SLOTS == G, "one cell slot per lane of a GJK group");
+    const unsigned short* L = &UG_SC_IDX[(scb + cell) * UG_SC_SLOTS];
+    const int s = L[gl], s0 = L[0];
+    if (s0 != UG_SC_OVF) {
+        const double* p = &UG_HULL_V[3 * (v0 + s)];
+        bv = ugk::V3(p[0], p[1], p[2]);
+        best = bv.x * d.x + bv.y * d.y + bv.z * d.z;
+        key = s * G + gl;
+        return;
+    }
+    const int cnt = L[1], off = L[2] | (L[3] << 16);
+    for (int t = 0; t < cnt; t += G) { /* the list is padded to whole trips */
+        const int i = UG_SC_IDX[off + t + gl];
+        const double* p = &UG_HULL_V[3 * (v0 + i)];
+        const double x = p[0], y = p[1], z = p[2];
+        const double dd = x * d.x + y * d.y + z * d.z;
+        const int k = i * G + gl;
+        if (dd > best || (dd == best && k < key)) {
+            best = dd;
+            key = k;
+            bv = ugk::V3(x, y, z);
+        }
+    }
+}
+UGK_FN ugk::gv ugk_hull_support(const ugk::GShape& sh, ugk::gv d) {
     constexpr int G = ugd::GJK_G;
     const int gl = threadIdx.x & (G - 1);
     PROF_T0(t_sup);
     double best = -__builtin_inf();
     int bi = 0x7fffffff;
     ugk::gv bv = ugk::V3(0.0, 0.0, 0.0);
-    hs_scan(v0, nv, d, gl, best, bi, bv);
-    ugd::group_best(best, bi, true);
+    const int cell = sh.scb >= 0 ? ugk_sc_cell(d.x, d.y, d.z, sh.sck) : -1;
     ugk::gv r;
-    if (bi == 0x7fffffff) { /* no comparable dot product (a NaN direction): vertex 0, as maxDot leaves it */
-        const double* p = &UG_HULL_V[3 * v0];
-        r = ugk::V3(p[0], p[1], p[2]);
-    } else { /* the winner's coordinates from the lane that dotted it (vertex i sits in lane i mod G) */
+    if (cell >= 0) { /* a finite direction: its cell holds every vertex that can win the full scan (build_supcells.py) */
+        hs_cells(sh.v0, sh.scb, cell, d, gl, best, bi, bv);
+        ugd::group_best(best, bi, true);
         const int src = (int)(threadIdx.x & ~(G - 1)) + (bi & (G - 1));
         r = ugk::V3(__shfl(bv.x, src, TEAM), __shfl(bv.y, src, TEAM), __shfl(bv.z, src, TEAM));
+    } else {
+        hs_scan(sh.v0, sh.nv, d, gl, best, bi, bv);
+        ugd::group_best(best, bi, true);
+        if (bi == 0x7fffffff) { /* no comparable dot product (a NaN direction): vertex 0, as maxDot leaves it */
+            const double* p = &UG_HULL_V[3 * sh.v0];
+            r = ugk::V3(p[0], p[1], p[2]);
+        } else { /* the winner's coordinates from the lane that dotted it (vertex i sits in lane i mod G) */
+            const int src = (int)(threadIdx.x & ~(G - 1)) + (bi & (G - 1));
+            r = ugk::V3(__shfl(bv.x, src, TEAM), __shfl(bv.y, src, TEAM), __shfl(bv.z, src, TEAM));
+        }
     }
 #ifdef UG_PROF
     if (gl == 0) {
@@ -1640,6 +1679,8 @@ __device__ __forceinline__ static ugk::GShape gshape_of(const Collider& c) {
     g.nv = c.kind == UG_SHAPE_HULL ? c.nv : 0;
     g.imp = ugk::V3(c.gimp.x, c.gimp.y, c.gimp.z);
     g.margin = c.gmargin;
+    g.scb = c.kind == UG_SHAPE_HULL ? c.scb : -1;
+    g.sck = c.sck;
     return g;
 }
 __device__ __forceinline__ static ugk::gx to_gx(const XF& T) {
@@ -3274,7 +3315,8 @@ __device__ __noinline__ static void serial_pre(const Scene* s) {
 #pragma unroll
         for (int i = 0; i < NB; i++) qdd[i] = -C[i];
         ldlt_solve_r(A, qdd);
-        for (int i = 0; i < NB; i++) { e.qd[i] = e.qd[i] + qdd[i] * dt; sh.v0[i] = e.qd[i]; }
+        /* every dof velocity clamped to +-m_maxCoordinateVelocity (oracle substep) */
+        for (int i = 0; i < NB; i++) { e.qd[i] = ug_vclamp(e.qd[i] + qdd[i] * dt, UG_MAX_COORD_VEL); sh.v0[i] = e.qd[i]; }
     } else if (lane <= s->nobj) { /* free bodies, one lane each (independent of the robot solve) */
         const int o = lane - 1;
         if (e.oactive[o] != 0.0 && s->ojoint[o].kind != UGJ_FREE) {
@@ -3285,14 +3327,14 @@ __device__ __noinline__ static void serial_pre(const Scene* s) {
             ugj_dynamics(&s->ojoint[o], qt, ob.v.x, s->gravity, &Mj, &Cj);
             sh.jM[o] = Mj;
             const double qdd = -Cj / Mj;
-            ob.v.x = ob.v.x + qdd * dt;
+            ob.v.x = ug_vclamp(ob.v.x + qdd * dt, UG_MAX_COORD_VEL);
             sh.v0[NB + 6 * o] = ob.v.x;
         } else if (e.oactive[o] != 0.0) {
             StObj& ob = e.obj[o];
             v3 v = ob.v;
             double vn = vlen(v);
             v3 a = vsub(V(0, 0, s->gravity), vscale(v, UG_LIN_DAMP + UG_LIN_DAMP * vn));
-            ob.v = vadd(v, vscale(a, dt));
+            ob.v = vclamp_coord(vadd(v, vscale(a, dt)));
             m3 R = qmat(ob.quat);
             v3 wl = mtv(R, ob.w);
             v3 I = s->oinertia[o];
@@ -3300,7 +3342,7 @@ __device__ __noinline__ static void serial_pre(const Scene* s) {
             double wn = vlen(wl);
             v3 z = vadd(vscale(Iw, UG_ANG_DAMP + UG_ANG_DAMP * wn), vcross(wl, Iw));
             v3 al = V(-z.x / I.x, -z.y / I.y, -z.z / I.z);
-            ob.w = vadd(ob.w, vscale(mv(R, al), dt));
+            ob.w = vclamp_coord(vadd(ob.w, vscale(mv(R, al), dt)));
             int off = NB + 6 * o;
             sh.v0[off] = ob.v.x; sh.v0[off + 1] = ob.v.y; sh.v0[off + 2] = ob.v.z;
             sh.v0[off + 3] = ob.w.x; sh.v0[off + 4] = ob.w.y; sh.v0[off + 5] = ob.w.z;
@@ -3322,7 +3364,7 @@ __device__ __noinline__ static void serial_post(const Scene* s, int split) {
         const double* DV = sh.dvout;
         const double* DVS = sh.dvsout;
         for (int i = 0; i < NB; i++) {
-            e.qd[i] = e.qd[i] + DV[i];
+            e.qd[i] = ug_vclamp(e.qd[i] + DV[i], UG_MAX_COORD_VEL);
             double vi = split ? e.qd[i] + DVS[i] : e.qd[i];
             e.q[i] = e.q[i] + vi * dt;
         }
@@ -3331,7 +3373,7 @@ __device__ __noinline__ static void serial_post(const Scene* s, int split) {
             StObj& ob = e.obj[o];
             int off = NB + 6 * o;
             if (s->ojoint[o].kind != UGJ_FREE) {
-                ob.v.x = ob.v.x + DV[off];
+                ob.v.x = ug_vclamp(ob.v.x + DV[off], UG_MAX_COORD_VEL);
                 double vi = split ? ob.v.x + DVS[off] : ob.v.x;
                 ob.w.x = ob.w.x + vi * dt;
                 double qt[4], pt[3];
@@ -3340,8 +3382,8 @@ __device__ __noinline__ static void serial_post(const Scene* s, int split) {
                 ob.pos = V(pt[0], pt[1], pt[2]);
                 continue;
             }
-            ob.v = vadd(ob.v, V(DV[off], DV[off + 1], DV[off + 2]));
-            ob.w = vadd(ob.w, V(DV[off + 3], DV[off + 4], DV[off + 5]));
+            ob.v = vclamp_coord(vadd(ob.v, V(DV[off], DV[off + 1], DV[off + 2])));
+            ob.w = vclamp_coord(vadd(ob.w, V(DV[off + 3], DV[off + 4], DV[off + 5])));
             v3 vl = ob.v, wa = ob.w;
             if (split) {
                 vl = vadd(vl, V(DVS[off], DVS[off + 1], DVS[off + 2]));
