@@ -1061,6 +1061,9 @@ static v3 g_support_ab(const gshape* A, const xf* TA, const gshape* B, const xf*
 /* btGjkPairDetector::getClosestPointsNonVirtual + the btManifoldResult input it forms.  TA / TB: world transforms of
  * the two shapes; thr: the manifold's contact breaking threshold.  Returns 1 with (normal on B, point on B, distance)
  * when the detector reports a point (the caller's addContactPoint still drops distance > thr), else 0. */
+/* test hook (tests/test_gjk_independent.py): the last query's exits -- the classic GJK's degenerate code and iteration
+ * count, the libccd status, whether the penetration path ran */
+static _Thread_local int g_gjk_dbg[4];
 static int gjk_pair(const gshape* A, const xf* TA0, const gshape* B, const xf* TB0, double thr, v3* nOut, v3* pOut,
                     double* dOut) {
     static _Thread_local gepa g; /* the EPA's stores (btGjkEpaSolver2 keeps them on its stack) */
@@ -1126,6 +1129,8 @@ static int gjk_pair(const gshape* A, const xf* TA0, const gshape* B, const xf* T
             if (curIter++ > G_MAX_ITER) break;
             if (vs.n == 4) { degenerate = 13; break; }
         }
+        g_gjk_dbg[0] = degenerate;
+        g_gjk_dbg[1] = curIter;
         if (checkSimplex) {
             vs_update(&vs); /* compute_points */
             pointOnA = vs.cP1;
@@ -1147,6 +1152,8 @@ static int gjk_pair(const gshape* A, const xf* TA0, const gshape* B, const xf* T
     }
     /* 3. penetration (EPA) */
     const int catchDegenerate = degenerate && ((distance + margin) < G_PEN_TOL);
+    g_gjk_dbg[2] = status;
+    g_gjk_dbg[3] = (!isValid || catchDegenerate) || status == 0;
     if ((!isValid || catchDegenerate) || status == 0) {
         v3 tA, tB;
         axis = V(0, 0, 0);

@@ -895,6 +895,10 @@ int ugo_gjk_pair(int kA, int v0A, int nvA, const double* impA, double mA, const 
     out[6] = d;
     return 1;
 }
+/* test hook: the last ugo_gjk_pair query's exits (ug_gjk_ref.h g_gjk_dbg) */
+void ugo_gjk_debug(int* out) {
+    for (int i = 0; i < 4; i++) out[i] = g_gjk_dbg[i];
+}
 /* debug aid (tools/debug_gjk.py): the convex-convex queries of this thread, as urgym_debug_gjk packs them, with
  * their results (ok, normal, point, distance) */
 #define GREC_MAX 8192
@@ -1576,6 +1580,37 @@ static void manifold_add(manifold* M, const xf* TA, const xf* TB, const cand* c,
     else M->npts++;
     if (ins < 0) ins = 0;
     M->pt[ins] = np;
+}
+/* test hook (tests/test_manifold_kat.py): manifold_add on a crafted manifold.  pts: npts x 13 doubles (lpA, lpB, n,
+ * dist, imp, imp1, imp2); TA, TB: R (row-major 9) + p (3); c: n, pB, d.  Writes the manifold back (4 x 13) and returns
+ * its point count. */
+int ugo_manifold_add(double* pts, int npts, const double* TA12, const double* TB12, const double* c7, double thr) {
+    manifold M;
+    M.npts = npts;
+    for (int i = 0; i < npts; i++) {
+        const double* q = pts + 13 * i;
+        M.pt[i].lpA = V(q[0], q[1], q[2]);
+        M.pt[i].lpB = V(q[3], q[4], q[5]);
+        M.pt[i].n = V(q[6], q[7], q[8]);
+        M.pt[i].dist = q[9];
+        M.pt[i].imp = q[10]; M.pt[i].imp1 = q[11]; M.pt[i].imp2 = q[12];
+    }
+    xf TA, TB;
+    TA.R = mload(TA12); TA.p = V(TA12[9], TA12[10], TA12[11]);
+    TB.R = mload(TB12); TB.p = V(TB12[9], TB12[10], TB12[11]);
+    cand c;
+    c.n = V(c7[0], c7[1], c7[2]);
+    c.pB = V(c7[3], c7[4], c7[5]);
+    c.d = c7[6];
+    manifold_add(&M, &TA, &TB, &c, thr);
+    for (int i = 0; i < M.npts; i++) {
+        double* q = pts + 13 * i;
+        q[0] = M.pt[i].lpA.x; q[1] = M.pt[i].lpA.y; q[2] = M.pt[i].lpA.z;
+        q[3] = M.pt[i].lpB.x; q[4] = M.pt[i].lpB.y; q[5] = M.pt[i].lpB.z;
+        q[6] = M.pt[i].n.x; q[7] = M.pt[i].n.y; q[8] = M.pt[i].n.z;
+        q[9] = M.pt[i].dist; q[10] = M.pt[i].imp; q[11] = M.pt[i].imp1; q[12] = M.pt[i].imp2;
+    }
+    return M.npts;
 }
 static void manifold_refresh(manifold* M, const xf* TA, const xf* TB, double thr) {
     for (int i = M->npts - 1; i >= 0; i--) {

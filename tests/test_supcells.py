@@ -158,3 +158,26 @@ def test_ties_resolve_to_the_lowest_index(host, model):
         n_tied += int(((dots == dots.max(1, keepdims=True)).sum(1) > 1).sum())
         assert np.array_equal(support(host, si, D, True), np.argmax(dots, 1)), si
     assert n_tied > 0  # some axis directions hit exact ties on these meshes
+
+
+@pytest.mark.parametrize("robot", ["r85", "r140"])
+def test_inline_coordinates_are_the_listed_vertices(robot):
+    """the kernels read a cell's candidates' coordinates from UG_SC_XYZ (the host build reads UG_SC_IDX): slot by slot
+    they are the listed vertices' coordinates, bit for bit"""
+    import re
+    _, mh, th = ROBOTS[robot]
+    model = B.read_model(os.path.join(ROOT, "urgym_amd", "csrc", mh))
+    X = model["UG_HULL_V"].reshape(-1, 3)
+    txt = open(os.path.join(ROOT, "urgym_amd", "csrc", th)).read()
+
+    def arr(name, dt):
+        m = re.search(r"%s\[\d+\] = \{([^}]*)\}" % name, txt)
+        return np.array([float(x) for x in m.group(1).split(",")], dt)
+    scb, sck = arr("UG_SHAPE_SCB", np.int64), arr("UG_SHAPE_SCK", np.int64)
+    idx, xyz = arr("UG_SC_IDX", np.int64), arr("UG_SC_XYZ", np.float64).reshape(-1, B.SLOTS, 3)
+    for si in np.nonzero(scb >= 0)[0]:
+        H = X[model["UG_SHAPE_FV0"][si]:model["UG_SHAPE_FV0"][si] + model["UG_SHAPE_FNV"][si]]
+        for c in range(scb[si], scb[si] + 6 * sck[si] ** 2):
+            sl = idx[c * B.SLOTS:(c + 1) * B.SLOTS]
+            if sl[0] != B.OVF:
+                assert np.array_equal(xyz[c], H[sl]), (si, c)

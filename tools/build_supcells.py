@@ -127,6 +127,20 @@ def build(model_path, out_path):
         n = -(-len(c) // SLOTS) * SLOTS
         idx.extend(list(c) + [int(c[-1])] * (n - len(c)))
     assert max(idx) < 65536
+    # each cell's candidates' coordinates, slot by slot (the kernels read a cell's vertices in one memory round; an
+    # overflow cell's slots are unused zeros, its long list goes through UG_SC_IDX)
+    xyz = []
+    for si in range(len(kind)):
+        if scb[si] < 0:
+            continue
+        H = X[fv0[si]:fv0[si] + fnv[si]]
+        for c in range(6 * sck[si] * sck[si]):
+            sl = idx[(scb[si] + c) * SLOTS:(scb[si] + c + 1) * SLOTS]
+            if sl[0] == OVF:
+                xyz.extend([0.0] * (3 * SLOTS))
+            else:
+                for v in sl:
+                    xyz.extend(H[v].tolist())
     name = os.path.basename(model_path)
     out = ["/* GENERATED by tools/build_supcells.py from %s. Do not edit. */" % name,
            "/* Support-cell tables of the full hulls (exactness argument: tools/build_supcells.py).  Per shape: the first",
@@ -140,6 +154,8 @@ def build(model_path, out_path):
            "UG_CONST int UG_SHAPE_SCB[%d] = {%s};" % (len(scb), ", ".join(map(str, scb))),
            "UG_CONST int UG_SHAPE_SCK[%d] = {%s};" % (len(sck), ", ".join(map(str, sck))),
            "UG_CONST unsigned short UG_SC_IDX[%d] = {%s};" % (len(idx), ", ".join(map(str, idx))),
+           "/* per cell (in UG_SC_IDX's cell order): its UG_SC_SLOTS candidates' x y z (zeros for a long list) */",
+           "UG_CONST double UG_SC_XYZ[%d] = {%s};" % (len(xyz), ", ".join("%.17g" % x for x in xyz)),
            "#endif"]
     open(out_path, "w").write("\n".join(out) + "\n")
     print("\n".join(report))

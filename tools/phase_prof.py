@@ -43,7 +43,7 @@ def main():
     from urgym_amd.envs import spaces_for
     _, asp = spaces_for(a.task)
     sim.set_autoreset(True, 500)
-    buf = np.zeros(101, np.uint64)
+    buf = np.zeros(104, np.uint64)
     sim.reset()
     sim.sync()
     rc = sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
@@ -93,6 +93,11 @@ def main():
                    "classic_support_cycles", "classic_simplex_cycles", "gjk_recertified"], [float(x) for x in buf[80:101]]))
     out["gjk_per_substep"] = {k: v / max(d["substeps"], 1) for k, v in gj.items()}
     out["gjk_cycles_per_hull_support"] = gj["gjk_hull_support_cycles"] / max(gj["gjk_hull_supports"], 1)
+    # inside a support (cumulative from its start): the cell known, the cell's loads landed (forced wait)
+    sc = dict(zip(["cell", "mem", "cells"], [float(x) for x in buf[101:104]]))
+    out["hull_support_split"] = {"supports_through_a_cell": sc["cells"] / max(gj["gjk_hull_supports"], 1),
+                                 "cycles_to_cell": sc["cell"] / max(gj["gjk_hull_supports"], 1),
+                                 "cycles_to_loads_landed": sc["mem"] / max(sc["cells"], 1)}
     print(json.dumps(out, indent=1))
     sim.close()
 

@@ -35,7 +35,7 @@ namespace ugd {
 #define TEAM 64
 typedef __attribute__((address_space(1))) const double gcdouble;
 typedef __attribute__((address_space(1))) double gdouble;
-#define UG_NPROF 101 /* phase accumulators of the -DUG_PROF build */
+#define UG_NPROF 104 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* a row's J and M^-1 J^T over the NVP = 32 dof slots (robot 12, objects 3 x 6, 2 zero pads) */
@@ -210,7 +210,10 @@ enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_
        PF_EPA_GJK, PF_EPA_SETUP, PF_EPA_SUP, PF_EPA_EXPAND, PF_EPA_BEST,
        /* inside the libccd test and the classic GJK: the support pairs, the simplex work */
        PF_CCD_SUP, PF_CCD_DO, PF_CLS_SUP, PF_CLS_VS,
-       PC_GJK_RECERT /* GJK pairs skipped by the exact certificate re-test (gjk_one) */ };
+       PC_GJK_RECERT, /* GJK pairs skipped by the exact certificate re-test (gjk_one) */
+       /* inside the hull support: the cycles until its cell is known, until its loads have landed (a forced wait,
+        * profiling build only), and the supports that took a cell (not the whole scan) */
+       PF_SUP_CELL, PF_SUP_MEM, PC_SUP_CELLS };
 #define UG_FREE_SPLIT_N 14
 #ifdef UG_PROF
 __device__ static const int kFreeSplit[UG_FREE_SPLIT_N] = {PF_FK, PF_BROAD, PF_HULL, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST,
@@ -357,30 +360,32 @@ __device__ __forceinline__ void hs_scan(int v0, int nv, ugk::gv d, int gl, doubl
 }
 #define UGK_RCPF(x) __builtin_amdgcn_rcpf(x)
 #include "ug_supcell.h"
-/* the direction cell's candidates (supcell_data.h): lane l of the group dots candidate l of the cell's list (a longer
- * list in trips of G), keeping its first maximum with the candidate's key (vertex index x G + lane: the lower vertex
- * wins a tie, and the key names the lane that holds the winner's coordinates) */
+/* the direction cell's candidates (supcell_data.h): lane l of the group dots candidate l of the cell, its coordinates
+ * read straight from the cell's slot (one memory round), keyed by the slot (the list ascends, so the lower slot is the
+ * lower vertex: a tie goes to it, as in maxDot, and the key names the lane that holds the winner's coordinates).  A
+ * cell with a longer list (UG_SC_OVF) walks it in trips of G through the indices, keyed by vertex index x G + lane. */
 __device__ __forceinline__ void hs_cells(int v0, int scb, int cell, ugk::gv d, int gl, double& best, int& key, ugk::gv& bv) {
     constexpr int G = ugd::GJK_G;
     static_assert(UG_SC_SLOTS == G, "one cell slot per lane of a GJK group");
-    const unsigned short* L = &UG_SC_IDX[(scb + cell) * UG_SC_SLOTS];
-    const int s = L[gl], s0 = L[0];
-    if (s0 != UG_SC_OVF) {
-        const double* p = &UG_HULL_V[3 * (v0 + s)];
-        bv = ugk::V3(p[0], p[1], p[2]);
-        best = bv.x * d.x + bv.y * d.y + bv.z * d.z;
-        key = s * G + gl;
-        return;
-    }
+    const int c = scb + cell;
+    const unsigned short* L = &UG_SC_IDX[c * UG_SC_SLOTS];
+    const double* P = &UG_SC_XYZ[(c * UG_SC_SLOTS + gl) * 3];
+    const int s0 = L[0];
+    bv = ugk::V3(P[0], P[1], P[2]); /* loaded with the list head: the common case needs nothing else */
+    const double dd = bv.x * d.x + bv.y * d.y + bv.z * d.z;
+    const bool ovf = s0 == UG_SC_OVF;
+    best = ovf ? best : dd;
+    key = ovf ? key : gl;
+    if (!ovf) return;
     const int cnt = L[1], off = L[2] | (L[3] << 16);
     for (int t = 0; t < cnt; t += G) { /* the list is padded to whole trips */
         const int i = UG_SC_IDX[off + t + gl];
         const double* p = &UG_HULL_V[3 * (v0 + i)];
         const double x = p[0], y = p[1], z = p[2];
-        const double dd = x * d.x + y * d.y + z * d.z;
+        const double e = x * d.x + y * d.y + z * d.z;
         const int k = i * G + gl;
-        if (dd > best || (dd == best && k < key)) {
-            best = dd;
+        if (e > best || (e == best && k < key)) {
+            best = e;
             key = k;
             bv = ugk::V3(x, y, z);
         }
@@ -395,8 +400,18 @@ UGK_FN ugk::gv ugk_hull_support(const ugk::GShape& sh, ugk::gv d) {
     ugk::gv bv = ugk::V3(0.0, 0.0, 0.0);
     const int cell = sh.scb >= 0 ? ugk_sc_cell(d.x, d.y, d.z, sh.sck) : -1;
     ugk::gv r;
+#ifdef UG_PROF
+    if (gl == 0) atomicAdd(&ugd::g_sh.prof[ugd::PF_SUP_CELL], __builtin_readcyclecounter() - t_sup);
+#endif
     if (cell >= 0) { /* a finite direction: its cell holds every vertex that can win the full scan (build_supcells.py) */
         hs_cells(sh.v0, sh.scb, cell, d, gl, best, bi, bv);
+#ifdef UG_PROF
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (gl == 0) {
+            atomicAdd(&ugd::g_sh.prof[ugd::PF_SUP_MEM], __builtin_readcyclecounter() - t_sup);
+            atomicAdd(&ugd::g_sh.prof[ugd::PC_SUP_CELLS], 1ull);
+        }
+#endif
         ugd::group_best(best, bi, true);
         const int src = (int)(threadIdx.x & ~(G - 1)) + (bi & (G - 1));
         r = ugk::V3(__shfl(bv.x, src, TEAM), __shfl(bv.y, src, TEAM), __shfl(bv.z, src, TEAM));
