@@ -150,8 +150,9 @@ int urgym_set_rng(urgym_handle* h, const uint32_t* mt, const int32_t* elapsed);
  * pair's A side; A/B fields exchanged and the normal negated when it names the B side), then body_b, link_a and
  * link_b filter in that orientation.  A pair's A side: the robot link (robot pairs), the object (object-static
  * pairs), the sphere or else the lower-numbered object (object-object pairs).
- * Deviation: positions are the points' body-local anchors under the current poses; Bullet reports the world
- * points of the last narrowphase, taken before that substep's integration (one substep's motion apart). */
+ * Positions: the points' world positions at the last substep's narrowphase (their local anchors under the poses it
+ * saw, kept in the state record before that substep's integration), as Bullet's refreshContactPoints leaves
+ * m_positionWorldOnA/B. */
 int urgym_contact_points(urgym_handle* h, int body_a, int body_b, int link_a, int link_b, int max_pts, double* out,
                          int32_t* count);
 

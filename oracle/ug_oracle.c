@@ -303,6 +303,9 @@ struct ugo_env {
     int pgs_bullet;        /* tests only: solve with the velocity-space Bullet-shaped PGS (pgs_bullet) */
     int flags;             /* UG_FLAG_* of the last step / reset call */
     int stats[UG_NSTAT];   /* UG_STAT_* counters */
+    double prevq[NB];      /* the last substep's narrowphase poses (ug_layout.h UG_F_PREV): the contact query's */
+    v3 prevpos[MAXOBJ];    /* world positions are the points' anchors under these, as Bullet's refreshContactPoints */
+    q4 prevquat[MAXOBJ];   /* leaves m_positionWorldOnA/B */
 };
 
 static void box_collider(collider* c, double hx, double hy, double hz, double margin, double friction) {
@@ -2359,6 +2362,9 @@ static void substep(ugo_env* e) {
         if (r->kind == 2) e->man[r->man].pt[r->pt].imp1 = r->imp;
         else e->man[r->man].pt[r->pt].imp2 = r->imp;
     }
+    /* the poses this substep's narrowphase saw, before they move (the contact query's world positions) */
+    for (int i = 0; i < NB; i++) e->prevq[i] = e->q[i];
+    for (int o = 0; o < MAXOBJ; o++) { e->prevpos[o] = e->opos[o]; e->prevquat[o] = e->oquat[o]; }
     /* velocities += solver delta; positions integrate (v + split velocity) */
     for (int i = 0; i < NB; i++) {
         e->qd[i] = ug_vclamp(e->qd[i] + dv[i], UG_MAX_COORD_VEL);
@@ -3111,8 +3117,9 @@ int ugo_step(ugo_env* e, const float* action, double* obs, double* reward, uint8
  * flag 0, bodyA, bodyB, linkA, linkB, positionOnA[3], positionOnB[3], contactNormalOnB[3], distance,
  * normalForce, lateralFriction1, lateralFrictionDir1[3], lateralFriction2, lateralFrictionDir2[3]; forces are
  * the last solve's impulses / dt, the friction directions btPlaneSpace1 of the normal (the solver's rows),
- * world positions from the points' body-local anchors with the current poses (a deviation: Bullet reports the
- * narrowphase's world points, taken before that substep's integration).  Filters as pybullet applies them
+ * world positions = the points' body-local anchors under the poses of the last substep's narrowphase (prevq /
+ * prevpos / prevquat, taken before that substep's integration) -- Bullet's m_positionWorldOnA/B as its
+ * refreshContactPoints left them.  Filters as pybullet applies them
  * (PhysicsServerCommandProcessor's contact query): the tuple is swapped (A/B fields exchanged, normal negated)
  * when bodyA names the pair's B side, then bodyB / linkA / linkB filter that orientation; a pair's A side is the
  * robot link for robot pairs, the object for object-static pairs, the sphere (else the lower object) for
@@ -3126,10 +3133,18 @@ static int link_of_collider(const scene* s, int ci) {
 }
 static int match(int want, int have) { return want == -1 || want == have; }
 static int match_link(int want, int have) { return want == -2 || want == have; }
+/* an owner frame as the last substep's narrowphase saw it (the poses in prevq / prevpos / prevquat) */
+static xf prev_owner_xf(const ugo_env* e, const kin* k, int owner) {
+    xf T;
+    if (owner >= 0) { T.R = k->R[owner]; T.p = k->p[owner]; }
+    else if (owner <= -2 && owner > -100) { int o = -2 - owner; T.R = qmat(e->prevquat[o]); T.p = e->prevpos[o]; }
+    else { T.R = mident(); T.p = V(0, 0, 0); }
+    return T;
+}
 int ugo_contact_points(const ugo_env* e, int bodyA, int bodyB, int linkA, int linkB, double* out, int max_pts) {
     const scene* s = &e->sc;
     kin k;
-    fk(e->q, &k);
+    fk(e->prevq, &k); /* the narrowphase's poses: Bullet reports m_positionWorldOnA/B from its last refresh */
     int cnt = 0;
     for (int m = 0; m < e->nman; m++) {
         const manifold* M = &e->man[m];
@@ -3146,7 +3161,7 @@ int ugo_contact_points(const ugo_env* e, int bodyA, int bodyB, int linkA, int li
         }
         if (!match(bodyB, swap ? ea : eb) || !match_link(linkA, swap ? lb : la) || !match_link(linkB, swap ? la : lb))
             continue;
-        xf OA = owner_xf(e, &k, s->col[P->a].owner), OB = owner_xf(e, &k, s->col[P->b].owner);
+        xf OA = prev_owner_xf(e, &k, s->col[P->a].owner), OB = prev_owner_xf(e, &k, s->col[P->b].owner);
         for (int j = 0; j < M->npts; j++) {
             const cpoint* c = &M->pt[j];
             if (cnt < max_pts) {
@@ -3305,6 +3320,11 @@ void ugo_get_state(const ugo_env* e, double* s) {
     s[i++] = e->goal_grasped;
     s[i++] = e->overflow;
     s[i++] = e->goal_closed;
+    for (int j = 0; j < NB; j++) s[i++] = e->prevq[j];
+    for (int o = 0; o < MAXOBJ; o++) {
+        s[i++] = e->prevpos[o].x; s[i++] = e->prevpos[o].y; s[i++] = e->prevpos[o].z;
+        s[i++] = e->prevquat[o].x; s[i++] = e->prevquat[o].y; s[i++] = e->prevquat[o].z; s[i++] = e->prevquat[o].w;
+    }
 }
 void ugo_set_state(ugo_env* e, const double* s) {
     int i = 0;
@@ -3336,6 +3356,11 @@ void ugo_set_state(ugo_env* e, const double* s) {
     e->goal_grasped = (int)s[i++];
     e->overflow = (int)s[i++];
     e->goal_closed = (int)s[i++];
+    for (int j = 0; j < NB; j++) e->prevq[j] = s[i++];
+    for (int o = 0; o < MAXOBJ; o++) {
+        e->prevpos[o].x = s[i++]; e->prevpos[o].y = s[i++]; e->prevpos[o].z = s[i++];
+        e->prevquat[o].x = s[i++]; e->prevquat[o].y = s[i++]; e->prevquat[o].z = s[i++]; e->prevquat[o].w = s[i++];
+    }
 }
 void ugo_rng_seed(ugo_env* e, uint32_t seed) { mt_seed(&e->rng, seed); }
 double ugo_rng_random(ugo_env* e) { return mt_random(&e->rng); }

@@ -564,8 +564,9 @@ __global__ void __launch_bounds__(WAVE) k_ik(const double* S, int n, const doubl
  * 1 + i object i, 10 table, 11 plane, 12 pitch, -1 any), links (robot link index, object base -1 / club parts
  * 0, 1, -2 any), 24 doubles per point in pybullet's tuple order, forces = impulse / dt, friction directions
  * btPlaneSpace1 of the normal; the tuple is swapped when bodyA names the pair's B side, and bodyB / linkA /
- * linkB filter in that orientation (pybullet's order).  Positions use the current poses (Bullet: the
- * narrowphase's world points, before that substep's integration -- a documented deviation). */
+ * linkB filter in that orientation (pybullet's order).  Positions are the points' local anchors under the poses of
+ * the last substep's narrowphase (the state's UG_F_PREV record, taken before that substep's integration): Bullet's
+ * m_positionWorldOnA/B as refreshContactPoints left them. */
 __device__ static int link_of_collider(const Scene* s, int ci) {
     const Collider& c = s->col[ci];
     if (c.ent == 0) return c.link;
@@ -579,7 +580,17 @@ __global__ void __launch_bounds__(WAVE) k_contacts(const Scene* sc, const double
     if (i >= n) return;
     const EnvState& e = *(const EnvState*)(S + (size_t)i * UG_STATE_DIM);
     Kin k;
-    fk(e.q, k);
+    fk(e.prevq, k); /* the last narrowphase's poses */
+    auto prev_xf = [&](int owner) {
+        XF T;
+        if (owner >= 0) { T.R = k.R[owner]; T.p = k.p[owner]; }
+        else if (owner <= -2 && owner > -100) {
+            const double* P = e.prevpose[-2 - owner];
+            T.R = qmat(Q(P[3], P[4], P[5], P[6]));
+            T.p = V(P[0], P[1], P[2]);
+        } else { T.R = mident(); T.p = V(0, 0, 0); }
+        return T;
+    };
     int cnt = 0;
     const int nm = (int)e.nman;
     for (int m = 0; m < nm; m++) {
@@ -596,7 +607,7 @@ __global__ void __launch_bounds__(WAVE) k_contacts(const Scene* sc, const double
             else continue;
         }
         if (!mt(bodyB, swap ? ea : eb) || !ml(linkA, swap ? lb : la) || !ml(linkB, swap ? la : lb)) continue;
-        const XF OA = owner_xf(e, k, sc->col[P.a].owner), OB = owner_xf(e, k, sc->col[P.b].owner);
+        const XF OA = prev_xf(sc->col[P.a].owner), OB = prev_xf(sc->col[P.b].owner);
         const int np = (int)M.npts;
         for (int j = 0; j < np; j++) {
             const StPt& c = M.pt[j];

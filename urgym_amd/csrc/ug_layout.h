@@ -26,7 +26,12 @@
 #define UG_F_NMAN (UG_F_OBJ + UG_MAXOBJ * UG_OBJ_DOUBLES)
 #define UG_F_MAN (UG_F_NMAN + 1)   /* per manifold: pair, npts, 4 x (lpA3 lpB3 n3 dist imp imp1 imp2) */
 #define UG_F_TASK (UG_F_MAN + UG_MAXMAN * UG_MAN_DOUBLES)   /* approached, grasped, overflow (dropped contacts), spare */
-#define UG_STATE_DIM (UG_F_TASK + 4)
+/* the poses of the last substep's narrowphase (q, then per object pos3 quat4), taken before that substep's
+ * integration: the manifold points' world positions as Bullet reports them (m_positionWorldOnA/B, set by
+ * refreshContactPoints at narrowphase time) are their local anchors under these poses (urgym_contact_points) */
+#define UG_F_PREV (UG_F_TASK + 4)
+#define UG_PREV_DOUBLES (12 + 7 * UG_MAXOBJ)
+#define UG_STATE_DIM (UG_F_PREV + UG_PREV_DOUBLES)
 
 /* per-env event counters (urgym_get_stats / ugo_get_stats), cumulative over the handle's life */
 #define UG_STAT_UNSTABLE 0   /* wait_until_stable loops that hit 480 substeps without settling (env_*:102-103) */

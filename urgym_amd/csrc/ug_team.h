@@ -105,6 +105,7 @@ struct EnvState {
     double nman;
     StMan man[MAXMAN];
     double goal_approached, goal_grasped, overflow, spare;
+    double prevq[NB], prevpose[MAXOBJ][7]; /* the last substep's narrowphase poses (ug_layout.h UG_F_PREV) */
 };
 static_assert(sizeof(EnvState) == UG_STATE_DIM * sizeof(double), "EnvState must match ug_layout.h");
 static_assert(sizeof(Manifold) * MAXOV <= 88 * MAXROWS, "working manifolds must fit in the rows' LDS");
@@ -3378,6 +3379,14 @@ __device__ __noinline__ static void serial_post(const Scene* s, int split) {
     if (lane == 0) {
         const double* DV = sh.dvout;
         const double* DVS = sh.dvsout;
+        /* the poses this substep's narrowphase saw, before they move (the contact query's world positions) */
+        for (int i = 0; i < NB; i++) e.prevq[i] = e.q[i];
+        for (int o = 0; o < MAXOBJ; o++) {
+            const StObj& ob = e.obj[o];
+            e.prevpose[o][0] = ob.pos.x; e.prevpose[o][1] = ob.pos.y; e.prevpose[o][2] = ob.pos.z;
+            e.prevpose[o][3] = ob.quat.x; e.prevpose[o][4] = ob.quat.y; e.prevpose[o][5] = ob.quat.z;
+            e.prevpose[o][6] = ob.quat.w;
+        }
         for (int i = 0; i < NB; i++) {
             e.qd[i] = ug_vclamp(e.qd[i] + DV[i], UG_MAX_COORD_VEL);
             double vi = split ? e.qd[i] + DVS[i] : e.qd[i];

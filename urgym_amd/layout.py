@@ -24,6 +24,7 @@ F_Q, F_QD, F_MTARGET, F_MON = _L["UG_F_Q"], _L["UG_F_QD"], _L["UG_F_MTARGET"], _
 F_OACTIVE, F_OBJ, OBJ_DOUBLES = _L["UG_F_OACTIVE"], _L["UG_F_OBJ"], _L["UG_OBJ_DOUBLES"]
 F_NMAN, F_MAN, MAN_DOUBLES, PT_DOUBLES = _L["UG_F_NMAN"], _L["UG_F_MAN"], _L["UG_MAN_DOUBLES"], _L["UG_PT_DOUBLES"]
 F_TASK, STATE_DIM = _L["UG_F_TASK"], _L["UG_STATE_DIM"]
+F_PREV = _L["UG_F_PREV"]  # the last narrowphase's poses: q (12), then per object pos3 quat4
 MT_WORDS = _L["UG_MT_WORDS"]
 
 
