@@ -97,7 +97,7 @@ def main():
     sc = dict(zip(["cell", "mem", "cells"], [float(x) for x in buf[101:104]]))
     out["hull_support_split"] = {"supports_through_a_cell": sc["cells"] / max(gj["gjk_hull_supports"], 1),
                                  "cycles_to_cell": sc["cell"] / max(gj["gjk_hull_supports"], 1),
-                                 "cycles_to_loads_landed": sc["mem"] / max(sc["cells"], 1)}
+                                 "cycles_to_reduced": sc["mem"] / max(sc["cells"], 1)}
     print(json.dumps(out, indent=1))
     sim.close()
 

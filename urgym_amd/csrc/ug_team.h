@@ -361,62 +361,75 @@ __device__ __forceinline__ void hs_scan(int v0, int nv, ugk::gv d, int gl, doubl
 }
 #define UGK_RCPF(x) __builtin_amdgcn_rcpf(x)
 #include "ug_supcell.h"
-/* the direction cell's candidates (supcell_data.h): lane l of the group dots candidate l of the cell, its coordinates
- * read straight from the cell's slot (one memory round), keyed by the slot (the list ascends, so the lower slot is the
- * lower vertex: a tie goes to it, as in maxDot, and the key names the lane that holds the winner's coordinates).  A
- * cell with a longer list (UG_SC_OVF) walks it in trips of G through the indices, keyed by vertex index x G + lane. */
-__device__ __forceinline__ void hs_cells(int v0, int scb, int cell, ugk::gv d, int gl, double& best, int& key, ugk::gv& bv) {
+/* the direction cell's candidates (supcell_data.h).  Lane l of the group dots candidate l of the cell, its coordinates
+ * read straight from the cell's slot (one memory round).  The list ascends, so the first maximal dot product over it
+ * is the lowest lane holding the group's maximum: a DPP max of the dot products (all finite on this path), then the
+ * lowest lane of the group whose product equals it (a ballot), whose coordinates the group reads.  A cell with a
+ * longer list (UG_SC_OVF, tied flat faces) walks it in trips of G through the vertex indices instead, keeping each
+ * lane's first maximum keyed by vertex index x G + lane, and takes the group's arg-max. */
+__device__ __forceinline__ double group_max(double x) {
+    x = ug_max(x, ugd::dpp<0xB1>(x));
+    x = ug_max(x, ugd::dpp<0x4E>(x));
+    x = ug_max(x, ugd::dpp<0x141>(x));
+    return ug_max(x, ugd::dpp<0x140>(x));
+}
+__device__ __forceinline__ ugk::gv hs_cells(int v0, int scb, int cell, ugk::gv d, int gl) {
     constexpr int G = ugd::GJK_G;
     static_assert(UG_SC_SLOTS == G, "one cell slot per lane of a GJK group");
     const int c = scb + cell;
     const unsigned short* L = &UG_SC_IDX[c * UG_SC_SLOTS];
     const double* P = &UG_SC_XYZ[(c * UG_SC_SLOTS + gl) * 3];
     const int s0 = L[0];
-    bv = ugk::V3(P[0], P[1], P[2]); /* loaded with the list head: the common case needs nothing else */
-    const double dd = bv.x * d.x + bv.y * d.y + bv.z * d.z;
-    const bool ovf = s0 == UG_SC_OVF;
-    best = ovf ? best : dd;
-    key = ovf ? key : gl;
-    if (!ovf) return;
-    const int cnt = L[1], off = L[2] | (L[3] << 16);
-    for (int t = 0; t < cnt; t += G) { /* the list is padded to whole trips */
-        const int i = UG_SC_IDX[off + t + gl];
-        const double* p = &UG_HULL_V[3 * (v0 + i)];
-        const double x = p[0], y = p[1], z = p[2];
-        const double e = x * d.x + y * d.y + z * d.z;
-        const int k = i * G + gl;
-        if (e > best || (e == best && k < key)) {
-            best = e;
-            key = k;
-            bv = ugk::V3(x, y, z);
+    ugk::gv bv = ugk::V3(P[0], P[1], P[2]); /* loaded with the list head: the common case needs nothing else */
+    const int base = (int)(threadIdx.x & ~(G - 1));
+    int src;
+    if (s0 != UG_SC_OVF) {
+        const double dd = bv.x * d.x + bv.y * d.y + bv.z * d.z;
+        const double M = group_max(dd);
+        const unsigned long long hit = ugd::ballot(dd == M);
+        src = base + __builtin_ctzll((hit >> base) & ((1ull << G) - 1ull));
+    } else {
+        double best = -__builtin_inf();
+        int key = 0x7fffffff;
+        const int cnt = L[1], off = L[2] | (L[3] << 16);
+        for (int t = 0; t < cnt; t += G) { /* the list is padded to whole trips */
+            const int i = UG_SC_IDX[off + t + gl];
+            const double* p = &UG_HULL_V[3 * (v0 + i)];
+            const double x = p[0], y = p[1], z = p[2];
+            const double e = x * d.x + y * d.y + z * d.z;
+            const int k = i * G + gl;
+            if (e > best || (e == best && k < key)) {
+                best = e;
+                key = k;
+                bv = ugk::V3(x, y, z);
+            }
         }
+        ugd::group_best(best, key, true);
+        src = base + (key & (G - 1));
     }
+    return ugk::V3(__shfl(bv.x, src, TEAM), __shfl(bv.y, src, TEAM), __shfl(bv.z, src, TEAM));
 }
 UGK_FN ugk::gv ugk_hull_support(const ugk::GShape& sh, ugk::gv d) {
     constexpr int G = ugd::GJK_G;
     const int gl = threadIdx.x & (G - 1);
     PROF_T0(t_sup);
-    double best = -__builtin_inf();
-    int bi = 0x7fffffff;
-    ugk::gv bv = ugk::V3(0.0, 0.0, 0.0);
     const int cell = sh.scb >= 0 ? ugk_sc_cell(d.x, d.y, d.z, sh.sck) : -1;
     ugk::gv r;
 #ifdef UG_PROF
     if (gl == 0) atomicAdd(&ugd::g_sh.prof[ugd::PF_SUP_CELL], __builtin_readcyclecounter() - t_sup);
 #endif
     if (cell >= 0) { /* a finite direction: its cell holds every vertex that can win the full scan (build_supcells.py) */
-        hs_cells(sh.v0, sh.scb, cell, d, gl, best, bi, bv);
+        r = hs_cells(sh.v0, sh.scb, cell, d, gl);
 #ifdef UG_PROF
-        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (gl == 0) {
             atomicAdd(&ugd::g_sh.prof[ugd::PF_SUP_MEM], __builtin_readcyclecounter() - t_sup);
             atomicAdd(&ugd::g_sh.prof[ugd::PC_SUP_CELLS], 1ull);
         }
 #endif
-        ugd::group_best(best, bi, true);
-        const int src = (int)(threadIdx.x & ~(G - 1)) + (bi & (G - 1));
-        r = ugk::V3(__shfl(bv.x, src, TEAM), __shfl(bv.y, src, TEAM), __shfl(bv.z, src, TEAM));
     } else {
+        double best = -__builtin_inf();
+        int bi = 0x7fffffff;
+        ugk::gv bv = ugk::V3(0.0, 0.0, 0.0);
         hs_scan(sh.v0, sh.nv, d, gl, best, bi, bv);
         ugd::group_best(best, bi, true);
         if (bi == 0x7fffffff) { /* no comparable dot product (a NaN direction): vertex 0, as maxDot leaves it */
