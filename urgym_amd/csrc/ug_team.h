@@ -3038,6 +3038,16 @@ __device__ __forceinline__ void swap16_d(double& x, double& y) {
 #define FG_NC 16
 #define FG_F0 44
 #define FG_NF 52
+/* Golf's narrower solves (tools/row_hist.py UG_TASK=3: 12-13 non-contact rows, 4-17 normals, 2 friction rows per
+ * normal + 2 rolling rows, all 50 sweeps): a single-slot layout for up to 12 normals (friction + rolling from 28,
+ * 64 positions) and a two-slot one for up to 18 (friction + rolling from 34, 74 positions), so a solve's pads stay
+ * a fraction of its rows instead of filling FG's 96 positions or taking the chunked general path */
+#define FG12_NC 16
+#define FG12_F0 28
+#define FG12_NF 36
+#define FG18_NC 16
+#define FG18_F0 34
+#define FG18_NF 40
 template <int NC_, int F0_, int NF_>
 struct FLShape {
     static constexpr int NC = NC_, F0 = F0_, NF = NF_;
@@ -3558,9 +3568,15 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     const int flf0 = (fb <= FL_F0S && n - fb <= FL_NFS) ? FL_F0S : FL_F0;
     /* the single-slot layout: few normals (CubesPush 8, CubesGrasp 4-6), up to 20 non-contact rows */
     const bool fsok = !flok && nnc <= FS_NC && nn >= 3 && nn <= FS_F0 - FS_NC && n - fb <= FS_NF;
-    const bool fgok = !flok && !fsok && nnc <= FG_NC && nn >= 16 && nn <= FG_F0 - FG_NC && n - fb <= FG_NF;
+    const bool g12ok = !flok && !fsok && nnc <= FG12_NC && nn >= 3 && nn <= FG12_F0 - FG12_NC && n - fb <= FG12_NF;
+    const bool g18ok = !flok && !fsok && !g12ok && nnc <= FG18_NC && nn >= 3 && nn <= FG18_F0 - FG18_NC &&
+                       n - fb <= FG18_NF;
+    const bool fgok = !flok && !fsok && !g12ok && !g18ok && nnc <= FG_NC && nn >= 16 && nn <= FG_F0 - FG_NC &&
+                      n - fb <= FG_NF;
     const PosMap pm = flok ? PosMap{n, fb, flf0, nnc, nnc, flf0 + 2 * (flf0 - FL_NNC)}
                       : fsok ? PosMap{n, fb, FS_F0, nnc, FS_NC, FS_F0 + FS_NF}
+                      : g12ok ? PosMap{n, fb, FG12_F0, nnc, FG12_NC, FG12_F0 + FG12_NF}
+                      : g18ok ? PosMap{n, fb, FG18_F0, nnc, FG18_NC, FG18_F0 + FG18_NF}
                       : fgok ? PosMap{n, fb, FG_F0, nnc, FG_NC, FG_F0 + FG_NF}
                              : PosMap{n, fb, 0, nnc, nnc, n};
 #endif
@@ -3858,11 +3874,12 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         }
         return split;
     };
-    /* the single-slot fixed layout (FS_*): even sweeps the non-contact positions reversed then the normal
-     * positions, odd sweeps [0, FS_F0) forward, then the friction positions -- the general path's row order with
+    /* the single-slot fixed layouts (FS_*, FG12_*): even sweeps the non-contact positions reversed then the normal
+     * positions, odd sweeps [0, F0) forward, then the friction positions -- the general path's row order with
      * neutral pads and no chunk tests; one u register (all positions < 64) */
-    auto passes_fs = [&]() -> int {
-        constexpr int NC = FS_NC, F0 = FS_F0, NF = FS_NF;
+    auto passes_fs = [&](auto shape) -> int {
+        constexpr int NC = decltype(shape)::NC, F0 = decltype(shape)::F0, NF = decltype(shape)::NF;
+        static_assert(F0 + NF <= 64, "a single-slot layout");
         const int nf = n - fb;
         int split = 0;
         PROF_T0(t_sw);
@@ -3925,7 +3942,9 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         return split;
     };
     PROF_T0(t_post);
-    const int split = pm.fl == FS_F0          ? passes_fs()
+    const int split = pm.fl == FS_F0          ? passes_fs(FLShape<FS_NC, FS_F0, FS_NF>{})
+                      : pm.fl == FG12_F0      ? passes_fs(FLShape<FG12_NC, FG12_F0, FG12_NF>{})
+                      : pm.fl == FG18_F0      ? passes_fl(FLShape<FG18_NC, FG18_F0, FG18_NF>{})
                       : pm.fl == FG_F0        ? passes_fl(FLShape<FG_NC, FG_F0, FG_NF>{})
                       : pm.fl == FL_F0S       ? passes_fl(FLShape<FL_NNC, FL_F0S, FL_NFS>{})
                       : pm.fl                 ? passes_fl(FLShape<FL_NNC, FL_F0, FL_NF>{})
