@@ -17,12 +17,14 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math", 
          "-S"]
 
 
-def _isa(src, out, defs=()):
+def _isa(src, out, defs=(), ra=False):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
     subprocess.run([HIPCC] + FLAGS + list(defs) + ["-o", str(out), src], check=True, cwd=ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import scc_audit
+    if ra:
+        return scc_audit.audit(str(out)), scc_audit.ra_audit(open(out).read().split("\n"))
     return scc_audit.audit(str(out))
 
 
@@ -33,5 +35,21 @@ def test_audit_flags_the_reproducer(tmp_path):
 
 @pytest.mark.parametrize("defs", [(), ("-DUG_ROBOT_R140",)], ids=["ur5_robotiq_85", "ur5_robotiq_140"])
 def test_shipped_library_has_no_scc_clobbered_pick(tmp_path, defs):
-    hits = _isa(os.path.join(ROOT, "urgym_amd", "csrc", "ug_capi.hip"), tmp_path / "ug.s", defs)
+    """both miscompiles: no SCC reader fed by a frame-address add, and no device function that overwrites its unsaved
+    return address (a long branch through s[30:31] in a leaf function; team_pgs carries a never-taken call so it is
+    not a leaf -- see ug_nonleaf_guard in ug_team.h)"""
+    hits, ra = _isa(os.path.join(ROOT, "urgym_amd", "csrc", "ug_capi.hip"), tmp_path / "ug.s", defs, ra=True)
     assert hits == [], hits
+    assert ra == [], ra
+
+
+def test_return_address_audit_flags_a_leaf_long_branch():
+    """the shape the round-5 team_pgs build had: a leaf function whose long branch goes through s[30:31]"""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import scc_audit
+    leaf = ["_Z4leafv:", "\ts_cbranch_scc0 .LBB0_2", "\ts_getpc_b64 s[30:31]", ".Lpost_getpc0:",
+            "\ts_add_u32 s30, s30, (.LBB0_9-.Lpost_getpc0)&4294967295", "\ts_addc_u32 s31, s31, (.LBB0_9-.Lpost_getpc0)>>32",
+            "\ts_setpc_b64 s[30:31]", ".LBB0_2:", "\ts_setpc_b64 s[30:31]", ".Lfunc_end0:"]
+    assert [h[0] for h in scc_audit.ra_audit(leaf)] == ["_Z4leafv"]
+    saved = leaf[:1] + ["\tv_writelane_b32 v255, s30, 0", "\tv_writelane_b32 v255, s31, 1"] + leaf[1:]
+    assert scc_audit.ra_audit(saved) == []

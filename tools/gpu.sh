@@ -34,6 +34,8 @@ step() { # step <seconds> <log> <cmd...>: run under a limit, show the tail, stop
 case "$JOB" in
 tests)
     if [ $# -eq 0 ]; then set -- tests -m gpu; fi
+    # page the image in first (a fresh box's first `import torch` can take minutes), printing as it goes
+    step 300 "$OUT/warm.log" python -u -c "print('importing torch', flush=True); import torch; print('cuda', torch.cuda.is_available(), flush=True)" &&
     step 1500 "$OUT/tests.log" python -u -m pytest -x -v --timeout 400 --timeout-method thread "$@" ;;
 smoke)
     step 300 "$OUT/smoke.log" python -c "import __graft_entry__ as g; g.smoke()" ;;

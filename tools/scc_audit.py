@@ -5,6 +5,12 @@ s_cselect / s_cmov / s_cbranch_scc that reads it.  In the run-time-indexed team_
 turned `nR < 3 ? R1 : R2` into "always R2".  Reports every SCC reader whose last SCC writer in straight-line code
 is such a frame-address add.
 
+Also audits the second miscompile met on this toolchain (round 5): LLVM's branch relaxation expands a branch beyond
++-32 Ki instructions into s_getpc_b64 / s_add_u32 / s_addc_u32 / s_setpc_b64 through a scavenged SGPR pair, and in a
+leaf device function it scavenged s[30:31] -- the return address, which a leaf function never saves -- so the
+function's return jumped into its own body (team_pgs: a kernel that never finished).  ra_audit() reports every
+non-kernel function that writes s30 or s31 without first saving them (v_writelane_b32 vN, s30 / s31).
+
 usage: python tools/scc_audit.py file.s   (make one with: hipcc ... --cuda-device-only -S -o file.s)"""
 import re
 import sys
@@ -33,6 +39,35 @@ def audit(path):
     return hits
 
 
+RA_DEST = re.compile(r"^\s*(s_\w+|v_readlane_b32|v_readfirstlane_b32)\s+(s(\d+)|s\[(\d+):(\d+)\])\s*(,|$)")
+RA_SAVE = re.compile(r"^\s*(v_writelane_b32\s+v\d+,\s*s3[01]\b|s_mov_b64\s+s\[\d+:\d+\],\s*s\[30:31\])")
+
+
+def ra_audit(lines):
+    """functions returning through s[30:31] that overwrite s30 / s31 without saving them first: (function, line no,
+    instruction) of the first such write"""
+    hits, fn, saved, first = [], None, False, None
+    for no, line in enumerate(lines, 1):
+        if re.match(r"^[_A-Za-z0-9.$]+:", line) and not line.startswith(".L"):
+            fn, saved, first = line.split(":")[0], False, None
+            continue
+        if fn is None:
+            continue
+        if RA_SAVE.match(line):
+            saved = True
+        m = RA_DEST.match(line)
+        if m and not line.strip().startswith("s_setpc_b64") and not saved and first is None:
+            lo = int(m.group(3) or m.group(4))
+            hi = int(m.group(3) or m.group(5))
+            if lo <= 31 and hi >= 30 and not m.group(1).startswith(("s_cmp", "s_bitcmp")):
+                first = (no, line.strip())
+        if line.startswith(".Lfunc_end"):
+            if first is not None and any("s_setpc_b64 s[30:31]" in l for l in lines[max(0, no - 40):no]):
+                hits.append((fn, first[0], first[1]))
+            fn = None
+    return hits
+
+
 if __name__ == "__main__":
     total = 0
     for p in sys.argv[1:]:
@@ -41,4 +76,9 @@ if __name__ == "__main__":
         for fn, wl, w, rl, r in h:
             print(f"{p}:{rl}: {r}   <- SCC from line {wl}: {w}   [{fn}]")
         print(f"{p}: {len(h)} SCC reader(s) fed by a frame-address s_add_i32")
+        r = ra_audit(open(p).read().split("\n"))
+        total += len(r)
+        for fn, no, ins in r:
+            print(f"{p}:{no}: {ins}   <- writes the unsaved return address [{fn}]")
+        print(f"{p}: {len(r)} function(s) overwriting an unsaved return address")
     sys.exit(1 if total else 0)
