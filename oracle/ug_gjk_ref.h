@@ -24,6 +24,11 @@
  *   cylinder  CylinderLocalSupportZ over the implicit dimensions (outer - margin)      its collision margin
  * The kernels restate the same algorithm in urgym_amd/csrc/ug_gjk.h (a separate implementation: wave-parallel
  * support queries, indices instead of pointers, the recursions unrolled); GPU == this file bit for bit.
+ *
+ * Provenance: the algorithms and constants are Bullet3's (btGjkPairDetector, btVoronoiSimplexSolver, btGjkEpa2, the
+ * libccd-derived intersection test; Bullet3 is zlib-licensed, (c) Erwin Coumans and contributors; libccd is
+ * BSD-licensed, (c) Daniel Fiser), restated from their published description -- no Bullet source is in this
+ * repository or in /root/reference.  tests/test_gjk_independent.py pins the answers to exact geometry.
  */
 #ifndef UG_GJK_REF_H
 #define UG_GJK_REF_H

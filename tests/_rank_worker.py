@@ -21,6 +21,8 @@ def main():
     obs = ids[:, None] * 10 + torch.arange(od, dtype=torch.float64)[None, :]
     g = gather_returns(obs, ids * 0.5, (ids.long() % 3) == 0, (ids.long() % 5) == 0, final_obs=-obs,
                        success=(ids.long() % 7) == 0, substeps=ids.to(torch.int32) + 10)
+    t = gather_returns(obs, ids * 0.5, (ids.long() % 3) == 0, (ids.long() % 5) == 0, as_tuple=True)  # round-3 form
+    assert len(t) == 4 and all(torch.equal(a, g[k]) for a, k in zip(t, ("obs", "reward", "terminated", "truncated")))
     if rank == 0:
         json.dump({"world": world, "obs": g["obs"].tolist(), "rew": g["reward"].tolist(), "term": g["terminated"].tolist(),
                    "trunc": g["truncated"].tolist(), "final": g["final_obs"].tolist(), "succ": g["success"].tolist(),

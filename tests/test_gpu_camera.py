@@ -146,4 +146,14 @@ def test_vector_env_camera_hook(mods):
     venv.step(acts(2, np.random.default_rng(1), 4))
     r, d, s = cam.shot_batch(venv.sim)
     assert np.array_equal(venv.camera_obs["depth"], d) and np.array_equal(venv.camera_obs["seg"], s)
+    # a state change through the handle before the batch is read renders the step's state first
+    venv.step(acts(2, np.random.default_rng(2), 4))
+    r2, d2, s2 = cam.shot_batch(venv.sim)
+    st = venv.sim.get_state()
+    st[:, :6] += 0.3  # swing the arm: a different image
+    venv.sim.set_state(st)
+    assert np.array_equal(venv.camera_obs["depth"], d2) and np.array_equal(venv.camera_obs["seg"], s2)
+    assert not np.array_equal(cam.shot_batch(venv.sim)[1], d2)
+    venv.camera_obs = None  # assignable, as the single env's attribute
+    assert venv.camera_obs is None
     venv.close()

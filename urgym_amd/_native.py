@@ -121,6 +121,13 @@ class Sim:
         self.act_dim = self.L.urgym_act_dim(task)
         self.state_dim = self.L.urgym_state_dim()
         self.ndraw = self.L.urgym_num_draws(task)
+        # callables run before any call that changes the simulated state (the vector env's deferred camera batch
+        # renders there, so its images stay those of the state its last step / reset returned)
+        self.before_mutate = []
+
+    def _mutating(self):
+        for f in self.before_mutate:
+            f()
 
     def _chk(self, rc, what):
         if rc != 0:
@@ -141,6 +148,7 @@ class Sim:
         self._chk(self.L.urgym_set_autoreset(self.h, int(enable), int(max_episode_steps)), "urgym_set_autoreset")
 
     def reset(self, mask=None, draws=None, obs=None):
+        self._mutating()
         if obs is None:
             obs = np.zeros((self.n, self.obs_dim))
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
@@ -149,6 +157,7 @@ class Sim:
         return obs
 
     def step(self, actions):
+        self._mutating()
         a = np.ascontiguousarray(actions, dtype=np.float32).reshape(self.n, self.act_dim)
         n = self.n
         out = dict(obs=np.zeros((n, self.obs_dim)), final_obs=np.zeros((n, self.obs_dim)), reward=np.zeros(n),
@@ -161,6 +170,7 @@ class Sim:
 
     def step_device(self, d_act, d_obs, d_final=0, d_rew=0, d_term=0, d_trunc=0, d_succ=0, d_sub=0):
         """Device-pointer variant (ints = device addresses, e.g. torch.Tensor.data_ptr())."""
+        self._mutating()
         v = ctypes.c_void_p
         self._chk(self.L.urgym_step_device(self.h, v(d_act), v(d_obs), v(d_final or None), v(d_rew or None),
                                            v(d_term or None), v(d_trunc or None), v(d_succ or None),
@@ -178,10 +188,12 @@ class Sim:
         return s
 
     def set_state(self, s):
+        self._mutating()
         s = np.ascontiguousarray(s, dtype=np.float64).reshape(self.n, self.state_dim)
         self._chk(self.L.urgym_set_state(self.h, ptr(s)), "urgym_set_state")
 
     def substep(self):
+        self._mutating()
         self._chk(self.L.urgym_substep(self.h), "urgym_substep")
 
     def link_state(self, link):

@@ -17,6 +17,9 @@
  * 132 support vertices, 256 faces, their lists) lives in the env's global workspace (EpaMem, L2-resident); EPA's
  * recursive horizon walk (expand) runs on an explicit stack.
  *
+ * Provenance: the algorithms and constants are Bullet3's (zlib licence, (c) Erwin Coumans and contributors; its GJK
+ * intersection test follows libccd, BSD licence, (c) Daniel Fiser), restated -- no Bullet source is copied here.
+ *
  * The includer defines UGK_FN (the function qualifier: `__device__ static inline` in the kernels, `static inline` in
  * tools/gjk_host.cpp, the host build that checks this file against the oracle on the CPU) and, after including it,
  * ugk_hull_support (declared below).

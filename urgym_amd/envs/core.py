@@ -108,6 +108,14 @@ class URGymVectorEnv(_VecBase):
         self.sim.set_autoreset(True, self.max_episode_steps)
         self.render_mode = render_mode  # accepted; there is no GUI ('human' opens no window: documented deviation)
         self.camera, self._camera_obs, self._camera_dirty = camera, None, False
+        # a state change outside step / reset (sim.set_state, sim.substep, ...) renders the pending batch first
+        self.sim.before_mutate.append(self._render_pending)
+
+    def _render_pending(self):
+        if self._camera_dirty:  # every env's image, one launch per 65,535 envs
+            rgb, depth, seg = self.camera.shot_batch(self.sim)
+            self._camera_obs = dict(rgb=rgb, depth=depth, seg=seg)
+            self._camera_dirty = False
 
     def _shoot(self):
         # the reference shoots in get_observation but returns only the vector observation (env_cubes_grasp_v0.py,
@@ -117,11 +125,14 @@ class URGymVectorEnv(_VecBase):
 
     @property
     def camera_obs(self):
-        if self._camera_dirty:  # every env's image, one launch per 65,535 envs
-            rgb, depth, seg = self.camera.shot_batch(self.sim)
-            self._camera_obs = dict(rgb=rgb, depth=depth, seg=seg)
-            self._camera_dirty = False
+        """the camera batch of the state the last step / reset returned (rendered on first read, or before the state
+        changes through the handle, whichever comes first); None without a camera"""
+        self._render_pending()
         return self._camera_obs
+
+    @camera_obs.setter
+    def camera_obs(self, value):  # as the single env's plain attribute: an assignment replaces the pending batch
+        self._camera_obs, self._camera_dirty = value, False
 
     def reset(self, *, seed=None, options=None):
         obs = self.sim.reset()

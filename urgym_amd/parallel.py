@@ -94,12 +94,17 @@ class ReturnGather:
                 "truncated": v["truncated"] > 0.5, "success": v["success"] > 0.5, "substeps": v["substeps"].to(torch.int32)}
 
 
-def gather_returns(obs, reward, terminated, truncated, final_obs=None, success=None, substeps=None, group=None):
+def gather_returns(obs, reward, terminated, truncated, final_obs=None, success=None, substeps=None, group=None,
+                   as_tuple=False):
     """One-off form of ReturnGather (tests, scripts): every field gathered, missing ones as zeros; returns the
-    decoded dict in global env-id order.  Per-step loops keep one ReturnGather instead."""
+    decoded dict in global env-id order -- or, with as_tuple=True, the round-3 form (obs, reward, terminated,
+    truncated) that earlier callers unpack.  Per-step loops keep one ReturnGather instead."""
     n, o = obs.shape
     g = ReturnGather(n, o, obs.device, group)
     z = torch.zeros(n, dtype=torch.float64)
     g.gather(obs, obs if final_obs is None else final_obs, reward, terminated, truncated, z if success is None else success,
              z if substeps is None else substeps)
-    return g.decoded()
+    d = g.decoded()
+    if as_tuple:
+        return d["obs"], d["reward"], d["terminated"], d["truncated"]
+    return d
