@@ -426,12 +426,13 @@ struct EFace {
     gv n;
     double d;
     unsigned char c[3], f[3]; /* vertex ids (< 136), neighbour faces (< 256) */
-    unsigned char e3;         /* the neighbours' edge indices, 2 bits each */
+    unsigned char e[3];       /* the neighbours' edge indices, one byte each: a link is two plain byte stores (a packed
+                                 field made every e_bind a read-modify-write, a dependent load on the EPA's chain) */
     unsigned char pass;       /* expand()'s visit mark (<= 255 iterations) */
 };
-static_assert(sizeof(EFace) == 40, "the compact face record");
-UGK_FN int fe(const EFace& F, int j) { return (F.e3 >> (2 * j)) & 3; }
-UGK_FN void set_fe(EFace& F, int j, int v) { F.e3 = (unsigned char)((F.e3 & ~(3 << (2 * j))) | (v << (2 * j))); }
+static_assert(sizeof(EFace) == 48, "the face record");
+UGK_FN int fe(const EFace& F, int j) { return F.e[j]; }
+UGK_FN void set_fe(EFace& F, int j, int v) { F.e[j] = (unsigned char)v; }
 struct EHull { double d; int stamp, f; };
 /* copies in and out of the store's address space (a struct does not convert between address spaces implicitly) */
 UGK_FN gv ldw(const UGK_GMEM ESv& s) { return V3(s.w.x, s.w.y, s.w.z); }
@@ -813,7 +814,7 @@ UGK_FN int e_newface(UGK_GMEM EpaMem* E, Epa& P, int a, int b, int c, bool force
         const gv aw = ldw(E->sv[a]), bw = ldw(E->sv[b]), cw = ldw(E->sv[c]);
         EFace F; /* its three links are all set by e_bind before the hull is read again */
         F.f[0] = F.f[1] = F.f[2] = 0;
-        F.e3 = 0;
+        F.e[0] = F.e[1] = F.e[2] = 0;
         F.d = 0.0;
         F.pass = 0;
         F.c[0] = (unsigned char)a; F.c[1] = (unsigned char)b; F.c[2] = (unsigned char)c;
@@ -996,7 +997,7 @@ UGK_FN bool e_expand_group(UGK_GMEM EpaMem* E, Epa& P, int pass, int w, gv ww, c
         const int stamp = ++P.stampctr;
         EFace F;
         F.f[0] = F.f[1] = F.f[2] = 0;
-        F.e3 = 0;
+        F.e[0] = F.e[1] = F.e[2] = 0;
         F.pass = 0;
         F.c[0] = (unsigned char)((x >> 10) & 255); F.c[1] = (unsigned char)((x >> 18) & 255); F.c[2] = (unsigned char)w;
         const double d = ugk_gread(pd, i);
@@ -1039,7 +1040,6 @@ UGK_FN int e_evaluate(UGK_GMEM EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv gue
         if (P.hcount == 4) {
             int best = ugk_epa_findbest(E, P.hcount);
             UGK_ADD(PF_EPA_SETUP, t_setup);
-            EFace outer = ugk_face_get(E, best);
             int pass = 0;
             e_bind(E, tetra[0], 0, tetra[1], 0);
             e_bind(E, tetra[0], 1, tetra[2], 0);
@@ -1047,6 +1047,7 @@ UGK_FN int e_evaluate(UGK_GMEM EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv gue
             e_bind(E, tetra[1], 1, tetra[3], 2);
             e_bind(E, tetra[1], 2, tetra[2], 1);
             e_bind(E, tetra[2], 2, tetra[3], 1);
+            EFace outer = ugk_face_get(E, best); /* after the bindings: the loop walks from its links */
             P.status = EPA_VALID;
             for (int it = 0; it < kEpaMaxIterations; it++) {
                 UGK_COUNT(PC_EPA_IT, 1);
@@ -1056,10 +1057,14 @@ UGK_FN int e_evaluate(UGK_GMEM EpaMem* E, Epa& P, Gjk2& g, const Mink& M, gv gue
                 bool valid = true;
                 ugk_face_pass(E, best, ++pass);
                 UGK_T0(t_sup);
-                stsv(E->sv[w], g2_support(M, ugk_face_get(E, best).n));
+                /* the best face is `outer` (read after findbest; only its mark changed since), the new vertex the
+                 * value just stored: neither is read back from the store (each reread was a dependent load) */
+                const ESv sw = g2_support(M, outer.n);
+                stsv(E->sv[w], sw);
                 UGK_ADD(PF_EPA_SUP, t_sup);
-                const gv ww = ldw(E->sv[w]);
-                const EFace B = ugk_face_get(E, best);
+                const gv ww = sw.w;
+                EFace B = outer;
+                B.pass = (unsigned char)pass;
                 const double wdist = dot(B.n, ww) - B.d;
                 if (!(wdist > kEpaAccuracy)) { P.status = EPA_ACCURACYREACHED; break; }
                 UGK_T0(t_exp);

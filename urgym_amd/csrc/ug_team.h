@@ -481,8 +481,7 @@ UGK_FN ugk::EFace ugk_face_get(UGK_GMEM ugk::EpaMem* E, int f) {
     ugk::EFace F;
     F.n = ugk::V3(G.n.x, G.n.y, G.n.z);
     F.d = G.d;
-    for (int j = 0; j < 3; j++) { F.c[j] = G.c[j]; F.f[j] = G.f[j]; }
-    F.e3 = G.e3;
+    for (int j = 0; j < 3; j++) { F.c[j] = G.c[j]; F.f[j] = G.f[j]; F.e[j] = G.e[j]; }
     F.pass = G.pass;
     return F;
 }
@@ -490,14 +489,13 @@ UGK_FN void ugk_face_put(UGK_GMEM ugk::EpaMem* E, int f, const ugk::EFace& F) {
     UGK_GMEM ugk::EFace& G = E->fc[f];
     G.n.x = F.n.x; G.n.y = F.n.y; G.n.z = F.n.z;
     G.d = F.d;
-    for (int j = 0; j < 3; j++) { G.c[j] = F.c[j]; G.f[j] = F.f[j]; }
-    G.e3 = F.e3;
+    for (int j = 0; j < 3; j++) { G.c[j] = F.c[j]; G.f[j] = F.f[j]; G.e[j] = F.e[j]; }
     G.pass = F.pass;
 }
 UGK_FN void ugk_face_pass(UGK_GMEM ugk::EpaMem* E, int f, int pass) { E->fc[f].pass = (unsigned char)pass; }
 UGK_FN void ugk_face_link(UGK_GMEM ugk::EpaMem* E, int f, int j, int nf, int ne) {
     E->fc[f].f[j] = (unsigned char)nf;
-    E->fc[f].e3 = (unsigned char)((E->fc[f].e3 & ~(3 << (2 * j))) | (ne << (2 * j)));
+    E->fc[f].e[j] = (unsigned char)ne;
 }
 UGK_FN ugk::EHull ugk_hull_get(UGK_GMEM ugk::EpaMem* E, int i) {
     ugk::EHull h;
