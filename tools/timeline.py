@@ -1,5 +1,6 @@
-"""Block timeline of k_step launches (development aid for the critical path): per block (= env) its
-start / end (s_memrealtime, 100 MHz), whether its env reset, its substeps.  Per launch it reports the launch time, the
+"""Block timeline of k_step launches (development aid for the critical path): per env, by its position
+in the launch order, its start / end (s_memrealtime, 100 MHz), whether it reset, its substeps, and where it ran (XCD,
+SIMD: the placement view below -- dispatch gaps on each SIMD, per-XCD work).  Per launch it reports the launch time, the
 balanced time (the blocks' summed durations over the slots that ran at once), the substep distribution, and what
 list scheduling predicts for three block orders on those slots: the launch order (block index), the blocks sorted
 by their measured durations (longest first: the bound any reordering can reach), and sorted by a predictor known
@@ -30,6 +31,46 @@ def list_schedule(durations, order, slots):
         end = max(end, t)
         heapq.heappush(free, t)
     return end
+
+
+def placement(b, st, en, dur):
+    """where the blocks ran (word 3: XCC_ID in bits 20-23, HW_ID in 32-63: SIMD 4-5, CU 8-11, SH 12, SE 13-15): per XCD
+    its blocks, work and slots; list scheduling of each XCD's own blocks in block order on its own slots (the launch if
+    the dispatcher deals blocks round-robin to the XCDs and each fills its slots greedily); and the dispatch delay --
+    a block's start minus the end of the block that ran before it on the same SIMD"""
+    xcc = (b[:, 3] >> 20) & 15
+    hw = (b[:, 3] >> 32) & 0xFFFFFFFF
+    slot = (xcc << 16) | ((hw >> 4) & 0xFFF)
+    n = len(st)
+    out = {"xcds": int(len(np.unique(xcc)))}
+    mod = np.arange(n) % 8
+    agree = sum(int(np.max(np.bincount(xcc[mod == m], minlength=16))) for m in range(8))
+    out["blockidx_mod8_same_xcd_frac"] = agree / n
+    per, ends = [], []
+    for x in np.unique(xcc):
+        sel = np.nonzero(xcc == x)[0]
+        s, e = st[sel], en[sel]
+        ev = np.concatenate([np.stack([s, np.ones(len(sel))], 1), np.stack([e, -np.ones(len(sel))], 1)])
+        ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
+        sl = int(np.cumsum(ev[:, 1]).max())
+        per.append(list_schedule(dur[sel], np.arange(len(sel)), sl))
+        ends.append(e.max())
+        out.setdefault("xcd_blocks", []).append(int(len(sel)))
+        out.setdefault("xcd_slots", []).append(sl)
+        out.setdefault("xcd_work_per_slot_ms", []).append(float(dur[sel].sum() / sl / 1e3))
+        out.setdefault("xcd_end_ms", []).append(float(e.max() / 1e3))
+    out["sched_per_xcd_ms"] = float(max(per) / 1e3)
+    gaps = []
+    for k in np.unique(slot):
+        sel = np.nonzero(slot == k)[0]
+        sel = sel[np.argsort(st[sel])]
+        if len(sel) > 1:
+            gaps.extend((st[sel[1:]] - en[sel[:-1]]).tolist())
+    g = np.asarray(gaps) if gaps else np.zeros(1)
+    out["simd_slots"] = int(len(np.unique(slot)))
+    out["dispatch_gap_us_mean_p99_max"] = [float(g.mean()), float(np.percentile(g, 99)), float(g.max())]
+    out["dispatch_gap_total_ms_per_slot"] = float(g.sum() / max(1, len(np.unique(slot))) / 1e3)
+    return out
 
 
 def main():
@@ -79,6 +120,7 @@ def main():
             if prev_ns is not None:
                 r["sched_prev_substeps_first_ms"] = list_schedule(dur, np.argsort(-prev_ns, kind="stable"), slots) / 1e3
                 r["corr_substeps_vs_prev"] = float(np.corrcoef(ns, prev_ns)[0, 1])
+            r.update(placement(b, st, en, dur))
             rows.append(r)
             print(json.dumps(r), flush=True)
         prev_ns = ns

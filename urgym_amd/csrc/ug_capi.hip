@@ -421,11 +421,9 @@ static __device__ int task_obs_dim(int variant) { return UG_OBS_DIM(variant); }
 static __device__ int task_act_dim(int variant) { return UG_ACT_DIM(variant); }
 static __device__ int task_ndraw(int variant) { return UG_NDRAW(variant); }
 
-__global__ void __launch_bounds__(TEAM, 1) k_reset(const Scene* sc, double* S, uint32_t* mt, int* elapsed, double* ws,
-                                                   int n, const uint8_t* mask, const double* draws, double* obs,
-                                                   int32_t* substeps, int* stats, uint8_t* flags) {
-    const int i = blockIdx.x;
-    if (i >= n) return;
+static __device__ __forceinline__ void reset_env(const Scene* sc, double* S, uint32_t* mt, int* elapsed, double* ws,
+                                                 const uint8_t* mask, const double* draws, double* obs,
+                                                 int32_t* substeps, int* stats, uint8_t* flags, int i) {
     if (mask && !mask[i]) { /* nothing happened to a masked-out env in this call */
         if (threadIdx.x == 0) flags[i] = 0;
         return;
@@ -450,13 +448,36 @@ __global__ void __launch_bounds__(TEAM, 1) k_reset(const Scene* sc, double* S, u
     }
 }
 
-__global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, uint32_t* mt, int* elapsed, double* ws,
-                                                  int n, const float* act, double* obs, double* final_obs, double* rew,
-                                                  uint8_t* term, uint8_t* trunc, uint8_t* succ, int32_t* substeps,
-                                                  int autoreset, int max_steps, const int* order, uint8_t* prio,
-                                                  int* stats, uint8_t* flags) {
-    if ((int)blockIdx.x >= n) return;
-    const int i = order[blockIdx.x];
+/* The step and reset launches are work queues: one block per wave slot the device holds at once (urgym_handle::slots),
+ * each taking the next env of the launch order from a global counter as soon as it is free, until the order is used
+ * up.  With one block per env (the hardware dispatcher dealing the grid's blocks round-robin to the 8 XCDs in block
+ * order) a wave slot sat idle 0.4-0.6 ms on average between the end of one block and the start of the next on it (p99
+ * 3-4 ms; BallBalance x4096: 1.5 ms of idle per slot per 24.4 ms launch, tools/timeline.py's placement view,
+ * profiles/round5_timeline_dispatch_hw.json).  The queue makes the launch the list schedule of the launch order.  An
+ * env's result does not depend on which block ran it (its state, workspace and streams are its own); every block
+ * leaves once the counter passes n.  The counter is zeroed (hipMemsetAsync on the launch's stream) before every
+ * launch. */
+__device__ __forceinline__ int queue_next(int* q) {
+    int k = 0;
+    if (threadIdx.x == 0) k = atomicAdd(q, 1);
+    return __builtin_amdgcn_readfirstlane(k);
+}
+
+__global__ void __launch_bounds__(TEAM, 1) k_reset(const Scene* sc, double* S, uint32_t* mt, int* elapsed, double* ws,
+                                                   int n, const uint8_t* mask, const double* draws, double* obs,
+                                                   int32_t* substeps, int* stats, uint8_t* flags, int* queue) {
+    for (;;) {
+        const int i = queue_next(queue);
+        if (i >= n) return;
+        reset_env(sc, S, mt, elapsed, ws, mask, draws, obs, substeps, stats, flags, i);
+    }
+}
+
+static __device__ __forceinline__ void step_env(const Scene* sc, double* S, uint32_t* mt, int* elapsed, double* ws,
+                                                const float* act, double* obs, double* final_obs, double* rew,
+                                                uint8_t* term, uint8_t* trunc, uint8_t* succ, int32_t* substeps,
+                                                int autoreset, int max_steps, int i, int k, uint8_t* prio, int* stats,
+                                                uint8_t* flags) {
 #ifdef UG_PROF
     const unsigned long long bt0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -486,14 +507,31 @@ __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, ui
         if (substeps) substeps[i] = ns;
         prio[i] = (uint8_t)team_priority(sc, ns, elapsed[i] + 1, max_steps, autoreset);
 #ifdef UG_PROF
-        if (blockIdx.x < UG_BT_MAX) {
-            unsigned long long* bt = &g_btime[4 * blockIdx.x];
+        if (k < UG_BT_MAX) { /* per launch-order position */
+            unsigned long long* bt = &g_btime[4 * k];
+            unsigned xcc, hwid; /* where the env ran: XCD, and SE / CU / SIMD (tools/timeline.py's placement view) */
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
             bt[0] = bt0;
             bt[1] = __builtin_amdgcn_s_memrealtime();
             bt[2] = (unsigned long long)i;
-            bt[3] = (unsigned long long)ns | ((unsigned long long)io.reset_done << 16);
+            bt[3] = (unsigned long long)ns | ((unsigned long long)io.reset_done << 16) |
+                    ((unsigned long long)(xcc & 15u) << 20) | ((unsigned long long)hwid << 32);
         }
 #endif
+    }
+}
+
+__global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, uint32_t* mt, int* elapsed, double* ws,
+                                                  int n, const float* act, double* obs, double* final_obs, double* rew,
+                                                  uint8_t* term, uint8_t* trunc, uint8_t* succ, int32_t* substeps,
+                                                  int autoreset, int max_steps, const int* order, uint8_t* prio,
+                                                  int* stats, uint8_t* flags, int* queue) {
+    for (;;) {
+        const int k = queue_next(queue);
+        if (k >= n) return;
+        step_env(sc, S, mt, elapsed, ws, act, obs, final_obs, rew, term, trunc, succ, substeps, autoreset, max_steps,
+                 order[k], k, prio, stats, flags);
     }
 }
 
@@ -725,7 +763,9 @@ struct urgym_handle {
     double *d_obs = nullptr, *d_final = nullptr, *d_rew = nullptr, *d_draws = nullptr, *d_aux = nullptr;
     uint8_t *d_term = nullptr, *d_trunc = nullptr, *d_succ = nullptr, *d_mask = nullptr;
     int32_t* d_sub = nullptr;
-    int* d_order = nullptr;   // k_step launch order (blockIdx -> env), from the previous step's priorities
+    int* d_order = nullptr;   // k_step launch order (queue position -> env), from the previous step's priorities
+    int* d_queue = nullptr;   // the step / reset work-queue counter
+    int slots = 0;            // k_step / k_reset blocks: the wave slots the device holds at once (CUs x blocks per CU)
     uint8_t* d_prio = nullptr;
     int* d_stats = nullptr;   // UG_NSTAT event counters per env
     uint8_t* d_flags = nullptr; // UG_FLAG_* of the last step / reset per env
@@ -806,6 +846,14 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     HIPCHK(h, hipMalloc(&h->d_sub, sizeof(int32_t) * N));
     HIPCHK(h, hipMalloc(&h->d_order, sizeof(int) * N));
     HIPCHK(h, hipMalloc(&h->d_prio, N));
+    HIPCHK(h, hipMalloc(&h->d_queue, sizeof(int)));
+    {
+        int cus = 0, per = 0;
+        HIPCHK(h, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_step, TEAM, 0));
+        h->slots = (cus > 0 ? cus : 1) * (per > 0 ? per : 1);
+        if (const char* e = getenv("URGYM_SLOTS")) h->slots = atoi(e) > 0 ? atoi(e) : h->slots; /* A/B measurement aid */
+    }
     HIPCHK(h, hipMalloc(&h->d_stats, sizeof(int) * UG_NSTAT * N));
     HIPCHK(h, hipMalloc(&h->d_flags, N));
     HIPCHK(h, hipMemsetAsync(h->d_stats, 0, sizeof(int) * UG_NSTAT * N, h->stream));
@@ -863,7 +911,7 @@ void urgym_destroy(urgym_handle* h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     void* ptrs[] = {h->d_scene, h->d_state, h->d_ws, h->d_mt, h->d_elapsed, h->d_act, h->d_obs, h->d_final, h->d_rew,
                     h->d_draws, h->d_aux, h->d_term, h->d_trunc, h->d_succ, h->d_mask, h->d_sub, h->d_order, h->d_prio,
-                    h->d_stats, h->d_flags, h->d_campose};
+                    h->d_stats, h->d_flags, h->d_campose, h->d_queue};
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -896,9 +944,11 @@ double urgym_last_kernel_ms(const urgym_handle* h) {
 int urgym_reset_device(urgym_handle* h, const uint8_t* d_mask, const double* d_draws, double* d_obs) {
     if (!h) return -1;
     HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipMemsetAsync(h->d_queue, 0, sizeof(int), h->stream));
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-    k_reset<<<h->n, TEAM, 0, h->stream>>>(h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->d_ws, h->n, d_mask,
-                                           d_draws, d_obs, nullptr, h->d_stats, h->d_flags);
+    k_reset<<<std::min(h->n, h->slots), TEAM, 0, h->stream>>>(h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->d_ws, h->n,
+                                                               d_mask, d_draws, d_obs, nullptr, h->d_stats, h->d_flags,
+                                                               h->d_queue);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     h->timed = true;
@@ -928,10 +978,12 @@ int urgym_step_device(urgym_handle* h, const float* d_act, double* d_obs, double
     if (!h) return -1;
     if (!d_act || !d_obs) return fail(h, "urgym_step_device: actions and obs must not be NULL");
     HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipMemsetAsync(h->d_queue, 0, sizeof(int), h->stream));
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-    k_step<<<h->n, TEAM, 0, h->stream>>>(h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->d_ws, h->n, d_act, d_obs,
-                                          d_final, d_rew, d_term, d_trunc, d_succ, d_sub, h->autoreset, h->max_steps, h->d_order,
-                                          h->d_prio, h->d_stats, h->d_flags);
+    k_step<<<std::min(h->n, h->slots), TEAM, 0, h->stream>>>(h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->d_ws, h->n,
+                                                              d_act, d_obs, d_final, d_rew, d_term, d_trunc, d_succ, d_sub,
+                                                              h->autoreset, h->max_steps, h->d_order, h->d_prio,
+                                                              h->d_stats, h->d_flags, h->d_queue);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     k_order<<<1, ORDER_THREADS, 0, h->stream>>>(h->d_prio, h->d_order, h->n);
