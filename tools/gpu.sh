@@ -13,7 +13,6 @@
 #   bash tools/gpu.sh profile <tag> [bench.py args...]  rocprofv3 kernel trace + stats, FETCH_SIZE / WRITE_SIZE PMC
 #                                                       passes (one counter group per run), traffic json, bench line
 #   bash tools/gpu.sh pmcmix <tag> [bench.py args...]   instruction-mix / stall PMC passes
-#   bash tools/gpu.sh pcsamp <tag> [bench.py args...]   stochastic PC sampling (host_trap fallback) -> <tag>/pcs/
 #   bash tools/gpu.sh world8 <tag> [bench.py args...]   the 8-rank path rehearsed on this one GPU: 8 gloo ranks
 #                                                       (torch.distributed.run, 127.0.0.1) -> <tag>/world8.json
 #   bash tools/gpu.sh icache <tag> [bench.py args...]   instruction-cache PMC pass (SQC_ICACHE_*, SQ_IFETCH) after
@@ -100,20 +99,6 @@ icache)
     timeout -s KILL 180 rocprofv3 --pmc $G2 --output-format csv -d "$OUT/if" -o run -- python3 bench.py $ARGS \
         > "$OUT/if.log" 2>&1 || { echo "IFETCH PASS FAILED"; exit 1; }
     echo ICACHE_OK ;;
-pcsamp)
-    # stochastic PC sampling of a short bench run (where the waves stall, by instruction); host_trap if unsupported
-    ARGS="${*:---steps 3 --warmup 1 --reps 1 --no-cpu-baseline}"
-    timeout -k 10 300 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method stochastic --pc-sampling-unit cycles \
-        --pc-sampling-interval 1048576 --output-format csv -d "$OUT/pcs" -o run -- python3 bench.py $ARGS \
-        > "$OUT/pcs.log" 2>&1; rc=$?
-    echo "[pcsamp] stochastic rc=$rc"; tail -3 "$OUT/pcs.log"
-    if [ $rc -eq 1 ] || [ $rc -eq 2 ]; then # a refused option only; nothing after a fault, abort or time limit
-        timeout -k 10 300 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method host_trap --pc-sampling-unit time \
-            --pc-sampling-interval 100 --output-format csv -d "$OUT/pch" -o run -- python3 bench.py $ARGS \
-            > "$OUT/pch.log" 2>&1; rc=$?
-        echo "[pcsamp] host_trap rc=$rc"; tail -3 "$OUT/pch.log"
-    fi
-    exit $rc ;;
 world8)
     timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29533 bench.py --gpus 8 --backend gloo --no-cpu-baseline "$@" > "$OUT/world8.json" \
