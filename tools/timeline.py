@@ -93,7 +93,7 @@ def main():
     lo, hi = np.asarray(act.low, np.float64), np.asarray(act.high, np.float64)
     rng = np.random.default_rng(0)
     buf = np.zeros(4 * 8192, np.uint64)
-    rows, prev_ns = [], None
+    rows, prev_ns, prev_cls = [], None, None
     for t in range(a.steps):
         sim.step(rng.uniform(lo, hi, size=(n, len(lo))).astype(np.float32))
         sim.sync()
@@ -121,8 +121,26 @@ def main():
                 r["sched_prev_substeps_first_ms"] = list_schedule(dur, np.argsort(-prev_ns, kind="stable"), slots) / 1e3
                 r["corr_substeps_vs_prev"] = float(np.corrcoef(ns, prev_ns)[0, 1])
             r.update(placement(b, st, en, dur))
+            # the launch order against the resets: their positions (a reset placed past the first `slots` envs
+            # starts its chain only when a slot frees), and the priority classes this launch was ordered by
+            # (word 3 bits 24-31: the class each env computed for the next launch, taken from the last launch)
+            kr = np.nonzero(rs)[0]
+            r["reset_pos_past_slots"] = int((kr >= slots).sum())
+            r["reset_pos_max"] = int(kr.max()) if len(kr) else -1
+            if prev_cls is not None:
+                cls = prev_cls[b[:, 2]]
+                r["class_hist"] = np.bincount(cls, minlength=16).tolist()
+                r["reset_class_hist"] = np.bincount(cls[rs == 1], minlength=16).tolist()
+                fresh = prev_rs[b[:, 2]] == 1  # the env reset in the last launch: its episode's first step now
+                r["fresh_envs_resets"] = [int(fresh.sum()), int((fresh & (rs == 1)).sum())]
+                r["fresh_class_hist"] = np.bincount(cls[fresh], minlength=16).tolist()
             rows.append(r)
             print(json.dumps(r), flush=True)
+        cur = np.zeros(n, np.int64)
+        cur[b[:, 2]] = (b[:, 3] >> 24) & 255
+        prev_cls = cur
+        prev_rs = np.zeros(n, np.int64)
+        prev_rs[b[:, 2]] = rs
         prev_ns = ns
     keys = [k for k in rows[0] if isinstance(rows[0][k], float) and k != "step"]
     summary = {"task": a.task, "envs": n, "steps": len(rows),

@@ -516,7 +516,8 @@ static __device__ __forceinline__ void step_env(const Scene* sc, double* S, uint
             bt[1] = __builtin_amdgcn_s_memrealtime();
             bt[2] = (unsigned long long)i;
             bt[3] = (unsigned long long)ns | ((unsigned long long)io.reset_done << 16) |
-                    ((unsigned long long)(xcc & 15u) << 20) | ((unsigned long long)hwid << 32);
+                    ((unsigned long long)(xcc & 15u) << 20) | ((unsigned long long)prio[i] << 24) |
+                    ((unsigned long long)hwid << 32);
         }
 #endif
     }
