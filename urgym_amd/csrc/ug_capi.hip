@@ -536,30 +536,62 @@ __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, ui
     }
 }
 
-/* next launch order: envs by descending priority (stable counting sort, one block; deterministic) */
+/* next launch order: envs by descending priority (0..255), ties by ascending env index (deterministic), one block.
+ * Up to ORDER_LDS envs: a bitonic sort of (255 - priority) << 24 | env in LDS (78 stages for 4096 envs); more: a
+ * two-pass stable counting sort by priority nibble (low, then high) through tmp. */
 #define ORDER_THREADS 1024
-__global__ void __launch_bounds__(ORDER_THREADS) k_order(const uint8_t* prio, int* order, int n) {
-    __shared__ int wsum[ORDER_THREADS / WAVE];
-    __shared__ int base;
+#define ORDER_LDS 8192
+__device__ static void order_pass(const uint8_t* prio, int shift, const int* src, int* dst, int n, int* wsum, int* base) {
     const int t = threadIdx.x, w = t / WAVE, l = t % WAVE;
-    if (t == 0) base = 0;
+    if (t == 0) *base = 0;
     __syncthreads();
     for (int b = 15; b >= 0; b--) {
         for (int c = 0; c < n; c += ORDER_THREADS) {
             const int i = c + t;
-            const bool f = i < n && prio[i] == b;
+            const int e = i < n ? (src ? src[i] : i) : 0;
+            const bool f = i < n && ((prio[e] >> shift) & 15) == b;
             const unsigned long long m = __ballot(f);
             if (l == 0) wsum[w] = __popcll(m);
             __syncthreads();
-            int off = base;
+            int off = *base;
             for (int k = 0; k < w; k++) off += wsum[k];
-            if (f) order[off + __popcll(m & ((1ull << l) - 1ull))] = i;
+            if (f) dst[off + __popcll(m & ((1ull << l) - 1ull))] = e;
             __syncthreads();
             if (t == 0)
-                for (int k = 0; k < ORDER_THREADS / WAVE; k++) base += wsum[k];
+                for (int k = 0; k < ORDER_THREADS / WAVE; k++) *base += wsum[k];
             __syncthreads();
         }
     }
+}
+__global__ void __launch_bounds__(ORDER_THREADS) k_order(const uint8_t* prio, int* order, int* tmp, int n) {
+    __shared__ uint32_t sk[ORDER_LDS];
+    __shared__ int wsum[ORDER_THREADS / WAVE];
+    __shared__ int base;
+    const int t = threadIdx.x;
+    if (n > ORDER_LDS) {
+        order_pass(prio, 0, nullptr, tmp, n, wsum, &base);
+        __threadfence_block();
+        __syncthreads();
+        order_pass(prio, 4, tmp, order, n, wsum, &base);
+        return;
+    }
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    for (int i = t; i < n2; i += ORDER_THREADS) sk[i] = i < n ? ((255u - prio[i]) << 24) | (uint32_t)i : 0xFFFFFFFFu;
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = t; i < n2; i += ORDER_THREADS) {
+                const int x = i ^ j;
+                if (x > i) {
+                    const uint32_t a = sk[i], b = sk[x];
+                    if ((a > b) == ((i & k) == 0)) { sk[i] = b; sk[x] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = t; i < n; i += ORDER_THREADS) order[i] = (int)(sk[i] & 0xFFFFFFu);
 }
 __global__ void k_iota(int* order, uint8_t* prio, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -765,6 +797,7 @@ struct urgym_handle {
     uint8_t *d_term = nullptr, *d_trunc = nullptr, *d_succ = nullptr, *d_mask = nullptr;
     int32_t* d_sub = nullptr;
     int* d_order = nullptr;   // k_step launch order (queue position -> env), from the previous step's priorities
+    int* d_order_tmp = nullptr; // k_order's first pass (more than ORDER_LDS envs)
     int* d_queue = nullptr;   // the step / reset work-queue counter
     int slots = 0;            // k_step / k_reset blocks: the wave slots the device holds at once (CUs x blocks per CU)
     uint8_t* d_prio = nullptr;
@@ -846,6 +879,7 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     HIPCHK(h, hipMalloc(&h->d_mask, N));
     HIPCHK(h, hipMalloc(&h->d_sub, sizeof(int32_t) * N));
     HIPCHK(h, hipMalloc(&h->d_order, sizeof(int) * N));
+    HIPCHK(h, hipMalloc(&h->d_order_tmp, sizeof(int) * N));
     HIPCHK(h, hipMalloc(&h->d_prio, N));
     HIPCHK(h, hipMalloc(&h->d_queue, sizeof(int)));
     {
@@ -912,7 +946,7 @@ void urgym_destroy(urgym_handle* h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     void* ptrs[] = {h->d_scene, h->d_state, h->d_ws, h->d_mt, h->d_elapsed, h->d_act, h->d_obs, h->d_final, h->d_rew,
                     h->d_draws, h->d_aux, h->d_term, h->d_trunc, h->d_succ, h->d_mask, h->d_sub, h->d_order, h->d_prio,
-                    h->d_stats, h->d_flags, h->d_campose, h->d_queue};
+                    h->d_stats, h->d_flags, h->d_campose, h->d_queue, h->d_order_tmp};
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -987,7 +1021,7 @@ int urgym_step_device(urgym_handle* h, const float* d_act, double* d_obs, double
                                                               h->d_stats, h->d_flags, h->d_queue);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
-    k_order<<<1, ORDER_THREADS, 0, h->stream>>>(h->d_prio, h->d_order, h->n);
+    k_order<<<1, ORDER_THREADS, 0, h->stream>>>(h->d_prio, h->d_order, h->d_order_tmp, h->n);
     HIPCHK(h, hipGetLastError());
     h->timed = true;
     return 0;

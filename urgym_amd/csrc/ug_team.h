@@ -28,6 +28,7 @@
 
 #include "ug_device.h"
 #include "prio_model.h"
+#include "prio_model_tb.h"
 #include "ug_glue.h"
 
 namespace ugd {
@@ -4682,11 +4683,10 @@ __device__ static void team_prof_flush() {
     for (int i = threadIdx.x; i < UG_NPROF; i += TEAM) atomicAdd(&g_prof[i], sh.prof[i]);
 #endif
 }
-/* BallBalance / TwoBalls reset predictor (scheduling only): ball i in the paddle frame -> the logit of "this
- * env ends its episode in the next env-step", a 14 -> 16 (ReLU) -> 1 MLP (prio_model.h, tools/fit_priority.py)
- * over the ball's paddle-frame offset, velocities and in-plane gravity and the log times of an edge-roll +
- * free-fall estimate */
-__device__ static double bb_reset_logit(const EnvState& e, const m3& R, int o) {
+/* BallBalance / TwoBalls reset predictor inputs (scheduling only): ball o in the paddle frame -> its paddle-frame
+ * offset, velocities and in-plane gravity and the log times of an edge-roll + free-fall estimate (14 inputs,
+ * tools/fit_priority.py features()) */
+__device__ static void bb_ball_inputs(const EnvState& e, const m3& R, int o, double (&x)[UG_PM_IN]) {
     const v3 l = mtv(R, vsub(e.obj[o].pos, e.obj[0].pos));
     const v3 lv = mtv(R, vsub(e.obj[o].v, e.obj[0].v));
     const v3 gl = mtv(R, V(0.0, 0.0, -9.81));
@@ -4697,35 +4697,72 @@ __device__ static double bb_reset_logit(const EnvState& e, const m3& R, int o) {
     const double tf = dz < 0.0 ? 0.0 : (bvz + sqrt(bvz * bvz + 2.0 * 9.81 * dz)) / 9.81;
     const double tex = fx >= 1.0 ? 0.0 : (1.0 - fx) * UG_BB_PADDLE_HX / fmax(vx, 0.05);
     const double tey = fy >= 1.0 ? 0.0 : (1.0 - fy) * UG_BB_PADDLE_HY / fmax(vy, 0.05);
-    const double x[UG_PM_IN] = {fx, fy, l.z, vx, vy, lv.z, dz, bvz, gl.x * sx, gl.y * sy,
+    const double v[UG_PM_IN] = {fx, fy, l.z, vx, vy, lv.z, dz, bvz, gl.x * sx, gl.y * sy,
                                 log(fmin(tex, tey) + tf + 1e-3), log(tex + 1e-3), log(tey + 1e-3), log(tf + 1e-3)};
-    double z[UG_PM_IN];
-    for (int i = 0; i < UG_PM_IN; i++) z[i] = (x[i] - UG_PM_MU[i]) / UG_PM_SD[i];
-    double out = UG_PM_B2;
-    for (int h = 0; h < UG_PM_HID; h++) {
-        double a = UG_PM_B1[h];
-        for (int i = 0; i < UG_PM_IN; i++) a += z[i] * UG_PM_W1[i * UG_PM_HID + h];
-        out += fmax(a, 0.0) * UG_PM_W2[h];
+    for (int i = 0; i < UG_PM_IN; i++) x[i] = v[i];
+}
+/* a 1-hidden-layer ReLU MLP's logit over standardised inputs */
+template <int IN, int HID>
+__device__ static double mlp_logit(const double* x, const double* mu, const double* sd, const double* W1,
+                                   const double* B1, const double* W2, double b2) {
+    double z[IN];
+    for (int i = 0; i < IN; i++) z[i] = (x[i] - mu[i]) / sd[i];
+    double out = b2;
+    for (int h = 0; h < HID; h++) {
+        double a = B1[h];
+        for (int i = 0; i < IN; i++) a += z[i] * W1[i * HID + h];
+        out += fmax(a, 0.0) * W2[h];
     }
     return out;
 }
-/* Launch-order priority of an env for the next k_step (0..15, higher runs first).  The launch time is the
+/* BallBalance: the logit of "this env ends its episode in the next env-step" from one ball, a 14 -> 16 (ReLU) -> 1 MLP
+ * (prio_model.h, tools/fit_priority.py) */
+__device__ static double bb_reset_logit(const EnvState& e, const m3& R, int o) {
+    double x[UG_PM_IN];
+    bb_ball_inputs(e, R, o, x);
+    return mlp_logit<UG_PM_IN, UG_PM_HID>(x, UG_PM_MU, UG_PM_SD, UG_PM_W1, UG_PM_B1, UG_PM_W2, UG_PM_B2);
+}
+/* TwoBallsBalance: one model over both balls' inputs, the episode's elapsed steps and the paddle's vertical velocity,
+ * 31 -> 16 (ReLU) -> 1 (prio_model_tb.h, tools/fit_priority.py --task 6): the larger of two single-ball logits
+ * ranked the resets where both balls hit the paddle together last (~55 per step, the launch 37 ms against 23.5 ms
+ * for the longest-first order) */
+__device__ static double tb_reset_logit(const EnvState& e, const m3& R, int el) {
+    static_assert(UG_PT_IN == 2 * UG_PM_IN + 3, "two balls' inputs, elapsed (clipped, log) and the paddle's vz");
+    double x[UG_PT_IN], b[UG_PM_IN];
+    for (int o = 1; o <= 2; o++) {
+        bb_ball_inputs(e, R, o, b);
+        for (int i = 0; i < UG_PM_IN; i++) x[(o - 1) * UG_PM_IN + i] = b[i];
+    }
+    x[2 * UG_PM_IN] = fmin((double)el, 10.0);
+    x[2 * UG_PM_IN + 1] = log((double)el + 1.0);
+    x[2 * UG_PM_IN + 2] = e.obj[0].v.z;
+    return mlp_logit<UG_PT_IN, UG_PT_HID>(x, UG_PT_MU, UG_PT_SD, UG_PT_W1, UG_PT_B1, UG_PT_W2, UG_PT_B2);
+}
+/* Launch-order priority of an env for the next k_step (0..255, higher runs first).  The launch time is the
  * longest env chain, and an env-step that ends its episode carries a ~170-substep autoreset: envs likely
  * to end next step are dispatched first so their reset overlaps the other envs' steps.  Scheduling only --
- * every env computes the same thing whatever its position in the launch.  Predicted truncation: 15;
- * BallBalance / TwoBalls: the reset predictor's logit in 15 levels (held-out random-action BallBalance x 4096:
+ * every env computes the same thing whatever its position in the launch.  Predicted truncation: 255;
+ * TwoBalls: its own two-ball model (tb_reset_logit) in 255 levels; BallBalance: the reset predictor's logit in 255 levels
+ * (held-out random-action BallBalance x 4096:
  * 0.44 of ~270 resets per step ranked outside the first 1024 launch slots, against 1.1 for an edge-roll +
  * free-fall time and 5.8 for a position-extrapolation score); otherwise the env's last substep count. */
+#define UG_PM_FINE_L0 -12.0 /* BallBalance's logit in 255 launch levels: [-12, 5.78) in steps of 0.07 */
+#define UG_PM_FINE_DL 0.07
+__device__ static int logit_level(double lg, double l0, double dl) {
+    const double b = floor((lg - l0) / dl);
+    return b > 254.0 ? 254 : (b < 0.0 ? 0 : (int)b); /* a NaN logit: level 0 */
+}
 __device__ static int team_priority(const Scene* s, int nsub, int el_next, int max_steps, int autoreset) {
     const EnvState& e = g_sh.e;
-    if (autoreset && max_steps > 0 && el_next >= max_steps) return 15;
+    if (autoreset && max_steps > 0 && el_next >= max_steps) return 255;
+    if (s->variant == UG_TASK_TWOBALLS && e.oactive[0] != 0.0 && e.oactive[1] != 0.0 && e.oactive[2] != 0.0)
+        return logit_level(tb_reset_logit(e, qmat(e.obj[0].quat), el_next - 1), UG_PT_L0, UG_PT_DL);
     if (s->task == UG_TASK_BALLBALANCE && e.oactive[0] != 0.0) {
         const m3 R = qmat(e.obj[0].quat);
         double lg = -1e300;
         for (int o = 1; o < s->nobj; o++)
             if (e.oactive[o] != 0.0) lg = fmax(lg, bb_reset_logit(e, R, o));
-        const double b = floor((lg - UG_PM_L0) / UG_PM_DL);
-        return b > 14.0 ? 14 : (b < 0.0 ? 0 : (int)b);
+        return logit_level(lg, UG_PM_FINE_L0, UG_PM_FINE_DL);
     }
     int b = 0;
     while (b < 14 && (2 << b) <= nsub) b++;
