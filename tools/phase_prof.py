@@ -17,6 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("URGYM_LIB", os.path.join(ROOT, "urgym_amd", "_lib", "liburgym_prof.so"))
 
+CALLS = ["team_gjk", "team_collide", "team_enumerate", "team_unit_solves", "team_robot_dynamics", "serial_pre",
+         "serial_post", "serial_fk", "team_pgs", "glue", "team_reduce4_g"]  # ug_team.h CALL_* (buf[104 + k])
 NAMES = ["collide", "dyn+enum", "rows", "pgs", "pgs_setup", "integrate", "glue", "total",
          "substeps", "nrows", "pgs_iters", "overlap_pairs", "hull_pairs", "manifolds", "pgs_sweeps", "hull_narrowphase",
          "robot_dynamics", "enumerate", "broadphase", "pair_narrowphase",
@@ -43,7 +45,7 @@ def main():
     from urgym_amd.envs import spaces_for
     _, asp = spaces_for(a.task)
     sim.set_autoreset(True, 500)
-    buf = np.zeros(104, np.uint64)
+    buf = np.zeros(116, np.uint64)
     sim.reset()
     sim.sync()
     rc = sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
@@ -55,6 +57,7 @@ def main():
     free_split = ["fk", "broadphase", "hull_narrowphase", "pr_lookup", "pr_narrow", "pr_manifold", "pr_store",
                   "pairs", "overlap_pairs", "hull_pairs", "robot_dynamics", "lane0_ldl_objects", "enumerate",
                   "unit_solves"]
+    print("reset, calls per env:", json.dumps({k: round(float(buf[104 + i]) / a.envs, 2) for i, k in enumerate(CALLS)}))
     print("reset, contact-free substeps' sub-phases (cycles or counts per substep):",
           json.dumps({k: round(float(buf[64 + i]) / max(r["free_substeps"], 1), 1) for i, k in enumerate(free_split)}))
     rng = np.random.default_rng(1)
@@ -98,6 +101,7 @@ def main():
     out["hull_support_split"] = {"supports_through_a_cell": sc["cells"] / max(gj["gjk_hull_supports"], 1),
                                  "cycles_to_cell": sc["cell"] / max(gj["gjk_hull_supports"], 1),
                                  "cycles_to_reduced": sc["mem"] / max(sc["cells"], 1)}
+    out["calls_per_env_step"] = {k: float(buf[104 + i]) / es for i, k in enumerate(CALLS)}
     print(json.dumps(out, indent=1))
     sim.close()
 

@@ -36,7 +36,7 @@ namespace ugd {
 #define TEAM 64
 typedef __attribute__((address_space(1))) const double gcdouble;
 typedef __attribute__((address_space(1))) double gdouble;
-#define UG_NPROF 104 /* phase accumulators of the -DUG_PROF build */
+#define UG_NPROF 116 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* a row's J and M^-1 J^T over the NVP = 32 dof slots (robot 12, objects 3 x 6, 2 zero pads) */
@@ -215,7 +215,12 @@ enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_
        PC_GJK_RECERT, /* GJK pairs skipped by the exact certificate re-test (gjk_one) */
        /* inside the hull support: the cycles until its cell is known, until its loads have landed (a forced wait,
         * profiling build only), and the supports that took a cell (not the whole scan) */
-       PF_SUP_CELL, PF_SUP_MEM, PC_SUP_CELLS };
+       PF_SUP_CELL, PF_SUP_MEM, PC_SUP_CELLS,
+       /* calls of the __noinline__ phases (tools/scratch_attr.py: their callee-saved saves and spills x calls) */
+       PC_CALL0 = 104 };
+enum { CALL_GJK = 0, CALL_COLLIDE, CALL_ENUM, CALL_UNIT, CALL_RDYN, CALL_PRE, CALL_POST, CALL_FK, CALL_PGS, CALL_GLUE,
+       CALL_REDUCE4, CALL_N };
+#define PROF_CALL(k) PROF_CNT(PC_CALL0 + (k), 1)
 #define UG_FREE_SPLIT_N 14
 #ifdef UG_PROF
 __device__ static const int kFreeSplit[UG_FREE_SPLIT_N] = {PF_FK, PF_BROAD, PF_HULL, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST,
@@ -860,6 +865,7 @@ __device__ __forceinline__ static void team_reduce4(int n, int k);
 __device__ __forceinline__ void fc_reduce(int n, int k, gdouble* gc);
 /* candidates gc[0..n) -> at most 4 in sh.u.cand.c[k] (oracle reduce4) */
 __device__ __noinline__ static void team_reduce4_g(int n, int k, gdouble* gc) {
+    PROF_CALL(CALL_REDUCE4);
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
     if (n <= 4) {
@@ -1805,6 +1811,7 @@ __device__ __forceinline__ static void gjk_one(const Scene* s, int k, UGK_GMEM u
  * EPA store.  One call per chunk: the callee-saved registers this solver needs are saved once per substep with GJK
  * pairs, not once per pair (they were 441 dwords per lane per call, most of the k_step's HBM traffic). */
 __device__ __noinline__ static void team_gjk(const Scene* s, unsigned long long hq, int c0, double* ws) {
+    PROF_CALL(CALL_GJK);
     Shared& sh = g_sh;
     const int nq = __popcll(hq), g = threadIdx.x / GJK_G;
     for (int r0 = 0; r0 < nq; r0 += GJK_NG) {
@@ -1821,6 +1828,7 @@ __device__ __noinline__ static void team_gjk(const Scene* s, unsigned long long 
 
 template <bool FULL, bool GJK>
 __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
+    PROF_CALL(CALL_COLLIDE);
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
     EnvState& e = sh.e;
@@ -2303,6 +2311,7 @@ __device__ static void enumerate_rows(Shared& sh, const Scene* s) {
  * counts.  Identical output when every contact point fits (the usual case); when the capacity check
  * of the serial code would reject points, the serial enumeration runs instead. */
 __device__ __noinline__ static void team_enumerate(const Scene* s) {
+    PROF_CALL(CALL_ENUM);
     Shared& sh = g_sh;
     EnvState& e = sh.e;
     const int lane = threadIdx.x;
@@ -2503,6 +2512,7 @@ __device__ __forceinline__ void ent_jac_r(const Scene* sc, const EnvState& e, co
 /* the LDL solves every limit / motor / gear row would repeat, once per substep: lane d < NB solves for the
  * unit vector e_d, lane NB + g for gear g's ratio * e_child (the same computation as the row's own) */
 __device__ __noinline__ static void team_unit_solves() {
+    PROF_CALL(CALL_UNIT);
     const int lane = threadIdx.x;
     if (lane < NB + 5) {
         const int g = lane - NB;
@@ -3163,6 +3173,7 @@ __device__ __forceinline__ int body_depth(int b) {
     return d;
 }
 __device__ __noinline__ static void team_robot_dynamics(double g_) {
+    PROF_CALL(CALL_RDYN);
     /* the LDS image is addressed directly (pointer arguments would turn every access into a flat one) */
     const double* qd = g_sh.e.qd;
     const Kin& k = g_sh.kin;
@@ -3316,6 +3327,7 @@ __device__ __noinline__ static void team_robot_dynamics(double g_) {
 /* lane 0: external forces (robot gravity/gyroscopic/damping via CRBA + RNEA, free objects), the LDL^T of
  * the mass matrix, and the row enumeration */
 __device__ __noinline__ static void serial_pre(const Scene* s) {
+    PROF_CALL(CALL_PRE);
     Shared& sh = g_sh;
     EnvState& e = sh.e;
     const double dt = UG_DT;
@@ -3403,6 +3415,7 @@ __device__ __noinline__ static void serial_pre(const Scene* s) {
 }
 /* lane 0: velocities += solver delta, positions integrate (v + split velocity) */
 __device__ __noinline__ static void serial_post(const Scene* s, int split) {
+    PROF_CALL(CALL_POST);
     Shared& sh = g_sh;
     EnvState& e = sh.e;
     const double dt = UG_DT;
@@ -3458,6 +3471,7 @@ __device__ __noinline__ static void serial_post(const Scene* s, int split) {
 /* fk() wave-parallel: lane b < NB forms its joint rotation, then composes its own root-to-body chain
  * (same operations and order as fk() along that path) */
 __device__ __noinline__ static void serial_fk() {
+    PROF_CALL(CALL_FK);
     Kin& k = g_sh.kin;
     const int lane = threadIdx.x;
     const bool own = lane < NB;
@@ -3562,6 +3576,7 @@ __device__ __forceinline__ void nc_direct_A(double (&A0)[PREG], int lane) {
  * so the pair is free.  tests/test_isa_audit.py fails the build if any function writes s[30:31] without saving it. */
 __device__ __noinline__ void ug_nonleaf_guard() { __asm__ volatile(""); }
 __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int nn_, int nobj_, double& dv, double& dvs) {
+    PROF_CALL(CALL_PGS);
     if (__builtin_expect(n_ < 0, 0)) ug_nonleaf_guard(); /* never: n_ >= 0 (see ug_nonleaf_guard) */
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
@@ -4367,6 +4382,7 @@ struct RunIO {
 };
 /* lane-0 glue of one program point; returns the physics loop to run next and sets *next */
 __device__ __noinline__ static int glue(const Scene* s, int pc, RunIO& io, int* next) {
+    PROF_CALL(CALL_GLUE);
     EnvState& e = g_sh.e;
     const int task = s->task;
     const int O = UG_OBS_DIM(s->variant);
