@@ -57,6 +57,7 @@ def main():
     free_split = ["fk", "broadphase", "hull_narrowphase", "pr_lookup", "pr_narrow", "pr_manifold", "pr_store",
                   "pairs", "overlap_pairs", "hull_pairs", "robot_dynamics", "lane0_ldl_objects", "enumerate",
                   "unit_solves"]
+    print("reset, quiescent substeps (collision skipped):", round(float(buf[115]) / max(r["substeps"], 1), 3))
     print("reset, calls per env:", json.dumps({k: round(float(buf[104 + i]) / a.envs, 2) for i, k in enumerate(CALLS)}))
     print("reset, contact-free substeps' sub-phases (cycles or counts per substep):",
           json.dumps({k: round(float(buf[64 + i]) / max(r["free_substeps"], 1), 1) for i, k in enumerate(free_split)}))
@@ -102,6 +103,7 @@ def main():
                                  "cycles_to_cell": sc["cell"] / max(gj["gjk_hull_supports"], 1),
                                  "cycles_to_reduced": sc["mem"] / max(sc["cells"], 1)}
     out["calls_per_env_step"] = {k: float(buf[104 + i]) / es for i, k in enumerate(CALLS)}
+    out["quiescent_substeps_fraction"] = float(buf[115]) / max(d["substeps"], 1)
     print(json.dumps(out, indent=1))
     sim.close()
 

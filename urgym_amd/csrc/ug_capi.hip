@@ -382,6 +382,25 @@ __global__ void k_build_scene(Scene* s, int variant, int flags) {
                 add_pair(s, c, statics[t]);
             }
     for (int i = 0; i < s->ncol; i++) gjk_params(&s->col[i]);
+    /* the quiescent-collision bound: every point of robot collider i -- its core (within |P| + gradius of the body
+     * origin) with its margin, and the corners of the box its AABB is formed from (|aP| + |ac| + |ah|) -- lies within
+     * rho of its body's origin, which lies within l(j, b) (the summed joint offsets) of body j's origin, through which
+     * joint j's axis passes: turning joint j by dq moves the point by at most |dq| (l + rho), whatever the other joints */
+    for (int i = 0; i < s->ncol; i++) {
+        const Collider& c = s->col[i];
+        for (int j = 0; j < NB; j++) s->qsw[i][j] = 0.0;
+        if (c.owner < 0) continue;
+        const double rho = fmax(vlen(c.P) + c.gradius + c.gmargin, vlen(c.aP) + vlen(c.ac) + vlen(c.ah));
+        for (int j = 0; j < NB; j++) {
+            double l = 0.0;
+            int b = c.owner;
+            while (b >= 0 && b != j) {
+                l += vlen(V(UG_BODY_P[3 * b], UG_BODY_P[3 * b + 1], UG_BODY_P[3 * b + 2]));
+                b = UG_BODY_PARENT[b];
+            }
+            if (b == j) s->qsw[i][j] = (l + rho) * (1.0 + 1e-9) + 1e-12;
+        }
+    }
 }
 
 // development / test aid: convex-convex queries as the kernels run them, one per 16-lane group (GJK_NG per wave, each

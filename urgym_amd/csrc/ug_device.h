@@ -260,6 +260,9 @@ struct Scene {
     int button_mode; /* Box-v0 button_touch_mode (UG_BX_TOUCH_*, urgym_set_button_mode) */
     int full;   /* full-geometry mode (UG_GEOM_FULL): robot hulls with every vertex and face */
     int gjk;    /* contact generation: 1 Bullet's convex-convex GJK / EPA (the default), 0 vertex-in-hull */
+    /* the quiescent-collision bound (ug_team.h quiescent_ok): robot collider c's points move by at most
+     * sum_j |q_j - q_ref_j| qsw[c][j] between two configurations (0 for dofs that do not move it, static colliders) */
+    double qsw[MAXCOL][NB];
 };
 
 struct CPoint { v3 lpA, lpB, n; double dist, imp, imp1, imp2; };

@@ -91,7 +91,11 @@ static_assert(UG_FULL_HULL_MAXV + 64 + 8 <= FC_MAX, "a full hull pair's candidat
  * B's frame then); GJK's (A, B) order (a sphere-first pair swapped) */
 #define GC_DOUBLES 18
 #define WS_GC (WS_EPA + EPA_DOUBLES * (64 / UG_GJK_G)) /* one EPA store per GJK lane group */
-#define WS_STRIDE(full, gjk) ((gjk) ? (size_t)(WS_GC + GC_DOUBLES * MAXPAIR) : WS_STRIDE_VIH(full))
+/* the quiescent-collision reference (team_collide / quiescent_ok): per pair the distance its colliders may still close
+ * without a contact (a certificate's slack, a padded-AABB gap; 1e300 for a pair with an inactive collider), then the
+ * robot's q when it was taken */
+#define WS_QS (WS_GC + GC_DOUBLES * MAXPAIR)
+#define WS_STRIDE(full, gjk) ((gjk) ? (size_t)(WS_QS + MAXPAIR + NB) : WS_STRIDE_VIH(full))
 
 #define MAXOV 26 /* pairs per lane-per-pair pass: their working manifolds share LDS with the rows (Shared::pm) */
 #define NBOXSLOT 5 /* box-box pairs run per round, one LDS clip-buffer slot each (they share the hull candidates' LDS) */
@@ -167,6 +171,7 @@ struct Shared {
     int flags;            /* UG_FLAG_* of this launch (lane 0) */
     int stats[UG_NSTAT];  /* the env's UG_STAT_* counters (lane 0), loaded / stored with the state */
     int bdepth[NB];       /* tree depth of body b (body_depth); filled by team_load */
+    int qsvalid;          /* the workspace holds a quiescent-collision reference (WS_QS) for the current program point */
 #ifdef UG_PROF
     unsigned long long prof[UG_NPROF];
 #endif
@@ -217,7 +222,7 @@ enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_
         * profiling build only), and the supports that took a cell (not the whole scan) */
        PF_SUP_CELL, PF_SUP_MEM, PC_SUP_CELLS,
        /* calls of the __noinline__ phases (tools/scratch_attr.py: their callee-saved saves and spills x calls) */
-       PC_CALL0 = 104 };
+       PC_CALL0 = 104, PC_QUIET = 115 /* substeps whose collision stage quiescent_ok proved empty */ };
 enum { CALL_GJK = 0, CALL_COLLIDE, CALL_ENUM, CALL_UNIT, CALL_RDYN, CALL_PRE, CALL_POST, CALL_FK, CALL_PGS, CALL_GLUE,
        CALL_REDUCE4, CALL_N };
 #define PROF_CALL(k) PROF_CNT(PC_CALL0 + (k), 1)
@@ -1852,15 +1857,24 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
     /* broadphase: ordered list of overlapping pairs */
     PROF_T0(t_broad);
     int base = 0;
+    gdouble* const qs = (gdouble*)(ws + WS_QS); /* the quiescent-collision reference (GJK, full geometry) */
     for (int p0 = 0; p0 < s->npair; p0 += TEAM) {
         int p = p0 + lane;
         int ovl = 0;
         if (p < s->npair) {
             const PairDef& P = s->pair[p];
             int a = P.a, b = P.b;
-            ovl = collider_active(e, s->col[a]) && collider_active(e, s->col[b]) &&
-                  !(sh.lo[a].x > sh.hi[b].x || sh.hi[a].x < sh.lo[b].x || sh.lo[a].y > sh.hi[b].y ||
-                    sh.hi[a].y < sh.lo[b].y || sh.lo[a].z > sh.hi[b].z || sh.hi[a].z < sh.lo[b].z);
+            const bool act = collider_active(e, s->col[a]) && collider_active(e, s->col[b]);
+            ovl = act && !(sh.lo[a].x > sh.hi[b].x || sh.hi[a].x < sh.lo[b].x || sh.lo[a].y > sh.hi[b].y ||
+                           sh.hi[a].y < sh.lo[b].y || sh.lo[a].z > sh.hi[b].z || sh.hi[a].z < sh.lo[b].z);
+            if (GJK && FULL) {
+                /* a separated pair's padded-AABB gap (each box moves by at most its collider's displacement);
+                 * an overlapping one's slack comes from its certificate below (-1: none) */
+                const double g = fmax(fmax(fmax(sh.lo[a].x - sh.hi[b].x, sh.lo[b].x - sh.hi[a].x),
+                                           fmax(sh.lo[a].y - sh.hi[b].y, sh.lo[b].y - sh.hi[a].y)),
+                                      fmax(sh.lo[a].z - sh.hi[b].z, sh.lo[b].z - sh.hi[a].z));
+                qs[p] = !act ? 1e300 : (ovl ? -1.0 : g);
+            }
         }
         unsigned long long m = ballot(ovl);
         if (ovl) sh.ov[base + lane_prefix(m)] = p;
@@ -1871,6 +1885,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
     PROF_ADD(PF_BROAD, t_broad);
     int nov = base;
     int nnew = 0;
+    bool allcert = true; /* every overlapping pair skipped by its certificate */
     for (int c0 = 0; c0 < nov; c0 += MAXOV) {
         int cn = nov - c0 < MAXOV ? nov - c0 : MAXOV;
         /* hull-box pairs of this chunk: cooperative narrowphase */
@@ -1921,6 +1936,8 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
                         hk = 0;
                         certd = true;
                         sh.u.cand.n[lane] = 0;
+                        /* the cores' separation along n may shrink by this much before GJK could keep a point */
+                        if (FULL) qs[p] = sep - C0.gmargin - C1.gmargin - P.thr - 1e-9 * (1.0 + ug_fabs(sep));
                     }
                 }
             }
@@ -1969,6 +1986,7 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
+        allcert = allcert && ballot(lane < cn && !certd) == 0ull;
         if (lane == 0) sh.is[3] = c0; /* the pass's first pair (team_poly_cyl's certificate slot) */
         if (GJK) {
             const unsigned long long hq = ballot(hk);
@@ -2136,6 +2154,14 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
     if (lane == 0) {
         if (nnew > MAXMAN) e.overflow += (double)(nnew - MAXMAN);
         e.nman = (double)(nnew < MAXMAN ? nnew : MAXMAN);
+    }
+    if (GJK && FULL) {
+        /* a quiescent-collision reference: no manifold, every overlapping pair certified, no free object (their
+         * motion is not bounded here) -- the robot's q now, with the slacks written above */
+        bool still = nnew == 0 && allcert;
+        for (int o = 0; o < s->nobj; o++) still = still && e.oactive[o] == 0.0;
+        if (still && lane < NB) qs[MAXPAIR + lane] = e.q[lane];
+        if (lane == 0) sh.qsvalid = still ? 1 : 0;
     }
     __syncthreads();
 }
@@ -4029,6 +4055,34 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     return split;
 }
 
+/* The collision stage of a substep with nothing to find (the contact-free stretches of a reset, the arm moving in
+ * free space): after a full pass that kept no manifold, certified every overlapping pair and saw no free object, each
+ * pair's slack -- how far its colliders may still close before GJK could keep a point (its certificate's margin
+ * beyond the contact threshold) or before its padded AABBs overlap (their gap) -- is in the workspace with the robot's
+ * q.  While every pair's colliders have moved less than that since (a robot collider's points by at most
+ * sum_j |q_j - q_ref_j| Scene::qsw[c][j], static ones not at all) and no glue ran (team_run clears the reference),
+ * the full pass would find exactly that again: no pair overlaps that did not, every certificate still holds, no
+ * manifold, nothing stored.  So it is skipped -- the same state, the same result bit for bit. */
+__device__ static bool quiescent_ok(const Scene* s, const double* ws) {
+    Shared& sh = g_sh;
+    const int lane = threadIdx.x;
+    const gcdouble* qs = (const gcdouble*)(ws + WS_QS);
+    if (lane < s->ncol) {
+        double D = 0.0;
+        for (int j = 0; j < NB; j++) D += ug_fabs(sh.e.q[j] - qs[MAXPAIR + j]) * s->qsw[lane][j];
+        sh.lo[lane].x = D; /* the collision stage's AABB scratch, unused until it runs */
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    bool bad = false;
+    for (int p = lane; p < s->npair; p += TEAM) {
+        const PairDef& P = s->pair[p];
+        bad = bad || !((sh.lo[P.a].x + sh.lo[P.b].x) * (1.0 + 1e-12) + 1e-12 < qs[p]); /* NaN: not quiet */
+    }
+    __builtin_amdgcn_wave_barrier();
+    return ballot(bad) == 0ull;
+}
+
 /* ---------------- one p.stepSimulation() (oracle substep()) ---------------- */
 __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) {
     Shared& sh = g_sh;
@@ -4043,8 +4097,10 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     PROF_ADD(PF_FK, t_col);
     const double ov0 = e.overflow;
     if (s->gjk) {
-        if (s->full) team_collide<true, true>(s, ws);
-        else team_collide<false, true>(s, ws);
+        if (s->full) {
+            if (!(uniform(sh.qsvalid) && quiescent_ok(s, ws))) team_collide<true, true>(s, ws);
+            else PROF_CNT(PC_QUIET, 1);
+        } else team_collide<false, true>(s, ws);
     } else {
         if (s->full) team_collide<true, false>(s, ws);
         else team_collide<false, false>(s, ws);
@@ -4634,6 +4690,7 @@ __device__ __forceinline__ static int team_run(const Scene* s, double* ws, int p
             int next;
             sh.is[1] = glue(s, pc, io, &next);
             sh.is[2] = next;
+            sh.qsvalid = 0; /* the glue may move, create or remove bodies: the next substep collides in full */
         }
         __syncthreads();
         PROF_ADD(PF_GLUE, t_glue);
@@ -4680,7 +4737,7 @@ __device__ static void team_load(const double* S, const int* stats) {
     double* dst = (double*)&sh.e;
     for (int i = threadIdx.x; i < UG_STATE_DIM; i += TEAM) dst[i] = S[i];
     if (threadIdx.x < UG_NSTAT) sh.stats[threadIdx.x] = stats ? stats[threadIdx.x] : 0;
-    if (threadIdx.x == 0) sh.flags = 0;
+    if (threadIdx.x == 0) { sh.flags = 0; sh.qsvalid = 0; }
     if (threadIdx.x < NB) {
         int m = 0;
         for (int b = threadIdx.x; b >= 0; b = UG_BODY_PARENT[b]) m |= 1 << b;
