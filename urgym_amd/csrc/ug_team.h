@@ -84,7 +84,9 @@ static_assert(UG_FULL_HULL_MAXV + 64 + 8 <= FC_MAX, "a full hull pair's candidat
 /* the convex-convex path (UG_CONTACT_GJK): the penetration solver's store (ug_gjk.h EpaMem: btGjkEpa2's 132 support
  * vertices, 256 faces and their lists, the horizon walk's stack) after everything else */
 #define WS_EPA WS_DOUBLES
+#ifndef UG_GJK_G
 #define UG_GJK_G 16 /* lanes per GJK pair (ugd::GJK_G): the wave runs 64 / UG_GJK_G pairs at once, one store each */
+#endif
 #define EPA_DOUBLES ((sizeof(ugk::EpaMem) + sizeof(double) - 1) / sizeof(double))
 /* the convex-convex path's separation certificates, per pair: [0] valid, [1..3] the separating axis n in B's frame,
  * [4] A's core extent along -n at the evaluation, [5] B's core extent along n, [6..14] R_AB, [15..17] p_AB (A's pose in
@@ -159,6 +161,9 @@ struct Shared {
     union {
         Cand hc[64];              /* hull narrowphase candidates */
         BoxScratch bs[NBOXSLOT];  /* lane-per-pair box-box clip buffers (after the hull pairs of the pass) */
+        /* 8-lane GJK groups (UG_GJK_G 8): per group the btGjkEpa2 GJK's four-vertex store (4 x 6 doubles) and the EPA's
+         * hull-slot table (256 bytes), during team_gjk only (16-lane groups keep them in v0 | dvout | dvsout and LDL) */
+        double gjk_lds[(64 / UG_GJK_G) * (4 * 6 + 32)];
     };
     double a12[NB];
     double jM[MAXOBJ];    /* effective inertia of the jointed objects in this substep (serial_pre; ug_joint.h) */
@@ -324,19 +329,16 @@ __device__ __forceinline__ void wave_best(double& v, int& idx, bool want_max) {
  * iterations differ.  group_best is wave_best over the group's row. */
 constexpr int GJK_G = UG_GJK_G, GJK_NG = TEAM / GJK_G;
 static_assert(TEAM == 64, "WS_GC counts 64 lanes");
-static_assert(GJK_G == 16, "a GJK lane group is one DPP row (the group masks and ds_bpermute reads assume it)");
+static_assert(GJK_G == 16 || GJK_G == 8, "a GJK lane group is one DPP row or half-row (the reductions below)");
 __device__ __forceinline__ void group_best(double& v, int& idx, bool want_max) {
-    if (GJK_G == TEAM) {
-        wave_best(v, idx, want_max);
-        return;
-    }
 #define STEP(CTRL)                                               \
     {                                                            \
         double w = dpp<CTRL>(v);                                 \
         int j = dppi<CTRL>(idx);                                 \
         if (!better(v, idx, w, j, want_max)) { v = w; idx = j; } \
     }
-    STEP(0xB1) STEP(0x4E) STEP(0x141) STEP(0x140)
+    STEP(0xB1) STEP(0x4E) STEP(0x141) /* quad xor 1, quad xor 2, half-row mirror: 8 lanes */
+    if constexpr (GJK_G == 16) STEP(0x140) /* row mirror: 16 */
 #undef STEP
 }
 
@@ -382,23 +384,37 @@ __device__ __forceinline__ double group_max(double x) {
     x = ug_max(x, ugd::dpp<0xB1>(x));
     x = ug_max(x, ugd::dpp<0x4E>(x));
     x = ug_max(x, ugd::dpp<0x141>(x));
-    return ug_max(x, ugd::dpp<0x140>(x));
+    if constexpr (ugd::GJK_G == 16) x = ug_max(x, ugd::dpp<0x140>(x));
+    return x;
 }
 __device__ __forceinline__ ugk::gv hs_cells(int v0, int scb, int cell, ugk::gv d, int gl) {
-    constexpr int G = ugd::GJK_G;
-    static_assert(UG_SC_SLOTS == G, "one cell slot per lane of a GJK group");
+    constexpr int G = ugd::GJK_G, K = UG_SC_SLOTS / G; /* candidates per lane: lane l holds slots l, l + G */
+    static_assert(UG_SC_SLOTS % G == 0 && K <= 2, "a cell's slots over the lanes of a GJK group");
     const int c = scb + cell;
     const unsigned short* L = &UG_SC_IDX[c * UG_SC_SLOTS];
     const double* P = &UG_SC_XYZ[(c * UG_SC_SLOTS + gl) * 3];
     const int s0 = L[0];
-    ugk::gv bv = ugk::V3(P[0], P[1], P[2]); /* loaded with the list head: the common case needs nothing else */
+    /* loaded with the list head: the common case needs nothing else */
+    ugk::gv bv = ugk::V3(P[0], P[1], P[2]);
+    ugk::gv bv2 = bv;
+    if constexpr (K == 2) bv2 = ugk::V3(P[3 * G], P[3 * G + 1], P[3 * G + 2]);
     const int base = (int)(threadIdx.x & ~(G - 1));
     int src;
     if (s0 != UG_SC_OVF) {
         const double dd = bv.x * d.x + bv.y * d.y + bv.z * d.z;
-        const double M = group_max(dd);
-        const unsigned long long hit = ugd::ballot(dd == M);
-        src = base + __builtin_ctzll((hit >> base) & ((1ull << G) - 1ull));
+        if constexpr (K == 1) {
+            const double M = group_max(dd);
+            const unsigned long long hit = ugd::ballot(dd == M);
+            src = base + __builtin_ctzll((hit >> base) & ((1ull << G) - 1ull));
+        } else {
+            /* the first maximum over the ascending list: slots l (< G) before slots G + l */
+            const double dd2 = bv2.x * d.x + bv2.y * d.y + bv2.z * d.z;
+            const double M = group_max(ug_max(dd, dd2));
+            const unsigned long long h1 = (ugd::ballot(dd == M) >> base) & ((1ull << G) - 1ull);
+            const unsigned long long h2 = (ugd::ballot(dd2 == M) >> base) & ((1ull << G) - 1ull);
+            src = base + __builtin_ctzll(h1 ? h1 : h2);
+            if (!h1) bv = bv2;
+        }
     } else {
         double best = -__builtin_inf();
         int key = 0x7fffffff;
@@ -467,11 +483,19 @@ UGK_FN ugk::gv ugk_hull_support(const ugk::GShape& sh, ugk::gv d) {
  * that may sit in either space would need a generic pointer, and every flat access waits for all outstanding memory
  * operations of the wave (measured: 308 full waits in the solver with LDS / workspace tiers for the faces). */
 #define UG_LDS __attribute__((address_space(3)))
+#if UG_GJK_G == 16
 static_assert(ugd::GJK_NG * 4 * sizeof(ugk::ESv) <= 3 * sizeof(double) * NVP, "the GJK stores in v0 | dvout | dvsout");
 static_assert(offsetof(ugd::Shared, dvsout) == offsetof(ugd::Shared, v0) + 2 * sizeof(double) * NVP, "v0, dvout, dvsout adjacent");
 static_assert(ugd::GJK_NG * ugk::kEpaMaxFaces <= sizeof(double) * NB * NB, "EPA hull-slot tables in LDL");
+#define UG_GJK_SV_BASE (&ugd::g_sh.v0[0])
+#define UG_GJK_HPOS_BASE (&ugd::g_sh.LDL[0])
+#else
+static_assert(sizeof(ugk::ESv) == 6 * sizeof(double) && ugk::kEpaMaxFaces == 256, "Shared::gjk_lds's sizing");
+#define UG_GJK_SV_BASE (&ugd::g_sh.gjk_lds[0])
+#define UG_GJK_HPOS_BASE (&ugd::g_sh.gjk_lds[ugd::GJK_NG * 4 * 6])
+#endif
 __device__ __forceinline__ int gjk_grp() { return (int)(threadIdx.x / ugd::GJK_G); }
-__device__ __forceinline__ UG_LDS ugk::ESv* lds_sv() { return (UG_LDS ugk::ESv*)(UG_LDS void*)&ugd::g_sh.v0[0] + gjk_grp() * 4; }
+__device__ __forceinline__ UG_LDS ugk::ESv* lds_sv() { return (UG_LDS ugk::ESv*)(UG_LDS void*)UG_GJK_SV_BASE + gjk_grp() * 4; }
 UGK_FN ugk::ESv ugk_svl_get(UGK_GMEM ugk::EpaMem*, int i) {
     const UG_LDS ugk::ESv& s = lds_sv()[i];
     ugk::ESv v;
@@ -485,7 +509,7 @@ UGK_FN void ugk_svl_put(UGK_GMEM ugk::EpaMem*, int i, const ugk::ESv& v) {
     s.w.x = v.w.x; s.w.y = v.w.y; s.w.z = v.w.z;
 }
 UGK_FN UGK_LMEM unsigned char* ugk_hpos(UGK_GMEM ugk::EpaMem*) {
-    return (UGK_LMEM unsigned char*)(UGK_LMEM void*)&ugd::g_sh.LDL[0] + gjk_grp() * ugk::kEpaMaxFaces;
+    return (UGK_LMEM unsigned char*)(UGK_LMEM void*)UG_GJK_HPOS_BASE + gjk_grp() * ugk::kEpaMaxFaces;
 }
 UGK_FN ugk::EFace ugk_face_get(UGK_GMEM ugk::EpaMem* E, int f) {
     const UGK_GMEM ugk::EFace& G = E->fc[f];
