@@ -19,10 +19,10 @@ def test_header_and_binding_agree(built):
     assert sorted(SYMBOLS) == header_symbols()
 
 
-@pytest.mark.parametrize("robot", ["ur5_robotiq_85", "ur5_robotiq_140"])
+@pytest.mark.parametrize("robot", ["ur5_robotiq_85", "ur5_robotiq_140", "g8"])
 def test_library_exports_every_declared_symbol(built, robot):
-    from urgym_amd._native import ROBOT_LIBS
-    L = ctypes.CDLL(ROBOT_LIBS[robot])  # both robots' builds carry the whole C-ABI
+    from urgym_amd._native import G8_LIB, ROBOT_LIBS
+    L = ctypes.CDLL(G8_LIB if robot == "g8" else ROBOT_LIBS[robot])  # every build carries the whole C-ABI
     for s in header_symbols():
         assert hasattr(L, s), s
 

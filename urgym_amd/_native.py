@@ -33,13 +33,20 @@ CONTACT_FIELDS = 24  # pybullet getContactPoints tuple, flattened
 # robot.py's arm + gripper classes -> their build of the library (same sources, the robot's model header):
 # UR5Robotiq85 (every registered env) and UR5Robotiq140 (robot.py:221-240, liburgym_r140.so)
 ROBOT_LIBS = {"ur5_robotiq_85": LIB_PATH, "ur5_robotiq_140": os.path.join(_HERE, "_lib", "liburgym_r140.so")}
+# Golf-v0 / GolfJoints-v0 run the build with 8-lane GJK groups (UG_GJK_G 8: eight convex pairs per round; Golf's
+# 6.3 GJK queries per substep fit one round instead of two -- Golf +3 %, GolfJoints +7 %; BallBalance, 3.4 queries,
+# loses 1.4 % with it, so every other task keeps the 16-lane build).  Same sources, same results bit for bit.
+G8_LIB = os.path.join(_HERE, "_lib", "liburgym_g8.so")
+G8_TASKS = (3, 5)
 _libs = {}
 
 
-def lib(robot="ur5_robotiq_85"):
+def lib(robot="ur5_robotiq_85", task=None):
     if robot not in ROBOT_LIBS:
         raise ValueError(f"robot must be one of {sorted(ROBOT_LIBS)}, not {robot!r}")
     path = ROBOT_LIBS[robot]
+    if robot == "ur5_robotiq_85" and task in G8_TASKS and not os.environ.get("URGYM_LIB"):
+        path = G8_LIB
     if path in _libs:
         return _libs[path]
     if not os.path.exists(path):
@@ -109,7 +116,7 @@ class Sim:
     def __init__(self, task, n_envs, device=0, seed=0, env_offset=0, flags=0, robot="ur5_robotiq_85"):
         """flags: 0 or GEOM_FULL = the full geometry (default), GEOM_LOD = the collision LOD; robot: the arm +
         gripper (robot.py's UR5Robotiq85, every registered env's, or UR5Robotiq140)"""
-        self.L = lib(robot)
+        self.L = lib(robot, task)
         self.robot = robot
         self.task = task
         self.n = n_envs
