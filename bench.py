@@ -172,6 +172,8 @@ def main(argv=None):
                          "pair and substep) or vih (rounds 1-3's vertex-in-hull generator: URGYM_FLAG_CONTACT_VIH)")
     ap.add_argument("--robot", choices=("ur5_robotiq_85", "ur5_robotiq_140"), default="ur5_robotiq_85",
                     help="arm + gripper (robot.py): UR5Robotiq85 (every registered env; default) or UR5Robotiq140")
+    ap.add_argument("--gather", action="store_true", help="all-gather the returns every step also at N=1 (a process "
+                    "group of one rank: RCCL's all-gather timed on one GPU; with N>1 the gather always runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL over xGMI); gloo only to rehearse several ranks "
@@ -188,8 +190,12 @@ def main(argv=None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     gpu = local % max(torch.cuda.device_count(), 1)  # == local on a node with a GPU per rank
-    if world > 1:
+    use_pg = world > 1 or args.gather
+    if use_pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            from urgym_amd.parallel import free_port
+            os.environ["MASTER_PORT"] = str(free_port())
         torch.cuda.set_device(gpu)
         dist.init_process_group(args.backend, rank=rank, world_size=world)
         world = dist.get_world_size()
@@ -216,7 +222,7 @@ def main(argv=None):
     succ = torch.zeros_like(term)
     sub = torch.zeros(n, dtype=torch.int32, device=dev)
     stream = torch.cuda.ExternalStream(sim.L.urgym_stream(sim.h), device=dev)
-    if world > 1:
+    if use_pg:
         from urgym_amd.parallel import ReturnGather
         gat = ReturnGather(n, O, dev)
 
@@ -225,7 +231,7 @@ def main(argv=None):
                         trunc.data_ptr(), succ.data_ptr(), sub.data_ptr())
         if e is not None:
             e.record(stream)
-        if world > 1:
+        if use_pg:
             # every return gathered over RCCL (xGMI) into one preallocated global buffer, global env-id order
             with torch.cuda.stream(stream):
                 gat.gather(obs, fin, rew, term, trunc, succ, sub)
@@ -248,7 +254,7 @@ def main(argv=None):
         sub_tot.zero_()
         res_tot.zero_()
         torch.cuda.synchronize()
-        if world > 1:
+        if use_pg:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -261,14 +267,14 @@ def main(argv=None):
                 res_tot += (term | trunc).sum()
         sim.sync()
         torch.cuda.synchronize()
-        if world > 1:
+        if use_pg:
             dist.barrier()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         kern_ms = [a.elapsed_time(b) for a, b in ev]
         vals = torch.tensor([dt, float(sub_tot.item()), float(res_tot.item()), float(np.mean(kern_ms))],
                             dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
-        if world > 1:
+        if use_pg:
             mx = vals.clone()
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
             dist.all_reduce(vals, op=dist.ReduceOp.SUM)
@@ -326,7 +332,7 @@ def main(argv=None):
                                f"{MAX_STEPS[args.task]}", "envs_per_gpu": n, "total_envs": n * world,
                    "parallelism": f"env-dp{world}", "world_size": world, "geometry": args.geometry,
                    "contact": args.contact,
-                   "backend": args.backend if world > 1 else None, "robot": args.robot},
+                   "backend": args.backend if use_pg else None, "returns_gathered": use_pg, "robot": args.robot},
         "rep_values": [env_steps / x[0] for x in reps],
         "substeps_per_env_step": substeps / env_steps,
         "resets": int(resets),
@@ -337,7 +343,7 @@ def main(argv=None):
     if rank == 0:
         print(json.dumps(line), flush=True)
     sim.close()
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
     return 0
 

@@ -4,7 +4,8 @@
   for bit, over 10 autoreset steps (a synchronized truncation reset of every env included), with envs sampled
   from every shard checked against the CPU restatement step by step;
 * two gloo ranks (torch.distributed.run children, both on this GPU) stepping their shards of a batch and
-  all-gathering the returns each step == one handle stepping the whole batch;
+  all-gathering the returns each step == one handle stepping the whole batch; the same through RCCL (nccl backend,
+  device tensors) with one rank;
 * full episodes at the configs' sizes: CubesPush x 4096 through its 50-step truncation, CubesGrasp x 8192 through
   its 20-step truncation, sampled envs bit-exact against the restatement at every step.
 Reference: BASELINE.json configs[2..4]; /root/reference/urgym/envs/env_golf_v0.py:115-446,
@@ -100,20 +101,23 @@ def test_config_e_eight_shards_equal_one_65536_handle(mods):
         s.close()
 
 
-def test_gloo_ranks_gather_real_sim_outputs(mods, tmp_path):
-    """two ranks (torch.distributed.run children on this GPU, gloo) step their halves of a BallBalance batch and
-    all-gather every return (obs, final_obs, reward, terminated, truncated, success, substeps) each step through one
-    ReturnGather; the gathered batches equal one handle stepping the
-    whole batch with the same action stream (autoreset through truncation at 4 steps)."""
+@pytest.mark.parametrize("backend,world", [("gloo", 2), ("nccl", 1)])
+def test_ranks_gather_real_sim_outputs(mods, tmp_path, backend, world):
+    """ranks (torch.distributed.run children on this GPU) step their shards of a BallBalance batch and all-gather
+    every return (obs, final_obs, reward, terminated, truncated, success, substeps) each step through one
+    ReturnGather; the gathered batches equal one handle stepping the whole batch with the same action stream
+    (autoreset through truncation at 4 steps).  gloo: two ranks sharing the GPU, returns through host memory.
+    nccl: RCCL, the production branch (device tensors gathered from HBM, parallel.py ReturnGather) -- one rank,
+    since RCCL refuses two ranks on one GPU and this box has one; the 8-rank node run is the driver's."""
     Sim, _ = mods
     from urgym_amd.parallel import spawn_ranks
     task, total, steps, max_steps, seed = 0, 256, 6, 4, 4242
     out = tmp_path / "gathered.npz"
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_sim_rank_worker.py")
-    rc = spawn_ranks(2, worker, [str(out), str(task), str(total), str(steps), str(max_steps), str(seed)])
+    rc = spawn_ranks(world, worker, [str(out), str(task), str(total), str(steps), str(max_steps), str(seed), backend])
     assert rc == 0
     g = np.load(out)
-    assert int(g["world"]) == 2
+    assert int(g["world"]) == world and str(g["backend"]) == backend
     sim = Sim(task, total, seed=seed)
     sim.set_autoreset(True, max_steps)
     sim.reset()
