@@ -115,6 +115,9 @@ def main():
                  "resets": int(rs.sum()),
                  "substeps_p50_p90_p99_max": [float(np.percentile(ns, q)) for q in (50, 90, 99)] + [float(ns.max())],
                  "us_per_substep_median": float(np.median(dur / np.maximum(ns, 1))),
+                 "work_ms": float(dur.sum() / 1e3),  # the blocks' summed durations (co-runner contention A/B)
+                 "reset_us_per_substep_median": float(np.median((dur / np.maximum(ns, 1))[rs == 1])) if rs.any() else 0.0,
+                 "cus_used": int(len(np.unique(((b[:, 3] >> 20) & 15) << 16 | ((b[:, 3] >> 40) & 0xFF)))),
                  "sched_launch_order_ms": list_schedule(dur, range(n), slots) / 1e3,
                  "sched_longest_first_ms": list_schedule(dur, np.argsort(-dur, kind="stable"), slots) / 1e3}
             if prev_ns is not None:
