@@ -9,6 +9,7 @@
 #   bash tools/gpu.sh sweep <tag> [bench.py args...]    every task at its BASELINE size -> <tag>/task<N>.json
 #   bash tools/gpu.sh phase <tag> [phase_prof args...]  phase cycles of the profiling build -> <tag>/phase.txt
 #   bash tools/gpu.sh chain <tag> [task envs]           reset-chain / step-chain timings -> <tag>/chain.txt
+#   bash tools/gpu.sh contend <tag> [bench.py args...]  co-runner contention: PMC at default slots vs one wave per CU
 #   bash tools/gpu.sh timeline <tag> [timeline args]    k_step block timeline + schedule predictions -> <tag>/timeline.txt, .json
 #   bash tools/gpu.sh profile <tag> [bench.py args...]  rocprofv3 kernel trace + stats, FETCH_SIZE / WRITE_SIZE PMC
 #                                                       passes (one counter group per run), traffic json, bench line
@@ -99,6 +100,21 @@ icache)
     timeout -s KILL 180 rocprofv3 --pmc $G2 --output-format csv -d "$OUT/if" -o run -- python3 bench.py $ARGS \
         > "$OUT/if.log" 2>&1 || { echo "IFETCH PASS FAILED"; exit 1; }
     echo ICACHE_OK ;;
+contend)
+    # co-runner contention: the same k_step work at the default wave slots and at URGYM_SLOTS=256
+    # (one wave per CU), two counter passes each; tools/contend_pmc.py compares them per env-step
+    ARGS="${*:---steps 5 --warmup 2 --reps 1 --no-cpu-baseline}"
+    for SL in 0 256; do
+        i=0
+        mkdir -p "$OUT/s$SL"
+        for G in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM SQ_IFETCH SQC_ICACHE_MISSES SQC_ICACHE_REQ SQ_BUSY_CYCLES" \
+                 "TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCC_HIT_sum TCC_MISS_sum TA_BUSY_avr SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAVES"; do
+            i=$((i+1))
+            URGYM_SLOTS=$SL timeout -s KILL 180 rocprofv3 --pmc $G --output-format csv -d "$OUT/s$SL/p$i" -o run -- \
+                python3 bench.py $ARGS > "$OUT/s$SL/p$i.log" 2>&1 || { echo "CONTEND $SL PASS $i FAILED"; exit 1; }
+        done
+    done
+    python3 tools/contend_pmc.py "$OUT" > "$OUT/contend.txt" && cat "$OUT/contend.txt" ;;
 world8)
     timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29533 bench.py --gpus 8 --backend gloo --no-cpu-baseline "$@" > "$OUT/world8.json" \
