@@ -126,12 +126,12 @@ def main():
             r.update(placement(b, st, en, dur))
             # the launch order against the resets: their positions (a reset placed past the first `slots` envs
             # starts its chain only when a slot frees), and the priority classes this launch was ordered by
-            # (word 3 bits 24-31: the level each env computed for the next launch, taken from the last launch; 16 bands)
+            # (word 3 bits 24-31: the level the env had when this launch was ordered; 16 bands)
             kr = np.nonzero(rs)[0]
             r["reset_pos_past_slots"] = int((kr >= slots).sum())
             r["reset_pos_max"] = int(kr.max()) if len(kr) else -1
             if prev_cls is not None:
-                cls = prev_cls[b[:, 2]] >> 4  # the 256 launch levels in 16 bands
+                cls = ((b[:, 3] >> 24) & 255) >> 4  # the level this launch was ordered by, in 16 bands
                 r["class_hist"] = np.bincount(cls, minlength=16).tolist()
                 r["reset_class_hist"] = np.bincount(cls[rs == 1], minlength=16).tolist()
                 fresh = prev_rs[b[:, 2]] == 1  # the env reset in the last launch: its episode's first step now

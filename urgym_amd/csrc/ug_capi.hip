@@ -496,9 +496,10 @@ static __device__ __forceinline__ void step_env(const Scene* sc, double* S, uint
                                                 const float* act, double* obs, double* final_obs, double* rew,
                                                 uint8_t* term, uint8_t* trunc, uint8_t* succ, int32_t* substeps,
                                                 int autoreset, int max_steps, int i, int k, uint8_t* prio, int* stats,
-                                                uint8_t* flags) {
+                                                uint8_t* flags, double* pfeat) {
 #ifdef UG_PROF
     const unsigned long long bt0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long lvl = prio[i]; /* the level this launch was ordered by */
 #endif
     double* Si = S + (size_t)i * UG_STATE_DIM;
     team_load(Si, stats + (size_t)i * UG_NSTAT);
@@ -524,7 +525,8 @@ static __device__ __forceinline__ void step_env(const Scene* sc, double* S, uint
         if (trunc) trunc[i] = (uint8_t)io.trunc;
         if (succ) succ[i] = (uint8_t)io.succ;
         if (substeps) substeps[i] = ns;
-        prio[i] = (uint8_t)team_priority(sc, ns, elapsed[i] + 1, max_steps, autoreset);
+        prio[i] = (uint8_t)team_priority(sc, ns, elapsed[i] + 1, max_steps, autoreset,
+                                         pfeat ? pfeat + (size_t)i * UG_PF_STRIDE : nullptr);
 #ifdef UG_PROF
         if (k < UG_BT_MAX) { /* per launch-order position */
             unsigned long long* bt = &g_btime[4 * k];
@@ -535,7 +537,7 @@ static __device__ __forceinline__ void step_env(const Scene* sc, double* S, uint
             bt[1] = __builtin_amdgcn_s_memrealtime();
             bt[2] = (unsigned long long)i;
             bt[3] = (unsigned long long)ns | ((unsigned long long)io.reset_done << 16) |
-                    ((unsigned long long)(xcc & 15u) << 20) | ((unsigned long long)prio[i] << 24) |
+                    ((unsigned long long)(xcc & 15u) << 20) | (lvl << 24) |
                     ((unsigned long long)hwid << 32);
         }
 #endif
@@ -546,13 +548,30 @@ __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, ui
                                                   int n, const float* act, double* obs, double* final_obs, double* rew,
                                                   uint8_t* term, uint8_t* trunc, uint8_t* succ, int32_t* substeps,
                                                   int autoreset, int max_steps, const int* order, uint8_t* prio,
-                                                  int* stats, uint8_t* flags, int* queue) {
+                                                  int* stats, uint8_t* flags, int* queue, double* pfeat) {
     for (;;) {
         const int k = queue_next(queue);
         if (k >= n) return;
         step_env(sc, S, mt, elapsed, ws, act, obs, final_obs, rew, term, trunc, succ, substeps, autoreset, max_steps,
-                 order[k], k, prio, stats, flags);
+                 order[k], k, prio, stats, flags, pfeat);
     }
+}
+
+/* TwoBallsBalance's launch levels from the step's own action (scheduling only): per env, the state inputs its last
+ * step left in pfeat (team_priority) and the 3 action components of this step -> the two-ball model's logit -> its
+ * level; envs whose record is not flagged (a predicted truncation, an inactive ball) keep their level.  One thread
+ * per env, before k_order. */
+static_assert(UG_ACT_DIM(UG_TASK_TWOBALLS) == UG_PT_IN - UG_PT_STATE_IN, "TwoBalls' action: the model's last inputs");
+__global__ void k_prio(const double* pfeat, const float* act, uint8_t* prio, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double* f = pfeat + (size_t)i * UG_PF_STRIDE;
+    if (f[UG_PF_STRIDE - 1] == 0.0) return;
+    double x[UG_PT_IN];
+    for (int k = 0; k < UG_PT_STATE_IN; k++) x[k] = f[k];
+    for (int a = 0; a < UG_PT_IN - UG_PT_STATE_IN; a++) x[UG_PT_STATE_IN + a] = (double)act[(size_t)i * 3 + a];
+    prio[i] = (uint8_t)logit_level(mlp_logit<UG_PT_IN, UG_PT_HID>(x, UG_PT_MU, UG_PT_SD, UG_PT_W1, UG_PT_B1, UG_PT_W2,
+                                                                   UG_PT_B2), UG_PT_L0, UG_PT_DL);
 }
 
 /* next launch order: envs by descending priority (0..255), ties by ascending env index (deterministic), one block.
@@ -820,6 +839,7 @@ struct urgym_handle {
     int* d_queue = nullptr;   // the step / reset work-queue counter
     int slots = 0;            // k_step / k_reset blocks: the wave slots the device holds at once (CUs x blocks per CU)
     uint8_t* d_prio = nullptr;
+    double* d_pfeat = nullptr; // TwoBalls: per env the predictor's state inputs for k_prio (UG_PF_STRIDE doubles)
     int* d_stats = nullptr;   // UG_NSTAT event counters per env
     uint8_t* d_flags = nullptr; // UG_FLAG_* of the last step / reset per env
     int autoreset = 0, max_steps = 0;
@@ -900,6 +920,10 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     HIPCHK(h, hipMalloc(&h->d_order, sizeof(int) * N));
     HIPCHK(h, hipMalloc(&h->d_order_tmp, sizeof(int) * N));
     HIPCHK(h, hipMalloc(&h->d_prio, N));
+    if (task == URGYM_TASK_TWOBALLSBALANCE) {
+        HIPCHK(h, hipMalloc(&h->d_pfeat, sizeof(double) * UG_PF_STRIDE * N));
+        HIPCHK(h, hipMemsetAsync(h->d_pfeat, 0, sizeof(double) * UG_PF_STRIDE * N, h->stream));
+    }
     HIPCHK(h, hipMalloc(&h->d_queue, sizeof(int)));
     {
         int cus = 0, per = 0;
@@ -965,7 +989,7 @@ void urgym_destroy(urgym_handle* h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     void* ptrs[] = {h->d_scene, h->d_state, h->d_ws, h->d_mt, h->d_elapsed, h->d_act, h->d_obs, h->d_final, h->d_rew,
                     h->d_draws, h->d_aux, h->d_term, h->d_trunc, h->d_succ, h->d_mask, h->d_sub, h->d_order, h->d_prio,
-                    h->d_stats, h->d_flags, h->d_campose, h->d_queue, h->d_order_tmp};
+                    h->d_stats, h->d_flags, h->d_campose, h->d_queue, h->d_order_tmp, h->d_pfeat};
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (h->ev0) hipEventDestroy(h->ev0);
@@ -1032,16 +1056,21 @@ int urgym_step_device(urgym_handle* h, const float* d_act, double* d_obs, double
     if (!h) return -1;
     if (!d_act || !d_obs) return fail(h, "urgym_step_device: actions and obs must not be NULL");
     HIPCHK(h, hipSetDevice(h->dev));
+    /* the launch order: the priorities the envs' last step left (TwoBalls: completed with this step's actions) */
+    if (h->d_pfeat) {
+        k_prio<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_pfeat, d_act, h->d_prio, h->n);
+        HIPCHK(h, hipGetLastError());
+    }
+    k_order<<<1, ORDER_THREADS, 0, h->stream>>>(h->d_prio, h->d_order, h->d_order_tmp, h->n);
+    HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipMemsetAsync(h->d_queue, 0, sizeof(int), h->stream));
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
     k_step<<<std::min(h->n, h->slots), TEAM, 0, h->stream>>>(h->d_scene, h->d_state, h->d_mt, h->d_elapsed, h->d_ws, h->n,
                                                               d_act, d_obs, d_final, d_rew, d_term, d_trunc, d_succ, d_sub,
                                                               h->autoreset, h->max_steps, h->d_order, h->d_prio,
-                                                              h->d_stats, h->d_flags, h->d_queue);
+                                                              h->d_stats, h->d_flags, h->d_queue, h->d_pfeat);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
-    k_order<<<1, ORDER_THREADS, 0, h->stream>>>(h->d_prio, h->d_order, h->d_order_tmp, h->n);
-    HIPCHK(h, hipGetLastError());
     h->timed = true;
     return 0;
 }

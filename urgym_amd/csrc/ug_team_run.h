@@ -712,13 +712,18 @@ __device__ static double bb_reset_logit(const EnvState& e, const m3& R, int o) {
     bb_ball_inputs(e, R, o, x);
     return mlp_logit<UG_PM_IN, UG_PM_HID>(x, UG_PM_MU, UG_PM_SD, UG_PM_W1, UG_PM_B1, UG_PM_W2, UG_PM_B2);
 }
-/* TwoBallsBalance: one model over both balls' inputs, the episode's elapsed steps and the paddle's vertical velocity,
- * 31 -> 16 (ReLU) -> 1 (prio_model_tb.h, tools/fit_priority.py --task 6): the larger of two single-ball logits
- * ranked the resets where both balls hit the paddle together last (~55 per step, the launch 37 ms against 23.5 ms
- * for the longest-first order) */
-__device__ static double tb_reset_logit(const EnvState& e, const m3& R, int el) {
-    static_assert(UG_PT_IN == 2 * UG_PM_IN + 3, "two balls' inputs, elapsed (clipped, log) and the paddle's vz");
-    double x[UG_PT_IN], b[UG_PM_IN];
+/* TwoBallsBalance: one model over both balls' inputs, the episode's elapsed steps, the paddle's vertical velocity and
+ * the next step's action, 34 -> 32 (ReLU) -> 1 (prio_model_tb.h, tools/fit_priority.py --task 6): the larger of two
+ * single-ball logits ranked the resets where both balls hit the paddle together last (~55 per step, the launch 37 ms
+ * against 23.5 ms for the longest-first order); without the action ~58 of ~420 resets per step ranked outside the
+ * first 1024 launch slots, with it ~15.  The env writes its 31 state inputs here (UG_PF_STRIDE doubles per env, the
+ * last one a "model applies" flag); k_prio adds the action once it is known and sets the launch level. */
+#define UG_PF_STRIDE 32
+#define UG_PT_STATE_IN (2 * UG_PM_IN + 3)
+static_assert(UG_PT_IN == UG_PT_STATE_IN + 3, "two balls' inputs, elapsed (clipped, log), the paddle's vz, the action");
+static_assert(UG_PT_STATE_IN < UG_PF_STRIDE, "the flag follows the state inputs");
+__device__ static void tb_state_inputs(const EnvState& e, const m3& R, int el, double* x) {
+    double b[UG_PM_IN];
     for (int o = 1; o <= 2; o++) {
         bb_ball_inputs(e, R, o, b);
         for (int i = 0; i < UG_PM_IN; i++) x[(o - 1) * UG_PM_IN + i] = b[i];
@@ -726,13 +731,12 @@ __device__ static double tb_reset_logit(const EnvState& e, const m3& R, int el) 
     x[2 * UG_PM_IN] = fmin((double)el, 10.0);
     x[2 * UG_PM_IN + 1] = log((double)el + 1.0);
     x[2 * UG_PM_IN + 2] = e.obj[0].v.z;
-    return mlp_logit<UG_PT_IN, UG_PT_HID>(x, UG_PT_MU, UG_PT_SD, UG_PT_W1, UG_PT_B1, UG_PT_W2, UG_PT_B2);
 }
 /* Launch-order priority of an env for the next k_step (0..255, higher runs first).  The launch time is the
  * longest env chain, and an env-step that ends its episode carries a ~170-substep autoreset: envs likely
  * to end next step are dispatched first so their reset overlaps the other envs' steps.  Scheduling only --
  * every env computes the same thing whatever its position in the launch.  Predicted truncation: 255;
- * TwoBalls: its own two-ball model (tb_reset_logit) in 255 levels; BallBalance: the reset predictor's logit in 255 levels
+ * TwoBalls: its own two-ball model in 255 levels (k_prio, with the action); BallBalance: the reset predictor's logit in 255 levels
  * (held-out random-action BallBalance x 4096:
  * 0.44 of ~270 resets per step ranked outside the first 1024 launch slots, against 1.1 for an edge-roll +
  * free-fall time and 5.8 for a position-extrapolation score); otherwise the env's last substep count. */
@@ -742,11 +746,15 @@ __device__ static int logit_level(double lg, double l0, double dl) {
     const double b = floor((lg - l0) / dl);
     return b > 254.0 ? 254 : (b < 0.0 ? 0 : (int)b); /* a NaN logit: level 0 */
 }
-__device__ static int team_priority(const Scene* s, int nsub, int el_next, int max_steps, int autoreset) {
+__device__ static int team_priority(const Scene* s, int nsub, int el_next, int max_steps, int autoreset, double* pf) {
     const EnvState& e = g_sh.e;
+    if (pf) pf[UG_PF_STRIDE - 1] = 0.0; /* k_prio keeps this level unless the TwoBalls model applies */
     if (autoreset && max_steps > 0 && el_next >= max_steps) return 255;
-    if (s->variant == UG_TASK_TWOBALLS && e.oactive[0] != 0.0 && e.oactive[1] != 0.0 && e.oactive[2] != 0.0)
-        return logit_level(tb_reset_logit(e, qmat(e.obj[0].quat), el_next - 1), UG_PT_L0, UG_PT_DL);
+    if (s->variant == UG_TASK_TWOBALLS && pf && e.oactive[0] != 0.0 && e.oactive[1] != 0.0 && e.oactive[2] != 0.0) {
+        tb_state_inputs(e, qmat(e.obj[0].quat), el_next - 1, pf);
+        pf[UG_PF_STRIDE - 1] = 1.0;
+        return 0;
+    }
     if (s->task == UG_TASK_BALLBALANCE && e.oactive[0] != 0.0) {
         const m3 R = qmat(e.obj[0].quat);
         double lg = -1e300;
