@@ -29,6 +29,7 @@
 #include "ug_device.h"
 #include "prio_model.h"
 #include "prio_model_tb.h"
+#include "prio_model_cp.h"
 #include "ug_glue.h"
 
 namespace ugd {

@@ -736,7 +736,8 @@ __device__ static void tb_state_inputs(const EnvState& e, const m3& R, int el, d
  * longest env chain, and an env-step that ends its episode carries a ~170-substep autoreset: envs likely
  * to end next step are dispatched first so their reset overlaps the other envs' steps.  Scheduling only --
  * every env computes the same thing whatever its position in the launch.  Predicted truncation: 255;
- * TwoBalls: its own two-ball model in 255 levels (k_prio, with the action); BallBalance: the reset predictor's logit in 255 levels
+ * TwoBalls: its own two-ball model in 255 levels (k_prio, with the action); CubesPush(Diff): a step-length model
+ * (k_prio, with the action); BallBalance: the reset predictor's logit in 255 levels
  * (held-out random-action BallBalance x 4096:
  * 0.44 of ~270 resets per step ranked outside the first 1024 launch slots, against 1.1 for an edge-roll +
  * free-fall time and 5.8 for a position-extrapolation score); otherwise the env's last substep count. */
@@ -746,6 +747,10 @@ __device__ static int logit_level(double lg, double l0, double dl) {
     const double b = floor((lg - l0) / dl);
     return b > 254.0 ? 254 : (b < 0.0 ? 0 : (int)b); /* a NaN logit: level 0 */
 }
+/* CubesPush / CubesPushDiff: log(substeps) of the step from the arm's q, qd and the step's action, 27 -> 32 (ReLU) -> 1
+ * (prio_model_cp.h, tools/fit_priority.py --task 1): the launch is its longest env (45 ms against 16.8 ms balanced and
+ * 39.6 ms longest-first) and the last substep count does not predict it (correlation 0.02; the model 0.82) */
+static_assert(UG_PC_IN == 2 * 12 + 3, "q[12], qd[12], the action");
 __device__ static int team_priority(const Scene* s, int nsub, int el_next, int max_steps, int autoreset, double* pf) {
     const EnvState& e = g_sh.e;
     if (pf) pf[UG_PF_STRIDE - 1] = 0.0; /* k_prio keeps this level unless the TwoBalls model applies */
@@ -754,6 +759,13 @@ __device__ static int team_priority(const Scene* s, int nsub, int el_next, int m
         tb_state_inputs(e, qmat(e.obj[0].quat), el_next - 1, pf);
         pf[UG_PF_STRIDE - 1] = 1.0;
         return 0;
+    }
+    if constexpr (NB == 12) { /* CubesPush / CubesPushDiff: the step's length from q, qd and (k_prio) the action */
+        if (s->task == UG_TASK_CUBESPUSH && pf) {
+            for (int j = 0; j < NB; j++) { pf[j] = e.q[j]; pf[NB + j] = e.qd[j]; }
+            pf[UG_PF_STRIDE - 1] = 2.0;
+            return 0;
+        }
     }
     if (s->task == UG_TASK_BALLBALANCE && e.oactive[0] != 0.0) {
         const m3 R = qmat(e.obj[0].quat);
