@@ -557,12 +557,13 @@ __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, ui
     }
 }
 
-/* Launch levels from the step's own action (scheduling only; TwoBalls, CubesPush, CubesPushDiff): per env, the state
+/* Launch levels from the step's own action (scheduling only; BallBalance, TwoBalls, CubesPush, CubesPushDiff): per env, the state
  * inputs its last step left in pfeat (team_priority; the record's last double names the model) and the 3 action
  * components of this step -> the task's model -> the level; envs whose record is not flagged (a predicted truncation,
  * an inactive ball) keep their level.  One thread per env, before k_order. */
 static_assert(UG_ACT_DIM(UG_TASK_TWOBALLS) == UG_PT_IN - UG_PT_STATE_IN, "TwoBalls' action: the model's last inputs");
 static_assert(UG_ACT_DIM(UG_TASK_CUBESPUSH) == 3 && UG_ACT_DIM(UG_TASK_CUBESPUSHDIFF) == 3, "CubesPush's action: 3");
+static_assert(UG_ACT_DIM(UG_TASK_BALLBALANCE) == 3, "BallBalance's action: 3");
 __global__ void k_prio(const double* pfeat, const float* act, uint8_t* prio, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -574,6 +575,12 @@ __global__ void k_prio(const double* pfeat, const float* act, uint8_t* prio, int
         for (int a = 0; a < UG_PT_IN - UG_PT_STATE_IN; a++) x[UG_PT_STATE_IN + a] = (double)act[(size_t)i * 3 + a];
         prio[i] = (uint8_t)logit_level(mlp_logit<UG_PT_IN, UG_PT_HID>(x, UG_PT_MU, UG_PT_SD, UG_PT_W1, UG_PT_B1, UG_PT_W2,
                                                                        UG_PT_B2), UG_PT_L0, UG_PT_DL);
+    } else if (model == 3.0) { /* BallBalance: the ball's 14 inputs + the action */
+        double x[UG_PM_IN];
+        for (int k = 0; k < UG_BALL_IN; k++) x[k] = f[k];
+        for (int a = 0; a < 3; a++) x[UG_BALL_IN + a] = (double)act[(size_t)i * 3 + a];
+        prio[i] = (uint8_t)logit_level(mlp_logit<UG_PM_IN, UG_PM_HID>(x, UG_PM_MU, UG_PM_SD, UG_PM_W1, UG_PM_B1, UG_PM_W2,
+                                                                       UG_PM_B2), UG_PM_L0, UG_PM_DL);
     } else if (model == 2.0) { /* CubesPush(Diff): q, qd + the action */
         double x[UG_PC_IN];
         for (int k = 0; k < UG_PC_IN - 3; k++) x[k] = f[k];
@@ -848,7 +855,7 @@ struct urgym_handle {
     int* d_queue = nullptr;   // the step / reset work-queue counter
     int slots = 0;            // k_step / k_reset blocks: the wave slots the device holds at once (CUs x blocks per CU)
     uint8_t* d_prio = nullptr;
-    double* d_pfeat = nullptr; // TwoBalls, CubesPush(Diff): per env the predictor's state inputs for k_prio (UG_PF_STRIDE doubles)
+    double* d_pfeat = nullptr; // BallBalance, TwoBalls, CubesPush(Diff): per env the predictor's state inputs for k_prio (UG_PF_STRIDE doubles)
     int* d_stats = nullptr;   // UG_NSTAT event counters per env
     uint8_t* d_flags = nullptr; // UG_FLAG_* of the last step / reset per env
     int autoreset = 0, max_steps = 0;
@@ -929,7 +936,8 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     HIPCHK(h, hipMalloc(&h->d_order, sizeof(int) * N));
     HIPCHK(h, hipMalloc(&h->d_order_tmp, sizeof(int) * N));
     HIPCHK(h, hipMalloc(&h->d_prio, N));
-    if (task == URGYM_TASK_TWOBALLSBALANCE || task == URGYM_TASK_CUBESPUSH || task == URGYM_TASK_CUBESPUSHDIFF) {
+    if (task == URGYM_TASK_BALLBALANCE || task == URGYM_TASK_TWOBALLSBALANCE || task == URGYM_TASK_CUBESPUSH ||
+        task == URGYM_TASK_CUBESPUSHDIFF) {
         HIPCHK(h, hipMalloc(&h->d_pfeat, sizeof(double) * UG_PF_STRIDE * N));
         HIPCHK(h, hipMemsetAsync(h->d_pfeat, 0, sizeof(double) * UG_PF_STRIDE * N, h->stream));
     }

@@ -676,7 +676,8 @@ __device__ static void team_prof_flush() {
 /* BallBalance / TwoBalls reset predictor inputs (scheduling only): ball o in the paddle frame -> its paddle-frame
  * offset, velocities and in-plane gravity and the log times of an edge-roll + free-fall estimate (14 inputs,
  * tools/fit_priority.py features()) */
-__device__ static void bb_ball_inputs(const EnvState& e, const m3& R, int o, double (&x)[UG_PM_IN]) {
+#define UG_BALL_IN 14
+__device__ static void bb_ball_inputs(const EnvState& e, const m3& R, int o, double* x) {
     const v3 l = mtv(R, vsub(e.obj[o].pos, e.obj[0].pos));
     const v3 lv = mtv(R, vsub(e.obj[o].v, e.obj[0].v));
     const v3 gl = mtv(R, V(0.0, 0.0, -9.81));
@@ -687,9 +688,9 @@ __device__ static void bb_ball_inputs(const EnvState& e, const m3& R, int o, dou
     const double tf = dz < 0.0 ? 0.0 : (bvz + sqrt(bvz * bvz + 2.0 * 9.81 * dz)) / 9.81;
     const double tex = fx >= 1.0 ? 0.0 : (1.0 - fx) * UG_BB_PADDLE_HX / fmax(vx, 0.05);
     const double tey = fy >= 1.0 ? 0.0 : (1.0 - fy) * UG_BB_PADDLE_HY / fmax(vy, 0.05);
-    const double v[UG_PM_IN] = {fx, fy, l.z, vx, vy, lv.z, dz, bvz, gl.x * sx, gl.y * sy,
+    const double v[UG_BALL_IN] = {fx, fy, l.z, vx, vy, lv.z, dz, bvz, gl.x * sx, gl.y * sy,
                                 log(fmin(tex, tey) + tf + 1e-3), log(tex + 1e-3), log(tey + 1e-3), log(tf + 1e-3)};
-    for (int i = 0; i < UG_PM_IN; i++) x[i] = v[i];
+    for (int i = 0; i < UG_BALL_IN; i++) x[i] = v[i];
 }
 /* a 1-hidden-layer ReLU MLP's logit over standardised inputs */
 template <int IN, int HID>
@@ -705,13 +706,10 @@ __device__ static double mlp_logit(const double* x, const double* mu, const doub
     }
     return out;
 }
-/* BallBalance: the logit of "this env ends its episode in the next env-step" from one ball, a 14 -> 16 (ReLU) -> 1 MLP
- * (prio_model.h, tools/fit_priority.py) */
-__device__ static double bb_reset_logit(const EnvState& e, const m3& R, int o) {
-    double x[UG_PM_IN];
-    bb_ball_inputs(e, R, o, x);
-    return mlp_logit<UG_PM_IN, UG_PM_HID>(x, UG_PM_MU, UG_PM_SD, UG_PM_W1, UG_PM_B1, UG_PM_W2, UG_PM_B2);
-}
+/* BallBalance: the logit of "this env ends its episode in the next env-step" from the ball's 14 inputs and the step's
+ * action, a 17 -> 16 (ReLU) -> 1 MLP (prio_model.h, tools/fit_priority.py; the env leaves the 14 in its k_prio record,
+ * k_prio adds the action: held-out misses 0.45 -> 0 of ~264 resets per step) */
+static_assert(UG_PM_IN == UG_BALL_IN + 3, "the ball's inputs, the action");
 /* TwoBallsBalance: one model over both balls' inputs, the episode's elapsed steps, the paddle's vertical velocity and
  * the next step's action, 34 -> 32 (ReLU) -> 1 (prio_model_tb.h, tools/fit_priority.py --task 6): the larger of two
  * single-ball logits ranked the resets where both balls hit the paddle together last (~55 per step, the launch 37 ms
@@ -719,30 +717,24 @@ __device__ static double bb_reset_logit(const EnvState& e, const m3& R, int o) {
  * first 1024 launch slots, with it ~15.  The env writes its 31 state inputs here (UG_PF_STRIDE doubles per env, the
  * last one a "model applies" flag); k_prio adds the action once it is known and sets the launch level. */
 #define UG_PF_STRIDE 32
-#define UG_PT_STATE_IN (2 * UG_PM_IN + 3)
+#define UG_PT_STATE_IN (2 * UG_BALL_IN + 3)
 static_assert(UG_PT_IN == UG_PT_STATE_IN + 3, "two balls' inputs, elapsed (clipped, log), the paddle's vz, the action");
 static_assert(UG_PT_STATE_IN < UG_PF_STRIDE, "the flag follows the state inputs");
 __device__ static void tb_state_inputs(const EnvState& e, const m3& R, int el, double* x) {
-    double b[UG_PM_IN];
-    for (int o = 1; o <= 2; o++) {
-        bb_ball_inputs(e, R, o, b);
-        for (int i = 0; i < UG_PM_IN; i++) x[(o - 1) * UG_PM_IN + i] = b[i];
-    }
-    x[2 * UG_PM_IN] = fmin((double)el, 10.0);
-    x[2 * UG_PM_IN + 1] = log((double)el + 1.0);
-    x[2 * UG_PM_IN + 2] = e.obj[0].v.z;
+    for (int o = 1; o <= 2; o++) bb_ball_inputs(e, R, o, x + (o - 1) * UG_BALL_IN);
+    x[2 * UG_BALL_IN] = fmin((double)el, 10.0);
+    x[2 * UG_BALL_IN + 1] = log((double)el + 1.0);
+    x[2 * UG_BALL_IN + 2] = e.obj[0].v.z;
 }
 /* Launch-order priority of an env for the next k_step (0..255, higher runs first).  The launch time is the
  * longest env chain, and an env-step that ends its episode carries a ~170-substep autoreset: envs likely
  * to end next step are dispatched first so their reset overlaps the other envs' steps.  Scheduling only --
  * every env computes the same thing whatever its position in the launch.  Predicted truncation: 255;
  * TwoBalls: its own two-ball model in 255 levels (k_prio, with the action); CubesPush(Diff): a step-length model
- * (k_prio, with the action); BallBalance: the reset predictor's logit in 255 levels
+ * (k_prio, with the action); BallBalance: the reset predictor's logit in 255 levels (k_prio, with the action)
  * (held-out random-action BallBalance x 4096:
  * 0.44 of ~270 resets per step ranked outside the first 1024 launch slots, against 1.1 for an edge-roll +
  * free-fall time and 5.8 for a position-extrapolation score); otherwise the env's last substep count. */
-#define UG_PM_FINE_L0 -12.0 /* BallBalance's logit in 255 launch levels: [-12, 5.78) in steps of 0.07 */
-#define UG_PM_FINE_DL 0.07
 __device__ static int logit_level(double lg, double l0, double dl) {
     const double b = floor((lg - l0) / dl);
     return b > 254.0 ? 254 : (b < 0.0 ? 0 : (int)b); /* a NaN logit: level 0 */
@@ -767,12 +759,10 @@ __device__ static int team_priority(const Scene* s, int nsub, int el_next, int m
             return 0;
         }
     }
-    if (s->task == UG_TASK_BALLBALANCE && e.oactive[0] != 0.0) {
-        const m3 R = qmat(e.obj[0].quat);
-        double lg = -1e300;
-        for (int o = 1; o < s->nobj; o++)
-            if (e.oactive[o] != 0.0) lg = fmax(lg, bb_reset_logit(e, R, o));
-        return logit_level(lg, UG_PM_FINE_L0, UG_PM_FINE_DL);
+    if (s->variant == UG_TASK_BALLBALANCE && pf && e.oactive[0] != 0.0 && e.oactive[1] != 0.0) {
+        bb_ball_inputs(e, qmat(e.obj[0].quat), 1, pf);
+        pf[UG_PF_STRIDE - 1] = 3.0;
+        return 0;
     }
     int b = 0;
     while (b < 14 && (2 << b) <= nsub) b++;
