@@ -140,6 +140,26 @@ def work_model(task, geometry, contact):
         return None, None
 
 
+def action_stream(kind, rng, lo, hi, T, n):
+    """(T, n, A) float64 actions in [lo, hi].  uniform: the benchmark protocol.  ou: per env an
+    Ornstein-Uhlenbeck process x += theta (c - x) + sigma sqrt(2 theta) h N(0,1) in units of the half-range h about the
+    centre c (theta 0.15, sigma 0.5: lag-1 correlation 0.85, stationary spread half the half-range), clipped.  scaled:
+    c + 0.3 (u - c) for u uniform -- a policy-like stream that stays near the centre."""
+    A = lo.shape[0]
+    c, h = (lo + hi) / 2.0, (hi - lo) / 2.0
+    if kind == "uniform":
+        return rng.uniform(lo, hi, size=(T, n, A))
+    if kind == "scaled":
+        return c + 0.3 * (rng.uniform(lo, hi, size=(T, n, A)) - c)
+    theta, sigma = 0.15, 0.5
+    out = np.empty((T, n, A))
+    x = rng.uniform(-0.5, 0.5, size=(n, A))
+    for t in range(T):
+        x = x + theta * (0.0 - x) + sigma * np.sqrt(2.0 * theta) * rng.standard_normal((n, A))
+        out[t] = np.clip(c + h * x, lo, hi)
+    return out
+
+
 def maybe_spawn(args, argv):
     """--gpus N > 1 outside a launcher: start the N ranks as children (before any GPU call) and return their
     exit code; under a launcher, refuse a WORLD_SIZE that disagrees with --gpus.  None: run in-process."""
@@ -174,6 +194,10 @@ def main(argv=None):
                     help="arm + gripper (robot.py): UR5Robotiq85 (every registered env; default) or UR5Robotiq140")
     ap.add_argument("--gather", action="store_true", help="all-gather the returns every step also at N=1 (a process "
                     "group of one rank: RCCL's all-gather timed on one GPU; with N>1 the gather always runs)")
+    ap.add_argument("--actions", choices=("uniform", "ou", "scaled"), default="uniform",
+                    help="synthetic action stream: uniform in the action space (SURVEY 8(d), the default), ou "
+                         "(time-correlated Ornstein-Uhlenbeck around the space's centre, clipped) or scaled (uniform "
+                         "shrunk x0.3 about the centre) -- the last two check the launch-order models off-distribution")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--backend", default="nccl", help="nccl (RCCL over xGMI); gloo only to rehearse several ranks "
@@ -213,7 +237,7 @@ def main(argv=None):
     from urgym_amd.envs import spaces_for
     _, act_space = spaces_for(args.task)
     lo, hi = np.asarray(act_space.low, np.float64), np.asarray(act_space.high, np.float64)
-    acts = torch.from_numpy(rng.uniform(lo, hi, size=(W + K * R, n, A)).astype(np.float32)).to(dev)
+    acts = torch.from_numpy(action_stream(args.actions, rng, lo, hi, W + K * R, n).astype(np.float32)).to(dev)
     obs = torch.zeros(n, O, dtype=torch.float64, device=dev)
     fin = torch.zeros_like(obs)
     rew = torch.zeros(n, dtype=torch.float64, device=dev)
@@ -327,12 +351,15 @@ def main(argv=None):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: uniform random actions (PCG64 seed 20241220+rank), per-env MT19937 reset draws",
+        "data": f"synthetic: {args.actions} random actions (PCG64 seed 20241220+rank), per-env MT19937 reset draws",
         "config": {"workload": f"{TASK_NAMES[args.task]} x {n} envs per GPU, autoreset, max_episode_steps "
                                f"{MAX_STEPS[args.task]}", "envs_per_gpu": n, "total_envs": n * world,
                    "parallelism": f"env-dp{world}", "world_size": world, "geometry": args.geometry,
                    "contact": args.contact,
-                   "backend": args.backend if use_pg else None, "returns_gathered": use_pg, "robot": args.robot},
+                   "backend": args.backend if use_pg else None, "returns_gathered": use_pg, "robot": args.robot,
+                   "library": os.path.relpath(sim.L._name, ROOT), "actions": args.actions,
+                   "launch_order": "fallback (URGYM_NO_PRIO_MODEL)" if os.environ.get("URGYM_NO_PRIO_MODEL", "0") not in
+                                   ("", "0") else "k_prio models"},
         "rep_values": [env_steps / x[0] for x in reps],
         "substeps_per_env_step": substeps / env_steps,
         "resets": int(resets),

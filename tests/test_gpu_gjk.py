@@ -23,7 +23,10 @@ def pack(A, TA, B, TB, thr):
     return q
 
 
-def test_gpu_gjk_matches_oracle(built):
+@pytest.mark.parametrize("task", [None, 3], ids=["gjk16", "gjk8"])
+def test_gpu_gjk_matches_oracle(built, task):
+    """task None: the default library (16-lane groups); task 3 (Golf): liburgym_g8.so, the 8-lane build the Golf tasks
+    load (two cell candidates per lane, half-row reductions, the GJK / EPA stores in the hull-candidate LDS union)"""
     from urgym_amd._native import lib, ptr
     oracle = T._lib("libugoracle.so", "ugo_gjk_pair")
     import re
@@ -38,7 +41,7 @@ def test_gpu_gjk_matches_oracle(built):
     q = np.array([pack(A, TA, B, TB, thr) for (A, TA, B, TB), thr in zip(cases, thrs)], np.float64)
     out = np.zeros((len(cases), 7))
     ok = np.zeros(len(cases), np.int32)
-    assert lib().urgym_debug_gjk(len(cases), ptr(q), ptr(out), ptr(ok)) == 0
+    assert lib(task=task).urgym_debug_gjk(len(cases), ptr(q), ptr(out), ptr(ok)) == 0
     n_pt = n_pen = 0
     for k, ((A, TA, B, TB), thr) in enumerate(zip(cases, thrs)):
         r, o = T.query(oracle, A, TA, B, TB, thr)

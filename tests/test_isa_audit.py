@@ -33,7 +33,8 @@ def test_audit_flags_the_reproducer(tmp_path):
     assert len(hits) >= 1 and all("s_cselect" in h[4] for h in hits), hits
 
 
-@pytest.mark.parametrize("defs", [(), ("-DUG_ROBOT_R140",)], ids=["ur5_robotiq_85", "ur5_robotiq_140"])
+@pytest.mark.parametrize("defs", [(), ("-DUG_ROBOT_R140",), ("-DUG_GJK_G=8",)],
+                         ids=["ur5_robotiq_85", "ur5_robotiq_140", "gjk_g8"])
 def test_shipped_library_has_no_scc_clobbered_pick(tmp_path, defs):
     """both miscompiles: no SCC reader fed by a frame-address add, and no device function that overwrites its unsaved
     return address (a long branch through s[30:31] in a leaf function; team_pgs carries a never-taken call so it is

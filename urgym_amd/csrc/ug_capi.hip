@@ -590,6 +590,14 @@ __global__ void k_prio(const double* pfeat, const float* act, uint8_t* prio, int
     }
 }
 
+/* An explicit reset or set_state replaces the state the predictor record was taken from: clear the record's model flag
+ * (k_prio then keeps the level k_iota or the last step left) for every env the call touched (mask NULL = all). */
+__global__ void k_pfeat_clear(double* pfeat, const uint8_t* mask, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || (mask && !mask[i])) return;
+    pfeat[(size_t)i * UG_PF_STRIDE + UG_PF_STRIDE - 1] = 0.0;
+}
+
 /* next launch order: envs by descending priority (0..255), ties by ascending env index (deterministic), one block.
  * Up to ORDER_LDS envs: a bitonic sort of (255 - priority) << 24 | env in LDS (78 stages for 4096 envs); more: a
  * two-pass stable counting sort by priority nibble (low, then high) through tmp. */
@@ -936,8 +944,12 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     HIPCHK(h, hipMalloc(&h->d_order, sizeof(int) * N));
     HIPCHK(h, hipMalloc(&h->d_order_tmp, sizeof(int) * N));
     HIPCHK(h, hipMalloc(&h->d_prio, N));
-    if (task == URGYM_TASK_BALLBALANCE || task == URGYM_TASK_TWOBALLSBALANCE || task == URGYM_TASK_CUBESPUSH ||
-        task == URGYM_TASK_CUBESPUSHDIFF) {
+    /* URGYM_NO_PRIO_MODEL (a measurement aid, like URGYM_SLOTS): no predictor record, so every env is launched by the
+     * fallback level (its last substep count, predicted truncation first) -- the A/B baseline of the k_prio models */
+    const char* noprio = getenv("URGYM_NO_PRIO_MODEL");
+    if ((!noprio || !*noprio || *noprio == '0') &&
+        (task == URGYM_TASK_BALLBALANCE || task == URGYM_TASK_TWOBALLSBALANCE || task == URGYM_TASK_CUBESPUSH ||
+         task == URGYM_TASK_CUBESPUSHDIFF)) {
         HIPCHK(h, hipMalloc(&h->d_pfeat, sizeof(double) * UG_PF_STRIDE * N));
         HIPCHK(h, hipMemsetAsync(h->d_pfeat, 0, sizeof(double) * UG_PF_STRIDE * N, h->stream));
     }
@@ -1046,6 +1058,10 @@ int urgym_reset_device(urgym_handle* h, const uint8_t* d_mask, const double* d_d
                                                                h->d_queue);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+    if (h->d_pfeat) {
+        k_pfeat_clear<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_pfeat, d_mask, h->n);
+        HIPCHK(h, hipGetLastError());
+    }
     h->timed = true;
     return 0;
 }
@@ -1130,6 +1146,10 @@ int urgym_set_state(urgym_handle* h, const double* state) {
     size_t tot = (size_t)h->n * UG_STATE_DIM;
     HIPCHK(h, hipSetDevice(h->dev));
     HIPCHK(h, hipMemcpyAsync(h->d_state, state, sizeof(double) * tot, hipMemcpyHostToDevice, h->stream));
+    if (h->d_pfeat) {
+        k_pfeat_clear<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_pfeat, nullptr, h->n);
+        HIPCHK(h, hipGetLastError());
+    }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
 }
