@@ -13,6 +13,15 @@
  * owns its device memory and stream; it is not thread-safe, distinct handles
  * are.  One handle per GPU (device_ordinal); env batches shard across GPUs
  * by creating one handle per rank.
+ *
+ * Three builds of the same sources export this ABI (__graft_entry__.build):
+ *   liburgym.so      UR5Robotiq85, 16-lane GJK groups -- every task;
+ *   liburgym_g8.so   UR5Robotiq85, 8-lane GJK groups (-DUG_GJK_G=8) -- the same results bit for bit, faster for
+ *                    Golf-v0 / GolfJoints-v0 (6.3 convex queries per substep: one round of eight pairs instead of
+ *                    two of four); the Python binding loads it for those two tasks (urgym_amd/_native.py G8_TASKS),
+ *                    a C caller picks it the same way or keeps liburgym.so (Golf ~3 % slower);
+ *   liburgym_r140.so the UR5Robotiq140 arm (robot.py:221-240).
+ * bench.py's JSON line names the library it ran (config.library).
  */
 #ifndef URGYM_H
 #define URGYM_H
@@ -198,6 +207,11 @@ int urgym_debug_ws_doubles(void);
  * start, vertex count, implicit dimensions[3], margin, R[9] (row-major), p[3]; then the contact breaking threshold.
  * out: n x 7 (normal on B, point on B, distance), ok: n (1 = a point).  Returns 0 on success. */
 int urgym_debug_gjk(int n, const double* q, double* out, int* ok);
+/* Test aid, no reference counterpart: for a CubesGrasp handle, the branch each env's next urgym_step would take for the
+ * given actions (n x 9 floats, host) -- random.choices([0, 1], weights=[a0, a1]) on the env's next random()
+ * (env_cubes_grasp_v0.py:127-130), peeked from its MT19937 stream as k_prio does for the launch order, nothing
+ * consumed.  sel: n ints, 0 = the joint move, 1 = the gripper command.  Returns 0 on success. */
+int urgym_debug_cg_branch(urgym_handle* h, const float* act, int* sel);
 
 #ifdef __cplusplus
 }

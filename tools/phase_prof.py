@@ -45,7 +45,7 @@ def main():
     from urgym_amd.envs import spaces_for
     _, asp = spaces_for(a.task)
     sim.set_autoreset(True, 500)
-    buf = np.zeros(116, np.uint64)
+    buf = np.zeros(134, np.uint64)
     sim.reset()
     sim.sync()
     rc = sim.L.urgym_debug_prof(sim.h, buf.ctypes.data_as(ctypes.c_void_p), 1)
@@ -104,6 +104,21 @@ def main():
                                  "cycles_to_reduced": sc["mem"] / max(sc["cells"], 1)}
     out["calls_per_env_step"] = {k: float(buf[104 + i]) / es for i, k in enumerate(CALLS)}
     out["quiescent_substeps_fraction"] = float(buf[115]) / max(d["substeps"], 1)
+    # the calling convention's cost (ug_team.h PF_CS0): call + prologue (callee-saved saves) and epilogue (restores,
+    # their wait, the return) of team_gjk / team_collide<full, gjk> / team_pgs, cycles per call and per substep
+    cs = {}
+    for i, (name, call) in enumerate((("team_gjk", 0), ("team_collide", 1), ("team_pgs", 8), ("serial_fk", 7),
+                                      ("serial_pre", 5), ("serial_post", 6), ("team_unit_solves", 3),
+                                      ("team_robot_dynamics", 4), ("team_enumerate", 2))):
+        ncall = max(float(buf[104 + call]), 1.0)
+        pro, epi = float(buf[116 + 2 * i]), float(buf[117 + 2 * i])
+        cs[name] = {"calls_per_substep": ncall / max(d["substeps"], 1), "prologue_cycles_per_call": pro / ncall,
+                    "epilogue_cycles_per_call": epi / ncall,
+                    "prologue_plus_epilogue_cycles_per_substep": (pro + epi) / max(d["substeps"], 1)}
+    # serial_pre's own figures include its two nested calls' (team_robot_dynamics, team_enumerate) only through its body
+    tot = sum(v["prologue_plus_epilogue_cycles_per_substep"] for v in cs.values())
+    cs["share_of_substep_cycles"] = tot / max(d["total"] / max(d["substeps"], 1), 1)
+    out["call_save_restore"] = cs
     print(json.dumps(out, indent=1))
     sim.close()
 

@@ -19,7 +19,7 @@ SYMBOLS = [
     "urgym_link_state", "urgym_ik", "urgym_last_kernel_ms", "urgym_debug_prof", "urgym_debug_workspace",
     "urgym_debug_ws_doubles", "urgym_set_reward_type", "urgym_get_flags", "urgym_flags_device", "urgym_get_stats",
     "urgym_get_rng", "urgym_set_rng", "urgym_contact_points", "urgym_set_button_mode",
-    "urgym_camera_shot", "urgym_camera_shot_device", "urgym_debug_gjk",
+    "urgym_camera_shot", "urgym_camera_shot_device", "urgym_debug_gjk", "urgym_debug_cg_branch",
 ]
 
 # UG_FLAG_* / UG_STAT_* (urgym_amd/csrc/ug_layout.h)
@@ -91,6 +91,7 @@ def lib(robot="ur5_robotiq_85", task=None):
     L.urgym_debug_workspace.argtypes = [P, I, P, I]
     L.urgym_debug_ws_doubles.argtypes = []
     L.urgym_debug_gjk.argtypes = [I, P, P, P]
+    L.urgym_debug_cg_branch.argtypes = [P, P, P]
     L.urgym_set_reward_type.argtypes = [P, I]
     L.urgym_set_button_mode.argtypes = [P, I]
     L.urgym_get_flags.argtypes = [P, P]

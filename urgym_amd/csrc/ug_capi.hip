@@ -564,11 +564,33 @@ __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, ui
 static_assert(UG_ACT_DIM(UG_TASK_TWOBALLS) == UG_PT_IN - UG_PT_STATE_IN, "TwoBalls' action: the model's last inputs");
 static_assert(UG_ACT_DIM(UG_TASK_CUBESPUSH) == 3 && UG_ACT_DIM(UG_TASK_CUBESPUSHDIFF) == 3, "CubesPush's action: 3");
 static_assert(UG_ACT_DIM(UG_TASK_BALLBALANCE) == 3, "BallBalance's action: 3");
-__global__ void k_prio(const double* pfeat, const float* act, uint8_t* prio, int n) {
+/* CubesGrasp (model 4 / 5): the branch the step's random.choices will take, from the env's stream without consuming it */
+__device__ static int cg_branch(const uint32_t* mt, const float* a, int i) {
+    return ugg_cg_choose(a[0], a[1], mt_peek_random(mt + (size_t)i * UG_MT_WORDS));
+}
+__global__ void k_prio(const double* pfeat, const float* act, const uint32_t* mt, uint8_t* prio, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const double* f = pfeat + (size_t)i * UG_PF_STRIDE;
     const double model = f[UG_PF_STRIDE - 1];
+    if constexpr (NB == 12) {
+        if (model == 4.0 || model == 5.0) { /* CubesGrasp: q, qd, targets - q, the branch, the truncation */
+            const float* a = act + (size_t)i * UG_ACT_DIM(UG_TASK_CUBESGRASP);
+            const int sel = cg_branch(mt, a, i);
+            double x[UG_PG_IN];
+            for (int k = 0; k < 2 * NB; k++) x[k] = f[k];
+            for (int j = 0; j < 7; j++) {
+                const double t = sel == 0 ? (j < 6 ? (double)a[2 + j] : f[2 * NB + 6])
+                                          : (j < 6 ? f[2 * NB + j] : gripper_angle(a[8] < 0.5f ? UG_GRIP_MAX : UG_GRIP_MIN));
+                x[2 * NB + j] = t - f[j];
+            }
+            x[2 * NB + 7] = (double)sel;
+            x[2 * NB + 8] = model == 5.0 ? 1.0 : 0.0;
+            prio[i] = (uint8_t)logit_level(mlp_logit<UG_PG_IN, UG_PG_HID>(x, UG_PG_MU, UG_PG_SD, UG_PG_W1, UG_PG_B1, UG_PG_W2,
+                                                                           UG_PG_B2), UG_PG_L0, UG_PG_DL);
+            return;
+        }
+    }
     if (model == 1.0) { /* TwoBalls: 31 state inputs + the action */
         double x[UG_PT_IN];
         for (int k = 0; k < UG_PT_STATE_IN; k++) x[k] = f[k];
@@ -949,7 +971,7 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     const char* noprio = getenv("URGYM_NO_PRIO_MODEL");
     if ((!noprio || !*noprio || *noprio == '0') &&
         (task == URGYM_TASK_BALLBALANCE || task == URGYM_TASK_TWOBALLSBALANCE || task == URGYM_TASK_CUBESPUSH ||
-         task == URGYM_TASK_CUBESPUSHDIFF)) {
+         task == URGYM_TASK_CUBESPUSHDIFF || task == URGYM_TASK_CUBESGRASP)) {
         HIPCHK(h, hipMalloc(&h->d_pfeat, sizeof(double) * UG_PF_STRIDE * N));
         HIPCHK(h, hipMemsetAsync(h->d_pfeat, 0, sizeof(double) * UG_PF_STRIDE * N, h->stream));
     }
@@ -1091,7 +1113,7 @@ int urgym_step_device(urgym_handle* h, const float* d_act, double* d_obs, double
     HIPCHK(h, hipSetDevice(h->dev));
     /* the launch order: the priorities the envs' last step left (TwoBalls: completed with this step's actions) */
     if (h->d_pfeat) {
-        k_prio<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_pfeat, d_act, h->d_prio, h->n);
+        k_prio<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_pfeat, d_act, h->d_mt, h->d_prio, h->n);
         HIPCHK(h, hipGetLastError());
     }
     k_order<<<1, ORDER_THREADS, 0, h->stream>>>(h->d_prio, h->d_order, h->d_order_tmp, h->n);
@@ -1363,6 +1385,24 @@ int urgym_debug_workspace(urgym_handle* h, int env, double* out, int count) {
     return 0;
 }
 int urgym_debug_ws_doubles(void) { return (int)WS_STRIDE(0, 0); } /* the LOD vertex-in-hull stride */
+
+__global__ void k_cg_branch(const float* act, const uint32_t* mt, int* sel, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) sel[i] = cg_branch(mt, act + (size_t)i * UG_ACT_DIM(UG_TASK_CUBESGRASP), i);
+}
+int urgym_debug_cg_branch(urgym_handle* h, const float* act, int* sel) {
+    if (!h || !act || !sel) return -1;
+    if (h->task != URGYM_TASK_CUBESGRASP) return fail(h, "urgym_debug_cg_branch: not a CubesGrasp handle");
+    const size_t N = (size_t)h->n;
+    HIPCHK(h, hipSetDevice(h->dev));
+    HIPCHK(h, hipMemcpyAsync(h->d_act, act, sizeof(float) * UG_ACT_DIM(UG_TASK_CUBESGRASP) * N, hipMemcpyHostToDevice,
+                             h->stream));
+    k_cg_branch<<<grid_of(h->n), WAVE, 0, h->stream>>>(h->d_act, h->d_mt, h->d_sub, h->n);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipMemcpyAsync(sel, h->d_sub, sizeof(int) * N, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return 0;
+}
 
 // Test aid: n convex-convex queries (39 doubles each, k_gjk_query) on device 0; out n x 7, ok n.
 int urgym_debug_gjk(int n, const double* q, double* out, int* ok) {

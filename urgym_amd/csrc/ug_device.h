@@ -218,6 +218,27 @@ DF double mt_random(const Rng& r) {
     uint32_t a = mt_next(r) >> 5, b = mt_next(r) >> 6;
     return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
 }
+/* the random() the next mt_random(Rng{m, 1, 0}) would return, without advancing the stream (m: one env's 624 words +
+ * index).  Past the end of a generation its first words are the next generation's, formed as mt_next's twist forms
+ * words 0 and 1 (both read only words of the current generation: 0, 1, 2, 397, 398). */
+DF uint32_t mt_temper(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+DF uint32_t mt_twist_word(const uint32_t* m, int k) {
+    const uint32_t y = (m[k] & 0x80000000u) | (m[k + 1] & 0x7fffffffu);
+    return m[k + 397] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+DF double mt_peek_random(const uint32_t* m) {
+    const uint32_t idx = m[624];
+    const uint32_t w0 = idx < 624 ? m[idx] : mt_twist_word(m, 0);
+    const uint32_t w1 = idx + 1 < 624 ? m[idx + 1] : mt_twist_word(m, idx < 624 ? 0 : 1);
+    const uint32_t a = mt_temper(w0) >> 5, b = mt_temper(w1) >> 6;
+    return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+}
 
 /* ---------------- scene (built on the host, read-only, wave-uniform) ---------------- */
 struct Collider {

@@ -30,6 +30,9 @@
 #include "scene_data.h"
 #include "ug_detmath.h"
 
+#ifndef UGK_FN_PAIR /* the includer's linkage for gjk_pair (the kernels: forced inline into its one caller, team_gjk) */
+#define UGK_FN_PAIR UGK_FN
+#endif
 #ifndef UGK_GMEM /* the address space of the EPA store (the kernels: global, so its accesses are global_*, not flat_*) */
 #define UGK_GMEM
 #endif
@@ -1355,7 +1358,7 @@ UGK_FN gv support_ab(const GShape& A, const gx& TA, const GShape& B, const gx& T
 }
 
 /* btGjkPairDetector::getClosestPointsNonVirtual: one point (normal on B, point on B, distance) or none */
-UGK_FN bool gjk_pair(UGK_GMEM EpaMem* E, const GShape& A0, const gx& TA0, const GShape& B0, const gx& TB0, double thr,
+UGK_FN_PAIR bool gjk_pair(UGK_GMEM EpaMem* E, const GShape& A0, const gx& TA0, const GShape& B0, const gx& TB0, double thr,
                      gv& nOut, gv& pOut, double& dOut, gv* sepAxis = nullptr) {
     UGK_COUNT(PC_GJK, 1);
     UGK_T0(t_all);

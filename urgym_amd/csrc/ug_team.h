@@ -30,6 +30,7 @@
 #include "prio_model.h"
 #include "prio_model_tb.h"
 #include "prio_model_cp.h"
+#include "prio_model_cg.h"
 #include "ug_glue.h"
 
 namespace ugd {
@@ -37,7 +38,7 @@ namespace ugd {
 #define TEAM 64
 typedef __attribute__((address_space(1))) const double gcdouble;
 typedef __attribute__((address_space(1))) double gdouble;
-#define UG_NPROF 116 /* phase accumulators of the -DUG_PROF build */
+#define UG_NPROF 134 /* phase accumulators of the -DUG_PROF build */
 #define NVP 32
 #define PREG 96             /* Delassus columns held in VGPRs; columns beyond stream from the global workspace */
 /* a row's J and M^-1 J^T over the NVP = 32 dof slots (robot 12, objects 3 x 6, 2 zero pads) */
@@ -180,6 +181,7 @@ struct Shared {
     int qsvalid;          /* the workspace holds a quiescent-collision reference (WS_QS) for the current program point */
 #ifdef UG_PROF
     unsigned long long prof[UG_NPROF];
+    unsigned long long tcall, tret; /* PROF_PRE_CALL / PROF_EXIT stamps (lane 0) */
 #endif
 };
 
@@ -228,10 +230,35 @@ enum { PF_COLLIDE = 0, PF_DYN, PF_ROWS, PF_PGS, PF_SPLIT, PF_INTEG, PF_GLUE, PF_
         * profiling build only), and the supports that took a cell (not the whole scan) */
        PF_SUP_CELL, PF_SUP_MEM, PC_SUP_CELLS,
        /* calls of the __noinline__ phases (tools/scratch_attr.py: their callee-saved saves and spills x calls) */
-       PC_CALL0 = 104, PC_QUIET = 115 /* substeps whose collision stage quiescent_ok proved empty */ };
+       PC_CALL0 = 104, PC_QUIET = 115, /* substeps whose collision stage quiescent_ok proved empty */
+       /* the calling-convention cost of the big __noinline__ phases: per phase, cycles from the
+        * caller's last instruction before the call to the callee's first statement (call + prologue: the callee-saved
+        * VGPR saves), and from the callee's last statement to the caller's first instruction after it (epilogue: the
+        * restores, the wait for them, the return) */
+       PF_CS0 = 116 /* [PF_CS0 + 2 k] prologue, [PF_CS0 + 2 k + 1] epilogue of CS_* */ };
+enum { CS_GJK = 0, CS_COLLIDE, CS_PGS, CS_FK, CS_PRE, CS_POST, CS_UNIT, CS_RDYN, CS_ENUM, CS_N };
 enum { CALL_GJK = 0, CALL_COLLIDE, CALL_ENUM, CALL_UNIT, CALL_RDYN, CALL_PRE, CALL_POST, CALL_FK, CALL_PGS, CALL_GLUE,
        CALL_REDUCE4, CALL_N };
 #define PROF_CALL(k) PROF_CNT(PC_CALL0 + (k), 1)
+#ifdef UG_PROF
+#define PROF_PRE_CALL() do { if (threadIdx.x == 0) g_sh.tcall = __builtin_readcyclecounter(); } while (0)
+#define PROF_ENTRY(k)                                                                              \
+    do {                                                                                           \
+        const unsigned long long t_ = __builtin_readcyclecounter();                                \
+        if (threadIdx.x == 0) g_sh.prof[PF_CS0 + 2 * (k)] += t_ - g_sh.tcall;                      \
+    } while (0)
+#define PROF_EXIT() do { if (threadIdx.x == 0) g_sh.tret = __builtin_readcyclecounter(); } while (0)
+#define PROF_POST_CALL(k)                                                                          \
+    do {                                                                                           \
+        const unsigned long long t_ = __builtin_readcyclecounter();                                \
+        if (threadIdx.x == 0) g_sh.prof[PF_CS0 + 2 * (k) + 1] += t_ - g_sh.tret;                   \
+    } while (0)
+#else
+#define PROF_PRE_CALL()
+#define PROF_ENTRY(k)
+#define PROF_EXIT()
+#define PROF_POST_CALL(k)
+#endif
 #define UG_FREE_SPLIT_N 14
 #ifdef UG_PROF
 __device__ static const int kFreeSplit[UG_FREE_SPLIT_N] = {PF_FK, PF_BROAD, PF_HULL, PF_PR_LOOK, PF_PR_NP, PF_PR_MAN, PF_PR_ST,
@@ -241,6 +268,12 @@ __device__ static const int kFreeSplit[UG_FREE_SPLIT_N] = {PF_FK, PF_BROAD, PF_H
 } /* namespace ugd */
 /* the convex-convex narrowphase (Bullet's GJK / EPA pair detector), run by the whole wave per pair */
 #define UGK_FN __device__ static inline
+/* gjk_pair is forced inline into team_gjk, which becomes a leaf (measured round 6): as a call inside
+ * team_gjk it left team_gjk's callee-saved SGPRs no free VGPR lane, so its prologue and epilogue saved and restored 34
+ * SGPRs each through scratch one at a time with a full memory wait per register -- 17 k + 52 k cycles per call, 7.5 %
+ * of a BallBalance substep (profiles/round6_phase_ballbalance_callsave_before.txt; after: 3.6 k + 7.0 k,
+ * round6_phase_ballbalance_callsave_after.txt) */
+#define UGK_FN_PAIR __device__ static __forceinline__
 #define UGK_GMEM __attribute__((address_space(1)))
 #define UGK_LMEM __attribute__((address_space(3)))
 #define UGK_OPAQUE(x) __asm__ volatile("" : "+v"(x))

@@ -1220,7 +1220,13 @@ __device__ __forceinline__ static void gjk_one(const Scene* s, int k, UGK_GMEM u
 /* the GJK pairs of a pair chunk (bits of hq), in rounds of GJK_NG: lane group g runs the round's g-th pair on its own
  * EPA store.  One call per chunk: the callee-saved registers this solver needs are saved once per substep with GJK
  * pairs, not once per pair (they were 441 dwords per lane per call, most of the k_step's HBM traffic). */
-__device__ __noinline__ static void team_gjk(const Scene* s, unsigned long long hq, int c0, double* ws) {
+#ifdef UG_GJK_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+static void team_gjk(const Scene* s, unsigned long long hq, int c0, double* ws) {
+    PROF_ENTRY(CS_GJK);
     PROF_CALL(CALL_GJK);
     Shared& sh = g_sh;
     const int nq = __popcll(hq), g = threadIdx.x / GJK_G;
@@ -1234,10 +1240,12 @@ __device__ __noinline__ static void team_gjk(const Scene* s, unsigned long long 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
     }
+    PROF_EXIT();
 }
 
 template <bool FULL, bool GJK>
 __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
+    PROF_ENTRY(CS_COLLIDE);
     PROF_CALL(CALL_COLLIDE);
     Shared& sh = g_sh;
     const int lane = threadIdx.x;
@@ -1395,7 +1403,11 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         if (lane == 0) sh.is[3] = c0; /* the pass's first pair (team_poly_cyl's certificate slot) */
         if (GJK) {
             const unsigned long long hq = ballot(hk);
-            if (hq) team_gjk(s, hq, c0, ws);
+            if (hq) {
+                PROF_PRE_CALL();
+                team_gjk(s, hq, c0, ws);
+                PROF_POST_CALL(CS_GJK);
+            }
             PROF_CNT(PC_HULL, __popcll(hq));
         }
         for (unsigned long long hm = GJK ? 0ull : ballot(hk); hm != 0ull; hm &= hm - 1ull) {
@@ -1569,5 +1581,6 @@ __device__ __noinline__ static void team_collide(const Scene* s, double* ws) {
         if (lane == 0) sh.qsvalid = still ? 1 : 0;
     }
     __syncthreads();
+    PROF_EXIT();
 }
 

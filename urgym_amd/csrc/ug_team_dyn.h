@@ -14,6 +14,7 @@ __device__ __forceinline__ int body_depth(int b) {
     return d;
 }
 __device__ __noinline__ static void team_robot_dynamics(double g_) {
+    PROF_ENTRY(CS_RDYN);
     PROF_CALL(CALL_RDYN);
     /* the LDS image is addressed directly (pointer arguments would turn every access into a flat one) */
     const double* qd = g_sh.e.qd;
@@ -164,17 +165,21 @@ __device__ __noinline__ static void team_robot_dynamics(double g_) {
     }
     __syncthreads();
     (void)Vbb;
+    PROF_EXIT();
 }
 /* lane 0: external forces (robot gravity/gyroscopic/damping via CRBA + RNEA, free objects), the LDL^T of
  * the mass matrix, and the row enumeration */
 __device__ __noinline__ static void serial_pre(const Scene* s) {
+    PROF_ENTRY(CS_PRE);
     PROF_CALL(CALL_PRE);
     Shared& sh = g_sh;
     EnvState& e = sh.e;
     const double dt = UG_DT;
     const int lane = threadIdx.x;
     PROF_T0(t_rd);
+    PROF_PRE_CALL();
     team_robot_dynamics(s->gravity);
+    PROF_POST_CALL(CS_RDYN);
     PROF_ADD(PF_RDYN, t_rd);
     PROF_T0(t_ldl);
     {
@@ -251,11 +256,15 @@ __device__ __noinline__ static void serial_pre(const Scene* s) {
     __syncthreads();
     PROF_ADD(PF_LDL, t_ldl);
     PROF_T0(t_en);
+    PROF_PRE_CALL();
     team_enumerate(s);
+    PROF_POST_CALL(CS_ENUM);
     PROF_ADD(PF_ENUM, t_en);
+    PROF_EXIT();
 }
 /* lane 0: velocities += solver delta, positions integrate (v + split velocity) */
 __device__ __noinline__ static void serial_post(const Scene* s, int split) {
+    PROF_ENTRY(CS_POST);
     PROF_CALL(CALL_POST);
     Shared& sh = g_sh;
     EnvState& e = sh.e;
@@ -308,10 +317,12 @@ __device__ __noinline__ static void serial_post(const Scene* s, int split) {
             ob.quat = qnormalize(qmul(dq, ob.quat));
         }
     }
+    PROF_EXIT();
 }
 /* fk() wave-parallel: lane b < NB forms its joint rotation, then composes its own root-to-body chain
  * (same operations and order as fk() along that path) */
 __device__ __noinline__ static void serial_fk() {
+    PROF_ENTRY(CS_FK);
     PROF_CALL(CALL_FK);
     Kin& k = g_sh.kin;
     const int lane = threadIdx.x;
@@ -349,5 +360,6 @@ __device__ __noinline__ static void serial_fk() {
         k.c[b] = vadd(pp, mv(Rp, com));
     }
     __syncthreads();
+    PROF_EXIT();
 }
 

@@ -171,6 +171,7 @@ __device__ static void enumerate_rows(Shared& sh, const Scene* s) {
  * counts.  Identical output when every contact point fits (the usual case); when the capacity check
  * of the serial code would reject points, the serial enumeration runs instead. */
 __device__ __noinline__ static void team_enumerate(const Scene* s) {
+    PROF_ENTRY(CS_ENUM);
     PROF_CALL(CALL_ENUM);
     Shared& sh = g_sh;
     EnvState& e = sh.e;
@@ -252,7 +253,7 @@ __device__ __noinline__ static void team_enumerate(const Scene* s) {
     const int total = nnc + 3 * tp + 2 * tr;
     if (total > MAXROWS) { /* the serial code's capacity checks decide which points are kept */
         if (lane == 0) enumerate_rows(sh, s);
-        return;
+        { PROF_EXIT(); return; }
     }
     const int nn = tp, nf = 2 * tp;
     if (lane < nman) {
@@ -280,6 +281,7 @@ __device__ __noinline__ static void team_enumerate(const Scene* s) {
         sh.nn = nn;
         sh.nf = nf;
     }
+    PROF_EXIT();
 }
 /* ---- register-resident row build: every array index below is a compile-time constant (fully unrolled
  * loops, selects instead of dynamic stores), so the per-lane arrays stay in VGPRs instead of scratch.
@@ -372,6 +374,7 @@ __device__ __forceinline__ void ent_jac_r(const Scene* sc, const EnvState& e, co
 /* the LDL solves every limit / motor / gear row would repeat, once per substep: lane d < NB solves for the
  * unit vector e_d, lane NB + g for gear g's ratio * e_child (the same computation as the row's own) */
 __device__ __noinline__ static void team_unit_solves() {
+    PROF_ENTRY(CS_UNIT);
     PROF_CALL(CALL_UNIT);
     const int lane = threadIdx.x;
     if (lane < NB + 5) {
@@ -386,6 +389,7 @@ __device__ __noinline__ static void team_unit_solves() {
         for (int i = 0; i < NB; i++) g_sh.u.mcol[lane][i] = x[i];
     }
     __syncthreads();
+    PROF_EXIT();
 }
 /* robot part of a point Jacobian along d (ANG: angular rows) -- ent_jac_r's robot branch without the
  * solve, with the row kind's ANG as a runtime select so that every contact lane runs the same code */

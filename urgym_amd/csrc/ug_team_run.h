@@ -9,14 +9,19 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     unsigned long long fsnap = lane < UG_FREE_SPLIT_N ? sh.prof[kFreeSplit[lane]] : 0ull; /* lane i: counter i */
 #endif
     PROF_T0(t_col);
+    PROF_PRE_CALL();
     serial_fk();
+    PROF_POST_CALL(CS_FK);
     __syncthreads();
     PROF_ADD(PF_FK, t_col);
     const double ov0 = e.overflow;
     if (s->gjk) {
         if (s->full) {
-            if (!(uniform(sh.qsvalid) && quiescent_ok(s, ws))) team_collide<true, true>(s, ws);
-            else PROF_CNT(PC_QUIET, 1);
+            if (!(uniform(sh.qsvalid) && quiescent_ok(s, ws))) {
+                PROF_PRE_CALL();
+                team_collide<true, true>(s, ws);
+                PROF_POST_CALL(CS_COLLIDE);
+            } else PROF_CNT(PC_QUIET, 1);
         } else team_collide<false, true>(s, ws);
     } else {
         if (s->full) team_collide<true, false>(s, ws);
@@ -29,7 +34,9 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     }
     PROF_ADD(PF_COLLIDE, t_col);
     PROF_T0(t_dyn);
+    PROF_PRE_CALL();
     serial_pre(s);
+    PROF_POST_CALL(CS_PRE);
     __syncthreads();
     if (lane == 0 && e.overflow != ov1) { sh.stats[UG_STAT_ROWCAP]++; sh.flags |= UG_FLAG_DROPPED; }
     PROF_ADD(PF_DYN, t_dyn);
@@ -46,7 +53,9 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     PROF_CNT(PC_NMAN, (int)e.nman);
     /* rows: built lane-per-row into the workspace (J | M^-1 J^T) and LDS (scalars) */
     PROF_T0(t_unit);
+    PROF_PRE_CALL();
     team_unit_solves();
+    PROF_POST_CALL(CS_UNIT);
     PROF_ADD(PF_UNIT, t_unit);
     PROF_T0(t_rowb);
     /* the motor / gear solve (team_pgs's direct path) reads its Delassus rows and M^-1 J^T from the unit
@@ -63,7 +72,9 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
     PROF_ADD(PF_ROWS, t_rows);
     PROF_T0(t_pgs);
     double dv, dvs;
+    PROF_PRE_CALL();
     int split = team_pgs(ws, n, nnc, nn, s->nobj, dv, dvs);
+    PROF_POST_CALL(CS_PGS);
     if (lane == 0 && split) sh.stats[UG_STAT_SPLIT]++;
     PROF_ADD(PF_PGS, t_pgs);
     PROF_T0(t_int);
@@ -77,7 +88,9 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
         else if (r.kind == 5) pt.imp2 = r.imp;
     }
     __syncthreads();
+    PROF_PRE_CALL();
     serial_post(s, split);
+    PROF_POST_CALL(CS_POST);
     __syncthreads();
     PROF_ADD(PF_INTEG, t_int);
 #ifdef UG_PROF
@@ -743,10 +756,27 @@ __device__ static int logit_level(double lg, double l0, double dl) {
  * (prio_model_cp.h, tools/fit_priority.py --task 1): the launch is its longest env (45 ms against 16.8 ms balanced and
  * 39.6 ms longest-first) and the last substep count does not predict it (correlation 0.02; the model 0.82) */
 static_assert(UG_PC_IN == 2 * 12 + 3, "q[12], qd[12], the action");
+/* CubesGrasp: the logit of "this step runs >= 450 substeps" from q, qd, the step's motor targets minus q, the branch its
+ * random.choices takes and a predicted truncation, 33 -> 32 (ReLU) -> 1 (prio_model_cg.h, tools/fit_priority.py --task
+ * 2; held-out list schedule 1.22x -> 1.18x of the balanced work, longest-first 1.02x): the branch is
+ * drawn in the step itself (env_cubes_grasp_v0.py:127-130) but it is a function of the env's MT19937 stream and the
+ * action, both known before the launch -- k_prio peeks the stream's next random() (mt_peek_random, nothing consumed)
+ * and evaluates ugg_cg_choose as the glue will.  The env leaves q, qd and its 7 motor targets here; the flag is 4 (5: the
+ * step truncates, so its autoreset follows) */
+static_assert(UG_PG_IN == 2 * 12 + 7 + 2, "q[12], qd[12], targets - q [7], the branch, the truncation");
 __device__ static int team_priority(const Scene* s, int nsub, int el_next, int max_steps, int autoreset, double* pf) {
     const EnvState& e = g_sh.e;
     if (pf) pf[UG_PF_STRIDE - 1] = 0.0; /* k_prio keeps this level unless the TwoBalls model applies */
-    if (autoreset && max_steps > 0 && el_next >= max_steps) return 255;
+    const bool trunc_next = autoreset && max_steps > 0 && el_next >= max_steps;
+    if constexpr (NB == 12) {
+        if (s->task == UG_TASK_CUBESGRASP && pf) {
+            for (int j = 0; j < NB; j++) { pf[j] = e.q[j]; pf[NB + j] = e.qd[j]; }
+            for (int m = 0; m < 7; m++) pf[2 * NB + m] = e.mtarget[m];
+            pf[UG_PF_STRIDE - 1] = trunc_next ? 5.0 : 4.0;
+            return trunc_next ? 255 : 0;
+        }
+    }
+    if (trunc_next) return 255;
     if (s->variant == UG_TASK_TWOBALLS && pf && e.oactive[0] != 0.0 && e.oactive[1] != 0.0 && e.oactive[2] != 0.0) {
         tb_state_inputs(e, qmat(e.obj[0].quat), el_next - 1, pf);
         pf[UG_PF_STRIDE - 1] = 1.0;

@@ -66,6 +66,7 @@ __device__ __forceinline__ void nc_direct_A(double (&A0)[PREG], int lane) {
  * so the pair is free.  tests/test_isa_audit.py fails the build if any function writes s[30:31] without saving it. */
 __device__ __noinline__ void ug_nonleaf_guard() { __asm__ volatile(""); }
 __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int nn_, int nobj_, double& dv, double& dvs) {
+    PROF_ENTRY(CS_PGS);
     PROF_CALL(CALL_PGS);
     if (__builtin_expect(n_ < 0, 0)) ug_nonleaf_guard(); /* never: n_ >= 0 (see ug_nonleaf_guard) */
     Shared& sh = g_sh;
@@ -516,6 +517,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     dvs = lane < NV ? accs : 0.0;
     __builtin_amdgcn_wave_barrier();
     if (direct) PROF_ADD(PF_FREE_PPOST, t_post);
+    PROF_EXIT();
     return split;
 }
 
