@@ -305,6 +305,8 @@ def main(argv=None):
             vals[0] = mx[0]
             vals[3] = mx[3]
         reps.append([float(x) for x in vals.tolist()])
+        if rank == 0:  # progress on stderr (a long repetition is otherwise silent)
+            print(f"[bench] rep {r + 1}/{R}: {reps[-1][0]:.3f} s for {K} steps", file=sys.stderr, flush=True)
     order = sorted(range(R), key=lambda i: reps[i][0])
     med = reps[order[R // 2]]
     dt, substeps, resets, avg_kernel_ms = med

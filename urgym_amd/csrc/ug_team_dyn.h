@@ -262,7 +262,8 @@ __device__ __noinline__ static void serial_pre(const Scene* s) {
     PROF_ADD(PF_ENUM, t_en);
     PROF_EXIT();
 }
-/* lane 0: velocities += solver delta, positions integrate (v + split velocity) */
+/* velocities += solver delta, positions integrate (v + split velocity): lane i < NB dof i, lane NB + o object o (each
+ * element's operations as the oracle's serial loops; no element reads another) */
 __device__ __noinline__ static void serial_post(const Scene* s, int split) {
     PROF_ENTRY(CS_POST);
     PROF_CALL(CALL_POST);
@@ -270,24 +271,24 @@ __device__ __noinline__ static void serial_post(const Scene* s, int split) {
     EnvState& e = sh.e;
     const double dt = UG_DT;
     const int lane = threadIdx.x;
-    if (lane == 0) {
-        const double* DV = sh.dvout;
-        const double* DVS = sh.dvsout;
-        /* the poses this substep's narrowphase saw, before they move (the contact query's world positions) */
-        for (int i = 0; i < NB; i++) e.prevq[i] = e.q[i];
-        for (int o = 0; o < MAXOBJ; o++) {
+    const double* DV = sh.dvout;
+    const double* DVS = sh.dvsout;
+    if (lane < NB) {
+        const int i = lane;
+        /* the pose this substep's narrowphase saw, before it moves (the contact query's world positions) */
+        e.prevq[i] = e.q[i];
+        e.qd[i] = ug_vclamp(e.qd[i] + DV[i], UG_MAX_COORD_VEL);
+        double vi = split ? e.qd[i] + DVS[i] : e.qd[i];
+        e.q[i] = e.q[i] + vi * dt;
+    } else if (lane < NB + MAXOBJ) {
+        const int o = lane - NB;
+        {
             const StObj& ob = e.obj[o];
             e.prevpose[o][0] = ob.pos.x; e.prevpose[o][1] = ob.pos.y; e.prevpose[o][2] = ob.pos.z;
             e.prevpose[o][3] = ob.quat.x; e.prevpose[o][4] = ob.quat.y; e.prevpose[o][5] = ob.quat.z;
             e.prevpose[o][6] = ob.quat.w;
         }
-        for (int i = 0; i < NB; i++) {
-            e.qd[i] = ug_vclamp(e.qd[i] + DV[i], UG_MAX_COORD_VEL);
-            double vi = split ? e.qd[i] + DVS[i] : e.qd[i];
-            e.q[i] = e.q[i] + vi * dt;
-        }
-        for (int o = 0; o < s->nobj; o++) {
-            if (e.oactive[o] == 0.0) continue;
+        if (o < s->nobj && e.oactive[o] != 0.0) {
             StObj& ob = e.obj[o];
             int off = NB + 6 * o;
             if (s->ojoint[o].kind != UGJ_FREE) {
@@ -298,23 +299,23 @@ __device__ __noinline__ static void serial_post(const Scene* s, int split) {
                 ugj_frame(&s->ojoint[o], ob.w.x, qt, pt);
                 ob.quat = Q(qt[0], qt[1], qt[2], qt[3]);
                 ob.pos = V(pt[0], pt[1], pt[2]);
-                continue;
+            } else {
+                ob.v = vclamp_coord(vadd(ob.v, V(DV[off], DV[off + 1], DV[off + 2])));
+                ob.w = vclamp_coord(vadd(ob.w, V(DV[off + 3], DV[off + 4], DV[off + 5])));
+                v3 vl = ob.v, wa = ob.w;
+                if (split) {
+                    vl = vadd(vl, V(DVS[off], DVS[off + 1], DVS[off + 2]));
+                    wa = vadd(wa, V(DVS[off + 3], DVS[off + 4], DVS[off + 5]));
+                }
+                ob.pos = vadd(ob.pos, vscale(vl, dt));
+                double ang = vlen(wa);
+                if (ang * dt > UG_ANGULAR_MOTION_THR) ang = UG_ANGULAR_MOTION_THR / dt;
+                v3 ax;
+                if (ang < 0.001) ax = vscale(wa, 0.5 * dt - (dt * dt * dt) * 0.020833333333 * ang * ang);
+                else ax = vscale(wa, ug_sin(0.5 * ang * dt) / ang);
+                q4 dq = Q(ax.x, ax.y, ax.z, ug_cos(0.5 * ang * dt));
+                ob.quat = qnormalize(qmul(dq, ob.quat));
             }
-            ob.v = vclamp_coord(vadd(ob.v, V(DV[off], DV[off + 1], DV[off + 2])));
-            ob.w = vclamp_coord(vadd(ob.w, V(DV[off + 3], DV[off + 4], DV[off + 5])));
-            v3 vl = ob.v, wa = ob.w;
-            if (split) {
-                vl = vadd(vl, V(DVS[off], DVS[off + 1], DVS[off + 2]));
-                wa = vadd(wa, V(DVS[off + 3], DVS[off + 4], DVS[off + 5]));
-            }
-            ob.pos = vadd(ob.pos, vscale(vl, dt));
-            double ang = vlen(wa);
-            if (ang * dt > UG_ANGULAR_MOTION_THR) ang = UG_ANGULAR_MOTION_THR / dt;
-            v3 ax;
-            if (ang < 0.001) ax = vscale(wa, 0.5 * dt - (dt * dt * dt) * 0.020833333333 * ang * ang);
-            else ax = vscale(wa, ug_sin(0.5 * ang * dt) / ang);
-            q4 dq = Q(ax.x, ax.y, ax.z, ug_cos(0.5 * ang * dt));
-            ob.quat = qnormalize(qmul(dq, ob.quat));
         }
     }
     PROF_EXIT();

@@ -654,4 +654,9 @@ __device__ __forceinline__ static void build_row(const Scene* s, int pos, double
     }
     PROF_ADD(PF_RB3, t_rb3);
 }
+/* the substep's rows, lane per row: outlined, so the row build's registers are its own and not live kernel state
+ * (inline, its loop spilled 31 / reloaded 80 kernel registers per substep) */
+__device__ __noinline__ static void team_build_rows(const Scene* s, int n, double* ws, bool store_j) {
+    for (int p = threadIdx.x; p < n; p += TEAM) build_row(s, p, ws + WS_ROWS + p * RS, store_j);
+}
 

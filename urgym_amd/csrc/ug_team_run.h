@@ -65,7 +65,7 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
 #else
     const bool nc_direct = n == 12 && nnc == 12 && ballot(lane < 12 && sh.rs[lane].kind == 0) == 0ull;
 #endif
-    for (int p = lane; p < n; p += TEAM) build_row(s, p, ws + WS_ROWS + p * RS, !nc_direct);
+    team_build_rows(s, n, ws, !nc_direct);
     PROF_ADD(PF_ROWB, t_rowb);
     __threadfence_block();
     __syncthreads();
