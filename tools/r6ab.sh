@@ -3,8 +3,8 @@
 set -u
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
 TAG=$1; shift; O=gpurun_out/$TAG; mkdir -p $O
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1 || { echo TESTS_FAIL; tail -30 $O/tests.log; exit 1; }
-tail -1 $O/tests.log
+[ "${SKIP_TESTS:-0}" = 1 ] || timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1 || { echo TESTS_FAIL; tail -30 $O/tests.log; exit 1; }
+[ -f $O/tests.log ] && tail -1 $O/tests.log
 for te in "$@"; do
   set -- $te
   BL=urgym_amd/_lib/base/liburgym.so; [ "$1" = 3 ] || [ "$1" = 5 ] && BL=urgym_amd/_lib/base/liburgym_g8.so

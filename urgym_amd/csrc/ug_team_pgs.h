@@ -259,6 +259,18 @@ __device__ __forceinline__ void swap16_d(double& x, double& y) {
  * normals from 20, friction from 26, 38 positions */
 #define FS6_F0 26
 #define FS6_NF 12
+/* narrower single-slot layouts for at most 14 non-contact rows (tools/row_hist.py, round 6): CubesPush's common solves
+ * (12-13 non-contact rows, 8 normals, 16 friction rows: 86 % of its step solves) at 38 positions instead of FS's 50
+ * (normals from 14, friction from 22), its 9-10-normal solves at 44, and CubesGrasp's (12-14 non-contact rows, 4-6
+ * normals) at 32 instead of FS6's 38 (normals from 14, friction from 20) -- every pad position costs a row update
+ * in each of the 50 sweeps */
+#define FS14_NC 14
+#define FS14G_F0 20
+#define FS14G_NF 12
+#define FS14P_F0 22
+#define FS14P_NF 16
+#define FS14W_F0 24
+#define FS14W_NF 20
 /* the two-slot layout for Golf's contact solves (13 non-contact rows with the club's limit row, up to 28
  * normals, friction + rolling rows up to 52): non-contact rows at [0, nnc), pads to 16, normals from 16,
  * friction from 44, 96 positions */

@@ -65,7 +65,11 @@ __device__ __forceinline__ static void team_substep(const Scene* s, double* ws) 
 #else
     const bool nc_direct = n == 12 && nnc == 12 && ballot(lane < 12 && sh.rs[lane].kind == 0) == 0ull;
 #endif
+#ifdef UG_INLINE_ROWS /* A/B aid: the row build inlined into the kernel as before round 6 */
+    for (int p = lane; p < n; p += TEAM) build_row(s, p, ws + WS_ROWS + p * RS, !nc_direct);
+#else
     team_build_rows(s, n, ws, !nc_direct);
+#endif
     PROF_ADD(PF_ROWB, t_rowb);
     __threadfence_block();
     __syncthreads();

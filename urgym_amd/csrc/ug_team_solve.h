@@ -93,6 +93,10 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                      : (fb <= FL_F0S && n - fb <= FL_NFS)                  ? FL_F0S
                                                                            : FL_F0;
     /* the single-slot layout: few normals (CubesPush 8, CubesGrasp 4-6), up to 20 non-contact rows */
+    const bool fs14ok = !flok && nnc <= FS14_NC && nn >= 3;
+    const bool fs14g = fs14ok && nn <= FS14G_F0 - FS14_NC && n - fb <= FS14G_NF;
+    const bool fs14p = fs14ok && !fs14g && nn <= FS14P_F0 - FS14_NC && n - fb <= FS14P_NF;
+    const bool fs14w = fs14ok && !fs14g && !fs14p && nn <= FS14W_F0 - FS14_NC && n - fb <= FS14W_NF;
     const bool fs6ok = !flok && nnc <= FS_NC && nn >= 3 && nn <= FS6_F0 - FS_NC && n - fb <= FS6_NF;
     const bool fsok = !flok && nnc <= FS_NC && nn >= 3 && nn <= FS_F0 - FS_NC && n - fb <= FS_NF;
     const bool g12ok = !flok && !fsok && nnc <= FG12_NC && nn >= 3 && nn <= FG12_F0 - FG12_NC && n - fb <= FG12_NF;
@@ -101,6 +105,9 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     const bool fgok = !flok && !fsok && !g12ok && !g18ok && nnc <= FG_NC && nn >= 16 && nn <= FG_F0 - FG_NC &&
                       n - fb <= FG_NF;
     const PosMap pm = flok ? PosMap{n, fb, flf0, nnc, nnc, flf0 + 2 * (flf0 - FL_NNC)}
+                      : fs14g ? PosMap{n, fb, FS14G_F0, nnc, FS14_NC, FS14G_F0 + FS14G_NF}
+                      : fs14p ? PosMap{n, fb, FS14P_F0, nnc, FS14_NC, FS14P_F0 + FS14P_NF}
+                      : fs14w ? PosMap{n, fb, FS14W_F0, nnc, FS14_NC, FS14W_F0 + FS14W_NF}
                       : fs6ok ? PosMap{n, fb, FS6_F0, nnc, FS_NC, FS6_F0 + FS6_NF}
                       : fsok ? PosMap{n, fb, FS_F0, nnc, FS_NC, FS_F0 + FS_NF}
                       : g12ok ? PosMap{n, fb, FG12_F0, nnc, FG12_NC, FG12_F0 + FG12_NF}
@@ -470,7 +477,10 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         return split;
     };
     PROF_T0(t_post);
-    const int split = pm.fl == FS6_F0         ? passes_fs(FLShape<FS_NC, FS6_F0, FS6_NF>{})
+    const int split = pm.fl == FS14G_F0       ? passes_fs(FLShape<FS14_NC, FS14G_F0, FS14G_NF>{})
+                      : pm.fl == FS14P_F0     ? passes_fs(FLShape<FS14_NC, FS14P_F0, FS14P_NF>{})
+                      : pm.fl == FS14W_F0     ? passes_fs(FLShape<FS14_NC, FS14W_F0, FS14W_NF>{})
+                      : pm.fl == FS6_F0       ? passes_fs(FLShape<FS_NC, FS6_F0, FS6_NF>{})
                       : pm.fl == FS_F0        ? passes_fs(FLShape<FS_NC, FS_F0, FS_NF>{})
                       : pm.fl == FG12_F0      ? passes_fs(FLShape<FG12_NC, FG12_F0, FG12_NF>{})
                       : pm.fl == FG18_F0 && pm.nb == FG18_NC ? passes_fl(FLShape<FG18_NC, FG18_F0, FG18_NF>{})
