@@ -271,6 +271,10 @@ __device__ __forceinline__ void swap16_d(double& x, double& y) {
 #define FS14P_NF 16
 #define FS14W_F0 24
 #define FS14W_NF 20
+/* and Golf's 11-15-normal solves (12-13 non-contact rows, friction + rolling rows 2 nn + 2): single-slot at 61 positions
+ * (normals from 14, friction + rolling from 29) instead of FG12's 64 (<= 12 normals) or FG18's two-slot 74 */
+#define FS14H_F0 29
+#define FS14H_NF 32
 /* the two-slot layout for Golf's contact solves (13 non-contact rows with the club's limit row, up to 28
  * normals, friction + rolling rows up to 52): non-contact rows at [0, nnc), pads to 16, normals from 16,
  * friction from 44, 96 positions */

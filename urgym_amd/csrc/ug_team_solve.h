@@ -97,6 +97,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     const bool fs14g = fs14ok && nn <= FS14G_F0 - FS14_NC && n - fb <= FS14G_NF;
     const bool fs14p = fs14ok && !fs14g && nn <= FS14P_F0 - FS14_NC && n - fb <= FS14P_NF;
     const bool fs14w = fs14ok && !fs14g && !fs14p && nn <= FS14W_F0 - FS14_NC && n - fb <= FS14W_NF;
+    const bool fs14h = fs14ok && !fs14g && !fs14p && !fs14w && nn <= FS14H_F0 - FS14_NC && n - fb <= FS14H_NF;
     const bool fs6ok = !flok && nnc <= FS_NC && nn >= 3 && nn <= FS6_F0 - FS_NC && n - fb <= FS6_NF;
     const bool fsok = !flok && nnc <= FS_NC && nn >= 3 && nn <= FS_F0 - FS_NC && n - fb <= FS_NF;
     const bool g12ok = !flok && !fsok && nnc <= FG12_NC && nn >= 3 && nn <= FG12_F0 - FG12_NC && n - fb <= FG12_NF;
@@ -110,6 +111,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                       : fs14w ? PosMap{n, fb, FS14W_F0, nnc, FS14_NC, FS14W_F0 + FS14W_NF}
                       : fs6ok ? PosMap{n, fb, FS6_F0, nnc, FS_NC, FS6_F0 + FS6_NF}
                       : fsok ? PosMap{n, fb, FS_F0, nnc, FS_NC, FS_F0 + FS_NF}
+                      : fs14h ? PosMap{n, fb, FS14H_F0, nnc, FS14_NC, FS14H_F0 + FS14H_NF}
                       : g12ok ? PosMap{n, fb, FG12_F0, nnc, FG12_NC, FG12_F0 + FG12_NF}
                       : g18ok ? PosMap{n, fb, FG18_F0, nnc, FG18_NC, FG18_F0 + FG18_NF}
                       : fgok ? PosMap{n, fb, FG_F0, nnc, FG_NC, FG_F0 + FG_NF}
@@ -480,6 +482,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     const int split = pm.fl == FS14G_F0       ? passes_fs(FLShape<FS14_NC, FS14G_F0, FS14G_NF>{})
                       : pm.fl == FS14P_F0     ? passes_fs(FLShape<FS14_NC, FS14P_F0, FS14P_NF>{})
                       : pm.fl == FS14W_F0     ? passes_fs(FLShape<FS14_NC, FS14W_F0, FS14W_NF>{})
+                      : pm.fl == FS14H_F0     ? passes_fs(FLShape<FS14_NC, FS14H_F0, FS14H_NF>{})
                       : pm.fl == FS6_F0       ? passes_fs(FLShape<FS_NC, FS6_F0, FS6_NF>{})
                       : pm.fl == FS_F0        ? passes_fs(FLShape<FS_NC, FS_F0, FS_NF>{})
                       : pm.fl == FG12_F0      ? passes_fs(FLShape<FG12_NC, FG12_F0, FG12_NF>{})
