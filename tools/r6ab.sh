@@ -10,7 +10,7 @@ for te in "$@"; do
   BL=urgym_amd/_lib/base/liburgym.so; [ "$1" = 3 ] || [ "$1" = 5 ] && BL=urgym_amd/_lib/base/liburgym_g8.so
   for v in new base; do
     if [ $v = base ]; then export URGYM_LIB=$PWD/$BL; else unset URGYM_LIB; fi
-    timeout -k 10 400 python bench.py --no-cpu-baseline --task $1 --envs $2 --steps 60 --warmup 10 --reps 3 > $O/t$1_$v.json 2> $O/t$1_$v.err || { echo "T$1 $v FAIL"; tail -3 $O/t$1_$v.err; exit 1; }
+    timeout -k 10 400 python bench.py --no-cpu-baseline --task $1 --envs $2 --steps 60 --warmup 10 --reps 3 ${BENCH_ARGS:-} > $O/t$1_$v.json 2> $O/t$1_$v.err || { echo "T$1 $v FAIL"; tail -3 $O/t$1_$v.err; exit 1; }
   done
   unset URGYM_LIB
   echo "task $1: new $(python -c "import json; d=json.load(open('$O/t$1_new.json')); print(round(d['value']), [round(v) for v in d['rep_values']])") base $(python -c "import json; d=json.load(open('$O/t$1_base.json')); print(round(d['value']), [round(v) for v in d['rep_values']])")"
