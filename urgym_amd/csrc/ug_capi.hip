@@ -557,17 +557,35 @@ __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, ui
     }
 }
 
-/* Launch levels from the step's own action (scheduling only; BallBalance, TwoBalls, CubesPush, CubesPushDiff): per env, the state
+/* Launch levels from the step's own action (scheduling only; BallBalance, TwoBalls, CubesPush, CubesPushDiff, CubesGrasp,
+ * Golf): per env, the state
  * inputs its last step left in pfeat (team_priority; the record's last double names the model) and the 3 action
  * components of this step -> the task's model -> the level; envs whose record is not flagged (a predicted truncation,
  * an inactive ball) keep their level.  One thread per env, before k_order. */
 static_assert(UG_ACT_DIM(UG_TASK_TWOBALLS) == UG_PT_IN - UG_PT_STATE_IN, "TwoBalls' action: the model's last inputs");
 static_assert(UG_ACT_DIM(UG_TASK_CUBESPUSH) == 3 && UG_ACT_DIM(UG_TASK_CUBESPUSHDIFF) == 3, "CubesPush's action: 3");
 static_assert(UG_ACT_DIM(UG_TASK_BALLBALANCE) == 3, "BallBalance's action: 3");
+static_assert(UG_ACT_DIM(UG_TASK_GOLF) == 3, "Golf's action: 3");
 /* CubesGrasp (model 4 / 5): the branch the step's random.choices will take, from the env's stream without consuming it */
 __device__ static int cg_branch(const uint32_t* mt, const float* a, int i) {
     return ugg_cg_choose(a[0], a[1], mt_peek_random(mt + (size_t)i * UG_MT_WORDS));
 }
+/* a gradient-boosted tree ensemble's log-odds (tools/fit_priority.py tree_header: flat node arrays UG_PF_<P>_*, a leaf
+ * has feature -1; x <= threshold goes left, so a NaN input goes right; the depth bound only guards a corrupt table) */
+__device__ static double trees_logodds(const double* x, int ntrees, double base, const short* root, const signed char* feat,
+                                       const double* thr, const short* left, const short* right, const double* val) {
+    double lg = base;
+    for (int t = 0; t < ntrees; t++) {
+        int k = root[t];
+        for (int d = 0; d < 64 && feat[k] >= 0; d++) k = x[feat[k]] <= thr[k] ? left[k] : right[k];
+        lg += val[k];
+    }
+    return lg;
+}
+#define UG_TREES_LOGODDS(P, x)                                                                                          \
+    trees_logodds(x, UG_PF_##P##_TREES, UG_PF_##P##_BASE, UG_PF_##P##_ROOT, UG_PF_##P##_FEAT, UG_PF_##P##_THR,         \
+                  UG_PF_##P##_LEFT, UG_PF_##P##_RIGHT, UG_PF_##P##_VAL)
+static_assert(UG_PF_TBT_IN == UG_PT_IN, "TwoBalls' trees take the MLP's inputs");
 __global__ void k_prio(const double* pfeat, const float* act, const uint32_t* mt, uint8_t* prio, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -591,18 +609,28 @@ __global__ void k_prio(const double* pfeat, const float* act, const uint32_t* mt
             return;
         }
     }
-    if (model == 1.0) { /* TwoBalls: 31 state inputs + the action */
+    if (model == 1.0) { /* TwoBalls: 31 state inputs + the action -> the tree ensemble (round 6; the MLP of
+                           * prio_model_tb.h under -DUG_TB_MLP) */
         double x[UG_PT_IN];
         for (int k = 0; k < UG_PT_STATE_IN; k++) x[k] = f[k];
         for (int a = 0; a < UG_PT_IN - UG_PT_STATE_IN; a++) x[UG_PT_STATE_IN + a] = (double)act[(size_t)i * 3 + a];
+#ifdef UG_TB_MLP
         prio[i] = (uint8_t)logit_level(mlp_logit<UG_PT_IN, UG_PT_HID>(x, UG_PT_MU, UG_PT_SD, UG_PT_W1, UG_PT_B1, UG_PT_W2,
                                                                        UG_PT_B2), UG_PT_L0, UG_PT_DL);
+#else
+        prio[i] = (uint8_t)logit_level(UG_TREES_LOGODDS(TBT, x), UG_PF_TBT_L0, UG_PF_TBT_DL);
+#endif
     } else if (model == 3.0) { /* BallBalance: the ball's 14 inputs + the action */
         double x[UG_PM_IN];
         for (int k = 0; k < UG_BALL_IN; k++) x[k] = f[k];
         for (int a = 0; a < 3; a++) x[UG_BALL_IN + a] = (double)act[(size_t)i * 3 + a];
         prio[i] = (uint8_t)logit_level(mlp_logit<UG_PM_IN, UG_PM_HID>(x, UG_PM_MU, UG_PM_SD, UG_PM_W1, UG_PM_B1, UG_PM_W2,
                                                                        UG_PM_B2), UG_PM_L0, UG_PM_DL);
+    } else if (model == 6.0) { /* Golf: q, qd, the ball's position + the action -> the tree ensemble's log-odds */
+        double x[UG_PF_GF_IN];
+        for (int k = 0; k < UG_PF_GF_IN - 3; k++) x[k] = f[k];
+        for (int a = 0; a < 3; a++) x[UG_PF_GF_IN - 3 + a] = (double)act[(size_t)i * 3 + a];
+        prio[i] = (uint8_t)logit_level(UG_TREES_LOGODDS(GF, x), UG_PF_GF_L0, UG_PF_GF_DL);
     } else if (model == 2.0) { /* CubesPush(Diff): q, qd + the action */
         double x[UG_PC_IN];
         for (int k = 0; k < UG_PC_IN - 3; k++) x[k] = f[k];
@@ -885,7 +913,7 @@ struct urgym_handle {
     int* d_queue = nullptr;   // the step / reset work-queue counter
     int slots = 0;            // k_step / k_reset blocks: the wave slots the device holds at once (CUs x blocks per CU)
     uint8_t* d_prio = nullptr;
-    double* d_pfeat = nullptr; // BallBalance, TwoBalls, CubesPush(Diff): per env the predictor's state inputs for k_prio (UG_PF_STRIDE doubles)
+    double* d_pfeat = nullptr; // BallBalance, TwoBalls, CubesPush(Diff), CubesGrasp, Golf: per env the predictor's state inputs for k_prio (UG_PF_STRIDE doubles)
     int* d_stats = nullptr;   // UG_NSTAT event counters per env
     uint8_t* d_flags = nullptr; // UG_FLAG_* of the last step / reset per env
     int autoreset = 0, max_steps = 0;
@@ -971,7 +999,7 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     const char* noprio = getenv("URGYM_NO_PRIO_MODEL");
     if ((!noprio || !*noprio || *noprio == '0') &&
         (task == URGYM_TASK_BALLBALANCE || task == URGYM_TASK_TWOBALLSBALANCE || task == URGYM_TASK_CUBESPUSH ||
-         task == URGYM_TASK_CUBESPUSHDIFF || task == URGYM_TASK_CUBESGRASP)) {
+         task == URGYM_TASK_CUBESPUSHDIFF || task == URGYM_TASK_CUBESGRASP || task == URGYM_TASK_GOLF)) {
         HIPCHK(h, hipMalloc(&h->d_pfeat, sizeof(double) * UG_PF_STRIDE * N));
         HIPCHK(h, hipMemsetAsync(h->d_pfeat, 0, sizeof(double) * UG_PF_STRIDE * N, h->stream));
     }

@@ -31,6 +31,8 @@
 #include "prio_model_tb.h"
 #include "prio_model_cp.h"
 #include "prio_model_cg.h"
+#include "prio_model_gf.h"
+#include "prio_model_tbt.h"
 #include "ug_glue.h"
 
 namespace ugd {

@@ -768,6 +768,11 @@ static_assert(UG_PC_IN == 2 * 12 + 3, "q[12], qd[12], the action");
  * and evaluates ugg_cg_choose as the glue will.  The env leaves q, qd and its 7 motor targets here; the flag is 4 (5: the
  * step truncates, so its autoreset follows) */
 static_assert(UG_PG_IN == 2 * 12 + 7 + 2, "q[12], qd[12], targets - q [7], the branch, the truncation");
+/* Golf: the log-odds of "this step runs >= 60 substeps" from q, qd, the ball's position and the step's action, a
+ * gradient-boosted tree ensemble (prio_model_gf.h, tools/fit_priority.py --task 3: held-out list schedule 351 -> 300
+ * substeps on 512 slots, longest-first 286; an MLP on the same inputs does not separate the long steps).  The env leaves
+ * q, qd and the ball's position here; the flag is 6 */
+static_assert(UG_PF_GF_IN == 2 * 12 + 3 + 3, "q[12], qd[12], the ball's position, the action");
 __device__ static int team_priority(const Scene* s, int nsub, int el_next, int max_steps, int autoreset, double* pf) {
     const EnvState& e = g_sh.e;
     if (pf) pf[UG_PF_STRIDE - 1] = 0.0; /* k_prio keeps this level unless the TwoBalls model applies */
@@ -785,6 +790,14 @@ __device__ static int team_priority(const Scene* s, int nsub, int el_next, int m
         tb_state_inputs(e, qmat(e.obj[0].quat), el_next - 1, pf);
         pf[UG_PF_STRIDE - 1] = 1.0;
         return 0;
+    }
+    if constexpr (NB == 12) { /* Golf (not GolfJoints): the step's length class from q, qd, the ball and (k_prio) the action */
+        if (s->variant == UG_TASK_GOLF && pf && e.oactive[1] != 0.0) {
+            for (int j = 0; j < NB; j++) { pf[j] = e.q[j]; pf[NB + j] = e.qd[j]; }
+            pf[2 * NB] = e.obj[1].pos.x; pf[2 * NB + 1] = e.obj[1].pos.y; pf[2 * NB + 2] = e.obj[1].pos.z;
+            pf[UG_PF_STRIDE - 1] = 6.0;
+            return 0;
+        }
     }
     if constexpr (NB == 12) { /* CubesPush / CubesPushDiff: the step's length from q, qd and (k_prio) the action */
         if (s->task == UG_TASK_CUBESPUSH && pf) {
