@@ -565,7 +565,7 @@ __global__ void __launch_bounds__(TEAM, 1) k_step(const Scene* sc, double* S, ui
 static_assert(UG_ACT_DIM(UG_TASK_TWOBALLS) == UG_PT_IN - UG_PT_STATE_IN, "TwoBalls' action: the model's last inputs");
 static_assert(UG_ACT_DIM(UG_TASK_CUBESPUSH) == 3 && UG_ACT_DIM(UG_TASK_CUBESPUSHDIFF) == 3, "CubesPush's action: 3");
 static_assert(UG_ACT_DIM(UG_TASK_BALLBALANCE) == 3, "BallBalance's action: 3");
-static_assert(UG_ACT_DIM(UG_TASK_GOLF) == 3, "Golf's action: 3");
+static_assert(UG_ACT_DIM(UG_TASK_GOLF) == 3 && UG_ACT_DIM(UG_TASK_GOLFJOINTS) == 6, "Golf's action: 3, GolfJoints' 6");
 /* CubesGrasp (model 4 / 5): the branch the step's random.choices will take, from the env's stream without consuming it */
 __device__ static int cg_branch(const uint32_t* mt, const float* a, int i) {
     return ugg_cg_choose(a[0], a[1], mt_peek_random(mt + (size_t)i * UG_MT_WORDS));
@@ -631,6 +631,11 @@ __global__ void k_prio(const double* pfeat, const float* act, const uint32_t* mt
         for (int k = 0; k < UG_PF_GF_IN - 3; k++) x[k] = f[k];
         for (int a = 0; a < 3; a++) x[UG_PF_GF_IN - 3 + a] = (double)act[(size_t)i * 3 + a];
         prio[i] = (uint8_t)logit_level(UG_TREES_LOGODDS(GF, x), UG_PF_GF_L0, UG_PF_GF_DL);
+    } else if (model == 7.0) { /* GolfJoints: the same state inputs + its 6 joint deltas -> its own trees */
+        double x[UG_PF_GJ_IN];
+        for (int k = 0; k < UG_PF_GJ_IN - 6; k++) x[k] = f[k];
+        for (int a = 0; a < 6; a++) x[UG_PF_GJ_IN - 6 + a] = (double)act[(size_t)i * 6 + a];
+        prio[i] = (uint8_t)logit_level(UG_TREES_LOGODDS(GJ, x), UG_PF_GJ_L0, UG_PF_GJ_DL);
     } else if (model == 2.0) { /* CubesPush(Diff): q, qd + the action */
         double x[UG_PC_IN];
         for (int k = 0; k < UG_PC_IN - 3; k++) x[k] = f[k];
@@ -999,7 +1004,8 @@ static int create_impl(urgym_handle* h, int task, int n, int dev, uint32_t seed,
     const char* noprio = getenv("URGYM_NO_PRIO_MODEL");
     if ((!noprio || !*noprio || *noprio == '0') &&
         (task == URGYM_TASK_BALLBALANCE || task == URGYM_TASK_TWOBALLSBALANCE || task == URGYM_TASK_CUBESPUSH ||
-         task == URGYM_TASK_CUBESPUSHDIFF || task == URGYM_TASK_CUBESGRASP || task == URGYM_TASK_GOLF)) {
+         task == URGYM_TASK_CUBESPUSHDIFF || task == URGYM_TASK_CUBESGRASP || task == URGYM_TASK_GOLF ||
+         task == URGYM_TASK_GOLFJOINTS)) {
         HIPCHK(h, hipMalloc(&h->d_pfeat, sizeof(double) * UG_PF_STRIDE * N));
         HIPCHK(h, hipMemsetAsync(h->d_pfeat, 0, sizeof(double) * UG_PF_STRIDE * N, h->stream));
     }

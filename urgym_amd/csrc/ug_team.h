@@ -33,6 +33,7 @@
 #include "prio_model_cg.h"
 #include "prio_model_gf.h"
 #include "prio_model_tbt.h"
+#include "prio_model_gj.h"
 #include "ug_glue.h"
 
 namespace ugd {

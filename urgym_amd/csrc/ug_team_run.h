@@ -773,6 +773,7 @@ static_assert(UG_PG_IN == 2 * 12 + 7 + 2, "q[12], qd[12], targets - q [7], the b
  * substeps on 512 slots, longest-first 286; an MLP on the same inputs does not separate the long steps).  The env leaves
  * q, qd and the ball's position here; the flag is 6 */
 static_assert(UG_PF_GF_IN == 2 * 12 + 3 + 3, "q[12], qd[12], the ball's position, the action");
+static_assert(UG_PF_GJ_IN == 2 * 12 + 3 + 6, "GolfJoints: q[12], qd[12], the ball's position, the 6 joint deltas");
 __device__ static int team_priority(const Scene* s, int nsub, int el_next, int max_steps, int autoreset, double* pf) {
     const EnvState& e = g_sh.e;
     if (pf) pf[UG_PF_STRIDE - 1] = 0.0; /* k_prio keeps this level unless the TwoBalls model applies */
@@ -792,10 +793,10 @@ __device__ static int team_priority(const Scene* s, int nsub, int el_next, int m
         return 0;
     }
     if constexpr (NB == 12) { /* Golf (not GolfJoints): the step's length class from q, qd, the ball and (k_prio) the action */
-        if (s->variant == UG_TASK_GOLF && pf && e.oactive[1] != 0.0) {
+        if ((s->variant == UG_TASK_GOLF || s->variant == UG_TASK_GOLFJOINTS) && pf && e.oactive[1] != 0.0) {
             for (int j = 0; j < NB; j++) { pf[j] = e.q[j]; pf[NB + j] = e.qd[j]; }
             pf[2 * NB] = e.obj[1].pos.x; pf[2 * NB + 1] = e.obj[1].pos.y; pf[2 * NB + 2] = e.obj[1].pos.z;
-            pf[UG_PF_STRIDE - 1] = 6.0;
+            pf[UG_PF_STRIDE - 1] = s->variant == UG_TASK_GOLF ? 6.0 : 7.0; /* GolfJoints: its own trees (6 joint deltas) */
             return 0;
         }
     }
