@@ -19,7 +19,7 @@ def load(hdr, P):
     return d
 
 
-@pytest.mark.parametrize("hdr,P", [("prio_model_gf.h", "GF"), ("prio_model_gj.h", "GJ"), ("prio_model_tbt.h", "TBT")])
+@pytest.mark.parametrize("hdr,P", [("prio_model_gf.h", "GF"), ("prio_model_gj.h", "GJ"), ("prio_model_tbt.h", "TBT"), ("prio_model_cgt.h", "CGT")])
 def test_tree_tables_well_formed(hdr, P):
     d = load(hdr, P)
     nt, nin = int(d["TREES"]), int(d["IN"])

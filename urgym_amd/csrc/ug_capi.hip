@@ -586,6 +586,7 @@ __device__ static double trees_logodds(const double* x, int ntrees, double base,
     trees_logodds(x, UG_PF_##P##_TREES, UG_PF_##P##_BASE, UG_PF_##P##_ROOT, UG_PF_##P##_FEAT, UG_PF_##P##_THR,         \
                   UG_PF_##P##_LEFT, UG_PF_##P##_RIGHT, UG_PF_##P##_VAL)
 static_assert(UG_PF_TBT_IN == UG_PT_IN, "TwoBalls' trees take the MLP's inputs");
+static_assert(UG_PF_CGT_IN == UG_PG_IN, "CubesGrasp's trees take the MLP's inputs");
 __global__ void k_prio(const double* pfeat, const float* act, const uint32_t* mt, uint8_t* prio, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -604,8 +605,12 @@ __global__ void k_prio(const double* pfeat, const float* act, const uint32_t* mt
             }
             x[2 * NB + 7] = (double)sel;
             x[2 * NB + 8] = model == 5.0 ? 1.0 : 0.0;
+#ifdef UG_CG_MLP /* the round-6 MLP classifier (prio_model_cg.h); the trees replace it */
             prio[i] = (uint8_t)logit_level(mlp_logit<UG_PG_IN, UG_PG_HID>(x, UG_PG_MU, UG_PG_SD, UG_PG_W1, UG_PG_B1, UG_PG_W2,
                                                                            UG_PG_B2), UG_PG_L0, UG_PG_DL);
+#else
+            prio[i] = (uint8_t)logit_level(UG_TREES_LOGODDS(CGT, x), UG_PF_CGT_L0, UG_PF_CGT_DL);
+#endif
             return;
         }
     }

@@ -34,6 +34,7 @@
 #include "prio_model_gf.h"
 #include "prio_model_tbt.h"
 #include "prio_model_gj.h"
+#include "prio_model_cgt.h"
 #include "ug_glue.h"
 
 namespace ugd {
