@@ -35,10 +35,10 @@ def test_every_env_stepped_once_per_launch(built):
     assert np.array_equal(sb[:small], ss)
 
 
-@pytest.mark.parametrize("task", [2, 0, 1, 6])
+@pytest.mark.parametrize("task", [2, 0, 1, 6, 3, 5])
 def test_launch_order_models_change_no_result(built, task, monkeypatch):
     """The k_prio models only order the launch (CubesGrasp's peeks each env's MT19937 stream for the branch its
-    random.choices will take): a handle with the models and one without them (URGYM_NO_PRIO_MODEL: the last-substep
+    random.choices will take; Golf, GolfJoints, TwoBalls and CubesGrasp walk tree ensembles): a handle with the models and one without them (URGYM_NO_PRIO_MODEL: the last-substep
     order) give the same results, states and streams bit for bit, across an autoreset (CubesGrasp truncates at 20)."""
     from urgym_amd._native import Sim
     from urgym_amd.envs import spaces_for
@@ -50,7 +50,7 @@ def test_launch_order_models_change_no_result(built, task, monkeypatch):
     for off in ("0", "1"):
         monkeypatch.setenv("URGYM_NO_PRIO_MODEL", off)
         sim = Sim(task, n, seed=SEED)
-        sim.set_autoreset(True, {0: 500, 1: 50, 2: 20, 6: 500}[task])
+        sim.set_autoreset(True, {0: 500, 1: 50, 2: 20, 6: 500, 3: 100, 5: 100}[task])
         sim.reset()
         outs = [sim.step(a) for a in acts]
         res.append((outs, sim.get_state(), sim.get_rng()))
