@@ -275,6 +275,12 @@ __device__ __forceinline__ void swap16_d(double& x, double& y) {
  * (normals from 14, friction + rolling from 29) instead of FG12's 64 (<= 12 normals) or FG18's two-slot 74 */
 #define FS14H_F0 29
 #define FS14H_NF 32
+/* solves with one or two normals and up to 22 non-contact rows (Box-v0's: 15-21 non-contact rows -- the box's joint
+ * limits and button motor beside the arm's 12 -- and one normal, 91 % of its step solves; BallBalance's first reset
+ * contacts): 28 positions (normals from 22, friction from 24) instead of the general path's chunked 32-span */
+#define FSB_NC 22
+#define FSB_F0 24
+#define FSB_NF 4
 /* the two-slot layout for Golf's contact solves (13 non-contact rows with the club's limit row, up to 28
  * normals, friction + rolling rows up to 52): non-contact rows at [0, nnc), pads to 16, normals from 16,
  * friction from 44, 96 positions */

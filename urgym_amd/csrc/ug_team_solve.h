@@ -93,6 +93,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
                      : (fb <= FL_F0S && n - fb <= FL_NFS)                  ? FL_F0S
                                                                            : FL_F0;
     /* the single-slot layout: few normals (CubesPush 8, CubesGrasp 4-6), up to 20 non-contact rows */
+    const bool fsb = !flok && nnc <= FSB_NC && nn >= 1 && nn <= FSB_F0 - FSB_NC && n - fb <= FSB_NF;
     const bool fs14ok = !flok && nnc <= FS14_NC && nn >= 3;
     const bool fs14g = fs14ok && nn <= FS14G_F0 - FS14_NC && n - fb <= FS14G_NF;
     const bool fs14p = fs14ok && !fs14g && nn <= FS14P_F0 - FS14_NC && n - fb <= FS14P_NF;
@@ -106,6 +107,7 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
     const bool fgok = !flok && !fsok && !g12ok && !g18ok && nnc <= FG_NC && nn >= 16 && nn <= FG_F0 - FG_NC &&
                       n - fb <= FG_NF;
     const PosMap pm = flok ? PosMap{n, fb, flf0, nnc, nnc, flf0 + 2 * (flf0 - FL_NNC)}
+                      : fsb ? PosMap{n, fb, FSB_F0, nnc, FSB_NC, FSB_F0 + FSB_NF}
                       : fs14g ? PosMap{n, fb, FS14G_F0, nnc, FS14_NC, FS14G_F0 + FS14G_NF}
                       : fs14p ? PosMap{n, fb, FS14P_F0, nnc, FS14_NC, FS14P_F0 + FS14P_NF}
                       : fs14w ? PosMap{n, fb, FS14W_F0, nnc, FS14_NC, FS14W_F0 + FS14W_NF}
@@ -479,7 +481,8 @@ __device__ __noinline__ static int team_pgs(double* ws_, int n_, int nnc_, int n
         return split;
     };
     PROF_T0(t_post);
-    const int split = pm.fl == FS14G_F0       ? passes_fs(FLShape<FS14_NC, FS14G_F0, FS14G_NF>{})
+    const int split = pm.fl == FSB_F0 && pm.nb == FSB_NC ? passes_fs(FLShape<FSB_NC, FSB_F0, FSB_NF>{})
+                      : pm.fl == FS14G_F0       ? passes_fs(FLShape<FS14_NC, FS14G_F0, FS14G_NF>{})
                       : pm.fl == FS14P_F0     ? passes_fs(FLShape<FS14_NC, FS14P_F0, FS14P_NF>{})
                       : pm.fl == FS14W_F0     ? passes_fs(FLShape<FS14_NC, FS14W_F0, FS14W_NF>{})
                       : pm.fl == FS14H_F0     ? passes_fs(FLShape<FS14_NC, FS14H_F0, FS14H_NF>{})
